@@ -1,0 +1,246 @@
+/*
+ * dbgpu_agg.h — C ABI of the MI355X-native filter + hash GROUP BY path for Databend.
+ *
+ * This is the drop-in boundary.  Every entry point replaces one seam of the
+ * reference's Rust pipeline; the seam is cited next to each declaration.  Paths are relative to
+ * the Databend tree (sundy-li/databend @ 2024-10-24):
+ *   EAGG/ = src/query/expression/src/aggregate/
+ *   AGG/  = src/query/service/src/pipelines/processors/transforms/aggregator/
+ *   FUN/  = src/query/functions/src/aggregates/
+ *   EXP/  = src/query/expression/src/
+ *
+ * Conventions (mirroring the reference):
+ *  - Every function returns a status code; DBG_OK == 0.  The message of the last failure on the
+ *    calling thread is returned by dbg_last_error() (reference: Result<_, ErrorCode>).
+ *  - Column buffers use Databend's in-memory layout (EXP/values.rs:157-176): fixed-width values are
+ *    contiguous little-endian; Decimal128 is i128 LE; String is bytes + (len+1) u64 offsets
+ *    (EXP/types/string.rs:220-223); validity and Boolean are arrow Bitmaps, LSB-first with a bit
+ *    offset (EXP/types/nullable.rs:245-248).  No torch types appear in any signature.
+ *  - A handle is used by one thread at a time (TransformPartialAggregate::transform takes &mut self);
+ *    distinct handles may be used concurrently.  Each handle owns a HIP stream (or borrows the
+ *    caller's, see dbg_agg_set_stream) and its device memory.
+ *  - on_device == 0: column pointers are host memory, borrowed for the duration of the call only.
+ *    on_device == 1: pointers are device memory on the handle's device and must stay valid and
+ *    unmodified until the next synchronising call on the handle (dbg_agg_finalize, dbg_agg_reset,
+ *    dbg_agg_partition, dbg_agg_destroy) returns — HIP stream semantics.
+ */
+#ifndef DBGPU_AGG_H
+#define DBGPU_AGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DBG_ABI_VERSION 1
+
+/* ---- status codes (reference ErrorCode variants on this path) ---- */
+enum {
+    DBG_OK = 0,
+    DBG_ERR_OVERFLOW = 1,    /* ErrorCode::Overflow — FUN/aggregate_sum.rs:147-153, aggregate_avg.rs:195-199 */
+    DBG_ERR_OOM = 2,         /* device allocation failed */
+    DBG_ERR_UNSUPPORTED = 3, /* type/function not on the GPU path: caller keeps the CPU path */
+    DBG_ERR_INTERNAL = 4,    /* ErrorCode::Internal */
+    DBG_ERR_INVALID = 5,     /* malformed argument */
+    DBG_ERR_DEVICE = 6       /* HIP runtime failure */
+};
+
+/* ---- data types (EXP/types/: Number, Decimal128, Date, Timestamp, String, Boolean) ---- */
+typedef enum {
+    DBG_INT8 = 0,
+    DBG_INT16 = 1,
+    DBG_INT32 = 2,
+    DBG_INT64 = 3,
+    DBG_UINT8 = 4,
+    DBG_UINT16 = 5,
+    DBG_UINT32 = 6,
+    DBG_UINT64 = 7,
+    DBG_FLOAT32 = 8,
+    DBG_FLOAT64 = 9,
+    DBG_DECIMAL128 = 10, /* i128 LE, (precision, scale) — EXP/types/decimal.rs:653-655 */
+    DBG_DATE = 11,       /* i32 days since epoch */
+    DBG_TIMESTAMP = 12,  /* i64 microseconds since epoch */
+    DBG_STRING = 13,     /* bytes + offsets */
+    DBG_BOOLEAN = 14     /* bitmap */
+} dbg_type;
+
+typedef struct dbg_datatype {
+    int32_t type;      /* dbg_type */
+    uint8_t precision; /* Decimal128 only */
+    uint8_t scale;     /* Decimal128 only */
+    uint8_t nullable;  /* DataType::Nullable(..) wrapper */
+    uint8_t reserved;
+} dbg_datatype;
+
+/* One Column (EXP/values.rs:157) — NullableColumn = inner column + validity Bitmap. */
+typedef struct dbg_column {
+    dbg_datatype dt;
+    const void* data;         /* values; STRING: payload bytes; BOOLEAN: LSB-first bitmap */
+    const uint64_t* offsets;  /* STRING: len+1 offsets into data; otherwise NULL */
+    const uint8_t* validity;  /* read only when dt.nullable; NULL = all valid */
+    uint64_t validity_offset; /* bit offset of row 0 in validity */
+    uint64_t data_offset;     /* BOOLEAN: bit offset of row 0 in data; otherwise 0 */
+    uint64_t len;             /* rows */
+} dbg_column;
+
+/* Writable output column: caller-allocated buffers sized from dbg_agg_finalize.
+ * data: n_groups * width (STRING: string_bytes); offsets: n_groups+1 (STRING);
+ * validity: ceil(n_groups/8) bytes, written LSB-first from bit 0 (only for nullable results). */
+typedef struct dbg_out_column {
+    dbg_datatype dt; /* filled by the library (result type) */
+    void* data;
+    uint64_t* offsets;
+    uint8_t* validity;
+} dbg_out_column;
+
+/* ---- aggregate functions (FUN/aggregate_{count,sum,avg,min_max_any}.rs) ---- */
+typedef enum {
+    DBG_AGG_COUNT = 0, /* AggregateCountFunction: count(*) when arg_type < 0, count(x) otherwise */
+    DBG_AGG_SUM = 1,   /* NumberSumState / DecimalSumState<OVERFLOW> */
+    DBG_AGG_MIN = 2,   /* MinMaxAnyState<T, CmpMin> */
+    DBG_AGG_MAX = 3,   /* MinMaxAnyState<T, CmpMax> */
+    DBG_AGG_AVG = 4    /* NumberAvgState / DecimalAvgState<OVERFLOW> */
+} dbg_agg_kind;
+
+typedef struct dbg_agg_spec {
+    int32_t kind;     /* dbg_agg_kind */
+    dbg_datatype arg; /* arg.type < 0 => no argument (count(*)) */
+    uint8_t or_null;  /* wrapped by AggregateFunctionOrNullAdaptor (factory.get(): 1) */
+    uint8_t reserved[3];
+} dbg_agg_spec;
+
+/* ---- predicates (EXP/filter/select_expr.rs SelectExpr tree, flattened to postfix) ---- */
+typedef enum { DBG_CMP_EQ = 0, DBG_CMP_NE, DBG_CMP_LT, DBG_CMP_LE, DBG_CMP_GT, DBG_CMP_GE } dbg_cmp;
+
+typedef enum {
+    DBG_PRED_CMP_CONST = 0, /* column <cmp> constant (constant in the column's own domain) */
+    DBG_PRED_CMP_COLS = 1,  /* column <cmp> column2 (same type) */
+    DBG_PRED_AND = 2,       /* pops 2, pushes 1 (SQL three-valued logic) */
+    DBG_PRED_OR = 3,
+    DBG_PRED_NOT = 4,       /* pops 1 */
+    DBG_PRED_IS_NULL = 5,
+    DBG_PRED_IS_NOT_NULL = 6,
+    DBG_PRED_TRUE = 7
+} dbg_pred_op;
+
+typedef struct dbg_pred_node {
+    int32_t op;   /* dbg_pred_op */
+    int32_t cmp;  /* dbg_cmp */
+    int32_t col;  /* index into dbg_filter.cols */
+    int32_t col2; /* DBG_PRED_CMP_COLS */
+    /* constant, interpreted by the column type: signed ints/date/timestamp/bool -> i64;
+     * unsigned ints -> u64 bits in i64; floats -> f64; Decimal128 -> (i128_hi:i128_lo) at the
+     * column's scale; String -> str/str_len bytes */
+    int64_t i64;
+    double f64;
+    uint64_t i128_lo;
+    int64_t i128_hi;
+    const uint8_t* str;
+    uint64_t str_len;
+} dbg_pred_node;
+
+/* A filter = predicate program over its own columns (TransformFilter over a DataBlock). */
+typedef struct dbg_filter {
+    const dbg_pred_node* nodes; /* postfix */
+    int32_t n_nodes;
+    int32_t n_cols;
+    const dbg_column* cols;
+} dbg_filter;
+
+/* ---- aggregate hash table handle (EAGG/aggregate_hashtable.rs:47 AggregateHashTable) ---- */
+typedef struct dbg_agg_handle dbg_agg_handle;
+
+typedef struct dbg_agg_params {
+    const dbg_datatype* group_types; /* AggregatorParams.group_data_types (AGG/aggregator_params.rs:31-94) */
+    int32_t n_group_cols;
+    const dbg_agg_spec* aggs; /* AggregatorParams.aggregate_functions */
+    int32_t n_aggs;
+    int32_t device;         /* HIP device ordinal; -1 = current device */
+    int32_t partial;        /* 1 = TransformPartialAggregate, 0 = TransformFinalAggregate */
+    uint64_t capacity_hint; /* expected groups; 0 = AggregateHashTable::initial_capacity() (32768) */
+} dbg_agg_params;
+
+const char* dbg_version(void);
+/* Message of the last error on this thread (thread-local). */
+const char* dbg_last_error(void);
+int dbg_device_count(int* n);
+
+/* Result type of an aggregate: AggregateFunction::return_type() after the factory's adaptors
+ * (FUN/aggregate_function_factory.rs:157-220). */
+int dbg_agg_result_type(const dbg_agg_spec* spec, dbg_datatype* out);
+
+/* AggregateHashTable::new + HashTableConfig (builder_aggregate.rs:132-164). */
+int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out);
+void dbg_agg_destroy(dbg_agg_handle* h);
+/* Launch on the caller's hipStream_t (NULL restores the handle's own stream). */
+int dbg_agg_set_stream(dbg_agg_handle* h, void* hip_stream);
+/* Drop all groups and retained inputs, keep device memory (a fresh table for the next query). */
+int dbg_agg_reset(dbg_agg_handle* h);
+
+/* TransformPartialAggregate::transform -> AggregateHashTable::add_groups
+ * (AGG/transform_aggregate_partial.rs:291-323, EAGG/aggregate_hashtable.rs:128-242), fused with the
+ * TransformFilter that precedes it when filter != NULL (transform_filter.rs:73-92).
+ * arg_cols holds n_aggs entries, one per aggregate (ignored for count(*)).  Asynchronous on the
+ * handle's stream. */
+int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols,
+                       const dbg_filter* filter, uint64_t rows, int on_device);
+
+/* Synchronise, resolve deferred work and report the result size (merge_result preparation,
+ * EAGG/aggregate_hashtable.rs:427-451).  string_bytes[i] = payload bytes of group column i
+ * (0 for non-string columns); may be NULL. */
+int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes);
+
+/* TransformFinalAggregate output DataBlock [agg results..., group cols...]
+ * (AGG/transform_aggregate_final.rs:128-133): fills caller buffers (host when on_device == 0). */
+int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device);
+
+/* ---- partial-state records: exchange / partition bucket (EAGG/payload.rs:356-391,
+ *      EAGG/partitioned_payload.rs:100-143, AGG/aggregate_exchange_injector.rs:154-235) ----
+ * A record = [hash u64][group keys, fixed part][state words]; string keys are (u64 offset, u64 len)
+ * into a per-partition string blob.  scheme 0: partition = hash % n_parts (cluster routing,
+ * StrengthReducedU64); scheme 1: partition = (hash & mask) >> (48 - r) with n_parts = 2^r
+ * (radix buckets). */
+int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width);
+int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t* rec_counts,
+                      uint64_t* string_bytes);
+/* Write every partition's records into dev_records (partition p at byte offset
+ * rec_offsets[p] * width) and strings into dev_strings (partition p at str_offsets[p]).
+ * Device buffers; asynchronous.  Call after dbg_agg_partition with the same n_parts/scheme. */
+int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strings,
+                           const uint64_t* rec_offsets, const uint64_t* str_offsets);
+/* merge_states of received records into this table (combine_payload,
+ * EAGG/aggregate_hashtable.rs:383-425).  The buffers hold n_segments concatenated segments
+ * (one per source); seg_records[i] / seg_string_bytes[i] give each segment's size so string
+ * offsets are rebased.  Device buffers, retained until the next synchronising call. */
+int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void* dev_strings,
+                          int32_t n_segments, const uint64_t* seg_records,
+                          const uint64_t* seg_string_bytes);
+
+/* ---- standalone filter (FilterExecutor::select + take, EXP/filter/filter_executor.rs:73-128) ----
+ * sel_out (device) receives the ascending u32 row indices where the predicate is TRUE;
+ * *n_sel its count (synchronous). */
+int dbg_filter_select(const dbg_filter* filter, uint64_t rows, uint32_t* sel_out, uint64_t* n_sel,
+                      void* hip_stream);
+/* DataBlock::take (EXP/kernels/take.rs:56-91) of one fixed-width column on device:
+ * out[i] = in[sel[i]] (value bytes; validity gathered into out_validity bit-packed when non-NULL). */
+int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, void* out_data,
+                   uint8_t* out_validity, void* hip_stream);
+
+/* ---- in-library kernel timing (HIP events around each launch; off by default) ---- */
+int dbg_prof_enable(int on);
+int dbg_prof_reset(void);
+/* i-th kernel seen so far: name, summed milliseconds, launches.  Returns DBG_ERR_INVALID past end. */
+int dbg_prof_get(int i, const char** name, double* total_ms, uint64_t* launches);
+
+/* ---- synthetic workload generator (the numbers_mt analog) ----
+ * Fills caller-allocated device columns for rows [row_start, row_start+rows) of config cfg
+ * (1..5), deterministically from seed (counter-based splitmix64).  Column sets per config are
+ * listed in DESIGN.md; C5 needs the phrase CDF table from dbg_datagen_c5_table. */
+int dbg_datagen(int cfg, uint64_t seed, uint64_t row_start, uint64_t rows, dbg_out_column* cols,
+                int n_cols, const uint64_t* aux, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DBGPU_AGG_H */

@@ -1,0 +1,126 @@
+"""Regenerate tests/golden/*.json from the reference's own test data (run in the build container,
+where /root/reference exists; the GPU box only reads the committed JSON).
+
+Sources (data, transcribed — no reference source is copied):
+  * src/query/functions/tests/it/aggregates/testdata/agg_group_by.txt  (two-group simulator golden)
+  * src/query/functions/tests/it/aggregates/testdata/agg.txt           (no-grouping golden)
+    inputs = get_example() column values, src/query/functions/tests/it/aggregates/agg.rs:137-192
+  * tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test  (numbers()-based
+    GROUP BY queries with expected rows; transcribed by hand below, line numbers cited)
+"""
+import json
+import os
+import re
+import sys
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+TESTDATA = "src/query/functions/tests/it/aggregates/testdata"
+
+# get_example() inputs (agg.rs:137-192), the columns usable by count/sum/avg/min/max
+EXAMPLE = {
+    "a": {"type": "Int64", "values": [4, 3, 2, 1], "validity": None},
+    "b": {"type": "UInt64", "values": [1, 2, 3, 4], "validity": None},
+    "c": {"type": "UInt64", "values": [1, 2, 1, 3], "validity": None},
+    "x_null": {"type": "UInt64", "values": [1, 2, 3, 4], "validity": [True, True, False, False]},
+    "y_null": {"type": "UInt64", "values": [1, 2, 3, 4], "validity": [False, False, True, True]},
+    "all_null": {"type": "UInt64", "values": [1, 2, 3, 4], "validity": [False, False, False, False]},
+    "dec": {"type": "Decimal(15,2)", "values": [110, 220, 0, 330], "validity": [True, True, False, True]},
+}
+
+AST = re.compile(r"^ast: (count|sum|avg|min|max)\((\w*)\)$")
+OUT_PLAIN = re.compile(r"\| Output\s*\| (\w+)\(\[([^\]]*)\]\)")
+OUT_NULL = re.compile(r"\| Output\s*\| NullableColumn \{ column: (\w+)\(\[([^\]]*)\]\), validity: \[0b_*([01]+)\] \}")
+
+
+def parse_values(typ, s):
+    vals = [v.strip() for v in s.split(",") if v.strip()]
+    if typ == "Decimal128":
+        return vals  # decimal strings, e.g. "1.1000"
+    if typ.startswith("Float"):
+        return [float(v) for v in vals]
+    return [int(v) for v in vals]
+
+
+def parse_file(name, grouped):
+    path = os.path.join(REF, TESTDATA, name)
+    lines = open(path).read().splitlines()
+    out = []
+    i = 0
+    while i < len(lines):
+        m = AST.match(lines[i])
+        if m:
+            fn, arg = m.group(1), m.group(2)
+            if arg == "" or arg in EXAMPLE:
+                for j in range(i + 1, min(i + 12, len(lines))):
+                    mn = OUT_NULL.search(lines[j])
+                    mp = OUT_PLAIN.search(lines[j])
+                    if mn:
+                        typ, vals, bits = mn.group(1), mn.group(2), mn.group(3)
+                        v = parse_values(typ, vals)
+                        validity = [bits[::-1][k] == "1" for k in range(len(v))]
+                        out.append(dict(source=f"{TESTDATA}/{name}:{i + 1}", fn=fn, arg=arg or None,
+                                        grouped=grouped, out_type=typ, nullable=True, values=v, validity=validity))
+                        break
+                    if mp:
+                        typ, vals = mp.group(1), mp.group(2)
+                        v = parse_values(typ, vals)
+                        out.append(dict(source=f"{TESTDATA}/{name}:{i + 1}", fn=fn, arg=arg or None,
+                                        grouped=grouped, out_type=typ, nullable=False, values=v,
+                                        validity=[True] * len(v)))
+                        break
+        i += 1
+    return out
+
+
+# 03_0043_new_agg_hashtable.test expected rows (hand transcription; file:line of each query).
+SLT = [
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:21-27",
+         sql="SELECT number%3 as c1, sum(c1) FROM numbers_mt(10) where number > 2 group by number%3 order by c1",
+         rows=[[0, 0], [1, 2], [2, 4]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:29-35",
+         sql="SELECT a,b,sum(a),sum(b),count() from (SELECT cast((number%6) AS bigint) as a, cast((number%15) AS bigint) as b "
+             "from numbers(1000)) group by a,b order by a,b limit 3",
+         rows=[[0, 0, 0, 0, 34], [0, 3, 0, 99, 33], [0, 6, 0, 204, 34]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:46-51",
+         sql="SELECT a%3 as a1, count(1) as ct from t GROUP BY a1 ORDER BY a1 NULLS FIRST,ct "
+             "(t.a = if(number % 3 = 2, null, number), numbers(10))",
+         rows=[[None, 3], [0, 4], [1, 3]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:53-61",
+         sql="SELECT a%2 as a1, a%3 as a2, count(0) as ct FROM t GROUP BY a1, a2",
+         rows=[[None, None, 3], [0, 0, 2], [0, 1, 1], [1, 0, 2], [1, 1, 2]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:95-100",
+         sql="select created_at, sum(count) from t_datetime group by created_at "
+             "(created_at = to_date('2024-04-01') + number % 3, count = 1, numbers(10))",
+         rows=[[19814, 4], [19815, 3], [19816, 3]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:122-130",
+         sql="SELECT number % 3 as a, number%4 as b, sum(a),avg(b) FROM numbers_mt(10000000) group by a,b order by a,b limit 5",
+         rows=[[0, 0, 0, 0.0], [0, 1, 0, 1.0], [0, 2, 0, 2.0], [0, 3, 0, 3.0], [1, 0, 833333, 0.0]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:178-186",
+         sql="select (number % 3)::Decimal(19, 2) a ,(number % 4)::Decimal(36, 4) b , count() from numbers(100) "
+             "group by a,b order by a,b limit 5",
+         rows=[["0.00", "0.0000", 9], ["0.00", "1.0000", 8], ["0.00", "2.0000", 8], ["0.00", "3.0000", 9],
+               ["1.00", "0.0000", 8]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:188-193",
+         sql="select (number % 3)::Decimal(19, 2) c, to_string(number % 3) d, count() from numbers(100) group by c,d",
+         rows=[["0.00", "0", 34], ["1.00", "1", 33], ["2.00", "2", 33]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:207-216",
+         sql="select number % 3 a, max(number) - 10, number % 2 b, sum(number) + 10 from numbers(1000000) group by all",
+         rows=[[0, 999986, 0, 83333166676], [0, 999989, 1, 83333666677], [1, 999984, 0, 83332833344],
+               [1, 999987, 1, 83333333343], [2, 999988, 0, 83333500010], [2, 999985, 1, 83333000010]]),
+]
+
+
+def main():
+    if not os.path.isdir(REF):
+        sys.exit("reference tree not present; the committed JSON is authoritative")
+    goldens = parse_file("agg_group_by.txt", True) + parse_file("agg.txt", False)
+    with open(os.path.join(HERE, "agg_function_goldens.json"), "w") as f:
+        json.dump(dict(inputs=EXAMPLE, cases=goldens), f, indent=1)
+    with open(os.path.join(HERE, "slt_group_by.json"), "w") as f:
+        json.dump(SLT, f, indent=1)
+    print(f"{len(goldens)} function goldens, {len(SLT)} sqllogictest cases")
+
+
+if __name__ == "__main__":
+    main()

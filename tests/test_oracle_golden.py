@@ -1,0 +1,246 @@
+"""Pin the oracle (oracle/dbagg_oracle.cpp) against the reference's own known answers.
+
+* agg_function_goldens.json — testdata/agg_group_by.txt and testdata/agg.txt goldens
+  (src/query/functions/tests/it/aggregates/), two-group simulator (agg.rs:77-114, mod.rs:182-219)
+* agg_hashtable.rs:57-182 closed form (8 key types, combine of two tables)
+* slt_group_by.json — numbers()-based expectations of 03_0043_new_agg_hashtable.test
+* an independent pure-Python restatement of group_hash.rs for the hash family (hash values are
+  pinned by no reference test: SURVEY.md §4)
+"""
+import json
+import os
+import struct
+from decimal import Decimal
+
+import numpy as np
+import pytest
+
+from databend_amd import abi
+from databend_amd import column as col
+from databend_amd.column import Column
+from databend_amd.filter import FilterProgram, cmp
+from oracle import oracle
+from tests.parity import assert_results_equal, rows_of
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "agg_function_goldens.json")))
+SLT = json.load(open(os.path.join(HERE, "golden", "slt_group_by.json")))
+
+KIND = {"count": abi.AGG_COUNT, "sum": abi.AGG_SUM, "avg": abi.AGG_AVG, "min": abi.AGG_MIN, "max": abi.AGG_MAX}
+
+
+def spec(kind, arg_dt=None, or_null=True):
+    s = abi.dbg_agg_spec()
+    s.kind = kind
+    s.arg = arg_dt.to_abi() if arg_dt is not None else abi.dbg_datatype(-1, 0, 0, 0, 0)
+    s.or_null = 1 if (or_null and kind != abi.AGG_COUNT) else 0
+    return s
+
+
+def example_column(name):
+    d = GOLD["inputs"][name]
+    if d["type"].startswith("Decimal"):
+        return Column.from_decimals(15, 2, d["values"], d["validity"])
+    dt = {"Int64": col.Int64, "UInt64": col.UInt64}[d["type"]]
+    return Column.from_numbers(dt, d["values"], d["validity"])
+
+
+@pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: f"{c['fn']}({c['arg'] or ''})-{'gb' if c['grouped'] else 'one'}")
+def test_function_goldens(case):
+    arg = example_column(case["arg"]) if case["arg"] else None
+    key = Column.from_numbers(col.Int64, [0, 1, 0, 1] if case["grouped"] else [0, 0, 0, 0])
+    s = spec(KIND[case["fn"]], arg.dtype if arg is not None else None)
+    keys, aggs = oracle.aggregate([key], [(s, arg)])
+    order = np.argsort(np.asarray(keys[0].values()))
+    res = aggs[0]
+    vals = res.values()
+    got = [vals[i] for i in order]
+    exp = []
+    for v, ok in zip(case["values"], case["validity"]):
+        if not ok:
+            exp.append(None)
+        elif case["out_type"] == "Decimal128":
+            exp.append(int(Decimal(v).scaleb(res.dtype.scale)))
+        else:
+            exp.append(v)
+    assert got == exp, f"{case['source']}: got {got} expected {exp}"
+    assert res.dtype.nullable == case["nullable"], case["source"]
+
+
+@pytest.mark.parametrize("n", [100, 1000, 10_000, 100_000])
+def test_agg_hashtable_closed_form(n):
+    """agg_hashtable.rs:57-182 — 8 key columns of x % 4, min/max/sum/count(Int64); two tables
+    over the same rows combined => per group count n/2 and sum [0, n/2, n, 3n/2]."""
+    m = 4
+    x = np.arange(n) % m
+    x2 = np.concatenate([x, x])  # the test adds the same rows to two tables and combines them
+    keys = [
+        Column.from_strings([str(v) for v in x2]),
+        Column.from_numbers(col.Int64, x2), Column.from_numbers(col.Int32, x2),
+        Column.from_numbers(col.Int16, x2), Column.from_numbers(col.Int8, x2),
+        Column.from_numbers(col.Float32, x2.astype(np.float32)), Column.from_numbers(col.Float64, x2.astype(np.float64)),
+        Column.from_bools(x2 != 0),
+    ]
+    arg = keys[1]
+    aggs = [(spec(abi.AGG_MIN, col.Int64), arg), (spec(abi.AGG_MAX, col.Int64), arg),
+            (spec(abi.AGG_SUM, col.Int64), arg), (spec(abi.AGG_COUNT, col.Int64), arg)]
+    for threads in (1, 3):
+        k, a = oracle.aggregate(keys, aggs, threads=threads)
+        assert len(k[0]) == m
+        rows = sorted(rows_of(k, a), key=lambda r: r[1])
+        for g, r in enumerate(rows):
+            assert r[0] == str(g).encode() and r[1] == g and r[2] == g and r[3] == g
+            assert r[5] == float(g) and r[7] == (g != 0)
+            assert r[8] == g and r[9] == g and r[10] == g * n // 2 and r[11] == n // 2
+
+
+def _numbers(n):
+    return np.arange(n, dtype=np.uint64)
+
+
+def _slt_inputs(i):
+    """Rebuild the inputs of SLT case i (numbers()-based) and the aggregate list."""
+    if i == 0:  # number%3 c1, sum(c1) where number > 2
+        num = _numbers(10)
+        c1 = Column.from_numbers(col.UInt8, num % 3)
+        flt = Column.from_numbers(col.UInt64, num)
+        return [c1], [(spec(abi.AGG_SUM, col.UInt8), c1)], (cmp(0, ">", 2), [flt])
+    if i == 1:
+        num = _numbers(1000)
+        a = Column.from_numbers(col.Int64, num % 6)
+        b = Column.from_numbers(col.Int64, num % 15)
+        return [a, b], [(spec(abi.AGG_SUM, col.Int64), a), (spec(abi.AGG_SUM, col.Int64), b),
+                        (spec(abi.AGG_COUNT), None)], None
+    if i in (2, 3):
+        num = _numbers(10)
+        valid = (num % 3) != 2
+        a1 = Column.from_numbers(col.UInt8, num % (3 if i == 2 else 2), validity=valid)
+        if i == 2:
+            return [a1], [(spec(abi.AGG_COUNT), None)], None
+        a2 = Column.from_numbers(col.UInt8, num % 3, validity=valid)
+        return [a1, a2], [(spec(abi.AGG_COUNT), None)], None
+    if i == 4:
+        num = _numbers(10)
+        d = Column.from_numbers(col.Date, 19814 + (num % 3).astype(np.int32))
+        one = Column.from_numbers(col.Int32, np.ones(10, np.int32))
+        return [d], [(spec(abi.AGG_SUM, col.Int32), one)], None
+    if i == 5:
+        num = _numbers(10_000_000)
+        a = Column.from_numbers(col.UInt8, num % 3)
+        b = Column.from_numbers(col.UInt8, num % 4)
+        return [a, b], [(spec(abi.AGG_SUM, col.UInt8), a), (spec(abi.AGG_AVG, col.UInt8), b)], None
+    if i == 6:
+        num = _numbers(100)
+        a = Column.from_decimals(19, 2, [int(v % 3) * 100 for v in num])
+        b = Column.from_decimals(36, 4, [int(v % 4) * 10000 for v in num])
+        return [a, b], [(spec(abi.AGG_COUNT), None)], None
+    if i == 7:
+        num = _numbers(100)
+        c = Column.from_decimals(19, 2, [int(v % 3) * 100 for v in num])
+        d = Column.from_strings([str(int(v % 3)) for v in num])
+        return [c, d], [(spec(abi.AGG_COUNT), None)], None
+    if i == 8:
+        num = _numbers(1_000_000)
+        a = Column.from_numbers(col.UInt8, num % 3)
+        b = Column.from_numbers(col.UInt8, num % 2)
+        n = Column.from_numbers(col.UInt64, num)
+        return [a, b], [(spec(abi.AGG_MAX, col.UInt64), n), (spec(abi.AGG_SUM, col.UInt64), n)], None
+    raise IndexError(i)
+
+
+def _slt_expected(i, case):
+    rows = case["rows"]
+    if i == 6:
+        return [[int(Decimal(r[0]) * 100), int(Decimal(r[1]) * 10000), r[2]] for r in rows]
+    if i == 7:
+        return [[int(Decimal(r[0]) * 100), r[1].encode(), r[2]] for r in rows]
+    if i == 8:  # max(number) - 10, sum(number) + 10 are post-aggregate scalars
+        return [[r[0], r[2], r[1] + 10, r[3] - 10] for r in rows]
+    return rows
+
+
+@pytest.mark.parametrize("i", range(len(SLT)))
+def test_slt_group_by(i):
+    case = SLT[i]
+    keys, aggs, flt = _slt_inputs(i)
+    prog = FilterProgram(flt[0], [c.to_abi() for c in flt[1]]) if flt else None
+    k, a = oracle.aggregate(keys, aggs, filter_program=prog, threads=4)
+    got = sorted([list(r) for r in rows_of(k, a)], key=lambda r: [(-1 if v is None else v) for v in r[:len(keys)]])
+    exp = _slt_expected(i, case)
+    got = got[:len(exp)] if "limit" in case["sql"] else got
+    assert got == exp, f"{case['source']}\n got {got}\n exp {exp}"
+
+
+# ---- independent pure-Python restatement of EAGG/group_hash.rs (checks the C++ one) ----
+M64 = (1 << 64) - 1
+
+
+def py_hash_prim(x):
+    x &= M64
+    x ^= x >> 32
+    x = (x * 0xd6e8feb86659fd93) & M64
+    x ^= x >> 32
+    x = (x * 0xd6e8feb86659fd93) & M64
+    x ^= x >> 32
+    return x
+
+
+def py_hash_bytes(b: bytes):
+    M, SEED, R = 0xc6a4a7935bd1e995, 0xe17a1465, 47
+    h = (SEED ^ (len(b) * M)) & M64
+    nb = len(b) // 8
+    for i in range(nb):
+        k = int.from_bytes(b[i * 8:i * 8 + 8], "little")
+        k = (k * M) & M64
+        k ^= k >> R
+        k = (k * M) & M64
+        h ^= k
+        h = (h * M) & M64
+    tail = b[nb * 8:]
+    for i, v in enumerate(tail):
+        h ^= v << (8 * (len(tail) - i - 1))
+    h ^= h >> R
+    h = (h * M) & M64
+    h ^= h >> R
+    return h
+
+
+def test_hash_family_matches_python_restatement():
+    rng = np.random.default_rng(7)
+    n = 300
+    i16 = rng.integers(-30000, 30000, n).astype(np.int16)
+    i64 = rng.integers(-2**62, 2**62, n).astype(np.int64)
+    u32 = rng.integers(0, 2**32, n).astype(np.uint32)
+    f64 = rng.standard_normal(n)
+    f64[::17] = np.nan
+    strs = [bytes(rng.integers(97, 123, rng.integers(0, 40)).astype(np.uint8)) for _ in range(n)]
+    dec = [int(v) for v in rng.integers(-10**15, 10**15, n)]
+    valid = rng.random(n) > 0.2
+    cols = [Column.from_numbers(col.Int16, i16), Column.from_numbers(col.Int64, i64, validity=valid),
+            Column.from_numbers(col.UInt32, u32), Column.from_numbers(col.Float64, f64),
+            Column.from_strings(strs), Column.from_decimals(20, 3, dec), Column.from_bools(i16 > 0)]
+    got = oracle.group_hash(cols)
+    N = 0xd1cefa08eb382d69
+    for r in range(n):
+        h = py_hash_prim(int(i16[r]))  # first column; sign-extended
+        cells = [
+            py_hash_prim(int(i64[r])) if valid[r] else None,
+            py_hash_prim(int(u32[r])),
+            py_hash_prim(0x7ff8000000000000 if np.isnan(f64[r]) else struct.unpack("<Q", struct.pack("<d", f64[r]))[0]),
+            py_hash_bytes(strs[r]),
+            py_hash_bytes(int(dec[r]).to_bytes(16, "little", signed=True)),
+            1 if i16[r] > 0 else 0,
+        ]
+        for c in cells:
+            h = ((h * N) & M64) ^ (N if c is None else c)
+        assert int(got[r]) == h, r
+
+
+def test_filter_three_valued_logic():
+    from databend_amd.filter import and_, is_null, not_, or_
+    v = Column.from_numbers(col.Int32, [1, 2, 3, 4, 5, 6], validity=[1, 1, 0, 1, 0, 1])
+    s = Column.from_strings(["", "a", "", "zz", "b", ""])
+    p = FilterProgram(or_(and_(cmp(0, ">=", 2), cmp(1, "<>", "")), is_null(0)), [v.to_abi(), s.to_abi()])
+    assert list(oracle.filter_select(p, 6)) == [1, 2, 3, 4]
+    p2 = FilterProgram(not_(cmp(0, ">", 3)), [v.to_abi()])
+    assert list(oracle.filter_select(p2, 6)) == [0, 1]  # NOT(NULL) is NULL -> dropped
