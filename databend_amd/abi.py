@@ -67,5 +67,5 @@ class dbg_agg_params(C.Structure):
 
 EXPECTED_SIZES = {
     "dbg_datatype": 8, "dbg_column": 56, "dbg_out_column": 32, "dbg_agg_spec": 16,
-    "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 40,
+    "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 48,
 }

@@ -1,0 +1,296 @@
+"""Host mirror of Databend's aggregator processors over the C ABI.
+
+Names, argument meaning and error behaviour follow the reference
+(src/query/service/src/pipelines/processors/transforms/aggregator/ = AGG/):
+
+* `AggregatorParams`            AGG/aggregator_params.rs:31-116
+* `HashTableConfig`             EAGG/mod.rs:59-132 (knobs that matter on the GPU: capacity hint)
+* `AggregateHashTable`          EAGG/aggregate_hashtable.rs:47-589, one table in HBM
+* `TransformPartialAggregate`   AGG/transform_aggregate_partial.rs:107-468 (transform / on_finish)
+* `TransformFinalAggregate`     AGG/transform_aggregate_final.rs:45-343 (transform -> DataBlock)
+* `AggregateMeta`               AGG/aggregate_meta.rs:124-134 (partial payloads between stages)
+
+Every call lands in libdbgpu_agg.so; the product path has no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import abi
+from .aggregates import AggregateFunction
+from .column import Column, DataBlock, DataType, abi_array, unpack_bits
+from .ffi import check, lib
+
+ColumnLike = Union[Column, "DeviceColumn"]  # noqa: F821
+
+
+@dataclass
+class AggregatorParams:
+    """AggregatorParams::try_create (AGG/aggregator_params.rs:48-94)."""
+    group_data_types: List[DataType]
+    aggregate_functions: List[AggregateFunction]
+    max_block_size: int = 65536
+
+    def to_abi(self, partial: bool, capacity_hint: int, device: int):
+        gt = (abi.dbg_datatype * max(1, len(self.group_data_types)))(*[t.to_abi() for t in self.group_data_types])
+        ag = (abi.dbg_agg_spec * max(1, len(self.aggregate_functions)))(*[f.to_abi() for f in self.aggregate_functions])
+        p = abi.dbg_agg_params(gt, len(self.group_data_types), ag, len(self.aggregate_functions), device,
+                               1 if partial else 0, capacity_hint)
+        return p, (gt, ag)
+
+    def empty_result_block(self) -> DataBlock:
+        """AggregatorParams::empty_result_block (:103-115): [agg results..., group cols...]."""
+        cols = []
+        for f in self.aggregate_functions:
+            rt = f.return_type()
+            cols.append(_empty_column(rt))
+        for t in self.group_data_types:
+            cols.append(_empty_column(t))
+        return DataBlock(cols)
+
+
+def _empty_column(t: DataType) -> Column:
+    if t.type_id == abi.STRING:
+        return Column(t, np.zeros(0, np.uint8), np.zeros(1, np.uint64), np.zeros(0, bool) if t.nullable else None)
+    if t.type_id == abi.DECIMAL128:
+        return Column(t, np.zeros(0, np.uint8), None, np.zeros(0, bool) if t.nullable else None)
+    if t.type_id == abi.BOOLEAN:
+        return Column(t, np.zeros(0, bool), None, np.zeros(0, bool) if t.nullable else None)
+    return Column(t, np.zeros(0, t.np_dtype), None, np.zeros(0, bool) if t.nullable else None)
+
+
+@dataclass
+class HashTableConfig:
+    """HashTableConfig (EAGG/mod.rs:59-83).  The radix/partial-capacity knobs of the CPU table have
+    no GPU meaning (the HBM table aggregates exactly); `capacity_hint` seeds the table size."""
+    partial_agg: bool = False
+    capacity_hint: int = 0
+
+    def with_partial(self, partial_agg: bool, active_threads: int = 1) -> "HashTableConfig":
+        return HashTableConfig(partial_agg, self.capacity_hint)
+
+
+def _current_torch_stream():
+    """Launch on torch's current stream so torch-produced device columns are stream-ordered."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.cuda.current_stream()
+    except Exception:
+        pass
+    return None
+
+
+def _arg_structs(aggs: Sequence[AggregateFunction], params: Sequence[Optional[ColumnLike]]):
+    out = []
+    for f, p in zip(aggs, params):
+        if p is None:
+            c = abi.dbg_column()
+            c.dt = abi.dbg_datatype(-1, 0, 0, 0, 0)
+            out.append(c)
+        else:
+            out.append(p.to_abi())
+    return abi_array(out)
+
+
+class AggregateHashTable:
+    """One GPU aggregate table (a `dbg_agg_handle`)."""
+
+    def __init__(self, params: AggregatorParams, config: HashTableConfig = None, device: int = -1, stream=None):
+        config = config or HashTableConfig()
+        self.params = params
+        p, self._keep = params.to_abi(config.partial_agg, config.capacity_hint, device)
+        h = C.c_void_p()
+        check(lib().dbg_agg_create(C.byref(p), C.byref(h)))
+        self.h = h
+        self._retained = []  # device inputs must outlive the table (include/dbgpu_agg.h)
+        if stream is None:
+            stream = _current_torch_stream()
+        if stream is not None:
+            self.set_stream(stream)
+
+    # ---- lifecycle
+    def close(self):
+        if self.h:
+            lib().dbg_agg_destroy(self.h)
+            self.h = None
+            self._retained.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream (its hipStream_t) or None for the handle's own."""
+        ptr = None if stream is None else stream.cuda_stream
+        check(lib().dbg_agg_set_stream(self.h, ptr))
+
+    def reset(self):
+        check(lib().dbg_agg_reset(self.h))
+        self._retained.clear()
+
+    # ---- AggregateHashTable::add_groups (+ fused filter)
+    def add_groups(self, group_columns: Sequence[ColumnLike], params: Sequence[Optional[ColumnLike]],
+                   rows: Optional[int] = None, filter_program=None, on_device: Optional[bool] = None) -> None:
+        if rows is None:
+            rows = len(group_columns[0])
+        if on_device is None:
+            on_device = not isinstance(group_columns[0], Column)
+        keys = abi_array([c.to_abi() for c in group_columns])
+        args = _arg_structs(self.params.aggregate_functions, params)
+        fp = filter_program.ptr() if filter_program is not None else None
+        check(lib().dbg_agg_add_groups(self.h, keys, args, fp, rows, 1 if on_device else 0))
+        if on_device:
+            self._retained.append((group_columns, params, filter_program))
+
+    # ---- merge_result
+    def finalize(self):
+        n = C.c_uint64()
+        sb = (C.c_uint64 * max(1, len(self.params.group_data_types)))()
+        check(lib().dbg_agg_finalize(self.h, C.byref(n), sb))
+        return n.value, list(sb)
+
+    def merge_result(self) -> DataBlock:
+        """All groups as one host DataBlock [agg results..., group cols...]
+        (TransformFinalAggregate output order, AGG/transform_aggregate_final.rs:128-133)."""
+        n, sbytes = self.finalize()
+        aggs, keys = self._out_buffers(n, sbytes)
+        out_a = (abi.dbg_out_column * max(1, len(aggs)))()
+        out_k = (abi.dbg_out_column * max(1, len(keys)))()
+        for i, b in enumerate(aggs):
+            out_a[i].data, out_a[i].offsets, out_a[i].validity = b["ptrs"]
+        for i, b in enumerate(keys):
+            out_k[i].data, out_k[i].offsets, out_k[i].validity = b["ptrs"]
+        check(lib().dbg_agg_result(self.h, out_a, out_k, 0))
+        cols = [self._to_column(b, n) for b in aggs] + [self._to_column(b, n) for b in keys]
+        return DataBlock(cols)
+
+    def _out_buffers(self, n, sbytes):
+        def buf(t: DataType, strbytes=0):
+            if t.type_id == abi.STRING:
+                data = np.zeros(max(1, strbytes), np.uint8)
+                offs = np.zeros(n + 1, np.uint64)
+            else:
+                data = np.zeros(max(1, n * t.width), np.uint8)
+                offs = None
+            val = np.zeros(max(1, (n + 7) // 8), np.uint8) if t.nullable else None
+            return dict(t=t, data=data, offs=offs, val=val,
+                        ptrs=(data.ctypes.data, offs.ctypes.data if offs is not None else None,
+                              val.ctypes.data if val is not None else None))
+        aggs = [buf(f.return_type()) for f in self.params.aggregate_functions]
+        keys = [buf(t, sbytes[i]) for i, t in enumerate(self.params.group_data_types)]
+        return aggs, keys
+
+    @staticmethod
+    def _to_column(b, n) -> Column:
+        t: DataType = b["t"]
+        if t.type_id == abi.STRING:
+            offs = b["offs"]
+            data = b["data"][:int(offs[-1])]
+        elif t.type_id == abi.DECIMAL128:
+            data, offs = b["data"][:16 * n], None
+        elif t.type_id == abi.BOOLEAN:
+            data, offs = b["data"][:n].astype(bool), None
+        else:
+            data, offs = b["data"][:n * t.width].view(t.np_dtype), None
+        val = unpack_bits(b["val"], n) if b["val"] is not None else None
+        return Column(t, data, offs, val)
+
+    # ---- partial-state records (exchange / partition bucket)
+    def record_width(self) -> int:
+        w = C.c_uint32()
+        check(lib().dbg_agg_record_width(self.h, C.byref(w)))
+        return w.value
+
+    def partition(self, n_parts: int, scheme: int = 0):
+        counts = (C.c_uint64 * n_parts)()
+        sbytes = (C.c_uint64 * n_parts)()
+        check(lib().dbg_agg_partition(self.h, n_parts, scheme, counts, sbytes))
+        return list(counts), list(sbytes)
+
+    def export_records(self, dev_records, dev_strings):
+        """dev_records / dev_strings: torch uint8 cuda tensors sized from partition()."""
+        check(lib().dbg_agg_export_records(self.h, dev_records.data_ptr(),
+                                           dev_strings.data_ptr() if dev_strings is not None else None))
+
+    def merge_records(self, dev_records, dev_strings, seg_records: Sequence[int], seg_strings: Sequence[int]):
+        n = len(seg_records)
+        sr = (C.c_uint64 * max(1, n))(*seg_records)
+        ss = (C.c_uint64 * max(1, n))(*seg_strings)
+        check(lib().dbg_agg_merge_records(self.h, dev_records.data_ptr(),
+                                          dev_strings.data_ptr() if dev_strings is not None else None, n, sr, ss))
+        self._retained.append((dev_records, dev_strings))
+
+
+@dataclass
+class AggregateMeta:
+    """AggregateMeta::AggregatePayload (AGG/aggregate_meta.rs:124-134): one partial table's
+    exact partial aggregation, still resident in HBM, with its bucket count."""
+    table: AggregateHashTable
+    bucket: int = 0
+    max_partition_count: int = 1
+
+
+class TransformPartialAggregate:
+    """AGG/transform_aggregate_partial.rs:107-468 — AccumulatingTransform over DataBlocks."""
+
+    def __init__(self, params: AggregatorParams, config: HashTableConfig = None, device: int = -1):
+        self.params = params
+        self.config = (config or HashTableConfig()).with_partial(True)
+        self.hashtable = AggregateHashTable(params, self.config, device)
+
+    @classmethod
+    def try_create(cls, params: AggregatorParams, config: HashTableConfig = None, device: int = -1):
+        return cls(params, config, device)
+
+    def transform(self, block: DataBlock, group_indices: Sequence[int], arg_indices: Sequence[Optional[int]],
+                  filter_program=None) -> List[DataBlock]:
+        """execute_one_block (:235-327): group columns and per-aggregate argument columns picked
+        from the block by index; the block's rows are added to the HBM table."""
+        groups = [block.columns[i] for i in group_indices]
+        args = [None if i is None else block.columns[i] for i in arg_indices]
+        self.hashtable.add_groups(groups, args, rows=block.num_rows(), filter_program=filter_program)
+        return []
+
+    def on_finish(self) -> List[AggregateMeta]:
+        """on_finish (:449-465): the partial payload(s)."""
+        return [AggregateMeta(self.hashtable)]
+
+
+class TransformFinalAggregate:
+    """AGG/transform_aggregate_final.rs:45-343 — merge_states of partial payloads, then the
+    output block [agg results..., group cols...]."""
+
+    def __init__(self, params: AggregatorParams, device: int = -1):
+        self.params = params
+        self.device = device
+
+    @classmethod
+    def try_create(cls, params: AggregatorParams, device: int = -1):
+        return cls(params, device)
+
+    def transform(self, metas: Sequence[AggregateMeta]) -> DataBlock:
+        import torch
+        metas = list(metas)
+        if not metas:
+            return self.params.empty_result_block()
+        final = AggregateHashTable(self.params, HashTableConfig(False), self.device)
+        try:
+            for m in metas:
+                counts, sbytes = m.table.partition(1, 0)
+                w = m.table.record_width()
+                dev = torch.device("cuda", torch.cuda.current_device())
+                recs = torch.empty(max(1, counts[0] * w), dtype=torch.uint8, device=dev)
+                strs = torch.empty(max(1, sbytes[0]), dtype=torch.uint8, device=dev)
+                m.table.export_records(recs, strs)
+                torch.cuda.synchronize()
+                final.merge_records(recs, strs, [counts[0]], [sbytes[0]])
+            return final.merge_result()
+        finally:
+            final.close()

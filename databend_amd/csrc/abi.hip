@@ -1,0 +1,1016 @@
+// abi.hip — the C ABI of libdbgpu_agg.so (include/dbgpu_agg.h): handles, device memory, streams,
+// deferred overflow handling, result extraction, record exchange, profiling.
+//
+// A handle is one AggregateHashTable (EAGG/aggregate_hashtable.rs:47) living in HBM.  It owns a
+// HIP stream (or borrows the caller's) and its allocations; nothing here runs on the CPU except
+// bookkeeping — there is no CPU fallback: a missing/unsupported case returns an error code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "agg.hpp"
+#include "filter.hpp"
+
+// ------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHECK(expr)                                                                         \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return fail(DBG_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));    \
+    } while (0)
+
+#define RETURN_IF(rc) \
+    do {              \
+        int _r = (rc); \
+        if (_r != DBG_OK) return _r; \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// profiling: HIP events around every launch (dbg_prof_enable)
+// ------------------------------------------------------------------------------------------
+namespace prof {
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+};
+static std::mutex mu;
+static bool enabled = false;
+static std::vector<Pending> pending;
+static std::vector<std::pair<std::string, std::pair<double, uint64_t>>> totals;
+
+static void resolve_locked() {
+    for (auto& p : pending) {
+        float ms = 0;
+        hipEventSynchronize(p.b);
+        hipEventElapsedTime(&ms, p.a, p.b);
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+        bool found = false;
+        for (auto& t : totals)
+            if (t.first == p.name) {
+                t.second.first += ms;
+                t.second.second += 1;
+                found = true;
+                break;
+            }
+        if (!found) totals.push_back({p.name, {(double)ms, 1}});
+    }
+    pending.clear();
+}
+
+struct Scope {
+    bool on;
+    hipStream_t s;
+    hipEvent_t a, b;
+    const char* name;
+    Scope(const char* n, hipStream_t st) : on(enabled), s(st), name(n) {
+        if (on) {
+            hipEventCreate(&a);
+            hipEventCreate(&b);
+            hipEventRecord(a, s);
+        }
+    }
+    ~Scope() {
+        if (on) {
+            hipEventRecord(b, s);
+            std::lock_guard<std::mutex> g(mu);
+            pending.push_back({name, a, b});
+        }
+    }
+};
+}  // namespace prof
+
+// ------------------------------------------------------------------------------------------
+// handle
+// ------------------------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct dbg_agg_handle {
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    Spec spec{};
+    Spec* dspec = nullptr;
+    std::vector<dbg_datatype> result_types;
+    bool partial = true;
+
+    // table
+    u64* slots = nullptr;
+    u64 cap = 0;
+    u64* counters = nullptr;   // device, CNT_WORDS
+    u64* hcounters = nullptr;  // pinned
+    // overflow lists (deferred)
+    u64* ovf_rows = nullptr;
+    u64 ovf_rows_cap = 0;
+    u64* ovf_recs = nullptr;
+    u64 ovf_recs_cap = 0;
+    u64 pending_rows = 0, pending_recs = 0;
+
+    // batches (ids 1..n_batches); descs in device memory, staged through pinned memory
+    BatchDesc* dbatches = nullptr;
+    u64 batch_cap = 0;
+    u32 n_batches = 0;
+    std::vector<BatchDesc*> pinned_descs;  // one pinned staging desc per batch (kept until reset)
+    std::vector<DevBuf> owned;             // device copies of host inputs / filter constants
+
+    // finalize state
+    bool finalized = false;
+    u64 n_groups = 0;
+    std::vector<u64> string_bytes;
+    u64* d_pos = nullptr;      // scanned per-block group counts
+    u64* d_str_pos = nullptr;  // [n_keys][blocks] scanned per column
+    u64 pos_cap = 0, str_pos_cap = 0;
+    // partition state
+    u32 part_n = 0;
+    int part_scheme = 0;
+    u64* d_part_pos = nullptr;
+    u64* d_part_str_pos = nullptr;
+    u64* d_part_str_base = nullptr;
+    u64 part_cap = 0, part_str_cap = 0;
+    std::vector<u64> part_counts, part_strings;
+};
+
+static int dev_alloc(void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(DBG_ERR_OOM, std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    return DBG_OK;
+}
+
+static int own_copy(dbg_agg_handle* h, const void* src, size_t bytes, const void** out) {
+    DevBuf b;
+    RETURN_IF(dev_alloc(&b.p, bytes));
+    h->owned.push_back(b);
+    if (bytes) HIPCHECK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, h->stream));
+    *out = b.p;
+    return DBG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// spec construction: AggregatorParams -> slot layout (+ result types, per the factory)
+// ------------------------------------------------------------------------------------------
+static bool is_signed_i(int t) { return t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64; }
+static bool is_unsigned_i(int t) { return t == DBG_UINT8 || t == DBG_UINT16 || t == DBG_UINT32 || t == DBG_UINT64; }
+static bool is_float(int t) { return t == DBG_FLOAT32 || t == DBG_FLOAT64; }
+static bool valid_type(int t) { return t >= DBG_INT8 && t <= DBG_BOOLEAN; }
+
+// AggregateFunction::return_type() of the factory-built function.
+static int result_type_of(const dbg_agg_spec& s, dbg_datatype* out) {
+    int t = s.arg.type;
+    dbg_datatype r{DBG_UINT64, 0, 0, 0, 0};
+    if (s.kind == DBG_AGG_COUNT) {
+        *out = r;  // AggregateCountFunction: UInt64, never nullable
+        return DBG_OK;
+    }
+    if (t < 0 || !valid_type(t)) return fail(DBG_ERR_INVALID, "aggregate needs an argument type");
+    switch (s.kind) {
+        case DBG_AGG_SUM:  // ResultTypeOfUnary::Sum
+            if (is_signed_i(t)) r.type = DBG_INT64;
+            else if (is_unsigned_i(t)) r.type = DBG_UINT64;
+            else if (is_float(t)) r.type = DBG_FLOAT64;
+            else if (t == DBG_DECIMAL128) r = dbg_datatype{DBG_DECIMAL128, 38, s.arg.scale, 0, 0};
+            else return fail(DBG_ERR_UNSUPPORTED, "sum: unsupported argument type");
+            break;
+        case DBG_AGG_AVG:
+            if (is_signed_i(t) || is_unsigned_i(t) || is_float(t)) r.type = DBG_FLOAT64;
+            else if (t == DBG_DECIMAL128) r = dbg_datatype{DBG_DECIMAL128, 38, (uint8_t)std::max<int>(s.arg.scale, 4), 0, 0};
+            else return fail(DBG_ERR_UNSUPPORTED, "avg: unsupported argument type");
+            break;
+        case DBG_AGG_MIN: case DBG_AGG_MAX:
+            if (t == DBG_STRING || t == DBG_BOOLEAN) return fail(DBG_ERR_UNSUPPORTED, "min/max: String/Boolean arguments stay on the CPU path");
+            if (t == DBG_DECIMAL128 && s.arg.precision > 18)
+                return fail(DBG_ERR_UNSUPPORTED, "min/max: Decimal128 with precision > 18 stays on the CPU path");
+            r = dbg_datatype{t, s.arg.precision, s.arg.scale, 0, 0};
+            break;
+        default: return fail(DBG_ERR_INVALID, "unknown aggregate kind");
+    }
+    r.nullable = (s.or_null || s.arg.nullable) ? 1 : 0;
+    *out = r;
+    return DBG_OK;
+}
+
+static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype>& rtypes) {
+    memset(&S, 0, sizeof(S));
+    if (p->n_group_cols < 1 || p->n_group_cols > DBG_MAX_KEYS) return fail(DBG_ERR_UNSUPPORTED, "1..8 group columns supported");
+    if (p->n_aggs < 0 || p->n_aggs > DBG_MAX_AGGS) return fail(DBG_ERR_UNSUPPORTED, "at most 32 aggregates");
+    S.n_keys = p->n_group_cols;
+    S.n_aggs = p->n_aggs;
+    // inline packing: row format [validity bytes][values] (EAGG/payload.rs:100-129)
+    int w = 0;
+    bool fixed = true;
+    for (int c = 0; c < S.n_keys; ++c) {
+        dbg_datatype t = p->group_types[c];
+        if (!valid_type(t.type)) return fail(DBG_ERR_INVALID, "bad group type");
+        S.key_types[c] = t;
+        if (t.type == DBG_STRING) S.has_strings = 1;
+        if (t.type == DBG_STRING || t.type == DBG_DECIMAL128) fixed = false;
+        if (t.nullable) S.voff[c] = (uint8_t)w++;
+    }
+    for (int c = 0; c < S.n_keys; ++c) {
+        S.koff[c] = (uint8_t)w;
+        w += type_width(S.key_types[c].type);
+    }
+    S.inline_keys = fixed && w <= 8;
+    S.inline_width = w;
+    // record layout: [hash][validity bytes][values, 8-aligned][state words]
+    u32 off = 8;
+    for (int c = 0; c < S.n_keys; ++c)
+        if (S.key_types[c].nullable) S.rec_val_off[c] = off++;
+    off = (off + 7) & ~7u;
+    for (int c = 0; c < S.n_keys; ++c) {
+        S.rec_key_off[c] = off;
+        int t = S.key_types[c].type;
+        off += (t == DBG_STRING || t == DBG_DECIMAL128) ? 16 : 8;
+    }
+    // state words
+    int word = 1, flag_bits = 0;
+    rtypes.clear();
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const dbg_agg_spec& s = p->aggs[a];
+        DAgg& A = S.aggs[a];
+        dbg_datatype rt;
+        RETURN_IF(result_type_of(s, &rt));
+        rtypes.push_back(rt);
+        A.kind = s.kind;
+        A.arg_type = s.kind == DBG_AGG_COUNT && s.arg.type < 0 ? -1 : s.arg.type;
+        A.arg_nullable = A.arg_type >= 0 ? s.arg.nullable : 0;
+        int t = A.arg_type;
+        A.sumk = t == DBG_DECIMAL128 ? SUMK_I128 : (is_float(t) ? SUMK_F64 : SUMK_I64);
+        A.mmk = is_unsigned_i(t) ? MMK_U64 : (is_float(t) ? MMK_F64 : MMK_I64);
+        A.w0 = word;
+        switch (s.kind) {
+            case DBG_AGG_COUNT: A.nwords = 1; break;
+            case DBG_AGG_SUM: A.nwords = A.sumk == SUMK_I128 ? 2 : 1; break;
+            case DBG_AGG_AVG: A.nwords = A.sumk == SUMK_I128 ? 3 : 2; break;
+            default: A.nwords = 1;
+        }
+        word += A.nwords;
+        A.flag_bit = -1;
+        if ((s.kind == DBG_AGG_SUM || s.kind == DBG_AGG_MIN || s.kind == DBG_AGG_MAX) && A.arg_nullable) A.flag_bit = flag_bits++;
+        A.res_type = rt.type;
+        A.res_precision = rt.precision;
+        A.res_scale = rt.scale;
+        A.res_nullable = rt.nullable;
+        A.dec_check = (s.kind == DBG_AGG_SUM && t == DBG_DECIMAL128 && s.arg.precision <= 18) ? 1 : 0;
+        A.scale_add = (s.kind == DBG_AGG_AVG && t == DBG_DECIMAL128) ? (int)rt.scale - (int)s.arg.scale : 0;
+        A.res_width = (int)type_width(rt.type);
+    }
+    if (flag_bits > 64) return fail(DBG_ERR_UNSUPPORTED, "too many nullable aggregates");
+    S.flags_word = flag_bits ? word++ : -1;
+    S.n_words = word - 1;
+    if (word > DBG_MAX_WORDS) return fail(DBG_ERR_UNSUPPORTED, "aggregate states too wide");
+    int sw = 1;
+    while (sw < word && sw < 8) sw <<= 1;
+    if (word > 8) sw = (word + 7) & ~7;
+    S.stride_words = sw;
+    S.rec_state_off = off;
+    S.rec_width = off + 8 * (u32)S.n_words;
+    return DBG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// table allocation / growth
+// ------------------------------------------------------------------------------------------
+static TableDesc table_desc(dbg_agg_handle* h) {
+    TableDesc t;
+    t.slots = h->slots;
+    t.cap = h->cap;
+    t.stride_words = (u32)h->spec.stride_words;
+    t.probe_limit = (u32)std::min<u64>(h->cap, 512);
+    t.counters = h->counters;
+    t.ovf_rows = h->ovf_rows;
+    t.ovf_rows_cap = h->ovf_rows_cap;
+    t.ovf_recs = h->ovf_recs;
+    t.ovf_recs_cap = h->ovf_recs_cap;
+    return t;
+}
+
+static u64 pow2_at_least(u64 x) {
+    u64 p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+static int alloc_table(dbg_agg_handle* h, u64 cap, u64** out) {
+    size_t bytes = (size_t)(cap + 1) * h->spec.stride_words * 8;
+    RETURN_IF(dev_alloc((void**)out, bytes));
+    prof::Scope ps("table_init", h->stream);
+    launch_table_init(h->stream, h->dspec, h->spec, *out, cap);
+    return DBG_OK;
+}
+
+static int grow_table(dbg_agg_handle* h, u64 new_cap) {
+    u64* ns = nullptr;
+    RETURN_IF(alloc_table(h, new_cap, &ns));
+    u64* old = h->slots;
+    u64 old_cap = h->cap;
+    h->slots = ns;
+    h->cap = new_cap;
+    {
+        prof::Scope ps("agg_rehash", h->stream);
+        launch_rehash(h->stream, h->dspec, h->spec, h->dbatches, old, old_cap, table_desc(h));
+    }
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    HIPCHECK(hipFree(old));
+    return DBG_OK;
+}
+
+static int read_counters(dbg_agg_handle* h) {
+    HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    return DBG_OK;
+}
+
+// Resolve deferred overflow: grow so that every pending group fits at <= 50% load, re-insert.
+static int resolve_overflow(dbg_agg_handle* h) {
+    RETURN_IF(read_counters(h));
+    for (int round = 0; round < 4; ++round) {
+        u64 claims = h->hcounters[CNT_CLAIMS], orows = h->hcounters[CNT_OVF_ROWS], orecs = h->hcounters[CNT_OVF_RECS];
+        if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+        if (orows == 0 && orecs == 0) {
+            h->pending_rows = h->pending_recs = 0;
+            // keep the load factor sane for the next batch (the reference resizes at 1/1.5)
+            if ((double)claims * 1.5 > (double)h->cap) RETURN_IF(grow_table(h, pow2_at_least((u64)(claims * 2.0) + 1)));
+            return DBG_OK;
+        }
+        u64 need = pow2_at_least(2 * (claims + orows + orecs) + 1);
+        if (need > h->cap) RETURN_IF(grow_table(h, need));
+        HIPCHECK(hipMemsetAsync(h->counters + CNT_OVF_ROWS, 0, 16, h->stream));
+        {
+            prof::Scope ps("agg_retry", h->stream);
+            launch_retry(h->stream, h->dspec, h->spec, h->dbatches, table_desc(h), orows, orecs, h->ovf_rows, h->ovf_recs);
+        }
+        RETURN_IF(read_counters(h));
+    }
+    return fail(DBG_ERR_INTERNAL, "overflow did not converge");
+}
+
+// Make sure the deferred-overflow lists can hold everything the next launch may push.
+static int ensure_ovf(dbg_agg_handle* h, u64 add_rows, u64 add_recs) {
+    u64 need_rows = h->pending_rows + add_rows, need_recs = h->pending_recs + add_recs;
+    if (need_rows <= h->ovf_rows_cap && need_recs <= h->ovf_recs_cap) {
+        h->pending_rows = need_rows;
+        h->pending_recs = need_recs;
+        return DBG_OK;
+    }
+    // drain what is pending, then reallocate the lists at the new size
+    RETURN_IF(resolve_overflow(h));
+    need_rows = add_rows;
+    need_recs = add_recs;
+    if (need_rows > h->ovf_rows_cap) {
+        if (h->ovf_rows) HIPCHECK(hipFree(h->ovf_rows));
+        h->ovf_rows_cap = std::max<u64>(need_rows, 1024);
+        RETURN_IF(dev_alloc((void**)&h->ovf_rows, h->ovf_rows_cap * 8));
+    }
+    if (need_recs > h->ovf_recs_cap) {
+        if (h->ovf_recs) HIPCHECK(hipFree(h->ovf_recs));
+        h->ovf_recs_cap = std::max<u64>(need_recs, 1024);
+        RETURN_IF(dev_alloc((void**)&h->ovf_recs, h->ovf_recs_cap * h->spec.stride_words * 8));
+    }
+    h->pending_rows = need_rows;
+    h->pending_recs = need_recs;
+    return DBG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// batches
+// ------------------------------------------------------------------------------------------
+static int new_batch(dbg_agg_handle* h, BatchDesc** staging, u32* bid) {
+    if (h->n_batches >= 0xFFFE) return fail(DBG_ERR_UNSUPPORTED, "more than 65534 batches before reset");
+    u32 id = h->n_batches + 1;
+    if (id >= h->batch_cap) {
+        u64 ncap = std::max<u64>(64, h->batch_cap * 2);
+        BatchDesc* nb = nullptr;
+        RETURN_IF(dev_alloc((void**)&nb, ncap * sizeof(BatchDesc)));
+        if (h->dbatches) {
+            HIPCHECK(hipMemcpyAsync(nb, h->dbatches, h->batch_cap * sizeof(BatchDesc), hipMemcpyDeviceToDevice, h->stream));
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipFree(h->dbatches));
+        }
+        h->dbatches = nb;
+        h->batch_cap = ncap;
+    }
+    BatchDesc* st = nullptr;
+    HIPCHECK(hipHostMalloc((void**)&st, sizeof(BatchDesc), hipHostMallocDefault));
+    memset(st, 0, sizeof(BatchDesc));
+    h->pinned_descs.push_back(st);
+    h->n_batches = id;
+    *staging = st;
+    *bid = id;
+    return DBG_OK;
+}
+
+static int upload_batch(dbg_agg_handle* h, BatchDesc* st, u32 bid) {
+    HIPCHECK(hipMemcpyAsync(h->dbatches + bid, st, sizeof(BatchDesc), hipMemcpyHostToDevice, h->stream));
+    return DBG_OK;
+}
+
+// dbg_column (host or device) -> DCol on device
+static int to_dcol(dbg_agg_handle* h, const dbg_column& c, const dbg_datatype& want, bool check_type, int on_device, DCol& d) {
+    memset(&d, 0, sizeof(d));
+    if (!valid_type(c.dt.type)) return fail(DBG_ERR_INVALID, "bad column type");
+    if (check_type && (c.dt.type != want.type || (c.dt.type == DBG_DECIMAL128 && c.dt.scale != want.scale)))
+        return fail(DBG_ERR_INVALID, "column type does not match the declared type");
+    if (check_type && c.dt.nullable && !want.nullable) return fail(DBG_ERR_INVALID, "nullable column for a non-nullable declared type");
+    d.type = c.dt.type;
+    d.precision = c.dt.precision;
+    d.scale = c.dt.scale;
+    d.nullable = check_type ? want.nullable : c.dt.nullable;
+    d.layout = LAYOUT_ARROW;
+    d.width = type_width(c.dt.type);
+    d.stride = d.width;
+    u64 n = c.len;
+    if (on_device) {
+        d.data = (const u8*)c.data;
+        d.offsets = c.offsets;
+        d.validity = c.dt.nullable ? c.validity : nullptr;
+        d.validity_offset = c.validity_offset;
+        d.data_offset = c.data_offset;
+        return DBG_OK;
+    }
+    // host: copy what the rows need
+    const void* p = nullptr;
+    if (c.dt.type == DBG_STRING) {
+        u64 lo = n ? c.offsets[0] : 0, hi = n ? c.offsets[n] : 0;
+        // copy offsets rebased to 0 and the payload slice
+        std::vector<uint64_t> offs(n + 1);
+        for (u64 i = 0; i <= n; ++i) offs[i] = c.offsets[i] - lo;
+        RETURN_IF(own_copy(h, offs.data(), (n + 1) * 8, &p));
+        d.offsets = (const u64*)p;
+        // the staging vector dies here: make the copy synchronous w.r.t. it
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        RETURN_IF(own_copy(h, (const u8*)c.data + lo, hi - lo, &p));
+        d.data = (const u8*)p;
+    } else if (c.dt.type == DBG_BOOLEAN) {
+        u64 bytes = (c.data_offset + n + 7) / 8;
+        RETURN_IF(own_copy(h, c.data, bytes, &p));
+        d.data = (const u8*)p;
+        d.data_offset = c.data_offset;
+    } else {
+        RETURN_IF(own_copy(h, c.data, n * d.width, &p));
+        d.data = (const u8*)p;
+    }
+    if (c.dt.nullable && c.validity) {
+        u64 bytes = (c.validity_offset + n + 7) / 8;
+        RETURN_IF(own_copy(h, c.validity, bytes, &p));
+        d.validity = (const u8*)p;
+        d.validity_offset = c.validity_offset;
+    }
+    return DBG_OK;
+}
+
+static int fill_filter(dbg_agg_handle* h, const dbg_filter* f, int on_device, DCol* cols, int* ncols, DNode* nodes, int* nnodes) {
+    if (f->n_cols > DBG_MAX_FCOLS || f->n_nodes > DBG_MAX_NODES) return fail(DBG_ERR_UNSUPPORTED, "filter too large");
+    int depth = 0;
+    for (int k = 0; k < f->n_nodes; ++k) {
+        const dbg_pred_node& n = f->nodes[k];
+        DNode& d = nodes[k];
+        memset(&d, 0, sizeof(d));
+        d.op = n.op;
+        d.cmp = n.cmp;
+        d.col = n.col;
+        d.col2 = n.col2;
+        d.i64v = n.i64;
+        d.f64v = n.f64;
+        d.lo = n.i128_lo;
+        d.hi = n.i128_hi;
+        if (n.op == DBG_PRED_CMP_CONST || n.op == DBG_PRED_CMP_COLS || n.op == DBG_PRED_IS_NULL || n.op == DBG_PRED_IS_NOT_NULL) {
+            if (n.col < 0 || n.col >= f->n_cols || (n.op == DBG_PRED_CMP_COLS && (n.col2 < 0 || n.col2 >= f->n_cols)))
+                return fail(DBG_ERR_INVALID, "predicate column index out of range");
+            depth++;
+        } else if (n.op == DBG_PRED_TRUE) {
+            depth++;
+        } else if (n.op == DBG_PRED_AND || n.op == DBG_PRED_OR) {
+            if (depth < 2) return fail(DBG_ERR_INVALID, "malformed predicate program");
+            depth--;
+        } else if (n.op == DBG_PRED_NOT) {
+            if (depth < 1) return fail(DBG_ERR_INVALID, "malformed predicate program");
+        } else {
+            return fail(DBG_ERR_INVALID, "unknown predicate op");
+        }
+        if (depth > 15) return fail(DBG_ERR_UNSUPPORTED, "predicate too deep");
+        if (n.op == DBG_PRED_CMP_CONST && f->cols[n.col].dt.type == DBG_STRING) {
+            const void* p = nullptr;
+            RETURN_IF(own_copy(h, n.str, n.str_len, &p));
+            d.str = (const u8*)p;
+            d.str_len = n.str_len;
+        }
+    }
+    if (f->n_nodes && depth != 1) return fail(DBG_ERR_INVALID, "malformed predicate program");
+    for (int c = 0; c < f->n_cols; ++c) RETURN_IF(to_dcol(h, f->cols[c], f->cols[c].dt, false, on_device, cols[c]));
+    *ncols = f->n_cols;
+    *nnodes = f->n_nodes;
+    return DBG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// C API
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* dbg_version(void) { return "dbgpu_agg 0.1 (gfx950)"; }
+const char* dbg_last_error(void) { return g_last_error.c_str(); }
+
+int dbg_device_count(int* n) {
+    HIPCHECK(hipGetDeviceCount(n));
+    return DBG_OK;
+}
+
+int dbg_agg_result_type(const dbg_agg_spec* spec, dbg_datatype* out) {
+    if (!spec || !out) return fail(DBG_ERR_INVALID, "null argument");
+    return result_type_of(*spec, out);
+}
+
+int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
+    if (!params || !out) return fail(DBG_ERR_INVALID, "null argument");
+    auto* h = new dbg_agg_handle();
+    int rc = build_spec(params, h->spec, h->result_types);
+    if (rc != DBG_OK) {
+        delete h;
+        return rc;
+    }
+    h->partial = params->partial != 0;
+    if (params->device >= 0) h->device = params->device;
+    else {
+        hipError_t e = hipGetDevice(&h->device);
+        if (e != hipSuccess) {
+            delete h;
+            return fail(DBG_ERR_DEVICE, std::string("hipGetDevice: ") + hipGetErrorString(e));
+        }
+    }
+    auto cleanup = [&](int code) {
+        dbg_agg_destroy(h);
+        return code;
+    };
+    if (hipSetDevice(h->device) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "hipStreamCreate failed"));
+    h->stream = h->own_stream;
+    if ((rc = dev_alloc((void**)&h->dspec, sizeof(Spec))) != DBG_OK) return cleanup(rc);
+    if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
+    if ((rc = dev_alloc((void**)&h->counters, CNT_WORDS * 8)) != DBG_OK) return cleanup(rc);
+    if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
+    if (hipHostMalloc((void**)&h->hcounters, CNT_WORDS * 8, hipHostMallocDefault) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
+    // initial capacity: AggregateHashTable::initial_capacity() = 32768, or 2x the hint
+    u64 hint = params->capacity_hint ? params->capacity_hint : 16384;
+    h->cap = pow2_at_least(std::max<u64>(hint * 2, 1024));
+    if ((rc = alloc_table(h, h->cap, &h->slots)) != DBG_OK) return cleanup(rc);
+    // the (empty) batch table
+    BatchDesc* st;
+    u32 bid;
+    if ((rc = new_batch(h, &st, &bid)) != DBG_OK) return cleanup(rc);
+    h->n_batches = 0;  // slot 0 reserved: ref entries always carry bid >= 1
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "sync"));
+    *out = h;
+    return DBG_OK;
+}
+
+void dbg_agg_destroy(dbg_agg_handle* h) {
+    if (!h) return;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    for (auto& b : h->owned) hipFree(b.p);
+    for (auto* p : h->pinned_descs) hipHostFree(p);
+    void* bufs[] = {h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
+                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base};
+    for (void* p : bufs)
+        if (p) hipFree(p);
+    if (h->hcounters) hipHostFree(h->hcounters);
+    if (h->own_stream) hipStreamDestroy(h->own_stream);
+    delete h;
+}
+
+int dbg_agg_set_stream(dbg_agg_handle* h, void* s) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    HIPCHECK(hipSetDevice(h->device));
+    hipStream_t ns = s ? (hipStream_t)s : h->own_stream;
+    if (ns != h->stream) {
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        h->stream = ns;
+    }
+    return DBG_OK;
+}
+
+int dbg_agg_reset(dbg_agg_handle* h) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    HIPCHECK(hipSetDevice(h->device));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    for (auto& b : h->owned) HIPCHECK(hipFree(b.p));
+    h->owned.clear();
+    for (size_t i = 1; i < h->pinned_descs.size(); ++i) HIPCHECK(hipHostFree(h->pinned_descs[i]));
+    h->pinned_descs.resize(std::min<size_t>(h->pinned_descs.size(), 1));
+    h->n_batches = 0;
+    h->pending_rows = h->pending_recs = 0;
+    h->finalized = false;
+    HIPCHECK(hipMemsetAsync(h->counters, 0, CNT_WORDS * 8, h->stream));
+    prof::Scope ps("table_init", h->stream);
+    launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap);
+    return DBG_OK;
+}
+
+int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols, const dbg_filter* filter,
+                       uint64_t rows, int on_device) {
+    if (!h || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
+    if (rows >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "a batch holds fewer than 2^32 rows");
+    HIPCHECK(hipSetDevice(h->device));
+    h->finalized = false;
+    if (rows == 0) return DBG_OK;
+    const Spec& S = h->spec;
+    BatchDesc* st;
+    u32 bid;
+    RETURN_IF(new_batch(h, &st, &bid));
+    st->rows = rows;
+    for (int c = 0; c < S.n_keys; ++c) {
+        if (group_cols[c].len < rows) return fail(DBG_ERR_INVALID, "group column shorter than rows");
+        RETURN_IF(to_dcol(h, group_cols[c], S.key_types[c], true, on_device, st->keys[c]));
+    }
+    for (int a = 0; a < S.n_aggs; ++a) {
+        if (S.aggs[a].arg_type < 0) continue;
+        if (!arg_cols) return fail(DBG_ERR_INVALID, "missing aggregate arguments");
+        dbg_datatype want{S.aggs[a].arg_type, 0, arg_cols[a].dt.scale, (uint8_t)S.aggs[a].arg_nullable, 0};
+        if (arg_cols[a].len < rows) return fail(DBG_ERR_INVALID, "argument column shorter than rows");
+        RETURN_IF(to_dcol(h, arg_cols[a], want, true, on_device, st->args[a]));
+    }
+    if (filter && filter->n_nodes) RETURN_IF(fill_filter(h, filter, on_device, st->fcols, &st->n_fcols, st->nodes, &st->n_nodes));
+    RETURN_IF(upload_batch(h, st, bid));
+    // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
+    u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
+    RETURN_IF(ensure_ovf(h, rows, blocks * 4096));
+    {
+        prof::Scope ps("agg_insert", h->stream);
+        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true);
+    }
+    HIPCHECK(hipGetLastError());
+    if (!on_device) RETURN_IF(resolve_overflow(h));  // host path: synchronous like the reference processor
+    return DBG_OK;
+}
+
+static int ensure_buf(u64** p, u64* cap, u64 n) {
+    if (n <= *cap) return DBG_OK;
+    if (*p) HIPCHECK(hipFree(*p));
+    *cap = std::max<u64>(n, 1024);
+    return dev_alloc((void**)p, *cap * 8);
+}
+
+int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(resolve_overflow(h));
+    const Spec& S = h->spec;
+    u64 nb = finalize_blocks(h->cap);
+    RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 8));
+    RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
+    TableDesc t = table_desc(h);
+    {
+        prof::Scope ps("count_groups", h->stream);
+        launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+    }
+    u64* totals = h->d_pos + nb;  // scratch after the histogram
+    launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
+    h->string_bytes.assign(S.n_keys, 0);
+    std::vector<u64> str_tot(S.n_keys, 0);
+    if (S.has_strings && !S.inline_keys)
+        for (int c = 0; c < S.n_keys; ++c)
+            if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
+    HIPCHECK(hipMemcpyAsync(h->hcounters + 4, totals, 8, hipMemcpyDeviceToHost, h->stream));
+    std::vector<u64> stot(S.n_keys + 1, 0);
+    HIPCHECK(hipMemcpyAsync(stot.data(), totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    h->n_groups = stot[0];
+    for (int c = 0; c < S.n_keys; ++c)
+        h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? stot[1 + c] : 0;
+    if (h->n_groups != h->hcounters[CNT_CLAIMS])
+        return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
+                                          std::to_string(h->hcounters[CNT_CLAIMS]));
+    h->finalized = true;
+    if (n_groups) *n_groups = h->n_groups;
+    if (string_bytes)
+        for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
+    return DBG_OK;
+}
+
+int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    if (!h->finalized) return fail(DBG_ERR_INVALID, "dbg_agg_finalize must precede dbg_agg_result");
+    HIPCHECK(hipSetDevice(h->device));
+    const Spec& S = h->spec;
+    u64 n = h->n_groups;
+    for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = h->result_types[a];
+    for (int c = 0; c < S.n_keys; ++c) out_keys[c].dt = S.key_types[c];
+    if (n == 0) {
+        for (int c = 0; c < S.n_keys; ++c)
+            if (S.key_types[c].type == DBG_STRING && out_keys[c].offsets) {
+                u64 z = 0;
+                if (on_device) HIPCHECK(hipMemcpy(out_keys[c].offsets, &z, 8, hipMemcpyHostToDevice));
+                else out_keys[c].offsets[0] = 0;
+            }
+        return DBG_OK;
+    }
+    std::vector<void*> temps;
+    auto tmp = [&](size_t bytes, void** p) -> int {
+        RETURN_IF(dev_alloc(p, bytes));
+        temps.push_back(*p);
+        return DBG_OK;
+    };
+    auto free_temps = [&]() {
+        for (void* p : temps) hipFree(p);
+    };
+    OutDesc od;
+    memset(&od, 0, sizeof(od));
+    int rc = DBG_OK;
+    // device destinations
+    for (int c = 0; c < S.n_keys && rc == DBG_OK; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        size_t bytes = t.type == DBG_STRING ? h->string_bytes[c] : n * type_width(t.type);
+        if (on_device) od.key_data[c] = out_keys[c].data;
+        else rc = tmp(bytes, &od.key_data[c]);
+        if (rc == DBG_OK && t.type == DBG_STRING) {
+            if (on_device) od.key_offsets[c] = out_keys[c].offsets;
+            else rc = tmp((n + 1) * 8, (void**)&od.key_offsets[c]);
+        }
+        if (rc == DBG_OK && t.nullable) rc = tmp(n, (void**)&od.key_valid[c]);
+    }
+    for (int a = 0; a < S.n_aggs && rc == DBG_OK; ++a) {
+        const dbg_datatype& t = h->result_types[a];
+        if (on_device) od.agg_data[a] = out_aggs[a].data;
+        else rc = tmp(n * type_width(t.type), &od.agg_data[a]);
+        if (rc == DBG_OK && t.nullable) rc = tmp(n, (void**)&od.agg_valid[a]);
+    }
+    if (rc != DBG_OK) {
+        free_temps();
+        return rc;
+    }
+    {
+        prof::Scope ps("write_results", h->stream);
+        launch_write_results(h->stream, h->dspec, S, h->dbatches, table_desc(h), h->d_pos, h->d_str_pos, od);
+    }
+    // offsets[n] and bit-packed validity
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        if (t.type == DBG_STRING) {
+            u64 tot = h->string_bytes[c];
+            hipMemcpyAsync(od.key_offsets[c] + n, &h->string_bytes[c], 8, hipMemcpyHostToDevice, h->stream);
+            (void)tot;
+        }
+        if (t.nullable) {
+            u8* bits = nullptr;
+            if (on_device) bits = out_keys[c].validity;
+            else if (tmp((n + 7) / 8, (void**)&bits) != DBG_OK) {
+                free_temps();
+                return DBG_ERR_OOM;
+            }
+            if (bits) launch_pack_bits(h->stream, od.key_valid[c], n, bits);
+            if (!on_device && out_keys[c].validity)
+                hipMemcpyAsync(out_keys[c].validity, bits, (n + 7) / 8, hipMemcpyDeviceToHost, h->stream);
+        }
+    }
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const dbg_datatype& t = h->result_types[a];
+        if (t.nullable) {
+            u8* bits = nullptr;
+            if (on_device) bits = out_aggs[a].validity;
+            else if (tmp((n + 7) / 8, (void**)&bits) != DBG_OK) {
+                free_temps();
+                return DBG_ERR_OOM;
+            }
+            if (bits) launch_pack_bits(h->stream, od.agg_valid[a], n, bits);
+            if (!on_device && out_aggs[a].validity)
+                hipMemcpyAsync(out_aggs[a].validity, bits, (n + 7) / 8, hipMemcpyDeviceToHost, h->stream);
+        }
+    }
+    if (!on_device) {
+        for (int c = 0; c < S.n_keys; ++c) {
+            const dbg_datatype& t = S.key_types[c];
+            size_t bytes = t.type == DBG_STRING ? h->string_bytes[c] : n * type_width(t.type);
+            if (out_keys[c].data && bytes) hipMemcpyAsync(out_keys[c].data, od.key_data[c], bytes, hipMemcpyDeviceToHost, h->stream);
+            if (t.type == DBG_STRING && out_keys[c].offsets)
+                hipMemcpyAsync(out_keys[c].offsets, od.key_offsets[c], (n + 1) * 8, hipMemcpyDeviceToHost, h->stream);
+        }
+        for (int a = 0; a < S.n_aggs; ++a)
+            if (out_aggs[a].data)
+                hipMemcpyAsync(out_aggs[a].data, od.agg_data[a], n * type_width(h->result_types[a].type), hipMemcpyDeviceToHost, h->stream);
+    }
+    HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+    hipError_t e = hipStreamSynchronize(h->stream);
+    free_temps();
+    if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("result: ") + hipGetErrorString(e));
+    if (h->hcounters[CNT_ERR] & ERR_DEC_OVERFLOW) {
+        HIPCHECK(hipMemsetAsync(h->counters + CNT_ERR, 0, 8, h->stream));
+        return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
+    }
+    return DBG_OK;
+}
+
+// ---- partial-state records ----
+int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width) {
+    if (!h || !width) return fail(DBG_ERR_INVALID, "null argument");
+    *width = h->spec.rec_width;
+    return DBG_OK;
+}
+
+int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t* rec_counts, uint64_t* string_bytes) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    if (n_parts < 1 || n_parts > 256) return fail(DBG_ERR_UNSUPPORTED, "1..256 partitions");
+    if (scheme == 1 && (n_parts & (n_parts - 1))) return fail(DBG_ERR_INVALID, "radix partitions must be a power of two");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(resolve_overflow(h));
+    const Spec& S = h->spec;
+    u64 nb = finalize_blocks(h->cap);
+    u64 nflat = (u64)n_parts * nb;
+    RETURN_IF(ensure_buf(&h->d_part_pos, &h->part_cap, nflat + 8));
+    RETURN_IF(ensure_buf(&h->d_part_str_pos, &h->part_str_cap, nflat * S.n_keys + 8));
+    if (!h->d_part_str_base) RETURN_IF(dev_alloc((void**)&h->d_part_str_base, 257 * 8));
+    HIPCHECK(hipMemsetAsync(h->d_part_str_pos, 0, (nflat * S.n_keys + 8) * 8, h->stream));
+    {
+        prof::Scope ps("count_groups", h->stream);
+        launch_count_groups(h->stream, h->dspec, S, h->dbatches, table_desc(h), n_parts, scheme, h->d_part_pos, h->d_part_str_pos);
+    }
+    std::vector<u64> hist(nflat), shist(nflat * S.n_keys);
+    HIPCHECK(hipMemcpyAsync(hist.data(), h->d_part_pos, nflat * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipMemcpyAsync(shist.data(), h->d_part_str_pos, nflat * S.n_keys * 8, hipMemcpyDeviceToHost, h->stream));
+    launch_exclusive_scan(h->stream, h->d_part_pos, nflat, h->d_part_pos + nflat);
+    launch_exclusive_scan(h->stream, h->d_part_str_pos, nflat * S.n_keys, h->d_part_str_pos + nflat * S.n_keys);
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    h->part_counts.assign(n_parts, 0);
+    h->part_strings.assign(n_parts, 0);
+    for (u32 p = 0; p < n_parts; ++p) {
+        for (u64 b = 0; b < nb; ++b) h->part_counts[p] += hist[(u64)p * nb + b];
+        for (u64 k = 0; k < (u64)S.n_keys * nb; ++k) h->part_strings[p] += shist[(u64)p * S.n_keys * nb + k];
+    }
+    std::vector<u64> base(n_parts + 1, 0);
+    for (u32 p = 0; p < n_parts; ++p) base[p + 1] = base[p] + h->part_strings[p];
+    HIPCHECK(hipMemcpyAsync(h->d_part_str_base, base.data(), (n_parts + 1) * 8, hipMemcpyHostToDevice, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    h->part_n = n_parts;
+    h->part_scheme = scheme;
+    for (u32 p = 0; p < n_parts; ++p) {
+        if (rec_counts) rec_counts[p] = h->part_counts[p];
+        if (string_bytes) string_bytes[p] = h->part_strings[p];
+    }
+    return DBG_OK;
+}
+
+int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strings) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    if (!h->part_n) return fail(DBG_ERR_INVALID, "dbg_agg_partition must precede dbg_agg_export_records");
+    HIPCHECK(hipSetDevice(h->device));
+    prof::Scope ps("export_records", h->stream);
+    launch_export(h->stream, h->dspec, h->spec, h->dbatches, table_desc(h), h->part_n, h->part_scheme, h->d_part_pos,
+                  h->d_part_str_pos, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void* dev_strings, int32_t n_segments,
+                          const uint64_t* seg_records, const uint64_t* seg_string_bytes) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    HIPCHECK(hipSetDevice(h->device));
+    h->finalized = false;
+    const Spec& S = h->spec;
+    u64 rec_off = 0, str_off = 0;
+    for (int g = 0; g < n_segments; ++g) {
+        u64 n = seg_records[g];
+        const u8* base = (const u8*)dev_records + rec_off * S.rec_width;
+        const u8* strs = (const u8*)dev_strings + str_off;
+        rec_off += n;
+        str_off += seg_string_bytes ? seg_string_bytes[g] : 0;
+        if (n == 0) continue;
+        if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
+        BatchDesc* st;
+        u32 bid;
+        RETURN_IF(new_batch(h, &st, &bid));
+        st->rows = n;
+        st->is_records = 1;
+        st->rec_width = S.rec_width;
+        st->rec_base = base;
+        for (int c = 0; c < S.n_keys; ++c) {
+            DCol& d = st->keys[c];
+            const dbg_datatype& t = S.key_types[c];
+            d.type = t.type;
+            d.precision = t.precision;
+            d.scale = t.scale;
+            d.nullable = t.nullable;
+            d.layout = LAYOUT_RECORD;
+            d.width = type_width(t.type);
+            d.stride = S.rec_width;
+            d.data = base + S.rec_key_off[c];
+            d.validity = t.nullable ? base + S.rec_val_off[c] : nullptr;
+            d.strings = strs;
+        }
+        RETURN_IF(upload_batch(h, st, bid));
+        u64 blocks = std::min<u64>(2048, (n + 4095) / 4096) + 1;
+        RETURN_IF(ensure_ovf(h, n, blocks * 4096));
+        prof::Scope ps("agg_merge", h->stream);
+        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, n, true, table_desc(h), true);
+        HIPCHECK(hipGetLastError());
+    }
+    return DBG_OK;
+}
+
+// ---- standalone filter ----
+int dbg_filter_select(const dbg_filter* filter, uint64_t rows, uint32_t* sel_out, uint64_t* n_sel, void* stream) {
+    if (!filter || !sel_out || !n_sel) return fail(DBG_ERR_INVALID, "null argument");
+    if (rows >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "selection indices are u32");
+    hipStream_t s = (hipStream_t)stream;
+    dbg_agg_handle tmp;  // for owned constant copies
+    tmp.stream = s;
+    FilterDesc fd;
+    memset(&fd, 0, sizeof(fd));
+    fd.rows = rows;
+    RETURN_IF(fill_filter(&tmp, filter, 1, fd.cols, &fd.n_cols, fd.nodes, &fd.n_nodes));
+    FilterDesc* dfd = nullptr;
+    u64* scratch = nullptr;
+    u64 nb = filter_blocks(rows);
+    int rc = dev_alloc((void**)&dfd, sizeof(FilterDesc));
+    if (rc == DBG_OK) rc = dev_alloc((void**)&scratch, (nb + 2) * 8);
+    if (rc == DBG_OK) {
+        hipMemcpyAsync(dfd, &fd, sizeof(fd), hipMemcpyHostToDevice, s);
+        {
+            prof::Scope ps("filter_select", s);
+            launch_filter_select(s, dfd, rows, scratch, scratch + nb, sel_out);
+        }
+        u64 tot = 0;
+        if (nb) hipMemcpyAsync(&tot, scratch + nb, 8, hipMemcpyDeviceToHost, s);
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = fail(DBG_ERR_DEVICE, std::string("filter: ") + hipGetErrorString(e));
+        *n_sel = tot;
+    }
+    if (dfd) hipFree(dfd);
+    if (scratch) hipFree(scratch);
+    for (auto& b : tmp.owned) hipFree(b.p);
+    tmp.owned.clear();
+    tmp.stream = nullptr;
+    return rc;
+}
+
+int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, void* out_data, uint8_t* out_validity, void* stream) {
+    if (!col || !sel || !out_data) return fail(DBG_ERR_INVALID, "null argument");
+    if (col->dt.type == DBG_STRING) return fail(DBG_ERR_UNSUPPORTED, "dbg_take_fixed: fixed-width columns only");
+    hipStream_t s = (hipStream_t)stream;
+    DCol d;
+    memset(&d, 0, sizeof(d));
+    d.type = col->dt.type;
+    d.nullable = col->dt.nullable;
+    d.width = type_width(col->dt.type);
+    d.stride = d.width;
+    d.data = (const u8*)col->data;
+    d.validity = col->validity;
+    d.validity_offset = col->validity_offset;
+    d.data_offset = col->data_offset;
+    u8* vbytes = nullptr;
+    if (out_validity && col->dt.nullable) RETURN_IF(dev_alloc((void**)&vbytes, n_sel + 1));
+    launch_take_fixed(s, d, sel, n_sel, (u8*)out_data, vbytes);
+    if (vbytes) launch_pack_bits(s, vbytes, n_sel, out_validity);
+    HIPCHECK(hipStreamSynchronize(s));
+    if (vbytes) hipFree(vbytes);
+    return DBG_OK;
+}
+
+// ---- profiling ----
+int dbg_prof_enable(int on) {
+    std::lock_guard<std::mutex> g(prof::mu);
+    prof::enabled = on != 0;
+    return DBG_OK;
+}
+int dbg_prof_reset(void) {
+    std::lock_guard<std::mutex> g(prof::mu);
+    prof::resolve_locked();
+    prof::totals.clear();
+    return DBG_OK;
+}
+int dbg_prof_get(int i, const char** name, double* total_ms, uint64_t* launches) {
+    std::lock_guard<std::mutex> g(prof::mu);
+    prof::resolve_locked();
+    if (i < 0 || (size_t)i >= prof::totals.size()) return DBG_ERR_INVALID;
+    *name = prof::totals[i].first.c_str();
+    *total_ms = prof::totals[i].second.first;
+    *launches = prof::totals[i].second.second;
+    return DBG_OK;
+}
+
+// ---- workload generator ----
+int dbg_datagen(int cfg, uint64_t seed, uint64_t row_start, uint64_t rows, void** outs, int n_outs, const uint64_t* aux,
+                void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (launch_datagen(s, cfg, seed, row_start, rows, outs, n_outs, aux) != 0) return fail(DBG_ERR_INVALID, "bad datagen config");
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+}  // extern "C"

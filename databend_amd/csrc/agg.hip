@@ -1,0 +1,891 @@
+// agg.hip — gfx950 kernels of the hash GROUP BY path.
+//
+//   table_init      : slots <- EMPTY entry + per-function initial state words
+//   agg_insert      : fused  predicate -> group hash -> LDS-staged partial table -> HBM table
+//                     (TransformFilter + AggregateHashTable::add_groups / combine_payload,
+//                      EAGG/aggregate_hashtable.rs:128-425)
+//   agg_retry       : deferred overflow rows / partial records after the table has grown
+//   agg_rehash      : grow the HBM table (AggregateHashTable::resize, :511-561)
+//   count / write   : merge_result + flush_column into output columns (:427-451, payload_flush.rs)
+//   export          : partial-state records partitioned by hash % n or radix bits
+//                     (Payload::scatter, payload.rs:356-391; PartitionedPayload, partitioned_payload.rs)
+//
+// Bandwidth/atomic-bound integer work: no MFMA.  Every kernel is grid-strided over >= 2048
+// workgroups of 256 threads (64-wide waves) or over contiguous row ranges per workgroup.
+#include "agg.hpp"
+
+#define BLOCK 256
+#define SLOTS_PER_THREAD 8
+#define SLOTS_PER_BLOCK (BLOCK * SLOTS_PER_THREAD)
+#define LDS_BUDGET_BYTES (32 * 1024)
+#define LDS_PROBE_CAP 64
+
+// Slot placement for inline keys: any good mixer works (placement is not observable); the
+// reference hash is recomputed from the key wherever routing needs it.
+__device__ __forceinline__ u64 slot_mix(u64 x) { return hash_prim(x ^ 0x9E3779B97F4A7C15ULL); }
+
+// ------------------------------------------------------------------------------------------
+// Key packing (inline mode): the row format of EAGG/payload.rs:100-129 in <= 8 bytes.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ u64 width_mask(u32 w) { return w >= 8 ? ~0ULL : ((1ULL << (8 * w)) - 1); }
+
+__device__ __forceinline__ u64 pack_key(const Spec& S, const DCol* keys, u64 i) {
+    u64 k = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const DCol& col = keys[c];
+        bool v = dcol_valid(col, i);
+        if (col.nullable) k |= (u64)(v ? 1 : 0) << (8 * S.voff[c]);
+        if (v) {
+            u64 b = dcol_bits(col, i);
+            if (col.type == DBG_FLOAT32 || col.type == DBG_FLOAT64) b = canon_float_bits(col.type, b);
+            k |= (b & width_mask(type_width(col.type))) << (8 * S.koff[c]);
+        }
+    }
+    return k;
+}
+
+// AggHash of a cell from its raw bits (inline keys / records).
+__device__ __forceinline__ u64 hash_bits(int type, u64 b) {
+    switch (type) {
+        case DBG_BOOLEAN: return b & 1;
+        case DBG_FLOAT32: case DBG_FLOAT64: return hash_prim(canon_float_bits(type, b));
+        case DBG_INT8: return hash_prim((u64)(i64)(int8_t)b);
+        case DBG_INT16: return hash_prim((u64)(i64)(int16_t)b);
+        case DBG_INT32: case DBG_DATE: return hash_prim((u64)(i64)(int32_t)b);
+        default: return hash_prim(b);
+    }
+}
+
+__device__ __forceinline__ u64 hash_packed(const Spec& S, u64 key) {
+    u64 h = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        bool v = t.nullable ? ((key >> (8 * S.voff[c])) & 0xff) != 0 : true;
+        u64 b = (key >> (8 * S.koff[c])) & width_mask(type_width(t.type));
+        u64 x = v ? hash_bits(t.type, b) : NULL_HASH_VAL;
+        h = c == 0 ? x : (h * NULL_HASH_VAL) ^ x;
+    }
+    return h;
+}
+
+__device__ __forceinline__ u32 ref_bid(u64 e) { return (u32)((e >> 32) & 0xFFFF); }
+__device__ __forceinline__ u32 ref_row(u64 e) { return (u32)e; }
+
+__device__ __forceinline__ bool ref_equal(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 e) {
+    const DCol* other = batches[ref_bid(e)].keys;
+    u64 j = ref_row(e);
+    for (int c = 0; c < S.n_keys; ++c)
+        if (!cell_equal(keys[c], i, other[c], j)) return false;
+    return true;
+}
+
+// Reference group hash of the group an entry stands for.
+__device__ __forceinline__ u64 entry_hash(const Spec& S, const BatchDesc* batches, u64 e, bool is_sentinel) {
+    if (S.inline_keys) return hash_packed(S, is_sentinel ? SLOT_EMPTY : e);
+    return group_hash(batches[ref_bid(e)].keys, S.n_keys, ref_row(e));
+}
+
+// ------------------------------------------------------------------------------------------
+// State updates (LDS or HBM — the same code, address space inferred after inlining)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void add128(u64* p, u64 lo, u64 hi) {
+    u64 old = atomicAdd((unsigned long long*)p, (unsigned long long)lo);
+    u64 carry = (old + lo) < old ? 1ULL : 0ULL;
+    u64 h = hi + carry;
+    if (h) atomicAdd((unsigned long long*)(p + 1), (unsigned long long)h);
+}
+
+__device__ __forceinline__ void set_flag(u64* st, int fw, int bit) {
+    u64 m = 1ULL << bit;
+    if (!(st[fw] & m)) atomicOr((unsigned long long*)(st + fw), (unsigned long long)m);
+}
+
+// accumulate_keys of every aggregate for input row i into the slot at st (word 0 = entry).
+__device__ __forceinline__ void apply_row(const Spec& S, u64* st, const BatchDesc& B, u64 i) {
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        const DCol& c = B.args[a];
+        if (A.arg_type >= 0 && A.arg_nullable && !dcol_valid(c, i)) continue;
+        u64* w = st + A.w0;
+        switch (A.kind) {
+            case DBG_AGG_COUNT: atomicAdd((unsigned long long*)w, 1ULL); break;
+            case DBG_AGG_SUM: case DBG_AGG_AVG: {
+                if (A.sumk == SUMK_I64) atomicAdd((unsigned long long*)w, (unsigned long long)dcol_i64(c, i));
+                else if (A.sumk == SUMK_F64) atomicAdd((double*)w, dcol_f64(c, i));
+                else add128(w, dcol_bits(c, i), dcol_hi(c, i));
+                if (A.kind == DBG_AGG_AVG) atomicAdd((unsigned long long*)(w + (A.sumk == SUMK_I128 ? 2 : 1)), 1ULL);
+                break;
+            }
+            case DBG_AGG_MIN: case DBG_AGG_MAX: {
+                bool mn = A.kind == DBG_AGG_MIN;
+                if (A.mmk == MMK_I64) {
+                    long long x = (long long)dcol_i64(c, i);
+                    if (mn) atomicMin((long long*)w, x); else atomicMax((long long*)w, x);
+                } else {
+                    unsigned long long x = A.mmk == MMK_U64 ? (unsigned long long)dcol_bits(c, i)
+                                                            : (unsigned long long)f64_order_key(dcol_f64(c, i));
+                    if (mn) atomicMin((unsigned long long*)w, x); else atomicMax((unsigned long long*)w, x);
+                }
+                break;
+            }
+        }
+        if (A.flag_bit >= 0) set_flag(st, S.flags_word, A.flag_bit);
+    }
+}
+
+// merge_states of a partial state (word array r, same layout) into st.
+__device__ __forceinline__ void apply_state(const Spec& S, u64* st, const u64* r) {
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        u64* w = st + A.w0;
+        const u64* x = r + A.w0;
+        switch (A.kind) {
+            case DBG_AGG_COUNT: if (x[0]) atomicAdd((unsigned long long*)w, (unsigned long long)x[0]); break;
+            case DBG_AGG_SUM: case DBG_AGG_AVG: {
+                if (A.sumk == SUMK_I64) { if (x[0]) atomicAdd((unsigned long long*)w, (unsigned long long)x[0]); }
+                else if (A.sumk == SUMK_F64) atomicAdd((double*)w, __longlong_as_double((long long)x[0]));
+                else add128(w, x[0], x[1]);
+                if (A.kind == DBG_AGG_AVG) {
+                    int k = A.sumk == SUMK_I128 ? 2 : 1;
+                    if (x[k]) atomicAdd((unsigned long long*)(w + k), (unsigned long long)x[k]);
+                }
+                break;
+            }
+            case DBG_AGG_MIN:
+                if (A.mmk == MMK_I64) atomicMin((long long*)w, (long long)x[0]);
+                else atomicMin((unsigned long long*)w, (unsigned long long)x[0]);
+                break;
+            case DBG_AGG_MAX:
+                if (A.mmk == MMK_I64) atomicMax((long long*)w, (long long)x[0]);
+                else atomicMax((unsigned long long*)w, (unsigned long long)x[0]);
+                break;
+        }
+    }
+    if (S.flags_word >= 0 && r[S.flags_word]) atomicOr((unsigned long long*)(st + S.flags_word), (unsigned long long)r[S.flags_word]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Probing
+// ------------------------------------------------------------------------------------------
+// Find or claim the HBM slot of `key` (inline: packed key; ref: salt|bid|row entry).
+// Returns the slot index or ~0 when the probe limit is hit (the caller records an overflow).
+template <bool INLINE>
+__device__ __forceinline__ u64 g_find(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 key,
+                                      u64 h, const TableDesc& t, u32 probe_limit, bool& claimed) {
+    claimed = false;
+    if (INLINE && key == SLOT_EMPTY) {  // only possible for 8-byte packed keys: sentinel slot
+        u64* e = t.slots + t.cap * t.stride_words;
+        u64 old = atomicCAS((unsigned long long*)e, SLOT_EMPTY, 0ULL);
+        claimed = old == SLOT_EMPTY;
+        return t.cap;
+    }
+    u64 mask = t.cap - 1;
+    u64 s = (INLINE ? slot_mix(key) : (h >> 16)) & mask;
+    for (u32 p = 0; p < probe_limit; ++p) {
+        u64* e = t.slots + s * t.stride_words;
+        u64 ev = *(volatile u64*)e;
+        if (ev == SLOT_EMPTY) {
+            u64 old = atomicCAS((unsigned long long*)e, SLOT_EMPTY, (unsigned long long)key);
+            if (old == SLOT_EMPTY) {
+                claimed = true;
+                return s;
+            }
+            ev = old;
+        }
+        if (INLINE) {
+            if (ev == key) return s;
+        } else if ((ev >> 48) == (key >> 48) && ref_equal(S, batches, keys, i, ev)) {
+            return s;
+        }
+        s = (s + 1) & mask;
+    }
+    return ~0ULL;
+}
+
+// Same against a table whose entries were claimed from a record/ovf entry that carries a
+// foreign key (ref of another batch): compare through the batch table.
+template <bool INLINE>
+__device__ __forceinline__ u64 g_find_entry(const Spec& S, const BatchDesc* batches, u64 key, u64 h,
+                                            const TableDesc& t, u32 probe_limit, bool& claimed) {
+    const DCol* keys = INLINE ? nullptr : batches[ref_bid(key)].keys;
+    return g_find<INLINE>(S, batches, keys, INLINE ? 0 : ref_row(key), key, h, t, probe_limit, claimed);
+}
+
+// LDS partial table: same probing, bounded occupancy; -1 = not staged (use HBM directly).
+template <bool INLINE>
+__device__ __forceinline__ int lds_find(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 key, u64 h,
+                                        u64* lds, u32 lmask, u32 sw, u32* lcount, u32 llimit) {
+    if (INLINE && key == SLOT_EMPTY) return -1;
+    u32 s = (u32)((INLINE ? slot_mix(key) : (h >> 16)) & lmask);
+    for (int p = 0; p < LDS_PROBE_CAP; ++p) {
+        u64* e = lds + (u64)s * sw;
+        u64 ev = *(volatile u64*)e;
+        if (ev == SLOT_EMPTY) {
+            if (*(volatile u32*)lcount >= llimit) return -1;
+            u64 old = atomicCAS((unsigned long long*)e, SLOT_EMPTY, (unsigned long long)key);
+            if (old == SLOT_EMPTY) {
+                atomicAdd(lcount, 1u);
+                return (int)s;
+            }
+            ev = old;
+        }
+        if (INLINE) {
+            if (ev == key) return (int)s;
+        } else if ((ev >> 48) == (key >> 48) && ref_equal(S, batches, keys, i, ev)) {
+            return (int)s;
+        }
+        s = (s + 1) & lmask;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void push_ovf_row(const TableDesc& t, u32 bid, u64 row) {
+    u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_ROWS), 1ULL);
+    if (k < t.ovf_rows_cap) t.ovf_rows[k] = ((u64)bid << 32) | row;
+    else atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+}
+__device__ __forceinline__ void push_ovf_rec(const Spec& S, const TableDesc& t, u64 key, const u64* words) {
+    u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), 1ULL);
+    if (k >= t.ovf_recs_cap) {
+        atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+        return;
+    }
+    u64* r = t.ovf_recs + k * t.stride_words;
+    r[0] = key;
+    for (int w = 1; w <= S.n_words; ++w) r[w] = words[w];
+}
+
+// ------------------------------------------------------------------------------------------
+// table_init
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restrict__ spec, u64* slots, u64 n_slots) {
+    const Spec& S = *spec;
+    u64 sw = S.stride_words;
+    for (u64 s = blockIdx.x * (u64)BLOCK + threadIdx.x; s < n_slots; s += (u64)gridDim.x * BLOCK) {
+        u64* p = slots + s * sw;
+        p[0] = SLOT_EMPTY;
+        for (u64 w = 1; w < sw; ++w) p[w] = 0;
+        for (int a = 0; a < S.n_aggs; ++a)
+            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+    }
+}
+
+void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap) {
+    u64 n = cap + 1;
+    u64 blocks = (n + BLOCK - 1) / BLOCK;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(table_init_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, slots, n);
+}
+
+// ------------------------------------------------------------------------------------------
+// agg_insert: one workgroup = one contiguous row range; LDS partial table, HBM fallback.
+// ------------------------------------------------------------------------------------------
+template <bool INLINE, bool RECORDS>
+__global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                          u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
+                                                          u32 lds_slots) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    const u32 sw = S.stride_words;
+    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);  // [0] lds claims, [1] hbm claims
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+
+    // init the LDS partial table
+    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+        u64* p = lds + (u64)s * sw;
+        p[0] = SLOT_EMPTY;
+        for (u32 w = 1; w < sw; ++w) p[w] = 0;
+        for (int a = 0; a < S.n_aggs; ++a)
+            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+    }
+    if (threadIdx.x == 0) {
+        lcount[0] = 0;
+        lcount[1] = 0;
+    }
+    __syncthreads();
+
+    u64 r0 = (u64)blockIdx.x * rows_per_block;
+    u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    u32 my_claims = 0;
+    for (u64 i = r0 + threadIdx.x; i < r1; i += BLOCK) {
+        if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+        u64 h, key;
+        if (RECORDS) {
+            h = *(const u64*)(B.rec_base + i * (u64)B.rec_width);
+        } else if (INLINE) {
+            h = 0;
+        } else {
+            h = group_hash(B.keys, S.n_keys, i);
+        }
+        if (INLINE) key = pack_key(S, B.keys, i);
+        else key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+
+        int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
+        u64* st;
+        if (ls >= 0) {
+            st = lds + (u64)ls * sw;
+        } else {
+            bool claimed;
+            u64 gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, t.probe_limit, claimed);
+            if (gs == ~0ULL) {
+                push_ovf_row(t, bid, i);
+                continue;
+            }
+            my_claims += claimed ? 1 : 0;
+            st = t.slots + gs * t.stride_words;
+        }
+        if (RECORDS) apply_state(S, st, (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1);
+        else apply_row(S, st, B, i);
+    }
+    __syncthreads();
+
+    // flush the LDS partial table into HBM (combine of the block's partial states)
+    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+        u64* p = lds + (u64)s * sw;
+        u64 e = p[0];
+        if (e == SLOT_EMPTY) continue;
+        u64 h = INLINE ? 0 : (RECORDS ? *(const u64*)(B.rec_base + (u64)ref_row(e) * B.rec_width) : group_hash(B.keys, S.n_keys, ref_row(e)));
+        bool claimed;
+        u64 gs = g_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_rec(S, t, e, p);
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_state(S, t.slots + gs * t.stride_words, p);
+    }
+    if (my_claims) atomicAdd(&lcount[1], my_claims);
+    __syncthreads();
+    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+}
+
+static u32 lds_slots_for(const Spec& S) {
+    u32 bytes_per = (u32)S.stride_words * 8;
+    u32 n = 1;
+    while ((n * 2) * bytes_per + 16 <= LDS_BUDGET_BYTES) n *= 2;
+    return n;
+}
+
+void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, u32 bid, u64 rows, bool records,
+                   const TableDesc& t, bool use_lds) {
+    if (rows == 0) return;
+    u32 lslots = use_lds ? lds_slots_for(S) : 1;
+    // enough workgroups to fill 256 CUs several times over, each a contiguous row range
+    u64 min_rows_per_block = (u64)BLOCK * 16;
+    u64 blocks = (rows + min_rows_per_block - 1) / min_rows_per_block;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    u64 rpb = (rows + blocks - 1) / blocks;
+    blocks = (rows + rpb - 1) / rpb;
+    size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
+    if (S.inline_keys) {
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+    } else {
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Deferred overflow: rows (bid,row) and partial records [entry][words] re-inserted after growth.
+// ------------------------------------------------------------------------------------------
+template <bool INLINE>
+__global__ void __launch_bounds__(BLOCK) agg_retry_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                         TableDesc t, u64 n_rows, u64 n_recs, const u64* rows_list,
+                                                         const u64* recs_list) {
+    const Spec& S = *spec;
+    u64 total = n_rows + n_recs;
+    for (u64 k = blockIdx.x * (u64)BLOCK + threadIdx.x; k < total; k += (u64)gridDim.x * BLOCK) {
+        bool claimed;
+        u64 gs;
+        if (k < n_rows) {
+            u64 it = rows_list[k];
+            u32 bid = (u32)(it >> 32);
+            u64 i = (u32)it;
+            const BatchDesc& B = batches[bid];
+            u64 h, key;
+            if (B.is_records) h = *(const u64*)(B.rec_base + i * (u64)B.rec_width);
+            else h = INLINE ? 0 : group_hash(B.keys, S.n_keys, i);
+            key = INLINE ? pack_key(S, B.keys, i) : ((h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i);
+            gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, (u32)(t.cap < 0xFFFFFFFFull ? t.cap : 0xFFFFFFFFull), claimed);
+            if (gs == ~0ULL) {
+                atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+                continue;
+            }
+            u64* st = t.slots + gs * t.stride_words;
+            if (B.is_records) apply_state(S, st, (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1);
+            else apply_row(S, st, B, i);
+        } else {
+            const u64* r = recs_list + (k - n_rows) * t.stride_words;
+            u64 key = r[0];
+            u64 h = 0;
+            if (!INLINE) {
+                const BatchDesc& B = batches[ref_bid(key)];
+                h = B.is_records ? *(const u64*)(B.rec_base + (u64)ref_row(key) * B.rec_width) : group_hash(B.keys, S.n_keys, ref_row(key));
+            }
+            gs = g_find_entry<INLINE>(S, batches, key, h, t, (u32)(t.cap < 0xFFFFFFFFull ? t.cap : 0xFFFFFFFFull), claimed);
+            if (gs == ~0ULL) {
+                atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+                continue;
+            }
+            apply_state(S, t.slots + gs * t.stride_words, r);
+        }
+        if (claimed) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), 1ULL);
+    }
+}
+
+void launch_retry(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t, u64 n_rows,
+                  u64 n_recs, const u64* rows_list, const u64* recs_list) {
+    u64 total = n_rows + n_recs;
+    if (!total) return;
+    u64 blocks = (total + BLOCK - 1) / BLOCK;
+    if (blocks > 4096) blocks = 4096;
+    if (S.inline_keys)
+        hipLaunchKernelGGL(agg_retry_kernel<true>, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, batches, t, n_rows, n_recs, rows_list, recs_list);
+    else
+        hipLaunchKernelGGL(agg_retry_kernel<false>, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, batches, t, n_rows, n_recs, rows_list, recs_list);
+}
+
+// ------------------------------------------------------------------------------------------
+// Rehash into a larger table (groups are distinct: claim the first empty slot, copy the words).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) agg_rehash_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                          const u64* old_slots, u64 old_cap, TableDesc t) {
+    const Spec& S = *spec;
+    u64 sw = t.stride_words;
+    u64 mask = t.cap - 1;
+    for (u64 s = blockIdx.x * (u64)BLOCK + threadIdx.x; s <= old_cap; s += (u64)gridDim.x * BLOCK) {
+        const u64* o = old_slots + s * sw;
+        u64 e = o[0];
+        if (e == SLOT_EMPTY) continue;
+        u64 ns;
+        if (s == old_cap) {
+            ns = t.cap;  // sentinel slot
+        } else {
+            u64 h = S.inline_keys ? 0 : entry_hash(S, batches, e, false);
+            ns = (S.inline_keys ? slot_mix(e) : (h >> 16)) & mask;
+            for (;;) {
+                u64 old = atomicCAS((unsigned long long*)(t.slots + ns * sw), SLOT_EMPTY, (unsigned long long)e);
+                if (old == SLOT_EMPTY) break;
+                ns = (ns + 1) & mask;
+            }
+        }
+        u64* d = t.slots + ns * sw;
+        if (s == old_cap) d[0] = e;
+        for (u64 w = 1; w < sw; ++w) d[w] = o[w];
+    }
+}
+
+void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const u64* old_slots, u64 old_cap,
+                   const TableDesc& t) {
+    u64 blocks = (old_cap + 1 + BLOCK - 1) / BLOCK;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(agg_rehash_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, batches, old_slots, old_cap, t);
+}
+
+// ------------------------------------------------------------------------------------------
+// Finalize / partition: per-block histograms over slot ranges.
+// ------------------------------------------------------------------------------------------
+u64 finalize_blocks(u64 cap) { return (cap + 1 + SLOTS_PER_BLOCK - 1) / SLOTS_PER_BLOCK; }
+
+__device__ __forceinline__ u32 part_of(u64 h, u32 n_parts, int scheme) {
+    if (n_parts <= 1) return 0;
+    if (scheme == 0) return (u32)(h % n_parts);  // Payload::scatter: hash % n (payload.rs:383)
+    u32 rb = 31 - __clz(n_parts);                // radix bits [48 - r, 48) (partitioned_payload.rs:121)
+    return (u32)((h >> (48 - rb)) & (n_parts - 1));
+}
+
+__device__ __forceinline__ u64 key_str_len(const Spec& S, const BatchDesc* batches, u64 e, int c) {
+    StrRef r = dcol_str(batches[ref_bid(e)].keys[c], ref_row(e));
+    return r.len;
+}
+
+#define MAX_PARTS_LDS 256
+
+__global__ void __launch_bounds__(BLOCK) count_groups_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                            TableDesc t, u32 n_parts, int scheme, u64* hist, u64* str_hist,
+                                                            u64 nblocks) {
+    const Spec& S = *spec;
+    __shared__ unsigned long long lh[MAX_PARTS_LDS];
+    __shared__ unsigned long long ls[DBG_MAX_KEYS][MAX_PARTS_LDS];
+    for (u32 p = threadIdx.x; p < n_parts; p += BLOCK) lh[p] = 0;
+    for (u32 p = threadIdx.x; p < DBG_MAX_KEYS * MAX_PARTS_LDS; p += BLOCK) ls[p / MAX_PARTS_LDS][p % MAX_PARTS_LDS] = 0;
+    __syncthreads();
+    u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK;
+    for (u32 k = threadIdx.x; k < SLOTS_PER_BLOCK; k += BLOCK) {
+        u64 s = base + k;
+        if (s > t.cap) break;
+        u64 e = t.slots[s * t.stride_words];
+        if (e == SLOT_EMPTY) continue;
+        u32 p = 0;
+        if (n_parts > 1) p = part_of(entry_hash(S, batches, e, s == t.cap), n_parts, scheme);
+        atomicAdd(&lh[p], 1ULL);
+        if (S.has_strings && !S.inline_keys)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) atomicAdd(&ls[c][p], (unsigned long long)key_str_len(S, batches, e, c));
+    }
+    __syncthreads();
+    for (u32 p = threadIdx.x; p < n_parts; p += BLOCK) {
+        hist[(u64)p * nblocks + blockIdx.x] = lh[p];
+        if (S.has_strings && !S.inline_keys)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) str_hist[((u64)p * S.n_keys + c) * nblocks + blockIdx.x] = ls[c][p];
+    }
+}
+
+void launch_count_groups(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t, u32 n_parts,
+                         int scheme, u64* hist, u64* str_hist) {
+    u64 nb = finalize_blocks(t.cap);
+    hipLaunchKernelGGL(count_groups_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, n_parts, scheme, hist, str_hist, nb);
+}
+
+// Single-workgroup exclusive scan (in place) over n u64; *total = sum.
+__global__ void __launch_bounds__(1024) exclusive_scan_kernel(u64* data, u64 n, u64* total) {
+    __shared__ u64 sums[1024];
+    u64 per = (n + 1023) / 1024;
+    u64 a = threadIdx.x * per, b = a + per < n ? a + per : n;
+    u64 acc = 0;
+    for (u64 k = a; k < b; ++k) acc += data[k];
+    sums[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        u64 v = threadIdx.x >= (u32)off ? sums[threadIdx.x - off] : 0;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    u64 run = threadIdx.x ? sums[threadIdx.x - 1] : 0;
+    for (u64 k = a; k < b; ++k) {
+        u64 v = data[k];
+        data[k] = run;
+        run += v;
+    }
+    if (threadIdx.x == 1023 && total) *total = sums[1023];
+}
+
+void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total) {
+    hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, s, data, n, total);
+}
+
+// ------------------------------------------------------------------------------------------
+// Results (merge_result + flush_column): deterministic order inside a workgroup via block scan.
+// ------------------------------------------------------------------------------------------
+struct U128 {
+    u64 lo, hi;
+};
+__device__ __forceinline__ U128 u128_neg(U128 a) {
+    U128 r;
+    r.lo = ~a.lo + 1;
+    r.hi = ~a.hi + (r.lo == 0 ? 1 : 0);
+    return r;
+}
+// magnitude * 10 with overflow detection (> limit)
+__device__ __forceinline__ bool u128_mul10(U128& a) {
+    u64 lo_hi = __umul64hi(a.lo, 10ULL);
+    u64 lo = a.lo * 10ULL;
+    u64 hi_hi = __umul64hi(a.hi, 10ULL);
+    u64 hi = a.hi * 10ULL;
+    u64 nhi = hi + lo_hi;
+    bool ovf = hi_hi != 0 || nhi < hi;
+    a.lo = lo;
+    a.hi = nhi;
+    return ovf;
+}
+// (a / d) truncating, d > 0
+__device__ __forceinline__ U128 u128_div_u64(U128 a, u64 d) {
+    U128 q{0, 0};
+    q.hi = a.hi / d;
+    u64 r = a.hi % d;
+    u64 lo = 0;
+    for (int b = 63; b >= 0; --b) {
+        u64 top = r >> 63;
+        r = (r << 1) | ((a.lo >> b) & 1);
+        if (top || r >= d) {
+            r -= d;
+            lo |= 1ULL << b;
+        }
+    }
+    q.lo = lo;
+    return q;
+}
+// 10^38 - 1 = 0x4B3B4CA85A86C47A_098A223FFFFFFFFF
+#define DEC38_MAX_HI 0x4B3B4CA85A86C47AULL
+#define DEC38_MAX_LO 0x098A223FFFFFFFFFULL
+__device__ __forceinline__ bool dec38_out_of_range(u64 lo, u64 hi) {
+    U128 m{lo, hi};
+    if ((i64)hi < 0) m = u128_neg(m);
+    if (m.hi != DEC38_MAX_HI) return m.hi > DEC38_MAX_HI;
+    return m.lo > DEC38_MAX_LO;
+}
+
+__device__ __forceinline__ void write_bytes(void* dst, u64 pos, u32 w, u64 lo, u64 hi) {
+    u8* p = (u8*)dst + pos * w;
+    switch (w) {
+        case 1: *p = (u8)lo; break;
+        case 2: *(uint16_t*)p = (uint16_t)lo; break;
+        case 4: *(u32*)p = (u32)lo; break;
+        case 8: *(u64*)p = lo; break;
+        default: ((u64*)p)[0] = lo; ((u64*)p)[1] = hi; break;
+    }
+}
+
+// Result value of aggregate A from its state words; returns validity.
+__device__ __forceinline__ bool agg_result(const Spec& S, const DAgg& A, const u64* st, u64& lo, u64& hi, u64* err) {
+    const u64* w = st + A.w0;
+    bool valid = true;
+    if (A.res_nullable) {
+        if (A.kind == DBG_AGG_AVG) valid = w[A.sumk == SUMK_I128 ? 2 : 1] != 0;
+        else if (A.flag_bit >= 0) valid = (st[S.flags_word] >> A.flag_bit) & 1;
+    }
+    hi = 0;
+    switch (A.kind) {
+        case DBG_AGG_COUNT: lo = w[0]; break;
+        case DBG_AGG_SUM:
+            lo = w[0];
+            if (A.sumk == SUMK_I128) {
+                hi = w[1];
+                if (valid && A.dec_check && dec38_out_of_range(lo, hi)) atomicOr((unsigned long long*)err, (unsigned long long)ERR_DEC_OVERFLOW);
+            }
+            if (!valid) lo = hi = 0;
+            break;
+        case DBG_AGG_AVG: {
+            u64 cnt = w[A.sumk == SUMK_I128 ? 2 : 1];
+            if (!valid || cnt == 0) {
+                lo = hi = 0;
+                break;
+            }
+            if (A.sumk == SUMK_I128) {
+                U128 m{w[0], w[1]};
+                bool neg = (i64)w[1] < 0;
+                if (neg) m = u128_neg(m);
+                bool ovf = false;
+                for (int k = 0; k < A.scale_add; ++k) ovf |= u128_mul10(m);
+                // checked_mul fits i128 iff magnitude <= 2^127 - 1 (+1 when negative)
+                if (m.hi >> 63) ovf |= !(neg && m.hi == 0x8000000000000000ULL && m.lo == 0);
+                if (ovf) atomicOr((unsigned long long*)err, (unsigned long long)ERR_DEC_OVERFLOW);
+                U128 q = u128_div_u64(m, cnt);
+                if (neg) q = u128_neg(q);
+                lo = q.lo;
+                hi = q.hi;
+            } else {
+                double sum;
+                if (A.sumk == SUMK_F64) sum = __longlong_as_double((long long)w[0]);
+                else if (A.arg_type == DBG_UINT8 || A.arg_type == DBG_UINT16 || A.arg_type == DBG_UINT32 || A.arg_type == DBG_UINT64)
+                    sum = (double)w[0];
+                else sum = (double)(i64)w[0];
+                double r = sum / (double)cnt;
+                lo = (u64)__double_as_longlong(r);
+            }
+            break;
+        }
+        case DBG_AGG_MIN: case DBG_AGG_MAX: {
+            if (!valid) {
+                lo = hi = 0;
+                break;
+            }
+            u64 v = w[0];
+            if (A.mmk == MMK_F64) {
+                double d = f64_from_order_key(v);
+                if (A.res_type == DBG_FLOAT32) lo = (u64)__float_as_uint((float)d);
+                else lo = (u64)__double_as_longlong(d);
+            } else {
+                lo = v;
+                if (A.res_type == DBG_DECIMAL128) hi = (i64)v < 0 ? ~0ULL : 0ULL;
+            }
+            break;
+        }
+    }
+    return valid;
+}
+
+__global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                             TableDesc t, const u64* pos, const u64* str_pos, u64 nblocks,
+                                                             OutDesc out) {
+    const Spec& S = *spec;
+    __shared__ u64 scan[BLOCK];
+    __shared__ u64 sscan[DBG_MAX_KEYS][BLOCK];
+    u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK + (u64)threadIdx.x * SLOTS_PER_THREAD;
+    bool ref_strings = S.has_strings && !S.inline_keys;
+    // pass 1: per-thread counts (groups, string bytes per key column)
+    u64 cnt = 0;
+    u64 sb[DBG_MAX_KEYS];
+    for (int c = 0; c < DBG_MAX_KEYS; ++c) sb[c] = 0;
+    for (int k = 0; k < SLOTS_PER_THREAD; ++k) {
+        u64 s = base + k;
+        if (s > t.cap) break;
+        u64 e = t.slots[s * t.stride_words];
+        if (e == SLOT_EMPTY) continue;
+        cnt++;
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) sb[c] += key_str_len(S, batches, e, c);
+    }
+    scan[threadIdx.x] = cnt;
+    if (ref_strings)
+        for (int c = 0; c < S.n_keys; ++c) sscan[c][threadIdx.x] = sb[c];
+    __syncthreads();
+    for (int off = 1; off < BLOCK; off <<= 1) {
+        u64 v = threadIdx.x >= (u32)off ? scan[threadIdx.x - off] : 0;
+        u64 vs[DBG_MAX_KEYS];
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c) vs[c] = threadIdx.x >= (u32)off ? sscan[c][threadIdx.x - off] : 0;
+        __syncthreads();
+        scan[threadIdx.x] += v;
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c) sscan[c][threadIdx.x] += vs[c];
+        __syncthreads();
+    }
+    u64 p = pos[blockIdx.x] + scan[threadIdx.x] - cnt;
+    u64 sp[DBG_MAX_KEYS];
+    if (ref_strings)
+        for (int c = 0; c < S.n_keys; ++c)
+            if (S.key_types[c].type == DBG_STRING) sp[c] = str_pos[(u64)c * nblocks + blockIdx.x] + sscan[c][threadIdx.x] - sb[c];
+    // pass 2: write
+    for (int k = 0; k < SLOTS_PER_THREAD; ++k) {
+        u64 s = base + k;
+        if (s > t.cap) break;
+        const u64* st = t.slots + s * t.stride_words;
+        u64 e = st[0];
+        if (e == SLOT_EMPTY) continue;
+        // group columns
+        if (S.inline_keys) {
+            u64 key = s == t.cap ? SLOT_EMPTY : e;
+            for (int c = 0; c < S.n_keys; ++c) {
+                const dbg_datatype& ty = S.key_types[c];
+                u32 w = type_width(ty.type);
+                u64 b = (key >> (8 * S.koff[c])) & width_mask(w);
+                bool v = ty.nullable ? ((key >> (8 * S.voff[c])) & 0xff) != 0 : true;
+                write_bytes(out.key_data[c], p, w, b, 0);
+                if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
+            }
+        } else {
+            const BatchDesc& RB = batches[ref_bid(e)];
+            u64 row = ref_row(e);
+            for (int c = 0; c < S.n_keys; ++c) {
+                const DCol& kc = RB.keys[c];
+                bool v = dcol_valid(kc, row);
+                if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
+                if (kc.type == DBG_STRING) {
+                    StrRef r = dcol_str(kc, row);
+                    out.key_offsets[c][p] = sp[c];
+                    u8* d = (u8*)out.key_data[c] + sp[c];
+                    for (u64 j = 0; j < r.len; ++j) d[j] = r.p[j];
+                    sp[c] += r.len;
+                } else {
+                    u32 w = type_width(kc.type);
+                    write_bytes(out.key_data[c], p, w, dcol_bits(kc, row), w == 16 ? dcol_hi(kc, row) : 0);
+                }
+            }
+        }
+        for (int a = 0; a < S.n_aggs; ++a) {
+            const DAgg& A = S.aggs[a];
+            u64 lo, hi;
+            bool v = agg_result(S, A, st, lo, hi, t.counters + CNT_ERR);
+            write_bytes(out.agg_data[a], p, A.res_width, lo, hi);
+            if (out.agg_valid[a]) out.agg_valid[a][p] = v ? 1 : 0;
+        }
+        p++;
+    }
+}
+
+void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t,
+                          const u64* pos, const u64* str_pos, const OutDesc& out) {
+    u64 nb = finalize_blocks(t.cap);
+    hipLaunchKernelGGL(write_results_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, pos, str_pos, nb, out);
+}
+
+__global__ void pack_bits_kernel(const u8* bytes, u64 n, u8* bits) {
+    u64 nb = (n + 7) / 8;
+    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) {
+        u8 b = 0;
+        for (int j = 0; j < 8; ++j) {
+            u64 i = k * 8 + j;
+            if (i < n && bytes[i]) b |= (u8)(1u << j);
+        }
+        bits[k] = b;
+    }
+}
+
+void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits) {
+    u64 nb = (n + 7) / 8;
+    u64 blocks = (nb + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (!blocks) return;
+    hipLaunchKernelGGL(pack_bits_kernel, dim3((u32)blocks), dim3(256), 0, s, bytes, n, bits);
+}
+
+// ------------------------------------------------------------------------------------------
+// Export partial-state records: [hash][key part][state words], partition-major.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) export_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                      TableDesc t, u32 n_parts, int scheme, const u64* pos, const u64* str_pos,
+                                                      u64 nblocks, u8* rec_out, u8* str_out, const u64* part_str_base) {
+    const Spec& S = *spec;
+    __shared__ unsigned long long cur[MAX_PARTS_LDS];
+    __shared__ unsigned long long scur[DBG_MAX_KEYS][MAX_PARTS_LDS];
+    for (u32 p = threadIdx.x; p < n_parts; p += BLOCK) cur[p] = pos[(u64)p * nblocks + blockIdx.x];
+    bool ref_strings = S.has_strings && !S.inline_keys;
+    if (ref_strings)
+        for (u32 p = threadIdx.x; p < n_parts; p += BLOCK)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) scur[c][p] = str_pos[((u64)p * S.n_keys + c) * nblocks + blockIdx.x];
+    __syncthreads();
+    u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK;
+    for (u32 k = threadIdx.x; k < SLOTS_PER_BLOCK; k += BLOCK) {
+        u64 s = base + k;
+        if (s > t.cap) break;
+        const u64* st = t.slots + s * t.stride_words;
+        u64 e = st[0];
+        if (e == SLOT_EMPTY) continue;
+        u64 h = entry_hash(S, batches, e, s == t.cap);
+        u32 p = part_of(h, n_parts, scheme);
+        u64 r = atomicAdd(&cur[p], 1ULL);
+        u8* rec = rec_out + r * S.rec_width;
+        *(u64*)rec = h;
+        if (S.inline_keys) {
+            u64 key = s == t.cap ? SLOT_EMPTY : e;
+            for (int c = 0; c < S.n_keys; ++c) {
+                const dbg_datatype& ty = S.key_types[c];
+                u32 w = type_width(ty.type);
+                u64 b = (key >> (8 * S.koff[c])) & width_mask(w);
+                if (ty.nullable) rec[S.rec_val_off[c]] = ((key >> (8 * S.voff[c])) & 0xff) != 0;
+                for (u32 j = 0; j < w; ++j) rec[S.rec_key_off[c] + j] = (u8)(b >> (8 * j));
+            }
+        } else {
+            const BatchDesc& RB = batches[ref_bid(e)];
+            u64 row = ref_row(e);
+            for (int c = 0; c < S.n_keys; ++c) {
+                const DCol& kc = RB.keys[c];
+                bool v = dcol_valid(kc, row);
+                if (S.key_types[c].nullable) rec[S.rec_val_off[c]] = v ? 1 : 0;
+                u8* kd = rec + S.rec_key_off[c];
+                if (kc.type == DBG_STRING) {
+                    StrRef sr = dcol_str(kc, row);
+                    u64 o = atomicAdd(&scur[c][p], (unsigned long long)sr.len);
+                    for (u64 j = 0; j < sr.len; ++j) str_out[o + j] = sr.p[j];
+                    ((u64*)kd)[0] = o - part_str_base[p];  // relative to the partition's blob
+                    ((u64*)kd)[1] = sr.len;
+                } else {
+                    u32 w = type_width(kc.type);
+                    u64 lo = dcol_bits(kc, row);
+                    u64 hi = w == 16 ? dcol_hi(kc, row) : 0;
+                    for (u32 j = 0; j < w && j < 8; ++j) kd[j] = (u8)(lo >> (8 * j));
+                    for (u32 j = 8; j < w; ++j) kd[j] = (u8)(hi >> (8 * (j - 8)));
+                }
+            }
+        }
+        u64* sw = (u64*)(rec + S.rec_state_off);
+        for (int w = 1; w <= S.n_words; ++w) sw[w - 1] = st[w];
+    }
+}
+
+void launch_export(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t, u32 n_parts,
+                   int scheme, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out, const u64* part_str_base) {
+    u64 nb = finalize_blocks(t.cap);
+    hipLaunchKernelGGL(export_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, n_parts, scheme, pos, str_pos, nb,
+                       rec_out, str_out, part_str_base);
+}
+

@@ -1,0 +1,86 @@
+// agg.hpp — host/device shared descriptors of the aggregate hash table.
+#pragma once
+#include "device.hpp"
+
+// Slot = [entry u64][state words...], `stride_words` u64 per slot, `cap` slots (power of two) plus
+// one sentinel slot at index cap (inline keys whose packed value equals EMPTY).
+//   inline keys (all group columns fixed-width and packed row-format width <= 8 bytes):
+//     entry = packed key bytes (row format of EAGG/payload.rs:100-129: validity bytes, then values)
+//   ref keys (strings, Decimal128, wide tuples):
+//     entry = salt16 | batch16 | row32 — the reference's Entry (salt | pointer,
+//     EAGG/aggregate_hashtable.rs:591-636) with the pointer aimed at the immutable input row
+#define SLOT_EMPTY 0xFFFFFFFFFFFFFFFFULL
+
+struct Spec {
+    int32_t n_keys;
+    int32_t inline_keys;
+    int32_t inline_width;     // bytes
+    int32_t n_aggs;
+    int32_t n_words;          // state words (without the entry word)
+    int32_t stride_words;     // entry + states, rounded
+    int32_t flags_word;       // -1 or word index (1-based, slot word)
+    int32_t has_strings;
+    uint8_t voff[DBG_MAX_KEYS];  // inline: byte offset of the validity byte
+    uint8_t koff[DBG_MAX_KEYS];  // inline: byte offset of the value
+    dbg_datatype key_types[DBG_MAX_KEYS];
+    // record format (exchange): [hash][key part][state words]
+    uint32_t rec_width;
+    uint32_t rec_key_off[DBG_MAX_KEYS];  // byte offset of the key value in a record
+    uint32_t rec_val_off[DBG_MAX_KEYS];  // byte offset of the validity byte
+    uint32_t rec_state_off;
+    DAgg aggs[DBG_MAX_AGGS];
+};
+
+struct BatchDesc {
+    u64 rows;
+    int32_t n_fcols, n_nodes;
+    int32_t is_records;
+    uint32_t rec_width;
+    const u8* rec_base;
+    DCol keys[DBG_MAX_KEYS];
+    DCol args[DBG_MAX_AGGS];
+    DCol fcols[DBG_MAX_FCOLS];
+    DNode nodes[DBG_MAX_NODES];
+};
+
+struct TableDesc {
+    u64* slots;
+    u64 cap;  // power of two
+    u32 stride_words;
+    u32 probe_limit;
+    u64* counters;  // [0] claims (groups created), [1] overflow rows, [2] overflow records, [3] error bits
+    u64* ovf_rows;  // (bid << 32) | row
+    u64 ovf_rows_cap;
+    u64* ovf_recs;  // [keyref][words...] per record, stride = stride_words
+    u64 ovf_recs_cap;
+};
+
+enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_WORDS = 8 };
+enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2 };
+
+// ---- launch wrappers (agg.hip) ----
+void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap);
+void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
+                   bool records, const TableDesc& t, bool use_lds);
+void launch_retry(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
+                  u64 n_rows, u64 n_recs, const u64* rows_list, const u64* recs_list);
+void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const u64* old_slots,
+                   u64 old_cap, const TableDesc& t);
+// finalize: counts per block of occupied slots (and string bytes per key col); returns blocks used
+u64 finalize_blocks(u64 cap);
+void launch_count_groups(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
+                         u32 n_parts, int scheme, u64* hist /* [n_parts][blocks] */, u64* str_hist /* [n_parts][n_keys][blocks] */);
+void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total);
+struct OutDesc {
+    void* key_data[DBG_MAX_KEYS];
+    u64* key_offsets[DBG_MAX_KEYS];
+    u8* key_valid[DBG_MAX_KEYS];  // bytes (packed later)
+    void* agg_data[DBG_MAX_AGGS];
+    u8* agg_valid[DBG_MAX_AGGS];  // bytes
+};
+void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
+                          const u64* pos /* scanned hist */, const u64* str_pos, const OutDesc& out);
+void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);
+void launch_export(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
+                   u32 n_parts, int scheme, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out,
+                   const u64* part_str_base);

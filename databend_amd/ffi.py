@@ -1,0 +1,113 @@
+"""ctypes binding of the in-tree libdbgpu_agg.so (include/dbgpu_agg.h).
+
+This is the Python analog of the Rust `extern "C"` block a Databend maintainer would add
+(INTEGRATION.md).  The library must be present: there is no CPU fallback in the product path —
+`lib()` raises if the HIP extension was not built (run `python -c "import __graft_entry__ as g; g.build()"`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdbgpu_agg.so")
+_LIB = None
+
+EXPORTED = [
+    "dbg_version", "dbg_last_error", "dbg_device_count", "dbg_agg_result_type", "dbg_agg_create",
+    "dbg_agg_destroy", "dbg_agg_set_stream", "dbg_agg_reset", "dbg_agg_add_groups", "dbg_agg_finalize",
+    "dbg_agg_result", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
+    "dbg_agg_merge_records", "dbg_filter_select", "dbg_take_fixed", "dbg_prof_enable", "dbg_prof_reset",
+    "dbg_prof_get", "dbg_datagen",
+]
+
+
+class DbgError(RuntimeError):
+    """A non-OK status from the C ABI (reference: ErrorCode)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class DecimalOverflow(DbgError):
+    pass
+
+
+class Unsupported(DbgError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: the HIP extension was not built "
+                              "(run __graft_entry__.build()); there is no CPU fallback")
+        # One HIP runtime per process: torch bundles its own libamdhip64/libhsa-runtime64 (same
+        # SONAME as /opt/rocm's).  Loading torch first makes the loader resolve this library's
+        # libamdhip64.so.7 to the already-loaded copy; the other order would bring up a second
+        # HSA runtime that cannot open the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB_PATH)
+        P, U64, I32, VP = C.POINTER, C.c_uint64, C.c_int32, C.c_void_p
+        L.dbg_version.restype = C.c_char_p
+        L.dbg_last_error.restype = C.c_char_p
+        L.dbg_device_count.argtypes = [P(C.c_int)]
+        L.dbg_agg_result_type.argtypes = [P(abi.dbg_agg_spec), P(abi.dbg_datatype)]
+        L.dbg_agg_create.argtypes = [P(abi.dbg_agg_params), P(VP)]
+        L.dbg_agg_destroy.argtypes = [VP]
+        L.dbg_agg_destroy.restype = None
+        L.dbg_agg_set_stream.argtypes = [VP, VP]
+        L.dbg_agg_reset.argtypes = [VP]
+        L.dbg_agg_add_groups.argtypes = [VP, P(abi.dbg_column), P(abi.dbg_column), P(abi.dbg_filter), U64, C.c_int]
+        L.dbg_agg_finalize.argtypes = [VP, P(U64), P(U64)]
+        L.dbg_agg_result.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), C.c_int]
+        L.dbg_agg_record_width.argtypes = [VP, P(C.c_uint32)]
+        L.dbg_agg_partition.argtypes = [VP, C.c_uint32, C.c_int, P(U64), P(U64)]
+        L.dbg_agg_export_records.argtypes = [VP, VP, VP]
+        L.dbg_agg_merge_records.argtypes = [VP, VP, VP, I32, P(U64), P(U64)]
+        L.dbg_filter_select.argtypes = [P(abi.dbg_filter), U64, VP, P(U64), VP]
+        L.dbg_take_fixed.argtypes = [P(abi.dbg_column), VP, U64, VP, VP, VP]
+        L.dbg_prof_enable.argtypes = [C.c_int]
+        L.dbg_prof_get.argtypes = [C.c_int, P(C.c_char_p), P(C.c_double), P(U64)]
+        L.dbg_datagen.argtypes = [C.c_int, U64, U64, U64, P(VP), C.c_int, VP, VP]
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int):
+    if rc == abi.DBG_OK:
+        return
+    msg = lib().dbg_last_error().decode(errors="replace")
+    if rc == abi.DBG_ERR_OVERFLOW:
+        raise DecimalOverflow(rc, msg)
+    if rc == abi.DBG_ERR_UNSUPPORTED:
+        raise Unsupported(rc, msg)
+    raise DbgError(rc, msg)
+
+
+def prof_enable(on: bool = True):
+    check(lib().dbg_prof_enable(1 if on else 0))
+
+
+def prof_reset():
+    check(lib().dbg_prof_reset())
+
+
+def prof_read() -> dict:
+    """{kernel name: (total_ms, launches)} from the in-library HIP event timers."""
+    out = {}
+    i = 0
+    while True:
+        name, ms, n = C.c_char_p(), C.c_double(), C.c_uint64()
+        if lib().dbg_prof_get(i, C.byref(name), C.byref(ms), C.byref(n)) != abi.DBG_OK:
+            break
+        out[name.value.decode()] = (ms.value, n.value)
+        i += 1
+    return out

@@ -20,9 +20,10 @@
  *    distinct handles may be used concurrently.  Each handle owns a HIP stream (or borrows the
  *    caller's, see dbg_agg_set_stream) and its device memory.
  *  - on_device == 0: column pointers are host memory, borrowed for the duration of the call only.
- *    on_device == 1: pointers are device memory on the handle's device and must stay valid and
- *    unmodified until the next synchronising call on the handle (dbg_agg_finalize, dbg_agg_reset,
- *    dbg_agg_partition, dbg_agg_destroy) returns — HIP stream semantics.
+ *    on_device == 1: pointers are device memory on the handle's device; the table refers to key
+ *    rows in place (the reference's Entry points into its payload, here into the input), so these
+ *    buffers must stay valid and unmodified until dbg_agg_reset or dbg_agg_destroy returns.
+ *    Host inputs are copied to device memory owned by the handle for the same lifetime.
  */
 #ifndef DBGPU_AGG_H
 #define DBGPU_AGG_H
@@ -204,15 +205,16 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
 int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width);
 int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t* rec_counts,
                       uint64_t* string_bytes);
-/* Write every partition's records into dev_records (partition p at byte offset
- * rec_offsets[p] * width) and strings into dev_strings (partition p at str_offsets[p]).
- * Device buffers; asynchronous.  Call after dbg_agg_partition with the same n_parts/scheme. */
-int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strings,
-                           const uint64_t* rec_offsets, const uint64_t* str_offsets);
+/* Write every partition's records, partition-major and contiguous, into dev_records
+ * (rec_counts[p] records of `width` bytes for p = 0..n_parts-1) and every partition's string blob
+ * into dev_strings (string_bytes[p] bytes each, same order; record string offsets are relative to
+ * the partition's blob).  Device buffers; asynchronous.  Call after dbg_agg_partition. */
+int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strings);
 /* merge_states of received records into this table (combine_payload,
  * EAGG/aggregate_hashtable.rs:383-425).  The buffers hold n_segments concatenated segments
- * (one per source); seg_records[i] / seg_string_bytes[i] give each segment's size so string
- * offsets are rebased.  Device buffers, retained until the next synchronising call. */
+ * (one per source, each as written by dbg_agg_export_records for one partition);
+ * seg_records[i] / seg_string_bytes[i] give each segment's size.  Device buffers, retained like
+ * on_device inputs (until dbg_agg_reset / dbg_agg_destroy). */
 int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void* dev_strings,
                           int32_t n_segments, const uint64_t* seg_records,
                           const uint64_t* seg_string_bytes);
@@ -234,11 +236,16 @@ int dbg_prof_reset(void);
 int dbg_prof_get(int i, const char** name, double* total_ms, uint64_t* launches);
 
 /* ---- synthetic workload generator (the numbers_mt analog) ----
- * Fills caller-allocated device columns for rows [row_start, row_start+rows) of config cfg
- * (1..5), deterministically from seed (counter-based splitmix64).  Column sets per config are
- * listed in DESIGN.md; C5 needs the phrase CDF table from dbg_datagen_c5_table. */
-int dbg_datagen(int cfg, uint64_t seed, uint64_t row_start, uint64_t rows, dbg_out_column* cols,
-                int n_cols, const uint64_t* aux, void* hip_stream);
+ * Fills caller-allocated device buffers for rows [row_start, row_start+rows) of config cfg,
+ * deterministically from seed (counter-based splitmix64, include/dbgpu_datagen.h).  outs[] per cfg:
+ *   1: shipdate i32, returnflag bytes, linestatus bytes, returnflag offsets u64 (rows+1),
+ *      linestatus offsets, quantity, extprice, discount, tax, disc_price, charge (Decimal128 each)
+ *   2: AdvEngineID i16            3: UserID i64
+ *   4: WatchID i64, ClientIP i32, IsRefresh i16, ResolutionWidth i16
+ *   5: SearchPhrase lengths u64 (pass 1; aux = phrase CDF, 2^23 u64)
+ *   6: SearchPhrase bytes (pass 2; outs = {offsets (rows+1), bytes}; aux = phrase CDF) */
+int dbg_datagen(int cfg, uint64_t seed, uint64_t row_start, uint64_t rows, void** outs, int n_outs,
+                const uint64_t* aux, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,95 @@
+"""CPU checks of the boundary: the C-ABI library loads and exports every symbol the header
+declares, the ctypes structs match the C layout, and the host-side type logic agrees with the
+oracle (no GPU compute is called here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from databend_amd import abi
+from databend_amd import column as col
+from databend_amd.aggregates import AggregateFunctionFactory
+from databend_amd.ffi import EXPORTED, LIB_PATH, lib
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dbgpu_agg.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(dbg_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB_PATH), "run __graft_entry__.build() first"
+    L = lib()
+    declared = header_functions()
+    assert set(declared) == set(EXPORTED), set(declared) ^ set(EXPORTED)
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared:
+        assert re.search(rf"\bT {name}\b", out), name
+        getattr(L, name)
+
+
+def test_struct_layout_matches_header():
+    src = '#include "dbgpu_agg.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){' + "".join(
+        f'printf("{n} %zu\\n", sizeof({n}));' for n in abi.EXPECTED_SIZES) + \
+        'printf("off_len %zu\\n", offsetof(dbg_column, len));printf("off_hint %zu\\n", offsetof(dbg_agg_params, capacity_hint));return 0;}'
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        out = dict(l.split() for l in subprocess.check_output([exe], text=True).splitlines())
+    for n in abi.EXPECTED_SIZES:
+        assert int(out[n]) == C.sizeof(getattr(abi, n)), n
+    assert int(out["off_len"]) == abi.dbg_column.len.offset
+    assert int(out["off_hint"]) == abi.dbg_agg_params.capacity_hint.offset
+
+
+ARG_TYPES = [col.Int8, col.Int16, col.Int32, col.Int64, col.UInt8, col.UInt16, col.UInt32, col.UInt64,
+             col.Float32, col.Float64, col.Decimal128(15, 2), col.Decimal128(38, 6), col.Date, col.Timestamp]
+
+
+@pytest.mark.parametrize("name", ["count", "sum", "avg", "min", "max"])
+@pytest.mark.parametrize("t", ARG_TYPES + [t.wrap_nullable() for t in ARG_TYPES[:4] + ARG_TYPES[9:11]], ids=repr)
+def test_result_types_match_oracle(name, t):
+    """AggregateFunction::return_type() of the GPU path == the restated factory's."""
+    f = AggregateFunctionFactory.instance().get(name, [], [t])
+    spec = f.to_abi()
+    out = abi.dbg_datatype()
+    rc = lib().dbg_agg_result_type(C.byref(spec), C.byref(out))
+    try:
+        exp = oracle.result_type(spec)
+    except oracle.OracleError:
+        assert rc != 0  # both sides reject (e.g. sum(Date))
+        return
+    if rc == abi.DBG_ERR_UNSUPPORTED:
+        # GPU path declines (documented: min/max of Decimal128 precision > 18); caller keeps the CPU path
+        assert name in ("min", "max") and t.type_id == abi.DECIMAL128 and t.precision > 18
+        return
+    assert rc == 0, lib().dbg_last_error()
+    got = col.DataType.from_abi(out)
+    assert got == exp, (got, exp)
+
+
+def test_count_star_is_not_nullable():
+    f = AggregateFunctionFactory.instance().get("count")
+    assert f.name() == "AggregateCountFunction"
+    assert f.return_type() == col.UInt64
+
+
+def test_library_refuses_bad_arguments_without_gpu():
+    L = lib()
+    assert L.dbg_agg_result_type(None, None) == abi.DBG_ERR_INVALID
+    spec = abi.dbg_agg_spec()
+    spec.kind = abi.AGG_SUM
+    spec.arg = abi.dbg_datatype(abi.STRING, 0, 0, 0, 0)
+    out = abi.dbg_datatype()
+    assert L.dbg_agg_result_type(C.byref(spec), C.byref(out)) == abi.DBG_ERR_UNSUPPORTED
+    assert b"sum" in L.dbg_last_error()
