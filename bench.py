@@ -1,0 +1,224 @@
+"""bench.py — the reference's headline metric on MI355X: input rows/s aggregated + % of HBM roofline.
+
+Default workload (BASELINE.json configs[1]): ClickBench Q8-style
+    SELECT AdvEngineID, COUNT(*) FROM hits WHERE AdvEngineID <> 0 GROUP BY AdvEngineID
+over 100M synthetic rows per GPU (AdvEngineID Int16, P(0) = 0.9937).  One step = one pass of the
+hot path over one batch: fresh table -> fused filter + GROUP BY over every row -> (N > 1: partial
+states routed by hash % N over RCCL and merged) -> result columns resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..5] [--rows R]
+
+Multi-GPU: launched by torch.distributed.run, one rank per GPU (backend nccl = RCCL); every rank
+aggregates its own 100M rows (weak scaling), timing = max over ranks, value = all ranks' rows / time.
+Rank 0 prints ONE JSON line.  See DESIGN.md for the roofline accounting.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", type=int, default=2)
+    p.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's size)")
+    p.add_argument("--copies", type=int, default=0, help="rotating input copies (default: enough to defeat the 256 MiB L3)")
+    p.add_argument("--cpu-sample-rows", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--capacity-hint", type=int, default=0)
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, sample_rows, gpu_check=None):
+    """Restated Databend CPU aggregator (oracle/, the reference's algorithm: per-thread partial
+    AggregateHashTable over 65536-row blocks -> partition bucket -> final) on the host's cores,
+    on a bounded sample of the same workload; median of 3 timed runs after 1 warm-up."""
+    from oracle import oracle
+    from databend_amd.workloads import SHAPES, F
+    from databend_amd.filter import FilterProgram, cmp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))  # the GPU box grants 16 CPUs per GPU
+    shape = SHAPES[cfg]
+    cols = oracle.datagen(cfg, sample_rows, threads=threads)
+    keys = [cols[k] for k in shape.keys]
+    aggs = [(F.get(f, [], [cols[c].dtype] if c else []).to_abi(), cols[c] if c else None) for f, c in shape.aggs]
+    prog = None
+    if shape.predicate:
+        name, op, const = shape.predicate
+        prog = FilterProgram(cmp(0, op, const), [cols[name].to_abi()])
+    times = []
+    result = None
+    for it in range(4):
+        t0 = time.perf_counter()
+        result = oracle.aggregate(keys, aggs, filter_program=prog, threads=threads)
+        dt = time.perf_counter() - t0
+        if it:
+            times.append(dt)
+    med = statistics.median(times)
+    return dict(value=sample_rows / med, unit="rows/s", cores=threads, kind="port",
+                sample=f"{sample_rows} rows of the same synthetic workload (rows 0..{sample_rows - 1}), "
+                       f"median of {len(times)} runs after 1 warm-up, {threads} threads",
+                seconds_per_run=med), result, cols
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from databend_amd import ffi
+    from databend_amd.aggregator import AggregateHashTable, HashTableConfig
+    from databend_amd.exchange import exchange_partial
+    from databend_amd.workloads import DEFAULT_ROWS, SHAPES, ConfigRunner, algorithmic_bytes
+
+    cfg = args.config
+    rows = args.rows or DEFAULT_ROWS[cfg]
+    shape = SHAPES[cfg]
+    in_bytes_per_row = {1: 100, 2: 2, 3: 8, 4: 16, 5: 27}[cfg]
+    copies = args.copies or max(1, min(4, -(-768 * 2**20 // max(1, rows * in_bytes_per_row))))
+    if cfg in (3, 4, 5):
+        copies = args.copies or 1
+    # rank r aggregates its own disjoint rows of the synthetic table (weak scaling)
+    # every rank aggregates disjoint row ranges of the same generator
+    runner = ConfigRunner(cfg, rows, copies=copies, capacity_hint=args.capacity_hint, start=rank * copies * rows)
+    final = None
+    if world > 1:
+        final = AggregateHashTable(runner.params, HashTableConfig(False, args.capacity_hint))
+
+    def step(k):
+        if world == 1:
+            return runner.step(k)
+        i = k % len(runner.inputs)
+        t = runner.table
+        t.reset()
+        t.add_groups(runner.key_abi[i], runner.arg_cols[i], rows=rows, filter_program=runner.programs[i], on_device=True)
+        final.reset()
+        exchange_partial(t, final, dev)
+        n, sb = final.finalize()
+        return n
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ffi.prof_reset()
+    ffi.prof_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ffi.prof_enable(False)
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    prof = ffi.prof_read()
+
+    # dominant kernel = the fused filter + GROUP BY insert
+    ins_ms, ins_n = prof.get("agg_insert", (0.0, 0))
+    avg_ms = ins_ms / max(1, ins_n)
+    # algorithmic bytes of one insert launch
+    if world == 1:
+        keys_h, aggs_h = runner.results_host()
+        n_groups = runner.n_groups
+        kstr = runner.key_string_bytes
+    else:
+        n_groups = runner.table.finalize()[0]
+        kstr = 0
+        keys_h, aggs_h = None, None
+    # selected rows: SUM of COUNT(*) over the partial table of this rank
+    sel = None
+    if world == 1:
+        ci = [f for f, _ in shape.aggs].index("count") if ("count", None) in shape.aggs else None
+        if ci is not None:
+            sel = int(sum(aggs_h[ci].values()))
+    if sel is None:
+        blk = runner.table.merge_result()
+        ci = [i for i, (f, c) in enumerate(shape.aggs) if f == "count" and c is None]
+        sel = int(sum(blk.columns[ci[0]].values())) if ci else rows
+    alg_bytes = algorithmic_bytes(cfg, runner.inputs[0], rows, sel, n_groups, runner.result_types, kstr)
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+
+    total_rows = rows * world * args.steps
+    value = total_rows / elapsed
+    out = {
+        "metric": "input rows/sec aggregated (filter + hash GROUP BY), % HBM roofline",
+        "value": value,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int16 key / u64 count" if cfg == 2 else "int64/decimal128/u64",
+        "data": "synthetic (device-generated, seeded splitmix64; SURVEY.md §8d)",
+        "config": {"workload": shape.name, "query": shape.sql, "rows_per_gpu": rows, "input_copies": copies,
+                   "groups": n_groups, "selected_rows": sel, "parallelism": f"dp{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "agg_insert", "kernel_avg_ms": avg_ms, "kernel_launches": ins_n,
+                     "algorithmic_bytes_per_launch": alg_bytes},
+        "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+    }
+    # measured PMC traffic (rocprofv3 --pmc, committed under profiles/) if present for this config
+    tf = os.path.join(ROOT, "profiles", f"pmc_traffic_c{cfg}.json")
+    if os.path.exists(tf):
+        try:
+            t = json.load(open(tf))
+            out["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
+            out["roofline"]["traffic_source"] = os.path.relpath(tf, ROOT)
+        except Exception:
+            pass
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample = args.cpu_sample_rows or {1: 6_001_215, 2: 100_000_000, 3: 20_000_000, 4: 10_000_000, 5: 20_000_000}[cfg]
+        sample = min(sample, rows)
+        cb, cres, _ = cpu_baseline(cfg, sample)
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        out["gpu_vs_cpu"] = value / cb["value"]
+        # parity of this bench's own GPU result against the CPU run when they cover the same rows
+        if sample == rows and keys_h is not None and copies >= 1:
+            try:
+                from tests.parity import assert_results_equal
+                runner.step(0)  # copy 0 == rows [0, rows) == the CPU sample
+                kh, ah = runner.results_host()
+                assert_results_equal(kh, ah, cres[0], cres[1])
+                out["parity_vs_cpu"] = "bit-exact"
+            except AssertionError as e:
+                out["parity_vs_cpu"] = f"MISMATCH: {e}"
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -51,15 +51,28 @@ struct Pending {
 static std::mutex mu;
 static bool enabled = false;
 static std::vector<Pending> pending;
+static std::vector<hipEvent_t> free_events;  // pooled: hipEventCreate is not free
 static std::vector<std::pair<std::string, std::pair<double, uint64_t>>> totals;
+
+static hipEvent_t get_event() {
+    std::lock_guard<std::mutex> g(mu);
+    if (!free_events.empty()) {
+        hipEvent_t e = free_events.back();
+        free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+}
 
 static void resolve_locked() {
     for (auto& p : pending) {
         float ms = 0;
-        hipEventSynchronize(p.b);
-        hipEventElapsedTime(&ms, p.a, p.b);
-        hipEventDestroy(p.a);
-        hipEventDestroy(p.b);
+        (void)hipEventSynchronize(p.b);
+        (void)hipEventElapsedTime(&ms, p.a, p.b);
+        free_events.push_back(p.a);
+        free_events.push_back(p.b);
         bool found = false;
         for (auto& t : totals)
             if (t.first == p.name) {
@@ -80,14 +93,14 @@ struct Scope {
     const char* name;
     Scope(const char* n, hipStream_t st) : on(enabled), s(st), name(n) {
         if (on) {
-            hipEventCreate(&a);
-            hipEventCreate(&b);
-            hipEventRecord(a, s);
+            a = get_event();
+            b = get_event();
+            (void)hipEventRecord(a, s);
         }
     }
     ~Scope() {
         if (on) {
-            hipEventRecord(b, s);
+            (void)hipEventRecord(b, s);
             std::lock_guard<std::mutex> g(mu);
             pending.push_back({name, a, b});
         }
@@ -127,7 +140,8 @@ struct dbg_agg_handle {
     BatchDesc* dbatches = nullptr;
     u64 batch_cap = 0;
     u32 n_batches = 0;
-    std::vector<BatchDesc*> pinned_descs;  // one pinned staging desc per batch (kept until reset)
+    std::vector<BatchDesc*> pinned_descs;   // pinned staging desc per batch id (pooled)
+    std::vector<BatchDesc*> pinned_chunks;  // their allocations
     std::vector<DevBuf> owned;             // device copies of host inputs / filter constants
 
     // finalize state
@@ -145,6 +159,9 @@ struct dbg_agg_handle {
     u64* d_part_str_base = nullptr;
     u64 part_cap = 0, part_str_cap = 0;
     std::vector<u64> part_counts, part_strings;
+    // fused finalize: validity bytes staging
+    u8* vbytes = nullptr;
+    u64 vbytes_cap = 0;
 };
 
 static int dev_alloc(void** p, size_t bytes) {
@@ -407,10 +424,16 @@ static int new_batch(dbg_agg_handle* h, BatchDesc** staging, u32* bid) {
         h->dbatches = nb;
         h->batch_cap = ncap;
     }
-    BatchDesc* st = nullptr;
-    HIPCHECK(hipHostMalloc((void**)&st, sizeof(BatchDesc), hipHostMallocDefault));
+    // pinned staging descriptors are pooled: slot id is reused after dbg_agg_reset (which
+    // synchronises the stream, so the previous upload from it has completed)
+    while (h->pinned_descs.size() <= id) {
+        BatchDesc* chunk = nullptr;
+        HIPCHECK(hipHostMalloc((void**)&chunk, 64 * sizeof(BatchDesc), hipHostMallocDefault));
+        h->pinned_chunks.push_back(chunk);
+        for (int k = 0; k < 64; ++k) h->pinned_descs.push_back(chunk + k);
+    }
+    BatchDesc* st = h->pinned_descs[id];
     memset(st, 0, sizeof(BatchDesc));
-    h->pinned_descs.push_back(st);
     h->n_batches = id;
     *staging = st;
     *bid = id;
@@ -566,9 +589,12 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
     if ((rc = dev_alloc((void**)&h->counters, CNT_WORDS * 8)) != DBG_OK) return cleanup(rc);
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
-    if (hipHostMalloc((void**)&h->hcounters, CNT_WORDS * 8, hipHostMallocDefault) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
+    if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocDefault) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
     // initial capacity: AggregateHashTable::initial_capacity() = 32768, or 2x the hint
-    u64 hint = params->capacity_hint ? params->capacity_hint : 16384;
+    // initial capacity: 2x the hint, or 4096 slots (the CPU table starts at 32768 =
+    // AggregateHashTable::initial_capacity(); on the GPU growth is a cheap rehash kernel and a
+    // small table keeps init / finalize scans short for low-cardinality queries)
+    u64 hint = params->capacity_hint ? params->capacity_hint : 2048;
     h->cap = pow2_at_least(std::max<u64>(hint * 2, 1024));
     if ((rc = alloc_table(h, h->cap, &h->slots)) != DBG_OK) return cleanup(rc);
     // the (empty) batch table
@@ -586,9 +612,9 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto& b : h->owned) hipFree(b.p);
-    for (auto* p : h->pinned_descs) hipHostFree(p);
+    for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
-                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base};
+                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->vbytes};
     for (void* p : bufs)
         if (p) hipFree(p);
     if (h->hcounters) hipHostFree(h->hcounters);
@@ -613,8 +639,6 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     HIPCHECK(hipStreamSynchronize(h->stream));
     for (auto& b : h->owned) HIPCHECK(hipFree(b.p));
     h->owned.clear();
-    for (size_t i = 1; i < h->pinned_descs.size(); ++i) HIPCHECK(hipHostFree(h->pinned_descs[i]));
-    h->pinned_descs.resize(std::min<size_t>(h->pinned_descs.size(), 1));
     h->n_batches = 0;
     h->pending_rows = h->pending_recs = 0;
     h->finalized = false;
@@ -654,7 +678,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     RETURN_IF(ensure_ovf(h, rows, blocks * 4096));
     {
         prof::Scope ps("agg_insert", h->stream);
-        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true);
+        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st);
     }
     HIPCHECK(hipGetLastError());
     if (!on_device) RETURN_IF(resolve_overflow(h));  // host path: synchronous like the reference processor
@@ -671,38 +695,53 @@ static int ensure_buf(u64** p, u64* cap, u64 n) {
 int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(resolve_overflow(h));
     const Spec& S = h->spec;
-    u64 nb = finalize_blocks(h->cap);
-    RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 8));
-    RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
-    TableDesc t = table_desc(h);
-    {
-        prof::Scope ps("count_groups", h->stream);
-        launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
-    }
-    u64* totals = h->d_pos + nb;  // scratch after the histogram
-    launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
-    h->string_bytes.assign(S.n_keys, 0);
-    std::vector<u64> str_tot(S.n_keys, 0);
-    if (S.has_strings && !S.inline_keys)
+    // Optimistic single round trip: count + scan are enqueued behind the inserts and read back
+    // together with the overflow counters; only when an insert overflowed does the table grow
+    // (resolve_overflow) and the count run again.
+    for (int round = 0; round < 3; ++round) {
+        u64 nb = finalize_blocks(h->cap);
+        RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
+        RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
+        TableDesc t = table_desc(h);
+        {
+            prof::Scope ps("count_groups", h->stream);
+            launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+        }
+        u64* totals = h->d_pos + nb;  // [0] groups, [1 + c] string bytes of key column c
+        launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
+        if (S.has_strings && !S.inline_keys)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
+        HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+        if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {
+            RETURN_IF(resolve_overflow(h));
+            continue;
+        }
+        h->pending_rows = h->pending_recs = 0;
+        const u64* tot = h->hcounters + CNT_WORDS;
+        h->n_groups = tot[0];
+        h->string_bytes.assign(S.n_keys, 0);
         for (int c = 0; c < S.n_keys; ++c)
-            if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
-    HIPCHECK(hipMemcpyAsync(h->hcounters + 4, totals, 8, hipMemcpyDeviceToHost, h->stream));
-    std::vector<u64> stot(S.n_keys + 1, 0);
-    HIPCHECK(hipMemcpyAsync(stot.data(), totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
-    HIPCHECK(hipStreamSynchronize(h->stream));
-    h->n_groups = stot[0];
-    for (int c = 0; c < S.n_keys; ++c)
-        h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? stot[1 + c] : 0;
-    if (h->n_groups != h->hcounters[CNT_CLAIMS])
-        return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
-                                          std::to_string(h->hcounters[CNT_CLAIMS]));
-    h->finalized = true;
-    if (n_groups) *n_groups = h->n_groups;
-    if (string_bytes)
-        for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
-    return DBG_OK;
+            h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? tot[1 + c] : 0;
+        if (h->n_groups != h->hcounters[CNT_CLAIMS])
+            return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
+                                              std::to_string(h->hcounters[CNT_CLAIMS]));
+        // keep the load factor sane for the next batch (the reference resizes at 1/1.5)
+        if ((double)h->n_groups * 1.5 > (double)h->cap) {
+            RETURN_IF(grow_table(h, pow2_at_least((u64)(h->n_groups * 2.0) + 1)));
+            continue;  // positions depend on the slot layout: count again
+        }
+        h->finalized = true;
+        if (n_groups) *n_groups = h->n_groups;
+        if (string_bytes)
+            for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
+        return DBG_OK;
+    }
+    return fail(DBG_ERR_INTERNAL, "finalize did not converge");
 }
 
 int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device) {
@@ -733,6 +772,8 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
     };
     OutDesc od;
     memset(&od, 0, sizeof(od));
+    od.cap_groups = n;
+    for (int c = 0; c < S.n_keys; ++c) od.cap_str[c] = h->string_bytes[c];
     int rc = DBG_OK;
     // device destinations
     for (int c = 0; c < S.n_keys && rc == DBG_OK; ++c) {
@@ -815,6 +856,99 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
         return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
     }
     return DBG_OK;
+}
+
+
+int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, uint64_t max_groups,
+                          const uint64_t* max_string_bytes, uint64_t* n_groups, uint64_t* string_bytes) {
+    if (!h || !out_aggs || !out_keys || !n_groups) return fail(DBG_ERR_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(h->device));
+    const Spec& S = h->spec;
+    for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = h->result_types[a];
+    for (int c = 0; c < S.n_keys; ++c) out_keys[c].dt = S.key_types[c];
+    // validity bytes staging (bit-packed into the caller's buffers by finish_outputs)
+    int n_nullable = 0;
+    for (int c = 0; c < S.n_keys; ++c) n_nullable += S.key_types[c].nullable ? 1 : 0;
+    for (int a = 0; a < S.n_aggs; ++a) n_nullable += h->result_types[a].nullable ? 1 : 0;
+    u64 need = (u64)n_nullable * (max_groups + 1);
+    if (need > h->vbytes_cap) {
+        if (h->vbytes) HIPCHECK(hipFree(h->vbytes));
+        h->vbytes_cap = std::max<u64>(need, 4096);
+        RETURN_IF(dev_alloc((void**)&h->vbytes, h->vbytes_cap));
+    }
+    for (int round = 0; round < 3; ++round) {
+        u64 nb = finalize_blocks(h->cap);
+        RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
+        RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
+        TableDesc t = table_desc(h);
+        {
+            prof::Scope ps("count_groups", h->stream);
+            launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+        }
+        u64* totals = h->d_pos + nb;
+        launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
+        if (S.has_strings && !S.inline_keys)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
+        OutDesc od;
+        memset(&od, 0, sizeof(od));
+        od.cap_groups = max_groups;
+        u8* vb = h->vbytes;
+        for (int c = 0; c < S.n_keys; ++c) {
+            od.key_data[c] = out_keys[c].data;
+            od.key_offsets[c] = S.key_types[c].type == DBG_STRING ? out_keys[c].offsets : nullptr;
+            od.cap_str[c] = (S.key_types[c].type == DBG_STRING && max_string_bytes) ? max_string_bytes[c] : 0;
+            if (S.key_types[c].nullable) {
+                od.key_valid[c] = vb;
+                od.key_bits[c] = out_keys[c].validity;
+                vb += max_groups + 1;
+            }
+        }
+        for (int a = 0; a < S.n_aggs; ++a) {
+            od.agg_data[a] = out_aggs[a].data;
+            if (h->result_types[a].nullable) {
+                od.agg_valid[a] = vb;
+                od.agg_bits[a] = out_aggs[a].validity;
+                vb += max_groups + 1;
+            }
+        }
+        {
+            prof::Scope ps("write_results", h->stream);
+            launch_write_results(h->stream, h->dspec, S, h->dbatches, t, h->d_pos, h->d_str_pos, od);
+            launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);
+        }
+        HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+        if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {
+            RETURN_IF(resolve_overflow(h));
+            continue;
+        }
+        h->pending_rows = h->pending_recs = 0;
+        const u64* tot = h->hcounters + CNT_WORDS;
+        h->n_groups = tot[0];
+        h->string_bytes.assign(S.n_keys, 0);
+        bool short_buf = h->n_groups > max_groups;
+        for (int c = 0; c < S.n_keys; ++c) {
+            h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? tot[1 + c] : 0;
+            if (S.key_types[c].type == DBG_STRING && h->string_bytes[c] > od.cap_str[c]) short_buf = true;
+        }
+        *n_groups = h->n_groups;
+        if (string_bytes)
+            for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
+        if (h->n_groups != h->hcounters[CNT_CLAIMS])
+            return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
+                                              std::to_string(h->hcounters[CNT_CLAIMS]));
+        h->finalized = true;
+        if (h->hcounters[CNT_ERR] & ERR_DEC_OVERFLOW) {
+            HIPCHECK(hipMemsetAsync(h->counters + CNT_ERR, 0, 8, h->stream));
+            return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
+        }
+        if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
+        return DBG_OK;
+    }
+    return fail(DBG_ERR_INTERNAL, "finalize did not converge");
 }
 
 // ---- partial-state records ----

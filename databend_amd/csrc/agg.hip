@@ -12,6 +12,10 @@
 //
 // Bandwidth/atomic-bound integer work: no MFMA.  Every kernel is grid-strided over >= 2048
 // workgroups of 256 threads (64-wide waves) or over contiguous row ranges per workgroup.
+#include <cstdlib>
+#include <limits>
+#include <type_traits>
+
 #include "agg.hpp"
 
 #define BLOCK 256
@@ -361,16 +365,355 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
     if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
 }
 
-static u32 lds_slots_for(const Spec& S) {
+static u32 lds_slots_for(const Spec& S, u32 budget = LDS_BUDGET_BYTES) {
     u32 bytes_per = (u32)S.stride_words * 8;
     u32 n = 1;
-    while ((n * 2) * bytes_per + 16 <= LDS_BUDGET_BYTES) n *= 2;
+    while ((n * 2) * bytes_per + 16 <= budget) n *= 2;
     return n;
 }
 
+// ------------------------------------------------------------------------------------------
+// agg_insert_fast: one non-null integer key column, optional `key <cmp> constant` predicate on
+// that same column (GROUP BY x WHERE x <> c: ClickBench Q8; or no predicate: Q16).  Streams the
+// key column with 16-byte loads (4 in flight per lane), evaluates the predicate on every value,
+// and stages the selected rows in the LDS table exactly like agg_insert.
+// ------------------------------------------------------------------------------------------
+#define FAST_UNROLL 4
+#define FBLOCK 1024  // one 16-wave workgroup per CU: fewer partial tables to merge per hot key
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ bool fast_pred(T v, int op, i64 c) {
+    // the constant is in the column's domain (signed / unsigned by T)
+    T k = (T)c;
+    switch (op) {
+        case DBG_CMP_EQ: return v == k;
+        case DBG_CMP_NE: return v != k;
+        case DBG_CMP_LT: return v < k;
+        case DBG_CMP_LE: return v <= k;
+        case DBG_CMP_GT: return v > k;
+        default: return v >= k;
+    }
+}
+
+// Element j of a 16-byte vector viewed as T[16 / sizeof(T)], from registers (no address taken).
+template <typename T>
+__device__ __forceinline__ T vget(const v4u& y, int j) {
+    constexpr int W = sizeof(T);
+    if constexpr (W == 8) {
+        u32 lo = j ? y.z : y.x, hi = j ? y.w : y.y;
+        return (T)(((u64)hi << 32) | lo);
+    } else {
+        int wi = (j * W) >> 2;
+        u32 word = wi == 0 ? y.x : (wi == 1 ? y.y : (wi == 2 ? y.z : y.w));
+        return (T)(word >> (((j * W) & 3) * 8));
+    }
+}
+
+// Selected rows are appended to a per-wave LDS queue (ballot + mbcnt) and staged 64 at a time
+// with every lane active: at low selectivity (Q8: 0.63 %) a lane-divergent insert per row would
+// leave 63 of 64 lanes idle on every LDS round trip.
+#define WQ 128  // queue entries per wave
+
+template <typename T, bool PRED>
+__global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                               u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots,
+                                                               T lo, T hi, int negate, int count_only, int xmode) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    constexpr int V = 16 / sizeof(T);
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    const T* __restrict__ col = (const T*)B.keys[0].data;
+    const u32 sw = S.stride_words;
+    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // per-wave queue (keys and rows) after the table and its 16 bytes of counters
+    u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * (2 * WQ);
+    u64* qrow = qkey + WQ;
+    for (u32 s = threadIdx.x; s < lds_slots; s += FBLOCK) {
+        u64* p = lds + (u64)s * sw;
+        p[0] = SLOT_EMPTY;
+        for (u32 w = 1; w < sw; ++w) p[w] = 0;
+        for (int a = 0; a < S.n_aggs; ++a)
+            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+    }
+    if (threadIdx.x == 0) {
+        lcount[0] = 0;
+        lcount[1] = 0;
+    }
+    __syncthreads();
+    u32 my_claims = 0;
+
+    // predicate in range form: lo <= v <= hi, xor negate (host maps =, <>, <, <=, >, >=)
+    auto pass = [&](T v) -> bool { return ((v >= lo) & (v <= hi)) ^ (negate != 0); };
+
+    // stage one selected row (key bits, row index) — all callers have full or near-full lanes
+    auto process = [&](u64 key, u64 i) {
+        int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
+        u64* st;
+        if (ls >= 0) {
+            st = lds + (u64)ls * sw;
+            if (count_only) {
+                atomicAdd((unsigned long long*)(st + 1), 1ULL);
+                return;
+            }
+        } else {
+            bool claimed;
+            u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
+            if (gs == ~0ULL) {
+                push_ovf_row(t, bid, i);
+                return;
+            }
+            my_claims += claimed ? 1 : 0;
+            st = t.slots + gs * t.stride_words;
+        }
+        apply_row(S, st, B, i);
+    };
+
+    u32 qn = 0;  // wave-uniform queue length
+    auto drain64 = [&]() {  // process entries [0, 64), shift [64, qn) down
+        u64 k = ((volatile u64*)qkey)[lane], r = ((volatile u64*)qrow)[lane];
+        u64 k2 = 0, r2 = 0;
+        bool mv = lane + 64 < (int)qn;
+        if (mv) {
+            k2 = ((volatile u64*)qkey)[lane + 64];
+            r2 = ((volatile u64*)qrow)[lane + 64];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (mv) {
+            ((volatile u64*)qkey)[lane] = k2;
+            ((volatile u64*)qrow)[lane] = r2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        qn -= 64;
+        process(k, r);
+    };
+
+    u32 sink = 0;  // experiment modes keep the loads alive through this
+    const u64 ltmask = (1ULL << lane) - 1;
+    auto key_of = [&](const v4u& y, int j) -> u64 { return (u64)(typename std::make_unsigned<T>::type)vget<T>(y, j); };
+    // Stage the selected rows of a group of NV vectors (one per lane and slot u), all lanes
+    // together.  A lane's vector slots hold rows base[u] .. base[u] + V - 1.
+    auto handle_group = [&](const v4u* y, const u64* base, int nv, bool act) {
+        if (xmode == 2) {
+            for (int u = 0; u < nv; ++u) sink ^= y[u].x ^ y[u].y ^ y[u].z ^ y[u].w;
+            return;
+        }
+        if (!PRED) {
+            if (act)
+                for (int u = 0; u < nv; ++u)
+#pragma unroll
+                    for (int j = 0; j < V; ++j) process(key_of(y[u], j), base[u] + j);
+            return;
+        }
+        u32 m[FAST_UNROLL];
+        u32 cnt = 0;
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) {
+            m[u] = 0;
+            if (u < nv) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) m[u] |= (pass(vget<T>(y[u], j)) ? 1u : 0u) << j;
+            }
+            if (!act) m[u] = 0;
+            cnt += __popc(m[u]);
+        }
+        if (xmode == 1) {
+            sink ^= cnt;
+            return;
+        }
+        if (__ballot(cnt != 0) == 0) return;
+        // exclusive prefix and wave total of cnt (<= 32 = 6 bits) from one ballot per bit
+        u32 pre = 0, tot = 0;
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) {
+            u64 bal = __ballot((cnt >> bb) & 1);
+            pre += (u32)__popcll(bal & ltmask) << bb;
+            tot += (u32)__popcll(bal) << bb;
+        }
+        if (qn + tot <= WQ) {
+            u32 pos = qn + pre;
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u32 mm = m[u];
+                while (mm) {
+                    int j = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    qkey[pos] = key_of(y[u], j);
+                    qrow[pos] = base[u] + j;
+                    pos++;
+                }
+            }
+            qn += tot;
+            while (qn >= 64) {
+                __builtin_amdgcn_wave_barrier();
+                drain64();
+            }
+        } else {  // dense selection: lanes already busy, insert directly
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u32 mm = m[u];
+                while (mm) {
+                    int j = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    process(key_of(y[u], j), base[u] + j);
+                }
+            }
+        }
+    };
+
+    u64 r0 = (u64)blockIdx.x * rows_per_block;
+    u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    u64 nvec = (r1 - r0) / V;  // full 16-byte vectors of this block
+    const uint4* vp = (const uint4*)(col + r0);
+    u64 k = threadIdx.x;
+    // Software-pipelined stream: the next FAST_UNROLL vectors are in flight while the current
+    // ones are filtered and staged.  Loop conditions are made wave-uniform (ballot) because the
+    // queue needs all 64 lanes; only the final round of a wave has inactive lanes.
+    const u64 step = (u64)FAST_UNROLL * FBLOCK;
+    v4u cur[FAST_UNROLL], nxt[FAST_UNROLL];
+    u64 bases[FAST_UNROLL];
+    bool act = k + (FAST_UNROLL - 1) * FBLOCK < nvec;
+    if (act) {
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) cur[u] = __builtin_nontemporal_load((const v4u*)(vp + k + u * FBLOCK));
+    } else {
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) cur[u] = v4u{0, 0, 0, 0};
+    }
+    while (__ballot(act) != 0) {
+        u64 kn = k + step;
+        bool more = act && kn + (FAST_UNROLL - 1) * FBLOCK < nvec;
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) nxt[u] = __builtin_nontemporal_load((const v4u*)(vp + kn + u * FBLOCK));
+        }
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) bases[u] = r0 + (k + u * FBLOCK) * V;
+        handle_group(cur, bases, FAST_UNROLL, act);
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) cur[u] = nxt[u];
+        }
+        if (act) k = kn;
+        act = more;
+    }
+    // remaining single vectors, same wave-uniform scheme
+    while (__ballot(k < nvec) != 0) {
+        bool a1 = k < nvec;
+        v4u y[1];
+        y[0] = a1 ? *(const v4u*)(vp + k) : v4u{0, 0, 0, 0};
+        u64 b1[1] = {r0 + k * V};
+        handle_group(y, b1, 1, a1);
+        if (a1) k += FBLOCK;
+    }
+    // drain the queue's rest (< 64 entries): lanes below qn take one each
+    if (PRED && qn) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane < (int)qn) process(((volatile u64*)qkey)[lane], ((volatile u64*)qrow)[lane]);
+        qn = 0;
+    }
+    for (u64 i = r0 + nvec * V + threadIdx.x; i < r1; i += FBLOCK) {
+        T v = col[i];
+        if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
+    }
+    if (xmode) asm volatile("" ::"v"(sink));
+    __syncthreads();
+
+    for (u32 s = threadIdx.x; s < (count_only < 0 ? 0u : lds_slots); s += FBLOCK) {  // count_only < 0: timing-only knob (no flush)
+        u64* p = lds + (u64)s * sw;
+        u64 e = p[0];
+        if (e == SLOT_EMPTY) continue;
+        bool claimed;
+        u64 gs = g_find<true>(S, batches, nullptr, 0, e, 0, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_rec(S, t, e, p);
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_state(S, t.slots + gs * t.stride_words, p);
+    }
+    if (my_claims) atomicAdd(&lcount[1], my_claims);
+    __syncthreads();
+    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+}
+
+template <typename T>
+static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* batches, u32 bid, u64 rows, const TableDesc& t,
+                          u32 lslots, size_t table_bytes, bool pred, int op, i64 c, int count_only) {
+    constexpr u64 V = 16 / sizeof(T);
+    static const int xmode = getenv("DBG_FAST_XMODE") ? atoi(getenv("DBG_FAST_XMODE")) : 0;  // timing experiments only
+    // `v <op> c` as `(lo <= v <= hi) ^ negate`, exact over T's range (constants outside it fold)
+    typedef __int128 W;
+    const W tmin = (W)std::numeric_limits<T>::min(), tmax = (W)std::numeric_limits<T>::max();
+    const W C = std::is_signed<T>::value ? (W)c : (W)(u64)c;
+    W lo = 1, hi = 0;  // empty range
+    int neg = 0;
+    auto all = [&]() { lo = tmin; hi = tmax; };
+    switch (op) {
+        case DBG_CMP_EQ: if (C >= tmin && C <= tmax) lo = hi = C; break;
+        case DBG_CMP_NE: neg = 1; if (C >= tmin && C <= tmax) lo = hi = C; break;
+        case DBG_CMP_LT: if (C > tmax) all(); else if (C > tmin) { lo = tmin; hi = C - 1; } break;
+        case DBG_CMP_LE: if (C >= tmax) all(); else if (C >= tmin) { lo = tmin; hi = C; } break;
+        case DBG_CMP_GT: if (C < tmin) all(); else if (C < tmax) { lo = C + 1; hi = tmax; } break;
+        default: if (C <= tmin) all(); else if (C <= tmax) { lo = C; hi = tmax; } break;  // GE
+    }
+    if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
+    size_t shmem = table_bytes + (size_t)(FBLOCK / 64) * 2 * WQ * 8;
+    u64 quantum = V * FBLOCK * FAST_UNROLL;
+    u64 blocks = (rows + quantum - 1) / quantum;
+    static const u64 max_blocks = getenv("DBG_FAST_MAXBLOCKS") ? strtoull(getenv("DBG_FAST_MAXBLOCKS"), nullptr, 10) : 256;
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks < 1) blocks = 1;
+    u64 rpb = (rows + blocks - 1) / blocks;
+    rpb = (rpb + V - 1) / V * V;  // keep every block's start 16-byte aligned
+    blocks = (rows + rpb - 1) / rpb;
+    if (pred)
+        hipLaunchKernelGGL((agg_insert_fast_kernel<T, true>), dim3((u32)blocks), dim3(FBLOCK), shmem, s, dspec, batches, bid, rows, rpb, t,
+                           lslots, (T)lo, (T)hi, neg, count_only, xmode);
+    else
+        hipLaunchKernelGGL((agg_insert_fast_kernel<T, false>), dim3((u32)blocks), dim3(FBLOCK), shmem, s, dspec, batches, bid, rows, rpb, t,
+                           lslots, (T)lo, (T)hi, neg, count_only, xmode);
+}
+
+// Host-side eligibility for the fast path (hb = host copy of the batch descriptor).
+static bool fast_eligible(const Spec& S, const BatchDesc& hb, bool records) {
+    if (records || !S.inline_keys || S.n_keys != 1 || S.key_types[0].nullable) return false;
+    const DCol& k = hb.keys[0];
+    int ty = k.type;
+    bool intlike = (ty >= DBG_INT8 && ty <= DBG_UINT64) || ty == DBG_DATE || ty == DBG_TIMESTAMP;
+    if (!intlike || k.layout != LAYOUT_ARROW || ((uintptr_t)k.data & 15)) return false;
+    if (hb.n_nodes == 0) return true;
+    if (hb.n_nodes != 1) return false;
+    const DNode& n = hb.nodes[0];
+    const DCol& f = hb.fcols[n.col];
+    return n.op == DBG_PRED_CMP_CONST && f.data == k.data && f.type == ty && !f.nullable;
+}
+
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, u32 bid, u64 rows, bool records,
-                   const TableDesc& t, bool use_lds) {
+                   const TableDesc& t, bool use_lds, const BatchDesc* hb) {
     if (rows == 0) return;
+    if (hb && use_lds && fast_eligible(S, *hb, records)) {
+        u32 lslots = lds_slots_for(S, 16 * 1024);
+        size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
+        bool pred = hb->n_nodes == 1;
+        int op = pred ? hb->nodes[0].cmp : 0;
+        i64 c = pred ? hb->nodes[0].i64v : 0;
+        int count_only = S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1;
+        if (getenv("DBG_FAST_NOFLUSH")) count_only = -1;  // timing experiments only: results are wrong
+        switch (hb->keys[0].type) {
+            case DBG_INT8: launch_fast_t<int8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_UINT8: launch_fast_t<uint8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_INT16: launch_fast_t<int16_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_UINT16: launch_fast_t<uint16_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_INT32: case DBG_DATE: launch_fast_t<int32_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_UINT32: launch_fast_t<uint32_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_INT64: case DBG_TIMESTAMP: launch_fast_t<int64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+            case DBG_UINT64: launch_fast_t<uint64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
+        }
+    }
     u32 lslots = use_lds ? lds_slots_for(S) : 1;
     // enough workgroups to fill 256 CUs several times over, each a contiguous row range
     u64 min_rows_per_block = (u64)BLOCK * 16;
@@ -743,13 +1086,15 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
     if (ref_strings)
         for (int c = 0; c < S.n_keys; ++c)
             if (S.key_types[c].type == DBG_STRING) sp[c] = str_pos[(u64)c * nblocks + blockIdx.x] + sscan[c][threadIdx.x] - sb[c];
-    // pass 2: write
+    // pass 2: write (guarded by the output capacity: the fused finalize writes before the host
+    // knows the group count, and retries with larger buffers when it was short)
     for (int k = 0; k < SLOTS_PER_THREAD; ++k) {
         u64 s = base + k;
         if (s > t.cap) break;
         const u64* st = t.slots + s * t.stride_words;
         u64 e = st[0];
         if (e == SLOT_EMPTY) continue;
+        if (p >= out.cap_groups) break;
         // group columns
         if (S.inline_keys) {
             u64 key = s == t.cap ? SLOT_EMPTY : e;
@@ -771,8 +1116,10 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
                 if (kc.type == DBG_STRING) {
                     StrRef r = dcol_str(kc, row);
                     out.key_offsets[c][p] = sp[c];
-                    u8* d = (u8*)out.key_data[c] + sp[c];
-                    for (u64 j = 0; j < r.len; ++j) d[j] = r.p[j];
+                    if (sp[c] + r.len <= out.cap_str[c]) {
+                        u8* d = (u8*)out.key_data[c] + sp[c];
+                        for (u64 j = 0; j < r.len; ++j) d[j] = r.p[j];
+                    }
                     sp[c] += r.len;
                 } else {
                     u32 w = type_width(kc.type);
@@ -789,6 +1136,38 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
         }
         p++;
     }
+}
+
+// Fused finalize tail: bit-pack every nullable output's validity and close the string offsets,
+// with the group count read from device memory (totals[0]; totals[1 + c] string bytes).
+__global__ void finish_outputs_kernel(OutDesc out, const u64* totals, int n_keys, int n_aggs) {
+    u64 n = totals[0];
+    if (n > out.cap_groups) n = out.cap_groups;
+    u64 nb = (n + 7) / 8;
+    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) {
+        for (int c = 0; c < n_keys + n_aggs; ++c) {
+            const u8* bytes = c < n_keys ? out.key_valid[c] : out.agg_valid[c - n_keys];
+            u8* bits = c < n_keys ? out.key_bits[c] : out.agg_bits[c - n_keys];
+            if (!bytes || !bits) continue;
+            u8 b = 0;
+            for (int j = 0; j < 8; ++j) {
+                u64 i = k * 8 + j;
+                if (i < n && bytes[i]) b |= (u8)(1u << j);
+            }
+            bits[k] = b;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int c = 0; c < n_keys; ++c)
+            if (out.key_offsets[c] && totals[0] <= out.cap_groups) out.key_offsets[c][n] = totals[1 + c];
+}
+
+void launch_finish_outputs(hipStream_t s, const OutDesc& out, const u64* totals, int n_keys, int n_aggs) {
+    u64 nb = (out.cap_groups + 7) / 8;
+    u64 blocks = (nb + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(finish_outputs_kernel, dim3((u32)blocks), dim3(256), 0, s, out, totals, n_keys, n_aggs);
 }
 
 void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t,

@@ -61,7 +61,7 @@ enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2 };
 // ---- launch wrappers (agg.hip) ----
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
-                   bool records, const TableDesc& t, bool use_lds);
+                   bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr);
 void launch_retry(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                   u64 n_rows, u64 n_recs, const u64* rows_list, const u64* recs_list);
 void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const u64* old_slots,
@@ -77,7 +77,12 @@ struct OutDesc {
     u8* key_valid[DBG_MAX_KEYS];  // bytes (packed later)
     void* agg_data[DBG_MAX_AGGS];
     u8* agg_valid[DBG_MAX_AGGS];  // bytes
+    u64 cap_groups;               // rows the output buffers hold
+    u64 cap_str[DBG_MAX_KEYS];    // payload bytes the string key buffers hold
+    u8* key_bits[DBG_MAX_KEYS];   // bit-packed destinations of key_valid (fused path)
+    u8* agg_bits[DBG_MAX_AGGS];
 };
+void launch_finish_outputs(hipStream_t s, const OutDesc& out, const u64* totals, int n_keys, int n_aggs);
 void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                           const u64* pos /* scanned hist */, const u64* str_pos, const OutDesc& out);
 void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);

@@ -196,6 +196,15 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
  * (AGG/transform_aggregate_final.rs:128-133): fills caller buffers (host when on_device == 0). */
 int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device);
 
+/* Fused finalize + result into device buffers (on_device outputs) in one host round trip:
+ * count, scan and write are enqueued together and the group count is read back once.  Buffers
+ * hold max_groups rows (and max_string_bytes[c] payload bytes per string key column, may be NULL
+ * without string keys).  *n_groups / string_bytes are always set; if the buffers were too small
+ * the call returns DBG_ERR_INVALID and can be repeated with larger ones (the table is intact). */
+int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys,
+                          uint64_t max_groups, const uint64_t* max_string_bytes, uint64_t* n_groups,
+                          uint64_t* string_bytes);
+
 /* ---- partial-state records: exchange / partition bucket (EAGG/payload.rs:356-391,
  *      EAGG/partitioned_payload.rs:100-143, AGG/aggregate_exchange_injector.rs:154-235) ----
  * A record = [hash u64][group keys, fixed part][state words]; string keys are (u64 offset, u64 len)
