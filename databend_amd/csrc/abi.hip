@@ -129,17 +129,25 @@ struct dbg_agg_handle {
     u64 cap = 0;
     u64* counters = nullptr;   // device, CNT_WORDS
     u64* hcounters = nullptr;  // pinned
+    u64* hcounters_dev = nullptr;  // its device mapping (finalize_small writes it directly)
     // overflow lists (deferred)
     u64* ovf_rows = nullptr;
     u64 ovf_rows_cap = 0;
     u64* ovf_recs = nullptr;
     u64 ovf_recs_cap = 0;
     u64 pending_rows = 0, pending_recs = 0;
+    // parking rows of per-workgroup partial tables (TableDesc::scratch)
+    u64* scratch = nullptr;
+    u32 scr_blocks = 0;
 
     // batches (ids 1..n_batches); descs in device memory, staged through pinned memory
     BatchDesc* dbatches = nullptr;
     u64 batch_cap = 0;
     u32 n_batches = 0;
+    // descriptor cache: ids 1..n_cached hold immutable descriptors of device-resident inputs
+    // (pointers only), kept across dbg_agg_reset so a re-submitted batch needs no upload
+    u32 n_cached = 0;
+    std::vector<std::pair<u64, BatchDesc>> desc_cache;  // (content hash, host copy); index = id - 1
     std::vector<BatchDesc*> pinned_descs;   // pinned staging desc per batch id (pooled)
     std::vector<BatchDesc*> pinned_chunks;  // their allocations
     std::vector<DevBuf> owned;             // device copies of host inputs / filter constants
@@ -316,6 +324,8 @@ static TableDesc table_desc(dbg_agg_handle* h) {
     t.ovf_rows_cap = h->ovf_rows_cap;
     t.ovf_recs = h->ovf_recs;
     t.ovf_recs_cap = h->ovf_recs_cap;
+    t.scratch = h->scratch;
+    t.scr_blocks = h->scr_blocks;
     return t;
 }
 
@@ -438,6 +448,13 @@ static int new_batch(dbg_agg_handle* h, BatchDesc** staging, u32* bid) {
     *staging = st;
     *bid = id;
     return DBG_OK;
+}
+
+static u64 desc_hash(const BatchDesc& d) {
+    const u64* w = (const u64*)&d;
+    u64 hv = 0x9E3779B97F4A7C15ULL;
+    for (size_t k = 0; k < sizeof(BatchDesc) / 8; ++k) hv = (hv ^ w[k]) * 0xff51afd7ed558ccdULL;
+    return hv;
 }
 
 static int upload_batch(dbg_agg_handle* h, BatchDesc* st, u32 bid) {
@@ -589,7 +606,8 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
     if ((rc = dev_alloc((void**)&h->counters, CNT_WORDS * 8)) != DBG_OK) return cleanup(rc);
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
-    if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocDefault) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
+    if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
+    if (hipHostGetDevicePointer((void**)&h->hcounters_dev, h->hcounters, 0) != hipSuccess) h->hcounters_dev = nullptr;
     // initial capacity: AggregateHashTable::initial_capacity() = 32768, or 2x the hint
     // initial capacity: 2x the hint, or 4096 slots (the CPU table starts at 32768 =
     // AggregateHashTable::initial_capacity(); on the GPU growth is a cheap rehash kernel and a
@@ -597,6 +615,11 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     u64 hint = params->capacity_hint ? params->capacity_hint : 2048;
     h->cap = pow2_at_least(std::max<u64>(hint * 2, 1024));
     if ((rc = alloc_table(h, h->cap, &h->slots)) != DBG_OK) return cleanup(rc);
+    // parking rows for every workgroup of an insert launch (launch_insert caps its grid here)
+    h->scr_blocks = DBG_INSERT_MAX_BLOCKS;
+    if ((rc = dev_alloc((void**)&h->scratch, (size_t)h->scr_blocks * 8 * (2 + SCR_ENTRIES * (size_t)h->spec.stride_words))) != DBG_OK)
+        return cleanup(rc);
+    if (hipMemset(h->scratch, 0, (size_t)h->scr_blocks * 16) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
     // the (empty) batch table
     BatchDesc* st;
     u32 bid;
@@ -613,7 +636,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto& b : h->owned) hipFree(b.p);
     for (auto* p : h->pinned_chunks) hipHostFree(p);
-    void* bufs[] = {h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
+    void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
                     h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->vbytes};
     for (void* p : bufs)
         if (p) hipFree(p);
@@ -636,15 +659,19 @@ int dbg_agg_set_stream(dbg_agg_handle* h, void* s) {
 int dbg_agg_reset(dbg_agg_handle* h) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
-    HIPCHECK(hipStreamSynchronize(h->stream));
-    for (auto& b : h->owned) HIPCHECK(hipFree(b.p));
-    h->owned.clear();
-    h->n_batches = 0;
+    // inputs copied by earlier batches, and the pinned batch descriptors reused below, may still
+    // be read by queued work: wait unless the stream is already idle (the usual case after a
+    // finalize, which synchronises)
+    if (!h->owned.empty() || hipStreamQuery(h->stream) != hipSuccess) {
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        for (auto& b : h->owned) HIPCHECK(hipFree(b.p));
+        h->owned.clear();
+    }
+    h->n_batches = h->n_cached;  // cached descriptors stay valid (immutable)
     h->pending_rows = h->pending_recs = 0;
     h->finalized = false;
-    HIPCHECK(hipMemsetAsync(h->counters, 0, CNT_WORDS * 8, h->stream));
     prof::Scope ps("table_init", h->stream);
-    launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap);
+    launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap, h->counters);
     return DBG_OK;
 }
 
@@ -658,6 +685,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     const Spec& S = h->spec;
     BatchDesc* st;
     u32 bid;
+    const size_t owned0 = h->owned.size();
     RETURN_IF(new_batch(h, &st, &bid));
     st->rows = rows;
     for (int c = 0; c < S.n_keys; ++c) {
@@ -672,7 +700,23 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
         RETURN_IF(to_dcol(h, arg_cols[a], want, true, on_device, st->args[a]));
     }
     if (filter && filter->n_nodes) RETURN_IF(fill_filter(h, filter, on_device, st->fcols, &st->n_fcols, st->nodes, &st->n_nodes));
-    RETURN_IF(upload_batch(h, st, bid));
+    if (on_device && h->owned.size() == owned0 && bid == h->n_cached + 1 && h->desc_cache.size() < 64) {
+        u64 hv = desc_hash(*st);
+        u32 hit = 0;
+        for (u32 k = 0; k < h->desc_cache.size() && !hit; ++k)
+            if (h->desc_cache[k].first == hv && memcmp(&h->desc_cache[k].second, st, sizeof(BatchDesc)) == 0) hit = k + 1;
+        if (hit) {
+            h->n_batches = bid - 1;  // give the fresh id back
+            bid = hit;
+            st = &h->desc_cache[hit - 1].second;
+        } else {
+            RETURN_IF(upload_batch(h, st, bid));
+            h->desc_cache.push_back({hv, *st});
+            h->n_cached = bid;
+        }
+    } else {
+        RETURN_IF(upload_batch(h, st, bid));
+    }
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
     u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
     RETURN_IF(ensure_ovf(h, rows, blocks * 4096));
@@ -881,15 +925,16 @@ int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_c
         RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
         RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
         TableDesc t = table_desc(h);
-        {
+        const bool small = h->cap + 1 <= FIN_SMALL_SLOTS;
+        u64* totals = h->d_pos + nb;
+        if (!small) {
             prof::Scope ps("count_groups", h->stream);
             launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+            launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
+            if (S.has_strings && !S.inline_keys)
+                for (int c = 0; c < S.n_keys; ++c)
+                    if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
         }
-        u64* totals = h->d_pos + nb;
-        launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
-        if (S.has_strings && !S.inline_keys)
-            for (int c = 0; c < S.n_keys; ++c)
-                if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
         OutDesc od;
         memset(&od, 0, sizeof(od));
         od.cap_groups = max_groups;
@@ -912,13 +957,19 @@ int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_c
                 vb += max_groups + 1;
             }
         }
-        {
+        const bool zero_copy = small && h->hcounters_dev != nullptr;
+        if (small) {
+            prof::Scope ps("finalize_small", h->stream);
+            launch_finalize_small(h->stream, h->dspec, h->dbatches, t, od, totals, zero_copy ? h->hcounters_dev : nullptr);
+        } else {
             prof::Scope ps("write_results", h->stream);
             launch_write_results(h->stream, h->dspec, S, h->dbatches, t, h->d_pos, h->d_str_pos, od);
             launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);
         }
-        HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
-        HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+        if (!zero_copy) {
+            HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+            HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+        }
         HIPCHECK(hipStreamSynchronize(h->stream));
         if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
         if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {

@@ -137,35 +137,48 @@ __device__ __forceinline__ void apply_row(const Spec& S, u64* st, const BatchDes
     }
 }
 
-// merge_states of a partial state (word array r, same layout) into st.
+// merge_states of a partial state (word array r, same layout) into st.  SC1: read r with sc1
+// loads (words parked by another workgroup in this launch, see block_flush).
+__device__ __forceinline__ u64 ld_sc1(const u64* p) {
+    return __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool SC1 = false>
+__device__ __forceinline__ u64 rdw(const u64* p) { return SC1 ? ld_sc1(p) : *p; }
+
+template <bool SC1 = false>
 __device__ __forceinline__ void apply_state(const Spec& S, u64* st, const u64* r) {
     for (int a = 0; a < S.n_aggs; ++a) {
         const DAgg& A = S.aggs[a];
         u64* w = st + A.w0;
         const u64* x = r + A.w0;
+        const u64 x0 = rdw<SC1>(x);
         switch (A.kind) {
-            case DBG_AGG_COUNT: if (x[0]) atomicAdd((unsigned long long*)w, (unsigned long long)x[0]); break;
+            case DBG_AGG_COUNT: if (x0) atomicAdd((unsigned long long*)w, (unsigned long long)x0); break;
             case DBG_AGG_SUM: case DBG_AGG_AVG: {
-                if (A.sumk == SUMK_I64) { if (x[0]) atomicAdd((unsigned long long*)w, (unsigned long long)x[0]); }
-                else if (A.sumk == SUMK_F64) atomicAdd((double*)w, __longlong_as_double((long long)x[0]));
-                else add128(w, x[0], x[1]);
+                if (A.sumk == SUMK_I64) { if (x0) atomicAdd((unsigned long long*)w, (unsigned long long)x0); }
+                else if (A.sumk == SUMK_F64) atomicAdd((double*)w, __longlong_as_double((long long)x0));
+                else add128(w, x0, rdw<SC1>(x + 1));
                 if (A.kind == DBG_AGG_AVG) {
                     int k = A.sumk == SUMK_I128 ? 2 : 1;
-                    if (x[k]) atomicAdd((unsigned long long*)(w + k), (unsigned long long)x[k]);
+                    u64 xk = rdw<SC1>(x + k);
+                    if (xk) atomicAdd((unsigned long long*)(w + k), (unsigned long long)xk);
                 }
                 break;
             }
             case DBG_AGG_MIN:
-                if (A.mmk == MMK_I64) atomicMin((long long*)w, (long long)x[0]);
-                else atomicMin((unsigned long long*)w, (unsigned long long)x[0]);
+                if (A.mmk == MMK_I64) atomicMin((long long*)w, (long long)x0);
+                else atomicMin((unsigned long long*)w, (unsigned long long)x0);
                 break;
             case DBG_AGG_MAX:
-                if (A.mmk == MMK_I64) atomicMax((long long*)w, (long long)x[0]);
-                else atomicMax((unsigned long long*)w, (unsigned long long)x[0]);
+                if (A.mmk == MMK_I64) atomicMax((long long*)w, (long long)x0);
+                else atomicMax((unsigned long long*)w, (unsigned long long)x0);
                 break;
         }
     }
-    if (S.flags_word >= 0 && r[S.flags_word]) atomicOr((unsigned long long*)(st + S.flags_word), (unsigned long long)r[S.flags_word]);
+    if (S.flags_word >= 0) {
+        u64 f = rdw<SC1>(r + S.flags_word);
+        if (f) atomicOr((unsigned long long*)(st + S.flags_word), (unsigned long long)f);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -248,6 +261,7 @@ __device__ __forceinline__ void push_ovf_row(const TableDesc& t, u32 bid, u64 ro
     if (k < t.ovf_rows_cap) t.ovf_rows[k] = ((u64)bid << 32) | row;
     else atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
 }
+template <bool SC1 = false>
 __device__ __forceinline__ void push_ovf_rec(const Spec& S, const TableDesc& t, u64 key, const u64* words) {
     u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), 1ULL);
     if (k >= t.ovf_recs_cap) {
@@ -256,14 +270,150 @@ __device__ __forceinline__ void push_ovf_rec(const Spec& S, const TableDesc& t, 
     }
     u64* r = t.ovf_recs + k * t.stride_words;
     r[0] = key;
-    for (int w = 1; w <= S.n_words; ++w) r[w] = words[w];
+    for (int w = 1; w <= S.n_words; ++w) r[w] = rdw<SC1>(words + w);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// End of an insert launch: merge the workgroup's LDS partial table into the HBM table.
+//
+// Low cardinality is the hard case for the flush: every workgroup holds the same few hot groups,
+// and G workgroups adding into the same HBM slots serialise at the memory side (device-scope
+// atomics bypass the per-XCD L2).  So a workgroup whose LDS table holds <= SCR_ENTRIES groups
+// parks it, compacted, in its scratch row; the last workgroup to finish (ticket) merges all
+// parked rows in its own LDS table and flushes that once.  Larger tables (diverse keys, little
+// contention) flush directly.  The combine of partial states follows combine_payload
+// (EAGG/aggregate_hashtable.rs:383-425).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void st_sc1(u64* p, u64 v) {
+    __hip_atomic_store((unsigned long long*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool INLINE, bool RECORDS>
+__device__ __forceinline__ u64 lds_entry_hash(const Spec& S, const BatchDesc& B, u64 e) {
+    if (INLINE) return 0;
+    if (RECORDS) return *(const u64*)(B.rec_base + (u64)ref_row(e) * B.rec_width);
+    return group_hash(B.keys, S.n_keys, ref_row(e));
+}
+
+template <bool INLINE, bool RECORDS>
+__device__ __forceinline__ void flush_lds_direct(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds,
+                                                 u32 lds_slots, u32 sw, u32 nt, const TableDesc& t, u32& my_claims) {
+    for (u32 s = threadIdx.x; s < lds_slots; s += nt) {
+        u64* p = lds + (u64)s * sw;
+        u64 e = p[0];
+        if (e == SLOT_EMPTY) continue;
+        u64 h = lds_entry_hash<INLINE, RECORDS>(S, B, e);
+        bool claimed;
+        u64 gs = g_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_rec(S, t, e, p);
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_state(S, t.slots + gs * t.stride_words, p);
+    }
+}
+
+__device__ __forceinline__ void lds_table_init(const Spec& S, u64* lds, u32 lds_slots, u32 sw, u32 nt) {
+    for (u32 s = threadIdx.x; s < lds_slots; s += nt) {
+        u64* p = lds + (u64)s * sw;
+        p[0] = SLOT_EMPTY;
+        for (u32 w = 1; w < sw; ++w) p[w] = 0;
+        for (int a = 0; a < S.n_aggs; ++a)
+            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+    }
+}
+
+// lcount: [0] LDS claims, [1] HBM claims, [2] parked entries, [3] last-workgroup flag.
+// Ends with the workgroup's HBM claims added to the table counter.
+template <bool INLINE, bool RECORDS>
+__device__ __forceinline__ void block_flush(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots, u32 sw,
+                            u32* lcount, u32 nt, const TableDesc& t, u32 my_claims) {
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    const bool use_scr = t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks;
+    if (use_scr) {
+        u64* counts = t.scratch;
+        u64* tickets = t.scratch + t.scr_blocks;
+        u64* rows = t.scratch + 2 * (u64)t.scr_blocks;
+        u64* row = rows + (u64)blockIdx.x * SCR_ENTRIES * sw;
+        if (lcount[0] <= SCR_ENTRIES) {  // park (uniform: lcount[0] is final after the barrier)
+            for (u32 s = threadIdx.x; s < lds_slots; s += nt) {
+                const u64* p = lds + (u64)s * sw;
+                if (p[0] == SLOT_EMPTY) continue;
+                u32 k = atomicAdd(&lcount[2], 1u);
+                u64* d = row + (u64)k * sw;
+                for (u32 w = 0; w <= (u32)S.n_words; ++w) st_sc1(d + w, p[w]);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) st_sc1(counts + blockIdx.x, lcount[2]);
+        } else {
+            if (threadIdx.x == 0) st_sc1(counts + blockIdx.x, 0);
+            flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, nt, t, my_claims);
+        }
+        // Hand-off without release fences (MI355X_MICROARCH.md, inter-workgroup visibility, valid
+        // forms): parked words are stored sc1 (write-through past the XCD's L2); every storing
+        // wave drains them and the barrier orders all waves before lane 0's ticket add; the last
+        // workgroup of each group of SCR_GROUP reads them back with sc1 loads behind one
+        // agent-scope acquire.  Groups keep the merge tail short and parallel, and cut the
+        // same-address atomics on the HBM table by SCR_GROUP.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const u32 g = blockIdx.x / SCR_GROUP;
+        const u32 gsize = min((u32)SCR_GROUP, gridDim.x - g * SCR_GROUP);
+        if (threadIdx.x == 0) {
+            u64 tk = atomicAdd((unsigned long long*)(tickets + g), 1ULL);
+            lcount[3] = tk == (u64)gsize - 1 ? 1u : 0u;
+        }
+        __syncthreads();
+        if (lcount[3]) {  // the group's last workgroup: acquire, merge the group's parked rows, flush
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                tickets[g] = 0;  // ready for the next launch on this table (all members have added)
+            }
+            lds_table_init(S, lds, lds_slots, sw, nt);
+            if (threadIdx.x == 0) lcount[0] = 0;
+            __syncthreads();
+            const u32 total = gsize * SCR_ENTRIES;
+            for (u32 f = threadIdx.x; f < total; f += nt) {
+                u64 b = (u64)g * SCR_GROUP + f / SCR_ENTRIES, k = f % SCR_ENTRIES;
+                const u64* r = rows + (b * SCR_ENTRIES + k) * sw;
+                u64 cnt = ld_sc1(counts + b);
+                u64 e = ld_sc1(r);  // issued with the count: rows are allocated in full
+                if (k >= cnt) continue;
+                u64 h = lds_entry_hash<INLINE, RECORDS>(S, B, e);
+                int ls = lds_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, lds, lmask, sw, lcount, llimit);
+                if (ls >= 0) {
+                    apply_state<true>(S, lds + (u64)ls * sw, r);
+                    continue;
+                }
+                bool claimed;
+                u64 gs = g_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, t, t.probe_limit, claimed);
+                if (gs == ~0ULL) {
+                    push_ovf_rec<true>(S, t, e, r);
+                    continue;
+                }
+                my_claims += claimed ? 1 : 0;
+                apply_state<true>(S, t.slots + gs * t.stride_words, r);
+            }
+            __syncthreads();
+            flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, nt, t, my_claims);
+        }
+    } else {
+        flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, nt, t, my_claims);
+    }
+    if (my_claims) atomicAdd(&lcount[1], my_claims);
+    __syncthreads();
+    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
 }
 
 // ------------------------------------------------------------------------------------------
 // table_init
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restrict__ spec, u64* slots, u64 n_slots) {
+__global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restrict__ spec, u64* slots, u64 n_slots, u64* counters) {
     const Spec& S = *spec;
+    if (counters && blockIdx.x == 0 && threadIdx.x < CNT_WORDS) counters[threadIdx.x] = 0;  // dbg_agg_reset
     u64 sw = S.stride_words;
     for (u64 s = blockIdx.x * (u64)BLOCK + threadIdx.x; s < n_slots; s += (u64)gridDim.x * BLOCK) {
         u64* p = slots + s * sw;
@@ -274,11 +424,11 @@ __global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restric
     }
 }
 
-void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap) {
+void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* counters) {
     u64 n = cap + 1;
     u64 blocks = (n + BLOCK - 1) / BLOCK;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(table_init_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, slots, n);
+    hipLaunchKernelGGL(table_init_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, slots, n, counters);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -296,18 +446,8 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
     const u32 lmask = lds_slots - 1;
     const u32 llimit = lds_slots - lds_slots / 4;
 
-    // init the LDS partial table
-    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
-        u64* p = lds + (u64)s * sw;
-        p[0] = SLOT_EMPTY;
-        for (u32 w = 1; w < sw; ++w) p[w] = 0;
-        for (int a = 0; a < S.n_aggs; ++a)
-            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
-    }
-    if (threadIdx.x == 0) {
-        lcount[0] = 0;
-        lcount[1] = 0;
-    }
+    lds_table_init(S, lds, lds_slots, sw, BLOCK);
+    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
 
     u64 r0 = (u64)blockIdx.x * rows_per_block;
@@ -344,25 +484,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         else apply_row(S, st, B, i);
     }
     __syncthreads();
-
-    // flush the LDS partial table into HBM (combine of the block's partial states)
-    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
-        u64* p = lds + (u64)s * sw;
-        u64 e = p[0];
-        if (e == SLOT_EMPTY) continue;
-        u64 h = INLINE ? 0 : (RECORDS ? *(const u64*)(B.rec_base + (u64)ref_row(e) * B.rec_width) : group_hash(B.keys, S.n_keys, ref_row(e)));
-        bool claimed;
-        u64 gs = g_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, t, t.probe_limit, claimed);
-        if (gs == ~0ULL) {
-            push_ovf_rec(S, t, e, p);
-            continue;
-        }
-        my_claims += claimed ? 1 : 0;
-        apply_state(S, t.slots + gs * t.stride_words, p);
-    }
-    if (my_claims) atomicAdd(&lcount[1], my_claims);
-    __syncthreads();
-    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+    block_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
 }
 
 static u32 lds_slots_for(const Spec& S, u32 budget = LDS_BUDGET_BYTES) {
@@ -432,17 +554,8 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
     // per-wave queue (keys and rows) after the table and its 16 bytes of counters
     u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * (2 * WQ);
     u64* qrow = qkey + WQ;
-    for (u32 s = threadIdx.x; s < lds_slots; s += FBLOCK) {
-        u64* p = lds + (u64)s * sw;
-        p[0] = SLOT_EMPTY;
-        for (u32 w = 1; w < sw; ++w) p[w] = 0;
-        for (int a = 0; a < S.n_aggs; ++a)
-            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
-    }
-    if (threadIdx.x == 0) {
-        lcount[0] = 0;
-        lcount[1] = 0;
-    }
+    lds_table_init(S, lds, lds_slots, sw, FBLOCK);
+    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
     u32 my_claims = 0;
 
@@ -621,23 +734,91 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
     }
     if (xmode) asm volatile("" ::"v"(sink));
     __syncthreads();
+    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, FBLOCK, t, my_claims);
+}
 
-    for (u32 s = threadIdx.x; s < (count_only < 0 ? 0u : lds_slots); s += FBLOCK) {  // count_only < 0: timing-only knob (no flush)
-        u64* p = lds + (u64)s * sw;
-        u64 e = p[0];
-        if (e == SLOT_EMPTY) continue;
-        bool claimed;
-        u64 gs = g_find<true>(S, batches, nullptr, 0, e, 0, t, t.probe_limit, claimed);
-        if (gs == ~0ULL) {
-            push_ovf_rec(S, t, e, p);
-            continue;
-        }
-        my_claims += claimed ? 1 : 0;
-        apply_state(S, t.slots + gs * t.stride_words, p);
-    }
-    if (my_claims) atomicAdd(&lcount[1], my_claims);
+
+// ------------------------------------------------------------------------------------------
+// agg_insert_sel: one non-null integer key column with a `key <op> c` predicate on itself
+// (ClickBench Q8: GROUP BY AdvEngineID WHERE AdvEngineID <> 0).  A grid-strided stream of
+// 16-byte nontemporal loads, SEL_UNROLL vectors in flight per lane (the shape that reads HBM
+// fastest, scripts/micro/stream.hip); the predicate is a branch-free range test on every value;
+// the few selected rows go straight into the workgroup's LDS table from their own lane (at 0.6 %
+// selectivity about one lane in six holds one selected row per round, so the divergent insert
+// costs a few hundred cycles per ~2k rows); block_flush merges the LDS tables at the end.
+// ------------------------------------------------------------------------------------------
+#define SEL_UNROLL 4
+template <typename T, int NT>
+__global__ void __launch_bounds__(NT) agg_insert_sel_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                           u32 bid, u64 rows, TableDesc t, u32 lds_slots, T lo, T hi, int negate,
+                                                           int count_only) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    constexpr int V = 16 / sizeof(T);
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    const T* __restrict__ col = (const T*)B.keys[0].data;
+    const u32 sw = S.stride_words;
+    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    lds_table_init(S, lds, lds_slots, sw, NT);
+    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
-    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+    u32 my_claims = 0;
+    using UT = typename std::make_unsigned<T>::type;
+    auto process = [&](u64 key, u64 i) {
+        int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
+        u64* st;
+        if (ls >= 0) {
+            st = lds + (u64)ls * sw;
+            if (count_only) {
+                atomicAdd((unsigned long long*)(st + 1), 1ULL);
+                return;
+            }
+        } else {
+            bool claimed;
+            u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
+            if (gs == ~0ULL) {
+                push_ovf_row(t, bid, i);
+                return;
+            }
+            my_claims += claimed ? 1 : 0;
+            st = t.slots + gs * t.stride_words;
+        }
+        apply_row(S, st, B, i);
+    };
+    auto handle = [&](const v4u& y, u64 vi) {
+        u32 m = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            T v = vget<T>(y, j);
+            m |= (u32)(((v >= lo) & (v <= hi)) ^ (negate != 0)) << j;
+        }
+        while (m) {
+            int j = __builtin_ctz(m);
+            m &= m - 1;
+            process((u64)(UT)vget<T>(y, j), vi * V + j);
+        }
+    };
+    const u64 nvec = rows / V;
+    const v4u* vp = (const v4u*)col;
+    const u64 stride = (u64)gridDim.x * NT;
+    u64 i = (u64)blockIdx.x * NT + threadIdx.x;
+    for (; i + (SEL_UNROLL - 1) * stride < nvec; i += SEL_UNROLL * stride) {
+        v4u y[SEL_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SEL_UNROLL; ++u) y[u] = __builtin_nontemporal_load(vp + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < SEL_UNROLL; ++u) handle(y[u], i + u * stride);
+    }
+    for (; i < nvec; i += stride) handle(__builtin_nontemporal_load(vp + i), i);
+    // ragged tail (< V rows)
+    for (u64 r = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; r < rows; r += stride) {
+        T v = col[r];
+        if (((v >= lo) & (v <= hi)) ^ (negate != 0)) process((u64)(UT)v, r);
+    }
+    __syncthreads();
+    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
 }
 
 template <typename T>
@@ -661,11 +842,24 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
         default: if (C <= tmin) all(); else if (C <= tmax) { lo = C; hi = tmax; } break;  // GE
     }
     if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
+    static const int sel_mode = getenv("DBG_SEL") ? atoi(getenv("DBG_SEL")) : 1;  // A/B knob: 0 = queue kernel
+    if (pred && sel_mode && ((uintptr_t)batches != 0)) {
+        static const u64 sel_grid = getenv("DBG_SEL_GRID") ? strtoull(getenv("DBG_SEL_GRID"), nullptr, 10) : 512;
+        u64 nvec = rows / V;
+        u64 blocks = (nvec + 512 * SEL_UNROLL - 1) / (512 * SEL_UNROLL);
+        if (blocks > sel_grid) blocks = sel_grid;
+        if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
+        if (blocks < 1) blocks = 1;
+        hipLaunchKernelGGL((agg_insert_sel_kernel<T, 512>), dim3((u32)blocks), dim3(512), table_bytes, s, dspec, batches, bid, rows, t,
+                           lslots, (T)lo, (T)hi, neg, count_only);
+        return;
+    }
     size_t shmem = table_bytes + (size_t)(FBLOCK / 64) * 2 * WQ * 8;
     u64 quantum = V * FBLOCK * FAST_UNROLL;
     u64 blocks = (rows + quantum - 1) / quantum;
     static const u64 max_blocks = getenv("DBG_FAST_MAXBLOCKS") ? strtoull(getenv("DBG_FAST_MAXBLOCKS"), nullptr, 10) : 256;
     if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
     u64 rpb = (rows + blocks - 1) / blocks;
     rpb = (rpb + V - 1) / V * V;  // keep every block's start 16-byte aligned
@@ -702,7 +896,6 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
         int op = pred ? hb->nodes[0].cmp : 0;
         i64 c = pred ? hb->nodes[0].i64v : 0;
         int count_only = S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1;
-        if (getenv("DBG_FAST_NOFLUSH")) count_only = -1;  // timing experiments only: results are wrong
         switch (hb->keys[0].type) {
             case DBG_INT8: launch_fast_t<int8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
             case DBG_UINT8: launch_fast_t<uint8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
@@ -718,7 +911,7 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     // enough workgroups to fill 256 CUs several times over, each a contiguous row range
     u64 min_rows_per_block = (u64)BLOCK * 16;
     u64 blocks = (rows + min_rows_per_block - 1) / min_rows_per_block;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
     u64 rpb = (rows + blocks - 1) / blocks;
     blocks = (rows + rpb - 1) / rpb;
@@ -1044,6 +1237,51 @@ __device__ __forceinline__ bool agg_result(const Spec& S, const DAgg& A, const u
     return valid;
 }
 
+// flush_column of one group (slot s, entry e, state words st) into output row p; sp[c] = string
+// write cursor of key column c (advanced).
+__device__ __forceinline__ void write_group(const Spec& S, const BatchDesc* batches, const TableDesc& t, u64 s, const u64* st,
+                                           u64 e, u64 p, u64* sp, const OutDesc& out) {
+    // group columns
+    if (S.inline_keys) {
+        u64 key = s == t.cap ? SLOT_EMPTY : e;
+        for (int c = 0; c < S.n_keys; ++c) {
+            const dbg_datatype& ty = S.key_types[c];
+            u32 w = type_width(ty.type);
+            u64 b = (key >> (8 * S.koff[c])) & width_mask(w);
+            bool v = ty.nullable ? ((key >> (8 * S.voff[c])) & 0xff) != 0 : true;
+            write_bytes(out.key_data[c], p, w, b, 0);
+            if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
+        }
+    } else {
+        const BatchDesc& RB = batches[ref_bid(e)];
+        u64 row = ref_row(e);
+        for (int c = 0; c < S.n_keys; ++c) {
+            const DCol& kc = RB.keys[c];
+            bool v = dcol_valid(kc, row);
+            if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
+            if (kc.type == DBG_STRING) {
+                StrRef r = dcol_str(kc, row);
+                out.key_offsets[c][p] = sp[c];
+                if (sp[c] + r.len <= out.cap_str[c]) {
+                    u8* d = (u8*)out.key_data[c] + sp[c];
+                    for (u64 j = 0; j < r.len; ++j) d[j] = r.p[j];
+                }
+                sp[c] += r.len;
+            } else {
+                u32 w = type_width(kc.type);
+                write_bytes(out.key_data[c], p, w, dcol_bits(kc, row), w == 16 ? dcol_hi(kc, row) : 0);
+            }
+        }
+    }
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        u64 lo, hi;
+        bool v = agg_result(S, A, st, lo, hi, t.counters + CNT_ERR);
+        write_bytes(out.agg_data[a], p, A.res_width, lo, hi);
+        if (out.agg_valid[a]) out.agg_valid[a][p] = v ? 1 : 0;
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                              TableDesc t, const u64* pos, const u64* str_pos, u64 nblocks,
                                                              OutDesc out) {
@@ -1095,47 +1333,115 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
         u64 e = st[0];
         if (e == SLOT_EMPTY) continue;
         if (p >= out.cap_groups) break;
-        // group columns
-        if (S.inline_keys) {
-            u64 key = s == t.cap ? SLOT_EMPTY : e;
-            for (int c = 0; c < S.n_keys; ++c) {
-                const dbg_datatype& ty = S.key_types[c];
-                u32 w = type_width(ty.type);
-                u64 b = (key >> (8 * S.koff[c])) & width_mask(w);
-                bool v = ty.nullable ? ((key >> (8 * S.voff[c])) & 0xff) != 0 : true;
-                write_bytes(out.key_data[c], p, w, b, 0);
-                if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
-            }
-        } else {
-            const BatchDesc& RB = batches[ref_bid(e)];
-            u64 row = ref_row(e);
-            for (int c = 0; c < S.n_keys; ++c) {
-                const DCol& kc = RB.keys[c];
-                bool v = dcol_valid(kc, row);
-                if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
-                if (kc.type == DBG_STRING) {
-                    StrRef r = dcol_str(kc, row);
-                    out.key_offsets[c][p] = sp[c];
-                    if (sp[c] + r.len <= out.cap_str[c]) {
-                        u8* d = (u8*)out.key_data[c] + sp[c];
-                        for (u64 j = 0; j < r.len; ++j) d[j] = r.p[j];
-                    }
-                    sp[c] += r.len;
-                } else {
-                    u32 w = type_width(kc.type);
-                    write_bytes(out.key_data[c], p, w, dcol_bits(kc, row), w == 16 ? dcol_hi(kc, row) : 0);
-                }
-            }
-        }
-        for (int a = 0; a < S.n_aggs; ++a) {
-            const DAgg& A = S.aggs[a];
-            u64 lo, hi;
-            bool v = agg_result(S, A, st, lo, hi, t.counters + CNT_ERR);
-            write_bytes(out.agg_data[a], p, A.res_width, lo, hi);
-            if (out.agg_valid[a]) out.agg_valid[a][p] = v ? 1 : 0;
-        }
+        write_group(S, batches, t, s, st, e, p, sp, out);
         p++;
     }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// finalize_small: count + scan + write + validity bits + string offsets in ONE workgroup, for
+// tables of at most FIN_SMALL_SLOTS slots (low-cardinality queries: the four-launch finalize
+// costs more than the work).  totals: [0] groups, [1 + c] string bytes of key column c.
+// ------------------------------------------------------------------------------------------
+#define FIN_NT 1024
+__global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                TableDesc t, OutDesc out, u64* totals, u64* host_mirror) {
+    const Spec& S = *spec;
+    __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
+    const u64 n_slots = t.cap + 1;
+    const u64 per = (n_slots + FIN_NT - 1) / FIN_NT;
+    const u64 base = (u64)threadIdx.x * per;
+    const bool ref_strings = S.has_strings && !S.inline_keys;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 cnt = 0, sb[DBG_MAX_KEYS];
+    for (int c = 0; c < DBG_MAX_KEYS; ++c) sb[c] = 0;
+    for (u64 k = 0; k < per; ++k) {
+        u64 s = base + k;
+        if (s >= n_slots) break;
+        u64 e = t.slots[s * t.stride_words];
+        if (e == SLOT_EMPTY) continue;
+        cnt++;
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) sb[c] += key_str_len(S, batches, e, c);
+    }
+    // block exclusive scan of cnt (and of the string bytes of each key column)
+    auto wave_incl = [&](u64 v) {
+        for (int off = 1; off < 64; off <<= 1) {
+            u64 o = __shfl_up(v, off, 64);
+            if (lane >= off) v += o;
+        }
+        return v;
+    };
+    u64 ic = wave_incl(cnt);
+    u64 isb[DBG_MAX_KEYS];
+    if (ref_strings)
+        for (int c = 0; c < S.n_keys; ++c) isb[c] = wave_incl(sb[c]);
+    if (lane == 63) {
+        wsum[wave][0] = ic;
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c) wsum[wave][1 + c] = isb[c];
+    }
+    __syncthreads();
+    u64 p = ic - cnt, sp[DBG_MAX_KEYS];
+    for (int w = 0; w < wave; ++w) p += wsum[w][0];
+    if (ref_strings)
+        for (int c = 0; c < S.n_keys; ++c) {
+            sp[c] = isb[c] - sb[c];
+            for (int w = 0; w < wave; ++w) sp[c] += wsum[w][1 + c];
+        }
+    u64 total = 0, stot[DBG_MAX_KEYS];
+    for (int w = 0; w < FIN_NT / 64; ++w) total += wsum[w][0];
+    for (int c = 0; c < S.n_keys; ++c) {
+        stot[c] = 0;
+        if (ref_strings)
+            for (int w = 0; w < FIN_NT / 64; ++w) stot[c] += wsum[w][1 + c];
+    }
+    for (u64 k = 0; k < per; ++k) {
+        u64 s = base + k;
+        if (s >= n_slots) break;
+        const u64* st = t.slots + s * t.stride_words;
+        u64 e = st[0];
+        if (e == SLOT_EMPTY) continue;
+        if (p >= out.cap_groups) break;
+        write_group(S, batches, t, s, st, e, p, sp, out);
+        p++;
+    }
+    __syncthreads();  // validity bytes of every row are written
+    u64 n = total < out.cap_groups ? total : out.cap_groups;
+    for (u64 k = threadIdx.x; k < (n + 7) / 8; k += FIN_NT)
+        for (int c = 0; c < S.n_keys + S.n_aggs; ++c) {
+            const u8* bytes = c < S.n_keys ? out.key_valid[c] : out.agg_valid[c - S.n_keys];
+            u8* bits = c < S.n_keys ? out.key_bits[c] : out.agg_bits[c - S.n_keys];
+            if (!bytes || !bits) continue;
+            u8 b = 0;
+            for (int j = 0; j < 8; ++j) {
+                u64 i = k * 8 + j;
+                if (i < n && bytes[i]) b |= (u8)(1u << j);
+            }
+            bits[k] = b;
+        }
+    if (threadIdx.x == 0) {
+        totals[0] = total;
+        for (int c = 0; c < S.n_keys; ++c) {
+            totals[1 + c] = stot[c];
+            if (out.key_offsets[c] && total <= out.cap_groups) out.key_offsets[c][total] = stot[c];
+        }
+    }
+    // zero-copy read-back: the table counters and the totals go straight to mapped pinned host
+    // memory ([0, CNT_WORDS) counters, then totals), so finalize needs no copy launches
+    __syncthreads();
+    if (host_mirror && threadIdx.x < CNT_WORDS) host_mirror[threadIdx.x] = ld_sc1(t.counters + threadIdx.x);
+    if (host_mirror && threadIdx.x == 0) {
+        host_mirror[CNT_WORDS] = total;
+        for (int c = 0; c < S.n_keys; ++c) host_mirror[CNT_WORDS + 1 + c] = stot[c];
+    }
+}
+
+void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
+                           u64* totals, u64* host_mirror) {
+    hipLaunchKernelGGL(finalize_small_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, out, totals, host_mirror);
 }
 
 // Fused finalize tail: bit-pack every nullable output's validity and close the string offsets,

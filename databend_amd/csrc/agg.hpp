@@ -53,13 +53,21 @@ struct TableDesc {
     u64 ovf_rows_cap;
     u64* ovf_recs;  // [keyref][words...] per record, stride = stride_words
     u64 ovf_recs_cap;
+    // per-workgroup parking rows of small LDS tables (merged by the last workgroup of each group,
+    // see block_flush in agg.hip): [count u64 x scr_blocks][group tickets u64 x scr_blocks]
+    // [scr_blocks x SCR_ENTRIES x stride_words]
+    u64* scratch;
+    u32 scr_blocks;
 };
+#define SCR_ENTRIES 64
+#define SCR_GROUP 16
+#define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
 enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_WORDS = 8 };
 enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2 };
 
 // ---- launch wrappers (agg.hip) ----
-void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap);
+void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
                    bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr);
 void launch_retry(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
@@ -82,6 +90,9 @@ struct OutDesc {
     u8* key_bits[DBG_MAX_KEYS];   // bit-packed destinations of key_valid (fused path)
     u8* agg_bits[DBG_MAX_AGGS];
 };
+#define FIN_SMALL_SLOTS 16384  // tables up to this many slots finalize in one workgroup
+void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
+                           u64* totals, u64* host_mirror /* mapped pinned: counters, then totals */);
 void launch_finish_outputs(hipStream_t s, const OutDesc& out, const u64* totals, int n_keys, int n_aggs);
 void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                           const u64* pos /* scanned hist */, const u64* str_pos, const OutDesc& out);
