@@ -501,8 +501,12 @@ static u32 lds_slots_for(const Spec& S, u32 budget = LDS_BUDGET_BYTES) {
 // and stages the selected rows in the LDS table exactly like agg_insert.
 // ------------------------------------------------------------------------------------------
 #define FAST_UNROLL 4
-#define FBLOCK 1024  // one 16-wave workgroup per CU: fewer partial tables to merge per hot key
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+// Column data reached through a descriptor is a generic pointer to the compiler, which then
+// emits flat loads: those count against lgkmcnt too and retire out of order, so every LDS wait
+// (and every use of a loaded value) drains ALL loads in flight and the prefetch pipeline
+// collapses.  Streams read through this address-space-1 view compile to global_load.
+typedef const v4u __attribute__((address_space(1)))* gv4p;
 
 template <typename T>
 __device__ __forceinline__ bool fast_pred(T v, int op, i64 c) {
@@ -537,9 +541,9 @@ __device__ __forceinline__ T vget(const v4u& y, int j) {
 // leave 63 of 64 lanes idle on every LDS round trip.
 #define WQ 128  // queue entries per wave
 
-template <typename T, bool PRED>
-__global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                               u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots,
+template <typename T, bool PRED, int NT>
+__global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                               u32 bid, u64 rows, TableDesc t, u32 lds_slots,
                                                                T lo, T hi, int negate, int count_only, int xmode) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     constexpr int V = 16 / sizeof(T);
@@ -554,7 +558,7 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
     // per-wave queue (keys and rows) after the table and its 16 bytes of counters
     u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * (2 * WQ);
     u64* qrow = qkey + WQ;
-    lds_table_init(S, lds, lds_slots, sw, FBLOCK);
+    lds_table_init(S, lds, lds_slots, sw, NT);
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
     u32 my_claims = 0;
@@ -609,14 +613,14 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
     auto key_of = [&](const v4u& y, int j) -> u64 { return (u64)(typename std::make_unsigned<T>::type)vget<T>(y, j); };
     // Stage the selected rows of a group of NV vectors (one per lane and slot u), all lanes
     // together.  A lane's vector slots hold rows base[u] .. base[u] + V - 1.
-    auto handle_group = [&](const v4u* y, const u64* base, int nv, bool act) {
+    auto handle_group = [&](const v4u* y, const u64* base, int nv, u32 actm) {
         if (xmode == 2) {
             for (int u = 0; u < nv; ++u) sink ^= y[u].x ^ y[u].y ^ y[u].z ^ y[u].w;
             return;
         }
         if (!PRED) {
-            if (act)
-                for (int u = 0; u < nv; ++u)
+            for (int u = 0; u < nv; ++u)
+                if ((actm >> u) & 1)
 #pragma unroll
                     for (int j = 0; j < V; ++j) process(key_of(y[u], j), base[u] + j);
             return;
@@ -630,7 +634,7 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
 #pragma unroll
                 for (int j = 0; j < V; ++j) m[u] |= (pass(vget<T>(y[u], j)) ? 1u : 0u) << j;
             }
-            if (!act) m[u] = 0;
+            if (!((actm >> u) & 1)) m[u] = 0;
             cnt += __popc(m[u]);
         }
         if (xmode == 1) {
@@ -677,50 +681,30 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
         }
     };
 
-    u64 r0 = (u64)blockIdx.x * rows_per_block;
-    u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-    u64 nvec = (r1 - r0) / V;  // full 16-byte vectors of this block
-    const uint4* vp = (const uint4*)(col + r0);
-    u64 k = threadIdx.x;
-    // Software-pipelined stream: the next FAST_UNROLL vectors are in flight while the current
-    // ones are filtered and staged.  Loop conditions are made wave-uniform (ballot) because the
-    // queue needs all 64 lanes; only the final round of a wave has inactive lanes.
-    const u64 step = (u64)FAST_UNROLL * FBLOCK;
-    v4u cur[FAST_UNROLL], nxt[FAST_UNROLL];
-    u64 bases[FAST_UNROLL];
-    bool act = k + (FAST_UNROLL - 1) * FBLOCK < nvec;
-    if (act) {
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) cur[u] = __builtin_nontemporal_load((const v4u*)(vp + k + u * FBLOCK));
-    } else {
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) cur[u] = v4u{0, 0, 0, 0};
-    }
-    while (__ballot(act) != 0) {
-        u64 kn = k + step;
-        bool more = act && kn + (FAST_UNROLL - 1) * FBLOCK < nvec;
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) nxt[u] = __builtin_nontemporal_load((const v4u*)(vp + kn + u * FBLOCK));
-        }
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) bases[u] = r0 + (k + u * FBLOCK) * V;
-        handle_group(cur, bases, FAST_UNROLL, act);
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) cur[u] = nxt[u];
-        }
-        if (act) k = kn;
-        act = more;
-    }
-    // remaining single vectors, same wave-uniform scheme
+    // Grid-strided stream (all waves of the chip sweep one window of the column together: DRAM
+    // rows stay open, scripts/micro/stream.hip): FAST_UNROLL unconditional 16-byte loads per lane
+    // per round (an index past the end is clamped and its lane-slot masked off), so no branch
+    // sits around the loads; other waves of the CU keep HBM busy while one filters.  The loop
+    // condition is wave-uniform (ballot) because the queue needs all 64 lanes.
+    const u64 nvec = rows / V;
+    gv4p vp = (gv4p)col;
+    const u64 gstride = (u64)gridDim.x * NT;
+    u64 k = (u64)blockIdx.x * NT + threadIdx.x;
+    const u64 step = (u64)FAST_UNROLL * gstride;
+    const u64 lastv = nvec ? nvec - 1 : 0;
     while (__ballot(k < nvec) != 0) {
-        bool a1 = k < nvec;
-        v4u y[1];
-        y[0] = a1 ? *(const v4u*)(vp + k) : v4u{0, 0, 0, 0};
-        u64 b1[1] = {r0 + k * V};
-        handle_group(y, b1, 1, a1);
-        if (a1) k += FBLOCK;
+        v4u y[FAST_UNROLL];
+        u64 bases[FAST_UNROLL];
+        u32 actm = 0;
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) {
+            u64 idx = k + u * gstride;
+            actm |= (idx < nvec ? 1u : 0u) << u;
+            y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+            bases[u] = idx * V;
+        }
+        handle_group(y, bases, FAST_UNROLL, actm);
+        k += step;
     }
     // drain the queue's rest (< 64 entries): lanes below qn take one each
     if (PRED && qn) {
@@ -728,13 +712,13 @@ __global__ void __launch_bounds__(FBLOCK) agg_insert_fast_kernel(const Spec* __r
         if (lane < (int)qn) process(((volatile u64*)qkey)[lane], ((volatile u64*)qrow)[lane]);
         qn = 0;
     }
-    for (u64 i = r0 + nvec * V + threadIdx.x; i < r1; i += FBLOCK) {
+    for (u64 i = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; i < rows; i += gstride) {
         T v = col[i];
         if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
     }
     if (xmode) asm volatile("" ::"v"(sink));
     __syncthreads();
-    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, FBLOCK, t, my_claims);
+    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
 }
 
 
@@ -801,7 +785,7 @@ __global__ void __launch_bounds__(NT) agg_insert_sel_kernel(const Spec* __restri
         }
     };
     const u64 nvec = rows / V;
-    const v4u* vp = (const v4u*)col;
+    gv4p vp = (gv4p)col;
     const u64 stride = (u64)gridDim.x * NT;
     u64 i = (u64)blockIdx.x * NT + threadIdx.x;
     for (; i + (SEL_UNROLL - 1) * stride < nvec; i += SEL_UNROLL * stride) {
@@ -842,7 +826,7 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
         default: if (C <= tmin) all(); else if (C <= tmax) { lo = C; hi = tmax; } break;  // GE
     }
     if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
-    static const int sel_mode = getenv("DBG_SEL") ? atoi(getenv("DBG_SEL")) : 1;  // A/B knob: 0 = queue kernel
+    static const int sel_mode = getenv("DBG_SEL") ? atoi(getenv("DBG_SEL")) : 0;  // A/B knob: 1 = direct-insert kernel
     if (pred && sel_mode && ((uintptr_t)batches != 0)) {
         static const u64 sel_grid = getenv("DBG_SEL_GRID") ? strtoull(getenv("DBG_SEL_GRID"), nullptr, 10) : 512;
         u64 nvec = rows / V;
@@ -854,22 +838,23 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
                            lslots, (T)lo, (T)hi, neg, count_only);
         return;
     }
-    size_t shmem = table_bytes + (size_t)(FBLOCK / 64) * 2 * WQ * 8;
-    u64 quantum = V * FBLOCK * FAST_UNROLL;
-    u64 blocks = (rows + quantum - 1) / quantum;
+    static const int nt = getenv("DBG_FAST_NT") ? atoi(getenv("DBG_FAST_NT")) : 1024;
     static const u64 max_blocks = getenv("DBG_FAST_MAXBLOCKS") ? strtoull(getenv("DBG_FAST_MAXBLOCKS"), nullptr, 10) : 256;
+    size_t shmem = table_bytes + (size_t)(nt / 64) * 2 * WQ * 8;
+    u64 quantum = V * (u64)nt * FAST_UNROLL;
+    u64 blocks = (rows + quantum - 1) / quantum;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
-    u64 rpb = (rows + blocks - 1) / blocks;
-    rpb = (rpb + V - 1) / V * V;  // keep every block's start 16-byte aligned
-    blocks = (rows + rpb - 1) / rpb;
-    if (pred)
-        hipLaunchKernelGGL((agg_insert_fast_kernel<T, true>), dim3((u32)blocks), dim3(FBLOCK), shmem, s, dspec, batches, bid, rows, rpb, t,
-                           lslots, (T)lo, (T)hi, neg, count_only, xmode);
-    else
-        hipLaunchKernelGGL((agg_insert_fast_kernel<T, false>), dim3((u32)blocks), dim3(FBLOCK), shmem, s, dspec, batches, bid, rows, rpb, t,
-                           lslots, (T)lo, (T)hi, neg, count_only, xmode);
+#define FAST_LAUNCH(P, N)                                                                                                     \
+    hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, lslots, \
+                       (T)lo, (T)hi, neg, count_only, xmode)
+    if (nt == 512) {
+        if (pred) FAST_LAUNCH(true, 512); else FAST_LAUNCH(false, 512);
+    } else {
+        if (pred) FAST_LAUNCH(true, 1024); else FAST_LAUNCH(false, 1024);
+    }
+#undef FAST_LAUNCH
 }
 
 // Host-side eligibility for the fast path (hb = host copy of the batch descriptor).
