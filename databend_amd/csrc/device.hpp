@@ -52,31 +52,40 @@ __host__ __device__ inline uint32_t type_width(int t) {
     }
 }
 
+// Loads of column data through a descriptor: the pointers come out of device memory, so the
+// compiler cannot infer their address space and would emit flat loads (which also count against
+// lgkmcnt and retire out of order, serialising LDS work behind them).  Column buffers are always
+// global memory (device or mapped host), so read them through address-space-1 views.
+template <typename V>
+__device__ __forceinline__ V gld(const void* p) {
+    return *(const V __attribute__((address_space(1)))*)p;
+}
+
 __device__ __forceinline__ bool dcol_valid(const DCol& c, u64 i) {
     if (!c.nullable) return true;
-    if (c.layout == LAYOUT_RECORD) return c.validity[i * c.stride] != 0;
+    if (c.layout == LAYOUT_RECORD) return gld<u8>(c.validity + i * c.stride) != 0;
     if (c.validity == nullptr) return true;
     u64 b = c.validity_offset + i;
-    return (c.validity[b >> 3] >> (b & 7)) & 1;
+    return (gld<u8>(c.validity + (b >> 3)) >> (b & 7)) & 1;
 }
 
 // Raw value bits of a fixed-width cell, zero-extended to 64 bits (Decimal128: low word).
 __device__ __forceinline__ u64 dcol_bits(const DCol& c, u64 i) {
     if (c.type == DBG_BOOLEAN) {
-        if (c.layout == LAYOUT_RECORD) return c.data[i * c.stride] != 0;
+        if (c.layout == LAYOUT_RECORD) return gld<u8>(c.data + i * c.stride) != 0;
         u64 b = c.data_offset + i;
-        return (c.data[b >> 3] >> (b & 7)) & 1;
+        return (gld<u8>(c.data + (b >> 3)) >> (b & 7)) & 1;
     }
     const u8* p = c.data + i * (u64)c.stride;
     switch (c.width) {
-        case 1: return *p;
-        case 2: return *(const uint16_t*)p;
-        case 4: return *(const uint32_t*)p;
-        default: return *(const u64*)p;
+        case 1: return gld<u8>(p);
+        case 2: return gld<uint16_t>(p);
+        case 4: return gld<uint32_t>(p);
+        default: return gld<u64>(p);
     }
 }
 __device__ __forceinline__ u64 dcol_hi(const DCol& c, u64 i) {  // Decimal128 high word
-    return *(const u64*)(c.data + i * (u64)c.stride + 8);
+    return gld<u64>(c.data + i * (u64)c.stride + 8);
 }
 
 struct StrRef {
@@ -85,10 +94,10 @@ struct StrRef {
 };
 __device__ __forceinline__ StrRef dcol_str(const DCol& c, u64 i) {
     if (c.layout == LAYOUT_RECORD) {
-        const u64* pr = (const u64*)(c.data + i * (u64)c.stride);
-        return StrRef{c.strings + pr[0], pr[1]};
+        const u8* pr = c.data + i * (u64)c.stride;
+        return StrRef{c.strings + gld<u64>(pr), gld<u64>(pr + 8)};
     }
-    u64 a = c.offsets[i], b = c.offsets[i + 1];
+    u64 a = gld<u64>(c.offsets + i), b = gld<u64>(c.offsets + i + 1);
     return StrRef{c.data + a, b - a};
 }
 
@@ -123,10 +132,14 @@ __host__ __device__ __forceinline__ u64 hash_prim(u64 x) {  // group_hash.rs:194
 }
 
 __device__ __forceinline__ u64 load_u64_unaligned(const u8* p) {
-    u64 v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v |= (u64)p[k] << (8 * k);
-    return v;
+    // two aligned 8-byte loads funnelled together (the second only when the bytes straddle)
+    uintptr_t a = (uintptr_t)p;
+    u32 off = (u32)(a & 7);
+    const u8* base = (const u8*)(a & ~(uintptr_t)7);
+    u64 w0 = gld<u64>(base);
+    if (off == 0) return w0;
+    u64 w1 = gld<u64>(base + 8);
+    return (w0 >> (8 * off)) | (w1 << (64 - 8 * off));
 }
 
 // impl AggHash for [u8] (group_hash.rs:161-192)
@@ -144,7 +157,7 @@ __device__ __forceinline__ u64 hash_bytes(const u8* p, u64 len) {
     }
     u64 tl = len & 7;
     const u8* t = p + nb * 8;
-    for (u64 i = 0; i < tl; ++i) h ^= (u64)t[i] << (8 * (tl - i - 1));
+    for (u64 i = 0; i < tl; ++i) h ^= (u64)gld<u8>(t + i) << (8 * (tl - i - 1));
     h ^= h >> R;
     h *= M;
     h ^= h >> R;
@@ -215,7 +228,7 @@ __device__ __forceinline__ bool bytes_equal(const u8* a, const u8* b, u64 n) {
     for (; i + 8 <= n; i += 8)
         if (load_u64_unaligned(a + i) != load_u64_unaligned(b + i)) return false;
     for (; i < n; ++i)
-        if (a[i] != b[i]) return false;
+        if (gld<u8>(a + i) != gld<u8>(b + i)) return false;
     return true;
 }
 
@@ -260,8 +273,10 @@ __device__ __forceinline__ int cmp3_i128(u64 alo, i64 ahi, u64 blo, i64 bhi) {
 }
 __device__ __forceinline__ int cmp3_bytes(const u8* a, u64 la, const u8* b, u64 lb) {
     u64 n = la < lb ? la : lb;
-    for (u64 k = 0; k < n; ++k)
-        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    for (u64 k = 0; k < n; ++k) {
+        u8 x = gld<u8>(a + k), y = gld<u8>(b + k);
+        if (x != y) return x < y ? -1 : 1;
+    }
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 __device__ __forceinline__ bool apply_cmp(int c, int o) {
