@@ -305,6 +305,9 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     while (sw < word && sw < 8) sw <<= 1;
     if (word > 8) sw = (word + 7) & ~7;
     S.stride_words = sw;
+    for (int w = 0; w < DBG_MAX_WORDS; ++w) S.slot_init[w] = w == 0 ? SLOT_EMPTY : 0;
+    for (int a = 0; a < S.n_aggs; ++a)
+        if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) S.slot_init[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
     S.rec_state_off = off;
     S.rec_width = off + 8 * (u32)S.n_words;
     return DBG_OK;

@@ -234,7 +234,11 @@ __device__ __forceinline__ int lds_find(const Spec& S, const BatchDesc* batches,
                                         u64* lds, u32 lmask, u32 sw, u32* lcount, u32 llimit) {
     if (INLINE && key == SLOT_EMPTY) return -1;
     u32 s = (u32)((INLINE ? slot_mix(key) : (h >> 16)) & lmask);
-    for (int p = 0; p < LDS_PROBE_CAP; ++p) {
+    // Once the table is full (high cardinality), a key found within two probes is staged, any
+    // other goes straight to HBM: a long probe through a full table of other keys is wasted LDS
+    // traffic.  A key may then hold state both here and in HBM; the flush merges them.
+    const int cap = *(volatile u32*)lcount >= llimit ? 2 : LDS_PROBE_CAP;
+    for (int p = 0; p < cap; ++p) {
         u64* e = lds + (u64)s * sw;
         u64 ev = *(volatile u64*)e;
         if (ev == SLOT_EMPTY) {
@@ -411,24 +415,31 @@ __device__ __forceinline__ void block_flush(const Spec& S, const BatchDesc* batc
 // ------------------------------------------------------------------------------------------
 // table_init
 // ------------------------------------------------------------------------------------------
+// A memset of the table in 16-byte stores: chunk c is word pair (2k, 2k+1) of slot c / (sw / 2),
+// its values from Spec::slot_init (stride_words is even: a power of two >= 2 or a multiple of 8).
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 __global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restrict__ spec, u64* slots, u64 n_slots, u64* counters) {
     const Spec& S = *spec;
     if (counters && blockIdx.x == 0 && threadIdx.x < CNT_WORDS) counters[threadIdx.x] = 0;  // dbg_agg_reset
-    u64 sw = S.stride_words;
-    for (u64 s = blockIdx.x * (u64)BLOCK + threadIdx.x; s < n_slots; s += (u64)gridDim.x * BLOCK) {
-        u64* p = slots + s * sw;
-        p[0] = SLOT_EMPTY;
-        for (u64 w = 1; w < sw; ++w) p[w] = 0;
-        for (int a = 0; a < S.n_aggs; ++a)
-            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+    const u32 half = (u32)S.stride_words / 2;
+    const u64 n_chunks = n_slots * half;
+    v2u64 __attribute__((address_space(1)))* out = (v2u64 __attribute__((address_space(1)))*)slots;
+    if (half == 1) {
+        const v2u64 v = {S.slot_init[0], S.slot_init[1]};
+        for (u64 c = blockIdx.x * (u64)BLOCK + threadIdx.x; c < n_chunks; c += (u64)gridDim.x * BLOCK) out[c] = v;
+        return;
+    }
+    for (u64 c = blockIdx.x * (u64)BLOCK + threadIdx.x; c < n_chunks; c += (u64)gridDim.x * BLOCK) {
+        u32 k = (u32)(c % half);
+        out[c] = v2u64{S.slot_init[2 * k], S.slot_init[2 * k + 1]};
     }
 }
 
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* counters) {
-    u64 n = cap + 1;
+    u64 n = (cap + 1) * (u64)(hspec.stride_words / 2);
     u64 blocks = (n + BLOCK - 1) / BLOCK;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(table_init_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, slots, n, counters);
+    hipLaunchKernelGGL(table_init_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, slots, cap + 1, counters);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1033,20 +1044,30 @@ __global__ void __launch_bounds__(BLOCK) count_groups_kernel(const Spec* __restr
     __shared__ unsigned long long lh[MAX_PARTS_LDS];
     __shared__ unsigned long long ls[DBG_MAX_KEYS][MAX_PARTS_LDS];
     for (u32 p = threadIdx.x; p < n_parts; p += BLOCK) lh[p] = 0;
-    for (u32 p = threadIdx.x; p < DBG_MAX_KEYS * MAX_PARTS_LDS; p += BLOCK) ls[p / MAX_PARTS_LDS][p % MAX_PARTS_LDS] = 0;
+    if (S.has_strings && !S.inline_keys)
+        for (u32 p = threadIdx.x; p < (u32)S.n_keys * MAX_PARTS_LDS; p += BLOCK) ls[p / MAX_PARTS_LDS][p % MAX_PARTS_LDS] = 0;
     __syncthreads();
     u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK;
+    u32 mine = 0;  // n_parts == 1: count in registers, reduce once (no LDS atomics on one word)
     for (u32 k = threadIdx.x; k < SLOTS_PER_BLOCK; k += BLOCK) {
         u64 s = base + k;
         if (s > t.cap) break;
         u64 e = t.slots[s * t.stride_words];
         if (e == SLOT_EMPTY) continue;
         u32 p = 0;
-        if (n_parts > 1) p = part_of(entry_hash(S, batches, e, s == t.cap), n_parts, scheme);
-        atomicAdd(&lh[p], 1ULL);
+        if (n_parts > 1) {
+            p = part_of(entry_hash(S, batches, e, s == t.cap), n_parts, scheme);
+            atomicAdd(&lh[p], 1ULL);
+        } else {
+            mine++;
+        }
         if (S.has_strings && !S.inline_keys)
             for (int c = 0; c < S.n_keys; ++c)
                 if (S.key_types[c].type == DBG_STRING) atomicAdd(&ls[c][p], (unsigned long long)key_str_len(S, batches, e, c));
+    }
+    if (n_parts == 1) {
+        for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, 64);
+        if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&lh[0], (unsigned long long)mine);
     }
     __syncthreads();
     for (u32 p = threadIdx.x; p < n_parts; p += BLOCK) {
@@ -1267,62 +1288,69 @@ __device__ __forceinline__ void write_group(const Spec& S, const BatchDesc* batc
     }
 }
 
+// Slot order within the block: iteration k covers slots base + k*BLOCK + tid (coalesced entry
+// reads); positions come from a block-wide exclusive scan per iteration (wave shuffles + one
+// LDS exchange), with running totals carried across iterations.  Same per-block ownership of
+// slots as count_groups, so the scanned block offsets line up.
 __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                              TableDesc t, const u64* pos, const u64* str_pos, u64 nblocks,
                                                              OutDesc out) {
     const Spec& S = *spec;
-    __shared__ u64 scan[BLOCK];
-    __shared__ u64 sscan[DBG_MAX_KEYS][BLOCK];
-    u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK + (u64)threadIdx.x * SLOTS_PER_THREAD;
-    bool ref_strings = S.has_strings && !S.inline_keys;
-    // pass 1: per-thread counts (groups, string bytes per key column)
-    u64 cnt = 0;
-    u64 sb[DBG_MAX_KEYS];
-    for (int c = 0; c < DBG_MAX_KEYS; ++c) sb[c] = 0;
-    for (int k = 0; k < SLOTS_PER_THREAD; ++k) {
-        u64 s = base + k;
-        if (s > t.cap) break;
-        u64 e = t.slots[s * t.stride_words];
-        if (e == SLOT_EMPTY) continue;
-        cnt++;
-        if (ref_strings)
-            for (int c = 0; c < S.n_keys; ++c)
-                if (S.key_types[c].type == DBG_STRING) sb[c] += key_str_len(S, batches, e, c);
-    }
-    scan[threadIdx.x] = cnt;
-    if (ref_strings)
-        for (int c = 0; c < S.n_keys; ++c) sscan[c][threadIdx.x] = sb[c];
-    __syncthreads();
-    for (int off = 1; off < BLOCK; off <<= 1) {
-        u64 v = threadIdx.x >= (u32)off ? scan[threadIdx.x - off] : 0;
-        u64 vs[DBG_MAX_KEYS];
-        if (ref_strings)
-            for (int c = 0; c < S.n_keys; ++c) vs[c] = threadIdx.x >= (u32)off ? sscan[c][threadIdx.x - off] : 0;
-        __syncthreads();
-        scan[threadIdx.x] += v;
-        if (ref_strings)
-            for (int c = 0; c < S.n_keys; ++c) sscan[c][threadIdx.x] += vs[c];
-        __syncthreads();
-    }
-    u64 p = pos[blockIdx.x] + scan[threadIdx.x] - cnt;
-    u64 sp[DBG_MAX_KEYS];
+    __shared__ u64 wsum[BLOCK / 64][1 + DBG_MAX_KEYS];
+    const bool ref_strings = S.has_strings && !S.inline_keys;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK;
+    u64 run = pos[blockIdx.x];
+    u64 srun[DBG_MAX_KEYS];
     if (ref_strings)
         for (int c = 0; c < S.n_keys; ++c)
-            if (S.key_types[c].type == DBG_STRING) sp[c] = str_pos[(u64)c * nblocks + blockIdx.x] + sscan[c][threadIdx.x] - sb[c];
-    // pass 2: write (guarded by the output capacity: the fused finalize writes before the host
-    // knows the group count, and retries with larger buffers when it was short)
-    for (int k = 0; k < SLOTS_PER_THREAD; ++k) {
-        u64 s = base + k;
-        if (s > t.cap) break;
-        const u64* st = t.slots + s * t.stride_words;
-        u64 e = st[0];
-        if (e == SLOT_EMPTY) continue;
-        if (p >= out.cap_groups) break;
-        write_group(S, batches, t, s, st, e, p, sp, out);
-        p++;
+            srun[c] = S.key_types[c].type == DBG_STRING ? str_pos[(u64)c * nblocks + blockIdx.x] : 0;
+    auto wave_incl = [&](u64 v) {
+        for (int off = 1; off < 64; off <<= 1) {
+            u64 o = __shfl_up(v, off, 64);
+            if (lane >= off) v += o;
+        }
+        return v;
+    };
+    for (u32 k = 0; k < SLOTS_PER_THREAD; ++k) {
+        if (base + (u64)k * BLOCK > t.cap) break;  // uniform
+        const u64 s = base + (u64)k * BLOCK + threadIdx.x;
+        const bool in = s <= t.cap;
+        const u64* st = t.slots + (in ? s : 0) * t.stride_words;
+        const u64 e = in ? st[0] : SLOT_EMPTY;
+        const u64 cnt = e != SLOT_EMPTY ? 1 : 0;
+        u64 sb[DBG_MAX_KEYS];
+        const u64 ic = wave_incl(cnt);
+        if (lane == 63) wsum[wave][0] = ic;
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c) {
+                sb[c] = (cnt && S.key_types[c].type == DBG_STRING) ? key_str_len(S, batches, e, c) : 0;
+                u64 is = wave_incl(sb[c]);
+                if (lane == 63) wsum[wave][1 + c] = is;
+                sb[c] = is - sb[c];  // exclusive within the wave
+            }
+        __syncthreads();
+        u64 p = run + ic - cnt, tot = 0;
+        for (int w = 0; w < BLOCK / 64; ++w) {
+            if (w < wave) p += wsum[w][0];
+            tot += wsum[w][0];
+        }
+        u64 sp[DBG_MAX_KEYS];
+        if (ref_strings)
+            for (int c = 0; c < S.n_keys; ++c) {
+                sp[c] = srun[c] + sb[c];
+                u64 stot = 0;
+                for (int w = 0; w < BLOCK / 64; ++w) {
+                    if (w < wave) sp[c] += wsum[w][1 + c];
+                    stot += wsum[w][1 + c];
+                }
+                srun[c] += stot;
+            }
+        __syncthreads();
+        run += tot;
+        if (cnt && p < out.cap_groups) write_group(S, batches, t, s, st, e, p, sp, out);
     }
 }
-
 
 // ------------------------------------------------------------------------------------------
 // finalize_small: count + scan + write + validity bits + string offsets in ONE workgroup, for

@@ -29,6 +29,7 @@ struct Spec {
     uint32_t rec_val_off[DBG_MAX_KEYS];  // byte offset of the validity byte
     uint32_t rec_state_off;
     DAgg aggs[DBG_MAX_AGGS];
+    u64 slot_init[DBG_MAX_WORDS];  // initial value of every slot word (EMPTY entry, MIN/MAX identities)
 };
 
 struct BatchDesc {
