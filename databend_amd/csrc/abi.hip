@@ -722,7 +722,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     }
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
     u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
-    RETURN_IF(ensure_ovf(h, rows, blocks * 4096));
+    RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
     {
         prof::Scope ps("agg_insert", h->stream);
         launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st);

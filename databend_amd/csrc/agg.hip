@@ -23,6 +23,7 @@
 #define SLOTS_PER_BLOCK (BLOCK * SLOTS_PER_THREAD)
 #define LDS_BUDGET_BYTES (32 * 1024)
 #define LDS_PROBE_CAP 64
+#define FLUSH_ROUND 16  // rounds of BLOCK rows between checks for a full LDS table
 
 // Slot placement for inline keys: any good mixer works (placement is not observable); the
 // reference hash is recomputed from the key wherever routing needs it.
@@ -464,7 +465,28 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
     u64 r0 = (u64)blockIdx.x * rows_per_block;
     u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
     u32 my_claims = 0;
-    for (u64 i = r0 + threadIdx.x; i < r1; i += BLOCK) {
+    const u64 n_iter = r1 > r0 ? (r1 - r0 + BLOCK - 1) / BLOCK : 0;
+    for (u64 it = 0; it < n_iter; ++it) {
+        // Every FLUSH_ROUND rounds: a full LDS table is flushed to HBM and started over (the
+        // reference's clear_ht of a full partial table, aggregate_hashtable.rs:225-239), so hot
+        // keys of a skewed stream keep being combined here instead of hammering one HBM slot.
+        if (it && (it % FLUSH_ROUND) == 0) {
+            // (not once the HBM table overflows: the deferred-overflow lists are sized for two
+            // flushes of every workgroup's table).  Thread 0 decides, so the branch is uniform.
+            __shared__ u32 do_flush;
+            if (threadIdx.x == 0)
+                do_flush = lcount[0] >= llimit && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+            __syncthreads();
+            if (do_flush) {
+                flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, BLOCK, t, my_claims);
+                __syncthreads();
+                lds_table_init(S, lds, lds_slots, sw, BLOCK);
+                if (threadIdx.x == 0) lcount[0] = 0;
+                __syncthreads();
+            }
+        }
+        const u64 i = r0 + it * BLOCK + threadIdx.x;
+        if (i >= r1) continue;
         if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
         u64 h, key;
         if (RECORDS) {
