@@ -477,7 +477,9 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
             if (threadIdx.x == 0)
                 do_flush = lcount[0] >= llimit && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
             __syncthreads();
-            if (do_flush) {
+            const bool flush_now = do_flush;
+            __syncthreads();  // everyone has read the flag before thread 0 may rewrite it
+            if (flush_now) {
                 flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, BLOCK, t, my_claims);
                 __syncthreads();
                 lds_table_init(S, lds, lds_slots, sw, BLOCK);
