@@ -91,94 +91,122 @@ __device__ __forceinline__ u64 entry_hash(const Spec& S, const BatchDesc* batche
 }
 
 // ------------------------------------------------------------------------------------------
-// State updates (LDS or HBM — the same code, address space inferred after inlining)
+// State updates on an LDS (AS_LDS) or HBM (AS_GLB) slot.  The address space is a template
+// parameter, never inferred: a slot pointer that may be either (a phi of the LDS and the HBM
+// branch) compiles to FLAT atomics, which count against vmcnt as well as lgkmcnt — every LDS
+// wait then drains all global loads in flight and the streaming pipeline collapses.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void add128(u64* p, u64 lo, u64 hi) {
-    u64 old = atomicAdd((unsigned long long*)p, (unsigned long long)lo);
+#define AS_GLB 1
+#define AS_LDS 3
+template <int AS> using wptr = __attribute__((address_space(AS))) u64*;
+template <int AS> using sptr = __attribute__((address_space(AS))) long long*;
+template <int AS> using dptr = __attribute__((address_space(AS))) double*;
+template <int AS> using vwptr = volatile __attribute__((address_space(AS))) u64*;
+template <int AS> __device__ __forceinline__ wptr<AS> asp(u64* p) { return (wptr<AS>)p; }
+template <int AS> __device__ __forceinline__ wptr<AS> asp(const u64* p) { return (wptr<AS>)(u64*)p; }
+#define AT_SCOPE(AS) ((AS) == AS_LDS ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT)
+template <int AS> __device__ __forceinline__ u64 at_add(wptr<AS> p, u64 v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+}
+template <int AS> __device__ __forceinline__ void at_addf(wptr<AS> p, double v) {
+    __hip_atomic_fetch_add((dptr<AS>)p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+}
+template <int AS> __device__ __forceinline__ void at_or(wptr<AS> p, u64 v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+}
+template <int AS> __device__ __forceinline__ void at_minmax(wptr<AS> p, u64 v, bool mn, bool sgn) {
+    if (sgn) {
+        if (mn) __hip_atomic_fetch_min((sptr<AS>)p, (long long)v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        else __hip_atomic_fetch_max((sptr<AS>)p, (long long)v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+    } else {
+        if (mn) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        else __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+    }
+}
+template <int AS> __device__ __forceinline__ u64 at_cas(wptr<AS> p, u64 expected, u64 desired) {
+    __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AT_SCOPE(AS));
+    return expected;  // the old value (== the expected one iff the exchange happened)
+}
+template <int AS> __device__ __forceinline__ u64 vld(wptr<AS> p) { return *(vwptr<AS>)p; }
+
+template <int AS>
+__device__ __forceinline__ void add128(wptr<AS> p, u64 lo, u64 hi) {
+    u64 old = at_add<AS>(p, lo);
     u64 carry = (old + lo) < old ? 1ULL : 0ULL;
     u64 h = hi + carry;
-    if (h) atomicAdd((unsigned long long*)(p + 1), (unsigned long long)h);
+    if (h) at_add<AS>(p + 1, h);
 }
 
-__device__ __forceinline__ void set_flag(u64* st, int fw, int bit) {
+template <int AS>
+__device__ __forceinline__ void set_flag(wptr<AS> st, int fw, int bit) {
     u64 m = 1ULL << bit;
-    if (!(st[fw] & m)) atomicOr((unsigned long long*)(st + fw), (unsigned long long)m);
+    if (!(st[fw] & m)) at_or<AS>(st + fw, m);
 }
 
 // accumulate_keys of every aggregate for input row i into the slot at st (word 0 = entry).
-__device__ __forceinline__ void apply_row(const Spec& S, u64* st, const BatchDesc& B, u64 i) {
+template <int AS>
+__device__ __forceinline__ void apply_row(const Spec& S, wptr<AS> st, const BatchDesc& B, u64 i) {
     for (int a = 0; a < S.n_aggs; ++a) {
         const DAgg& A = S.aggs[a];
         const DCol& c = B.args[a];
         if (A.arg_type >= 0 && A.arg_nullable && !dcol_valid(c, i)) continue;
-        u64* w = st + A.w0;
+        wptr<AS> w = st + A.w0;
         switch (A.kind) {
-            case DBG_AGG_COUNT: atomicAdd((unsigned long long*)w, 1ULL); break;
+            case DBG_AGG_COUNT: at_add<AS>(w, 1ULL); break;
             case DBG_AGG_SUM: case DBG_AGG_AVG: {
-                if (A.sumk == SUMK_I64) atomicAdd((unsigned long long*)w, (unsigned long long)dcol_i64(c, i));
-                else if (A.sumk == SUMK_F64) atomicAdd((double*)w, dcol_f64(c, i));
-                else add128(w, dcol_bits(c, i), dcol_hi(c, i));
-                if (A.kind == DBG_AGG_AVG) atomicAdd((unsigned long long*)(w + (A.sumk == SUMK_I128 ? 2 : 1)), 1ULL);
+                if (A.sumk == SUMK_I64) at_add<AS>(w, (u64)dcol_i64(c, i));
+                else if (A.sumk == SUMK_F64) at_addf<AS>(w, dcol_f64(c, i));
+                else add128<AS>(w, dcol_bits(c, i), dcol_hi(c, i));
+                if (A.kind == DBG_AGG_AVG) at_add<AS>(w + (A.sumk == SUMK_I128 ? 2 : 1), 1ULL);
                 break;
             }
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 bool mn = A.kind == DBG_AGG_MIN;
-                if (A.mmk == MMK_I64) {
-                    long long x = (long long)dcol_i64(c, i);
-                    if (mn) atomicMin((long long*)w, x); else atomicMax((long long*)w, x);
-                } else {
-                    unsigned long long x = A.mmk == MMK_U64 ? (unsigned long long)dcol_bits(c, i)
-                                                            : (unsigned long long)f64_order_key(dcol_f64(c, i));
-                    if (mn) atomicMin((unsigned long long*)w, x); else atomicMax((unsigned long long*)w, x);
-                }
+                if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)dcol_i64(c, i), mn, true);
+                else at_minmax<AS>(w, A.mmk == MMK_U64 ? dcol_bits(c, i) : f64_order_key(dcol_f64(c, i)), mn, false);
                 break;
             }
         }
-        if (A.flag_bit >= 0) set_flag(st, S.flags_word, A.flag_bit);
+        if (A.flag_bit >= 0) set_flag<AS>(st, S.flags_word, A.flag_bit);
     }
 }
 
 // merge_states of a partial state (word array r, same layout) into st.  SC1: read r with sc1
 // loads (words parked by another workgroup in this launch, see block_flush).
 __device__ __forceinline__ u64 ld_sc1(const u64* p) {
-    return __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load((wptr<AS_GLB>)(u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <bool SC1 = false>
-__device__ __forceinline__ u64 rdw(const u64* p) { return SC1 ? ld_sc1(p) : *p; }
+// RAS: address space of r (LDS table rows being flushed, or global records / parked rows)
+template <bool SC1, int RAS>
+__device__ __forceinline__ u64 rdw(const u64* p) { return SC1 ? ld_sc1(p) : *asp<RAS>(p); }
 
-template <bool SC1 = false>
-__device__ __forceinline__ void apply_state(const Spec& S, u64* st, const u64* r) {
+template <int AS, bool SC1 = false, int RAS = AS_GLB>
+__device__ __forceinline__ void apply_state(const Spec& S, wptr<AS> st, const u64* r) {
     for (int a = 0; a < S.n_aggs; ++a) {
         const DAgg& A = S.aggs[a];
-        u64* w = st + A.w0;
+        wptr<AS> w = st + A.w0;
         const u64* x = r + A.w0;
-        const u64 x0 = rdw<SC1>(x);
+        const u64 x0 = rdw<SC1, RAS>(x);
         switch (A.kind) {
-            case DBG_AGG_COUNT: if (x0) atomicAdd((unsigned long long*)w, (unsigned long long)x0); break;
+            case DBG_AGG_COUNT: if (x0) at_add<AS>(w, x0); break;
             case DBG_AGG_SUM: case DBG_AGG_AVG: {
-                if (A.sumk == SUMK_I64) { if (x0) atomicAdd((unsigned long long*)w, (unsigned long long)x0); }
-                else if (A.sumk == SUMK_F64) atomicAdd((double*)w, __longlong_as_double((long long)x0));
-                else add128(w, x0, rdw<SC1>(x + 1));
+                if (A.sumk == SUMK_I64) { if (x0) at_add<AS>(w, x0); }
+                else if (A.sumk == SUMK_F64) at_addf<AS>(w, __longlong_as_double((long long)x0));
+                else add128<AS>(w, x0, rdw<SC1, RAS>(x + 1));
                 if (A.kind == DBG_AGG_AVG) {
                     int k = A.sumk == SUMK_I128 ? 2 : 1;
-                    u64 xk = rdw<SC1>(x + k);
-                    if (xk) atomicAdd((unsigned long long*)(w + k), (unsigned long long)xk);
+                    u64 xk = rdw<SC1, RAS>(x + k);
+                    if (xk) at_add<AS>(w + k, xk);
                 }
                 break;
             }
-            case DBG_AGG_MIN:
-                if (A.mmk == MMK_I64) atomicMin((long long*)w, (long long)x0);
-                else atomicMin((unsigned long long*)w, (unsigned long long)x0);
-                break;
-            case DBG_AGG_MAX:
-                if (A.mmk == MMK_I64) atomicMax((long long*)w, (long long)x0);
-                else atomicMax((unsigned long long*)w, (unsigned long long)x0);
-                break;
+            case DBG_AGG_MIN: at_minmax<AS>(w, x0, true, A.mmk == MMK_I64); break;
+            case DBG_AGG_MAX: at_minmax<AS>(w, x0, false, A.mmk == MMK_I64); break;
         }
     }
     if (S.flags_word >= 0) {
-        u64 f = rdw<SC1>(r + S.flags_word);
-        if (f) atomicOr((unsigned long long*)(st + S.flags_word), (unsigned long long)f);
+        u64 f = rdw<SC1, RAS>(r + S.flags_word);
+        if (f) at_or<AS>(st + S.flags_word, f);
     }
 }
 
@@ -192,18 +220,17 @@ __device__ __forceinline__ u64 g_find(const Spec& S, const BatchDesc* batches, c
                                       u64 h, const TableDesc& t, u32 probe_limit, bool& claimed) {
     claimed = false;
     if (INLINE && key == SLOT_EMPTY) {  // only possible for 8-byte packed keys: sentinel slot
-        u64* e = t.slots + t.cap * t.stride_words;
-        u64 old = atomicCAS((unsigned long long*)e, SLOT_EMPTY, 0ULL);
+        u64 old = at_cas<AS_GLB>(asp<AS_GLB>(t.slots + t.cap * t.stride_words), SLOT_EMPTY, 0ULL);
         claimed = old == SLOT_EMPTY;
         return t.cap;
     }
     u64 mask = t.cap - 1;
     u64 s = (INLINE ? slot_mix(key) : (h >> 16)) & mask;
     for (u32 p = 0; p < probe_limit; ++p) {
-        u64* e = t.slots + s * t.stride_words;
-        u64 ev = *(volatile u64*)e;
+        wptr<AS_GLB> e = asp<AS_GLB>(t.slots + s * t.stride_words);
+        u64 ev = vld<AS_GLB>(e);
         if (ev == SLOT_EMPTY) {
-            u64 old = atomicCAS((unsigned long long*)e, SLOT_EMPTY, (unsigned long long)key);
+            u64 old = at_cas<AS_GLB>(e, SLOT_EMPTY, key);
             if (old == SLOT_EMPTY) {
                 claimed = true;
                 return s;
@@ -238,15 +265,17 @@ __device__ __forceinline__ int lds_find(const Spec& S, const BatchDesc* batches,
     // Once the table is full (high cardinality), a key found within two probes is staged, any
     // other goes straight to HBM: a long probe through a full table of other keys is wasted LDS
     // traffic.  A key may then hold state both here and in HBM; the flush merges them.
-    const int cap = *(volatile u32*)lcount >= llimit ? 2 : LDS_PROBE_CAP;
+    volatile __attribute__((address_space(3))) u32* lc = (volatile __attribute__((address_space(3))) u32*)lcount;
+    const int cap = *lc >= llimit ? 2 : LDS_PROBE_CAP;
     for (int p = 0; p < cap; ++p) {
-        u64* e = lds + (u64)s * sw;
-        u64 ev = *(volatile u64*)e;
+        wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)s * sw);
+        u64 ev = vld<AS_LDS>(e);
         if (ev == SLOT_EMPTY) {
-            if (*(volatile u32*)lcount >= llimit) return -1;
-            u64 old = atomicCAS((unsigned long long*)e, SLOT_EMPTY, (unsigned long long)key);
+            if (*lc >= llimit) return -1;
+            u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
             if (old == SLOT_EMPTY) {
-                atomicAdd(lcount, 1u);
+                __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                 return (int)s;
             }
             ev = old;
@@ -266,7 +295,7 @@ __device__ __forceinline__ void push_ovf_row(const TableDesc& t, u32 bid, u64 ro
     if (k < t.ovf_rows_cap) t.ovf_rows[k] = ((u64)bid << 32) | row;
     else atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
 }
-template <bool SC1 = false>
+template <bool SC1 = false, int RAS = AS_GLB>
 __device__ __forceinline__ void push_ovf_rec(const Spec& S, const TableDesc& t, u64 key, const u64* words) {
     u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), 1ULL);
     if (k >= t.ovf_recs_cap) {
@@ -275,7 +304,7 @@ __device__ __forceinline__ void push_ovf_rec(const Spec& S, const TableDesc& t, 
     }
     u64* r = t.ovf_recs + k * t.stride_words;
     r[0] = key;
-    for (int w = 1; w <= S.n_words; ++w) r[w] = rdw<SC1>(words + w);
+    for (int w = 1; w <= S.n_words; ++w) r[w] = rdw<SC1, RAS>(words + w);
 }
 
 
@@ -296,7 +325,7 @@ __device__ __forceinline__ void st_sc1(u64* p, u64 v) {
 template <bool INLINE, bool RECORDS>
 __device__ __forceinline__ u64 lds_entry_hash(const Spec& S, const BatchDesc& B, u64 e) {
     if (INLINE) return 0;
-    if (RECORDS) return *(const u64*)(B.rec_base + (u64)ref_row(e) * B.rec_width);
+    if (RECORDS) return gld<u64>(B.rec_base + (u64)ref_row(e) * B.rec_width);
     return group_hash(B.keys, S.n_keys, ref_row(e));
 }
 
@@ -311,11 +340,11 @@ __device__ __forceinline__ void flush_lds_direct(const Spec& S, const BatchDesc*
         bool claimed;
         u64 gs = g_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, t, t.probe_limit, claimed);
         if (gs == ~0ULL) {
-            push_ovf_rec(S, t, e, p);
+            push_ovf_rec<false, AS_LDS>(S, t, e, p);
             continue;
         }
         my_claims += claimed ? 1 : 0;
-        apply_state(S, t.slots + gs * t.stride_words, p);
+        apply_state<AS_GLB, false, AS_LDS>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), p);
     }
 }
 
@@ -390,7 +419,7 @@ __device__ __forceinline__ void block_flush(const Spec& S, const BatchDesc* batc
                 u64 h = lds_entry_hash<INLINE, RECORDS>(S, B, e);
                 int ls = lds_find<INLINE>(S, batches, B.keys, INLINE ? 0 : ref_row(e), e, h, lds, lmask, sw, lcount, llimit);
                 if (ls >= 0) {
-                    apply_state<true>(S, lds + (u64)ls * sw, r);
+                    apply_state<AS_LDS, true>(S, asp<AS_LDS>(lds + (u64)ls * sw), r);
                     continue;
                 }
                 bool claimed;
@@ -400,7 +429,7 @@ __device__ __forceinline__ void block_flush(const Spec& S, const BatchDesc* batc
                     continue;
                 }
                 my_claims += claimed ? 1 : 0;
-                apply_state<true>(S, t.slots + gs * t.stride_words, r);
+                apply_state<AS_GLB, true>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), r);
             }
             __syncthreads();
             flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, nt, t, my_claims);
@@ -492,7 +521,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
         u64 h, key;
         if (RECORDS) {
-            h = *(const u64*)(B.rec_base + i * (u64)B.rec_width);
+            h = gld<u64>(B.rec_base + i * (u64)B.rec_width);
         } else if (INLINE) {
             h = 0;
         } else {
@@ -502,21 +531,23 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         else key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
 
         int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
-        u64* st;
+        const u64* rec = RECORDS ? (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1 : nullptr;
         if (ls >= 0) {
-            st = lds + (u64)ls * sw;
-        } else {
-            bool claimed;
-            u64 gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, t.probe_limit, claimed);
-            if (gs == ~0ULL) {
-                push_ovf_row(t, bid, i);
-                continue;
-            }
-            my_claims += claimed ? 1 : 0;
-            st = t.slots + gs * t.stride_words;
+            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
+            if (RECORDS) apply_state<AS_LDS>(S, st, rec);
+            else apply_row<AS_LDS>(S, st, B, i);
+            continue;
         }
-        if (RECORDS) apply_state(S, st, (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1);
-        else apply_row(S, st, B, i);
+        bool claimed;
+        u64 gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_row(t, bid, i);
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        wptr<AS_GLB> st = asp<AS_GLB>(t.slots + gs * t.stride_words);
+        if (RECORDS) apply_state<AS_GLB>(S, st, rec);
+        else apply_row<AS_GLB>(S, st, B, i);
     }
     __syncthreads();
     block_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
@@ -576,7 +607,7 @@ __device__ __forceinline__ T vget(const v4u& y, int j) {
 // leave 63 of 64 lanes idle on every LDS round trip.
 #define WQ 128  // queue entries per wave
 
-template <typename T, bool PRED, int NT>
+template <typename T, bool PRED, int NT, bool PF>
 __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                u32 bid, u64 rows, TableDesc t, u32 lds_slots,
                                                                T lo, T hi, int negate, int count_only, int xmode) {
@@ -604,39 +635,36 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     // stage one selected row (key bits, row index) — all callers have full or near-full lanes
     auto process = [&](u64 key, u64 i) {
         int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
-        u64* st;
         if (ls >= 0) {
-            st = lds + (u64)ls * sw;
-            if (count_only) {
-                atomicAdd((unsigned long long*)(st + 1), 1ULL);
-                return;
-            }
-        } else {
-            bool claimed;
-            u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
-            if (gs == ~0ULL) {
-                push_ovf_row(t, bid, i);
-                return;
-            }
-            my_claims += claimed ? 1 : 0;
-            st = t.slots + gs * t.stride_words;
+            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
+            if (count_only) at_add<AS_LDS>(st + 1, 1ULL);
+            else apply_row<AS_LDS>(S, st, B, i);
+            return;
         }
-        apply_row(S, st, B, i);
+        bool claimed;
+        u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_row(t, bid, i);
+            return;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
     };
 
     u32 qn = 0;  // wave-uniform queue length
     auto drain64 = [&]() {  // process entries [0, 64), shift [64, qn) down
-        u64 k = ((volatile u64*)qkey)[lane], r = ((volatile u64*)qrow)[lane];
+        vwptr<AS_LDS> qk = (vwptr<AS_LDS>)qkey, qr = (vwptr<AS_LDS>)qrow;
+        u64 k = qk[lane], r = qr[lane];
         u64 k2 = 0, r2 = 0;
         bool mv = lane + 64 < (int)qn;
         if (mv) {
-            k2 = ((volatile u64*)qkey)[lane + 64];
-            r2 = ((volatile u64*)qrow)[lane + 64];
+            k2 = qk[lane + 64];
+            r2 = qr[lane + 64];
         }
         __builtin_amdgcn_wave_barrier();
         if (mv) {
-            ((volatile u64*)qkey)[lane] = k2;
-            ((volatile u64*)qrow)[lane] = r2;
+            qk[lane] = k2;
+            qr[lane] = r2;
         }
         __builtin_amdgcn_wave_barrier();
         qn -= 64;
@@ -727,28 +755,59 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     u64 k = (u64)blockIdx.x * NT + threadIdx.x;
     const u64 step = (u64)FAST_UNROLL * gstride;
     const u64 lastv = nvec ? nvec - 1 : 0;
-    while (__ballot(k < nvec) != 0) {
-        v4u y[FAST_UNROLL];
-        u64 bases[FAST_UNROLL];
-        u32 actm = 0;
+    if (PF) {
+        // Software pipeline: the next round's FAST_UNROLL loads are issued before this round is
+        // filtered and staged, so a wave busy in the LDS queue still has 64 B/lane in flight.
+        v4u y[FAST_UNROLL], yn[FAST_UNROLL];
 #pragma unroll
         for (int u = 0; u < FAST_UNROLL; ++u) {
             u64 idx = k + u * gstride;
-            actm |= (idx < nvec ? 1u : 0u) << u;
             y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
-            bases[u] = idx * V;
         }
-        handle_group(y, bases, FAST_UNROLL, actm);
-        k += step;
+        while (__ballot(k < nvec) != 0) {
+            const u64 kn = k + step;
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u64 idx = kn + u * gstride;
+                yn[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+            }
+            u64 bases[FAST_UNROLL];
+            u32 actm = 0;
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u64 idx = k + u * gstride;
+                actm |= (idx < nvec ? 1u : 0u) << u;
+                bases[u] = idx * V;
+            }
+            handle_group(y, bases, FAST_UNROLL, actm);
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
+            k = kn;
+        }
+    } else {
+        while (__ballot(k < nvec) != 0) {
+            v4u y[FAST_UNROLL];
+            u64 bases[FAST_UNROLL];
+            u32 actm = 0;
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u64 idx = k + u * gstride;
+                actm |= (idx < nvec ? 1u : 0u) << u;
+                y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+                bases[u] = idx * V;
+            }
+            handle_group(y, bases, FAST_UNROLL, actm);
+            k += step;
+        }
     }
     // drain the queue's rest (< 64 entries): lanes below qn take one each
     if (PRED && qn) {
         __builtin_amdgcn_wave_barrier();
-        if (lane < (int)qn) process(((volatile u64*)qkey)[lane], ((volatile u64*)qrow)[lane]);
+        if (lane < (int)qn) process(((vwptr<AS_LDS>)qkey)[lane], ((vwptr<AS_LDS>)qrow)[lane]);
         qn = 0;
     }
     for (u64 i = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; i < rows; i += gstride) {
-        T v = col[i];
+        T v = gld<T>(col + i);
         if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
     }
     if (xmode) asm volatile("" ::"v"(sink));
@@ -787,24 +846,20 @@ __global__ void __launch_bounds__(NT) agg_insert_sel_kernel(const Spec* __restri
     using UT = typename std::make_unsigned<T>::type;
     auto process = [&](u64 key, u64 i) {
         int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
-        u64* st;
         if (ls >= 0) {
-            st = lds + (u64)ls * sw;
-            if (count_only) {
-                atomicAdd((unsigned long long*)(st + 1), 1ULL);
-                return;
-            }
-        } else {
-            bool claimed;
-            u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
-            if (gs == ~0ULL) {
-                push_ovf_row(t, bid, i);
-                return;
-            }
-            my_claims += claimed ? 1 : 0;
-            st = t.slots + gs * t.stride_words;
+            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
+            if (count_only) at_add<AS_LDS>(st + 1, 1ULL);
+            else apply_row<AS_LDS>(S, st, B, i);
+            return;
         }
-        apply_row(S, st, B, i);
+        bool claimed;
+        u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_row(t, bid, i);
+            return;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
     };
     auto handle = [&](const v4u& y, u64 vi) {
         u32 m = 0;
@@ -833,7 +888,7 @@ __global__ void __launch_bounds__(NT) agg_insert_sel_kernel(const Spec* __restri
     for (; i < nvec; i += stride) handle(__builtin_nontemporal_load(vp + i), i);
     // ragged tail (< V rows)
     for (u64 r = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; r < rows; r += stride) {
-        T v = col[r];
+        T v = gld<T>(col + r);
         if (((v >= lo) & (v <= hi)) ^ (negate != 0)) process((u64)(UT)v, r);
     }
     __syncthreads();
@@ -881,13 +936,16 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
-#define FAST_LAUNCH(P, N)                                                                                                     \
-    hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, lslots, \
-                       (T)lo, (T)hi, neg, count_only, xmode)
+    static const int pf = getenv("DBG_FAST_PF") ? atoi(getenv("DBG_FAST_PF")) : 1;  // A/B knob: 0 = no prefetch
+#define FAST_LAUNCH(P, N, F)                                                                                                  \
+    hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, \
+                       lslots, (T)lo, (T)hi, neg, count_only, xmode)
     if (nt == 512) {
-        if (pred) FAST_LAUNCH(true, 512); else FAST_LAUNCH(false, 512);
+        if (pred) FAST_LAUNCH(true, 512, true); else FAST_LAUNCH(false, 512, true);
+    } else if (pf) {
+        if (pred) FAST_LAUNCH(true, 1024, true); else FAST_LAUNCH(false, 1024, true);
     } else {
-        if (pred) FAST_LAUNCH(true, 1024); else FAST_LAUNCH(false, 1024);
+        if (pred) FAST_LAUNCH(true, 1024, false); else FAST_LAUNCH(false, 1024, false);
     }
 #undef FAST_LAUNCH
 }
@@ -963,7 +1021,7 @@ __global__ void __launch_bounds__(BLOCK) agg_retry_kernel(const Spec* __restrict
             u64 i = (u32)it;
             const BatchDesc& B = batches[bid];
             u64 h, key;
-            if (B.is_records) h = *(const u64*)(B.rec_base + i * (u64)B.rec_width);
+            if (B.is_records) h = gld<u64>(B.rec_base + i * (u64)B.rec_width);
             else h = INLINE ? 0 : group_hash(B.keys, S.n_keys, i);
             key = INLINE ? pack_key(S, B.keys, i) : ((h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i);
             gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, (u32)(t.cap < 0xFFFFFFFFull ? t.cap : 0xFFFFFFFFull), claimed);
@@ -971,23 +1029,23 @@ __global__ void __launch_bounds__(BLOCK) agg_retry_kernel(const Spec* __restrict
                 atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
                 continue;
             }
-            u64* st = t.slots + gs * t.stride_words;
-            if (B.is_records) apply_state(S, st, (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1);
-            else apply_row(S, st, B, i);
+            wptr<AS_GLB> st = asp<AS_GLB>(t.slots + gs * t.stride_words);
+            if (B.is_records) apply_state<AS_GLB>(S, st, (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1);
+            else apply_row<AS_GLB>(S, st, B, i);
         } else {
             const u64* r = recs_list + (k - n_rows) * t.stride_words;
             u64 key = r[0];
             u64 h = 0;
             if (!INLINE) {
                 const BatchDesc& B = batches[ref_bid(key)];
-                h = B.is_records ? *(const u64*)(B.rec_base + (u64)ref_row(key) * B.rec_width) : group_hash(B.keys, S.n_keys, ref_row(key));
+                h = B.is_records ? gld<u64>(B.rec_base + (u64)ref_row(key) * B.rec_width) : group_hash(B.keys, S.n_keys, ref_row(key));
             }
             gs = g_find_entry<INLINE>(S, batches, key, h, t, (u32)(t.cap < 0xFFFFFFFFull ? t.cap : 0xFFFFFFFFull), claimed);
             if (gs == ~0ULL) {
                 atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
                 continue;
             }
-            apply_state(S, t.slots + gs * t.stride_words, r);
+            apply_state<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), r);
         }
         if (claimed) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), 1ULL);
     }
