@@ -90,7 +90,8 @@ def main():
 
     from databend_amd import ffi
     from databend_amd.aggregator import AggregateHashTable, HashTableConfig
-    from databend_amd.exchange import exchange_partial
+    from databend_amd import abi
+    from databend_amd.exchange import exchange_partial, gather_small
     from databend_amd.workloads import DEFAULT_ROWS, SHAPES, ConfigRunner, algorithmic_bytes
 
     cfg = args.config
@@ -104,12 +105,23 @@ def main():
     # every rank aggregates disjoint row ranges of the same generator
     runner = ConfigRunner(cfg, rows, copies=copies, capacity_hint=args.capacity_hint, start=rank * copies * rows)
     final = None
+    small = False
     if world > 1:
         final = AggregateHashTable(runner.params, HashTableConfig(False, args.capacity_hint))
+        ffi.check(ffi.lib().dbg_agg_set_recycle(final.h, 1))
+        # low cardinality: replicas + gather to rank 0 over one RCCL all-gather;
+        # otherwise partial states routed by hash % N with all-to-all (exchange_partial)
+        small = bool(shape.keys) and all(runner.inputs[0][k].dtype.width in (1, 2, 4, 8) and
+                                         runner.inputs[0][k].dtype.type_id != abi.STRING for k in shape.keys) \
+            and len(shape.keys) == 1 and runner.table.capacity <= 8192
 
     def step(k):
         if world == 1:
             return runner.step(k)
+        if small:
+            runner.insert(k)
+            gather_small(runner.table, final, dev, root=0)
+            return runner.finalize_into(final.h) if rank == 0 else 0
         i = k % len(runner.inputs)
         t = runner.table
         t.reset()
@@ -156,6 +168,7 @@ def main():
         n_groups = runner.n_groups
         kstr = runner.key_string_bytes
     else:
+        runner.insert(0)  # (untimed) this rank's partial of copy 0, for the byte accounting
         n_groups = runner.table.finalize()[0]
         kstr = 0
         keys_h, aggs_h = None, None

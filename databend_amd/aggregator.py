@@ -133,6 +133,9 @@ class AggregateHashTable:
 
     def reset(self):
         check(lib().dbg_agg_reset(self.h))
+        # retained device inputs may go: later reuse of their memory is stream-ordered after
+        # every launch that reads them (the handle runs on torch's current stream)
+        self._retained.clear()
         self._retained.clear()
 
     # ---- AggregateHashTable::add_groups (+ fused filter)
@@ -226,6 +229,22 @@ class AggregateHashTable:
         check(lib().dbg_agg_merge_records(self.h, dev_records.data_ptr(),
                                           dev_strings.data_ptr() if dev_strings is not None else None, n, sr, ss))
         self._retained.append((dev_records, dev_strings))
+
+    # ---- fixed-capacity exchange (low cardinality: replicas + gather)
+    @property
+    def capacity(self) -> int:
+        cap = C.c_uint64()
+        check(lib().dbg_agg_capacity(self.h, C.byref(cap)))
+        return cap.value
+
+    def export_fixed(self, dev_buf, cap_records: int):
+        """Write this table's groups into dev_buf ((cap_records + 1) * record_width bytes), the
+        group count staying on the device (include/dbgpu_agg.h, dbg_agg_export_fixed)."""
+        check(lib().dbg_agg_export_fixed(self.h, dev_buf.data_ptr(), cap_records))
+
+    def merge_fixed(self, dev_bufs, n_bufs: int, cap_records: int):
+        check(lib().dbg_agg_merge_fixed(self.h, dev_bufs.data_ptr(), n_bufs, cap_records))
+        self._retained.append(dev_bufs)
 
 
 @dataclass

@@ -13,6 +13,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <chrono>
 
 #include "agg.hpp"
 #include "filter.hpp"
@@ -170,6 +171,11 @@ struct dbg_agg_handle {
     // fused finalize: validity bytes staging
     u8* vbytes = nullptr;
     u64 vbytes_cap = 0;
+    // recycle mode (dbg_agg_set_recycle): a small-table finalize_into leaves the table empty
+    int recycle = 0;
+    bool clean = false;           // table already re-initialised by the last finalize
+    u64 fin_seq = 0;              // sequence number the finalize kernel posts to host_mirror
+    bool uploads_pending = false; // descriptor uploads from pinned staging since the last sync
 };
 
 static int dev_alloc(void** p, size_t bytes) {
@@ -462,7 +468,33 @@ static u64 desc_hash(const BatchDesc& d) {
 
 static int upload_batch(dbg_agg_handle* h, BatchDesc* st, u32 bid) {
     HIPCHECK(hipMemcpyAsync(h->dbatches + bid, st, sizeof(BatchDesc), hipMemcpyHostToDevice, h->stream));
+    h->uploads_pending = true;
     return DBG_OK;
+}
+
+// Upload a filled batch descriptor, or reuse an identical cached one (device-resident inputs
+// only: the descriptor is then pointers alone and immutable).  A cache hit needs no upload, so
+// a steady stream of re-submitted device batches never forces dbg_agg_reset to synchronise.
+static int submit_batch(dbg_agg_handle* h, BatchDesc** pst, u32* pbid, bool cacheable) {
+    BatchDesc* st = *pst;
+    u32 bid = *pbid;
+    if (cacheable && bid == h->n_cached + 1 && h->desc_cache.size() < 64) {
+        u64 hv = desc_hash(*st);
+        u32 hit = 0;
+        for (u32 k = 0; k < h->desc_cache.size() && !hit; ++k)
+            if (h->desc_cache[k].first == hv && memcmp(&h->desc_cache[k].second, st, sizeof(BatchDesc)) == 0) hit = k + 1;
+        if (hit) {
+            h->n_batches = bid - 1;  // give the fresh id back
+            *pbid = hit;
+            *pst = &h->desc_cache[hit - 1].second;
+            return DBG_OK;
+        }
+        RETURN_IF(upload_batch(h, st, bid));
+        h->desc_cache.push_back({hv, *st});
+        h->n_cached = bid;
+        return DBG_OK;
+    }
+    return upload_batch(h, st, bid);
 }
 
 // dbg_column (host or device) -> DCol on device
@@ -609,7 +641,7 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
     if ((rc = dev_alloc((void**)&h->counters, CNT_WORDS * 8)) != DBG_OK) return cleanup(rc);
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
-    if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
+    if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
     if (hipHostGetDevicePointer((void**)&h->hcounters_dev, h->hcounters, 0) != hipSuccess) h->hcounters_dev = nullptr;
     // initial capacity: AggregateHashTable::initial_capacity() = 32768, or 2x the hint
     // initial capacity: 2x the hint, or 4096 slots (the CPU table starts at 32768 =
@@ -663,18 +695,20 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
     // inputs copied by earlier batches, and the pinned batch descriptors reused below, may still
-    // be read by queued work: wait unless the stream is already idle (the usual case after a
-    // finalize, which synchronises)
-    if (!h->owned.empty() || hipStreamQuery(h->stream) != hipSuccess) {
+    // be read by queued work: wait if any were queued since the last synchronisation
+    if (!h->owned.empty() || h->uploads_pending) {
         HIPCHECK(hipStreamSynchronize(h->stream));
         for (auto& b : h->owned) HIPCHECK(hipFree(b.p));
         h->owned.clear();
+        h->uploads_pending = false;
     }
     h->n_batches = h->n_cached;  // cached descriptors stay valid (immutable)
     h->pending_rows = h->pending_recs = 0;
     h->finalized = false;
+    if (h->clean) return DBG_OK;  // the recycling finalize already re-initialised table + counters
     prof::Scope ps("table_init", h->stream);
     launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap, h->counters);
+    h->clean = true;
     return DBG_OK;
 }
 
@@ -685,6 +719,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     HIPCHECK(hipSetDevice(h->device));
     h->finalized = false;
     if (rows == 0) return DBG_OK;
+    h->clean = false;
     const Spec& S = h->spec;
     BatchDesc* st;
     u32 bid;
@@ -703,23 +738,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
         RETURN_IF(to_dcol(h, arg_cols[a], want, true, on_device, st->args[a]));
     }
     if (filter && filter->n_nodes) RETURN_IF(fill_filter(h, filter, on_device, st->fcols, &st->n_fcols, st->nodes, &st->n_nodes));
-    if (on_device && h->owned.size() == owned0 && bid == h->n_cached + 1 && h->desc_cache.size() < 64) {
-        u64 hv = desc_hash(*st);
-        u32 hit = 0;
-        for (u32 k = 0; k < h->desc_cache.size() && !hit; ++k)
-            if (h->desc_cache[k].first == hv && memcmp(&h->desc_cache[k].second, st, sizeof(BatchDesc)) == 0) hit = k + 1;
-        if (hit) {
-            h->n_batches = bid - 1;  // give the fresh id back
-            bid = hit;
-            st = &h->desc_cache[hit - 1].second;
-        } else {
-            RETURN_IF(upload_batch(h, st, bid));
-            h->desc_cache.push_back({hv, *st});
-            h->n_cached = bid;
-        }
-    } else {
-        RETURN_IF(upload_batch(h, st, bid));
-    }
+    RETURN_IF(submit_batch(h, &st, &bid, on_device && h->owned.size() == owned0));
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
     u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
     RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
@@ -764,6 +783,9 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
         HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
         HIPCHECK(hipStreamSynchronize(h->stream));
         if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+        if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
+            return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
+                                         "buffer, or unresolved overflow): use dbg_agg_partition + export_records");
         if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {
             RETURN_IF(resolve_overflow(h));
             continue;
@@ -906,6 +928,12 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
 }
 
 
+int dbg_agg_set_recycle(dbg_agg_handle* h, int on) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    h->recycle = on ? 1 : 0;
+    return DBG_OK;
+}
+
 int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, uint64_t max_groups,
                           const uint64_t* max_string_bytes, uint64_t* n_groups, uint64_t* string_bytes) {
     if (!h || !out_aggs || !out_keys || !n_groups) return fail(DBG_ERR_INVALID, "null argument");
@@ -961,20 +989,45 @@ int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_c
             }
         }
         const bool zero_copy = small && h->hcounters_dev != nullptr;
+        const u64 seq = ++h->fin_seq;
+        volatile u64* hseq = h->hcounters + CNT_WORDS + 2 + DBG_MAX_KEYS;
         if (small) {
             prof::Scope ps("finalize_small", h->stream);
-            launch_finalize_small(h->stream, h->dspec, h->dbatches, t, od, totals, zero_copy ? h->hcounters_dev : nullptr);
+            launch_finalize_small(h->stream, h->dspec, h->dbatches, t, od, totals, zero_copy ? h->hcounters_dev : nullptr,
+                                  h->recycle && zero_copy, seq);
         } else {
             prof::Scope ps("write_results", h->stream);
             launch_write_results(h->stream, h->dspec, S, h->dbatches, t, h->d_pos, h->d_str_pos, od);
             launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);
         }
+        bool recycled = false;
         if (!zero_copy) {
             HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
             HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+            HIPCHECK(hipStreamSynchronize(h->stream));
+        } else {
+            // the kernel posts `seq` last (system-scope release after every other write): spin
+            // on it instead of a stream synchronisation (whose wake-up costs several
+            // microseconds); after ~20 ms fall back to the blocking wait (long queued inserts)
+            bool seen = false;
+            auto t0 = std::chrono::steady_clock::now();
+            for (u64 it = 0;; ++it) {
+                if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == seq) {
+                    seen = true;
+                    break;
+                }
+                if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+                __builtin_ia32_pause();
+            }
+            if (!seen) HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipGetLastError());
+            recycled = h->hcounters[CNT_WORDS + 1 + DBG_MAX_KEYS] != 0;
         }
-        HIPCHECK(hipStreamSynchronize(h->stream));
+        h->uploads_pending = false;
         if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+        if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
+            return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
+                                         "buffer, or unresolved overflow): use dbg_agg_partition + export_records");
         if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {
             RETURN_IF(resolve_overflow(h));
             continue;
@@ -995,8 +1048,14 @@ int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_c
             return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
                                               std::to_string(h->hcounters[CNT_CLAIMS]));
         h->finalized = true;
+        if (recycled) {  // the table was re-initialised by the kernel: dbg_agg_reset state
+            h->clean = true;
+            h->finalized = false;
+            h->n_batches = h->n_cached;
+            h->pending_rows = h->pending_recs = 0;
+        }
         if (h->hcounters[CNT_ERR] & ERR_DEC_OVERFLOW) {
-            HIPCHECK(hipMemsetAsync(h->counters + CNT_ERR, 0, 8, h->stream));
+            if (!recycled) HIPCHECK(hipMemsetAsync(h->counters + CNT_ERR, 0, 8, h->stream));
             return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
         }
         if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
@@ -1065,11 +1124,78 @@ int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strin
     return DBG_OK;
 }
 
+int dbg_agg_capacity(dbg_agg_handle* h, uint64_t* slots) {
+    if (!h || !slots) return fail(DBG_ERR_INVALID, "null argument");
+    *slots = h->cap;
+    return DBG_OK;
+}
+
+// ---- fixed-capacity exchange (replicas + gather, low cardinality) ----
+int dbg_agg_export_fixed(dbg_agg_handle* h, void* dev_buf, uint64_t cap_records) {
+    if (!h || !dev_buf) return fail(DBG_ERR_INVALID, "null argument");
+    const Spec& S = h->spec;
+    if (!S.inline_keys) return fail(DBG_ERR_UNSUPPORTED, "fixed export needs fixed-width (inline) group keys");
+    if (h->cap + 1 > FIN_SMALL_SLOTS) return fail(DBG_ERR_UNSUPPORTED, "fixed export is for small tables");
+    if (S.rec_width < 16) return fail(DBG_ERR_INTERNAL, "record narrower than the fixed header");
+    HIPCHECK(hipSetDevice(h->device));
+    prof::Scope ps("export_fixed", h->stream);
+    launch_export_fixed(h->stream, h->dspec, h->dbatches, table_desc(h), (u8*)dev_buf, cap_records, h->recycle);
+    HIPCHECK(hipGetLastError());
+    if (h->recycle) {  // the kernel re-initialised the table: dbg_agg_reset state
+        h->clean = true;
+        h->finalized = false;
+        h->n_batches = h->n_cached;
+        h->pending_rows = h->pending_recs = 0;
+    }
+    return DBG_OK;
+}
+
+int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs, uint64_t cap_records) {
+    if (!h || !dev_bufs || n_bufs < 1) return fail(DBG_ERR_INVALID, "bad argument");
+    const Spec& S = h->spec;
+    if (!S.inline_keys) return fail(DBG_ERR_UNSUPPORTED, "fixed merge needs fixed-width (inline) group keys");
+    const u64 n = (u64)n_bufs * (cap_records + 1);
+    if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
+    HIPCHECK(hipSetDevice(h->device));
+    h->finalized = false;
+    h->clean = false;
+    BatchDesc* st;
+    u32 bid;
+    RETURN_IF(new_batch(h, &st, &bid));
+    const u8* base = (const u8*)dev_bufs;
+    st->rows = n;
+    st->is_records = 1;
+    st->rec_width = S.rec_width;
+    st->rec_base = base;
+    st->seg_records = cap_records + 1;
+    for (int c = 0; c < S.n_keys; ++c) {
+        DCol& d = st->keys[c];
+        const dbg_datatype& t = S.key_types[c];
+        d.type = t.type;
+        d.precision = t.precision;
+        d.scale = t.scale;
+        d.nullable = t.nullable;
+        d.layout = LAYOUT_RECORD;
+        d.width = type_width(t.type);
+        d.stride = S.rec_width;
+        d.data = base + S.rec_key_off[c];
+        d.validity = t.nullable ? base + S.rec_val_off[c] : nullptr;
+    }
+    RETURN_IF(submit_batch(h, &st, &bid, true));
+    u64 blocks = std::min<u64>(2048, (n + 4095) / 4096) + 1;
+    RETURN_IF(ensure_ovf(h, n, blocks * 4096));
+    prof::Scope ps("agg_merge", h->stream);
+    launch_insert(h->stream, h->dspec, S, h->dbatches, bid, n, true, table_desc(h), true);
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
 int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void* dev_strings, int32_t n_segments,
                           const uint64_t* seg_records, const uint64_t* seg_string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
     h->finalized = false;
+    h->clean = false;
     const Spec& S = h->spec;
     u64 rec_off = 0, str_off = 0;
     for (int g = 0; g < n_segments; ++g) {

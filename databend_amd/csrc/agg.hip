@@ -519,6 +519,15 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         const u64 i = r0 + it * BLOCK + threadIdx.x;
         if (i >= r1) continue;
         if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+        if (RECORDS && B.seg_records) {  // fixed-capacity segments: record 0 is [count][flags]
+            const u64 q = i % B.seg_records;
+            const u8* hdr = B.rec_base + (i - q) * (u64)B.rec_width;
+            if (q == 0) {
+                if (gld<u64>(hdr + 8)) atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_FIXED_INCOMPLETE);
+                continue;
+            }
+            if (q > gld<u64>(hdr)) continue;
+        }
         u64 h, key;
         if (RECORDS) {
             h = gld<u64>(B.rec_base + i * (u64)B.rec_width);
@@ -607,10 +616,10 @@ __device__ __forceinline__ T vget(const v4u& y, int j) {
 // leave 63 of 64 lanes idle on every LDS round trip.
 #define WQ 128  // queue entries per wave
 
-template <typename T, bool PRED, int NT, bool PF>
+template <typename T, bool PRED, int NT, bool CO>
 __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                u32 bid, u64 rows, TableDesc t, u32 lds_slots,
-                                                               T lo, T hi, int negate, int count_only, int xmode) {
+                                                               T lo, T hi, int negate, int xmode) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     constexpr int V = 16 / sizeof(T);
     const Spec& S = *spec;
@@ -637,7 +646,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
         if (ls >= 0) {
             wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
-            if (count_only) at_add<AS_LDS>(st + 1, 1ULL);
+            if (CO) at_add<AS_LDS>(st + 1, 1ULL);
             else apply_row<AS_LDS>(S, st, B, i);
             return;
         }
@@ -648,7 +657,9 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
             return;
         }
         my_claims += claimed ? 1 : 0;
-        apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
+        wptr<AS_GLB> gst = asp<AS_GLB>(t.slots + gs * t.stride_words);
+        if (CO) at_add<AS_GLB>(gst + 1, 1ULL);
+        else apply_row<AS_GLB>(S, gst, B, i);
     };
 
     u32 qn = 0;  // wave-uniform queue length
@@ -713,6 +724,11 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
             pre += (u32)__popcll(bal & ltmask) << bb;
             tot += (u32)__popcll(bal) << bb;
         }
+        if (xmode == 3) {  // timing experiment: ballots only
+            sink ^= pre;
+            qn = (qn + tot) & 63;
+            return;
+        }
         if (qn + tot <= WQ) {
             u32 pos = qn + pre;
 #pragma unroll
@@ -727,6 +743,10 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
                 }
             }
             qn += tot;
+            if (xmode == 4) {  // timing experiment: queue writes, no drain
+                qn &= 63;
+                return;
+            }
             while (qn >= 64) {
                 __builtin_amdgcn_wave_barrier();
                 drain64();
@@ -755,50 +775,35 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     u64 k = (u64)blockIdx.x * NT + threadIdx.x;
     const u64 step = (u64)FAST_UNROLL * gstride;
     const u64 lastv = nvec ? nvec - 1 : 0;
-    if (PF) {
-        // Software pipeline: the next round's FAST_UNROLL loads are issued before this round is
-        // filtered and staged, so a wave busy in the LDS queue still has 64 B/lane in flight.
-        v4u y[FAST_UNROLL], yn[FAST_UNROLL];
+    // Software pipeline: the next round's FAST_UNROLL loads are issued before this round is
+    // filtered and queued, so a wave busy with its ballots and LDS queue writes still has
+    // 64 B/lane in flight (without it the per-round processing sits on the load critical path).
+    v4u y[FAST_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FAST_UNROLL; ++u) {
+        u64 idx = k + u * gstride;
+        y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+    }
+    while (__ballot(k < nvec) != 0) {
+        const u64 kn = k + step;
+        v4u yn[FAST_UNROLL];
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) {
+            u64 idx = kn + u * gstride;
+            yn[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+        }
+        u64 bases[FAST_UNROLL];
+        u32 actm = 0;
 #pragma unroll
         for (int u = 0; u < FAST_UNROLL; ++u) {
             u64 idx = k + u * gstride;
-            y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+            actm |= (idx < nvec ? 1u : 0u) << u;
+            bases[u] = idx * V;
         }
-        while (__ballot(k < nvec) != 0) {
-            const u64 kn = k + step;
+        handle_group(y, bases, FAST_UNROLL, actm);
 #pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) {
-                u64 idx = kn + u * gstride;
-                yn[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
-            }
-            u64 bases[FAST_UNROLL];
-            u32 actm = 0;
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) {
-                u64 idx = k + u * gstride;
-                actm |= (idx < nvec ? 1u : 0u) << u;
-                bases[u] = idx * V;
-            }
-            handle_group(y, bases, FAST_UNROLL, actm);
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
-            k = kn;
-        }
-    } else {
-        while (__ballot(k < nvec) != 0) {
-            v4u y[FAST_UNROLL];
-            u64 bases[FAST_UNROLL];
-            u32 actm = 0;
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) {
-                u64 idx = k + u * gstride;
-                actm |= (idx < nvec ? 1u : 0u) << u;
-                y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
-                bases[u] = idx * V;
-            }
-            handle_group(y, bases, FAST_UNROLL, actm);
-            k += step;
-        }
+        for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
+        k = kn;
     }
     // drain the queue's rest (< 64 entries): lanes below qn take one each
     if (PRED && qn) {
@@ -928,7 +933,7 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
                            lslots, (T)lo, (T)hi, neg, count_only);
         return;
     }
-    static const int nt = getenv("DBG_FAST_NT") ? atoi(getenv("DBG_FAST_NT")) : 1024;
+    const int nt = 1024;
     static const u64 max_blocks = getenv("DBG_FAST_MAXBLOCKS") ? strtoull(getenv("DBG_FAST_MAXBLOCKS"), nullptr, 10) : 256;
     size_t shmem = table_bytes + (size_t)(nt / 64) * 2 * WQ * 8;
     u64 quantum = V * (u64)nt * FAST_UNROLL;
@@ -936,13 +941,12 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
-    static const int pf = getenv("DBG_FAST_PF") ? atoi(getenv("DBG_FAST_PF")) : 1;  // A/B knob: 0 = no prefetch
 #define FAST_LAUNCH(P, N, F)                                                                                                  \
     hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, \
-                       lslots, (T)lo, (T)hi, neg, count_only, xmode)
-    if (nt == 512) {
-        if (pred) FAST_LAUNCH(true, 512, true); else FAST_LAUNCH(false, 512, true);
-    } else if (pf) {
+                       lslots, (T)lo, (T)hi, neg, xmode)
+    // CO: COUNT(*) is the only aggregate (ClickBench Q8/Q16 shape) — the kernel then carries no
+    // apply_row code at all (smaller hot loop, fewer registers)
+    if (count_only) {
         if (pred) FAST_LAUNCH(true, 1024, true); else FAST_LAUNCH(false, 1024, true);
     } else {
         if (pred) FAST_LAUNCH(true, 1024, false); else FAST_LAUNCH(false, 1024, false);
@@ -1438,28 +1442,46 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
 // finalize_small: count + scan + write + validity bits + string offsets in ONE workgroup, for
 // tables of at most FIN_SMALL_SLOTS slots (low-cardinality queries: the four-launch finalize
 // costs more than the work).  totals: [0] groups, [1 + c] string bytes of key column c.
+//
+// Each thread owns FIN_MAXPER consecutive slots whose entries it loads once, all in flight
+// together, and keeps in registers for the write pass.  recycle != 0 (dbg_agg_set_recycle):
+// the table is left re-initialised for the next batch (this kernel already holds every slot, so
+// the reset costs no extra launch), unless an insert overflowed (the host then grows the table
+// and finalizes again).  host_mirror (mapped pinned memory) receives the counters, the totals and
+// finally `seq`, which the host polls instead of synchronising the stream.
 // ------------------------------------------------------------------------------------------
 #define FIN_NT 1024
+#define FIN_MAXPER (FIN_SMALL_SLOTS / FIN_NT)
 __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                                TableDesc t, OutDesc out, u64* totals, u64* host_mirror) {
+                                                                TableDesc t, OutDesc out, u64* totals, u64* host_mirror,
+                                                                int recycle, u64 seq) {
     const Spec& S = *spec;
     __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
+    __shared__ int do_recycle;
     const u64 n_slots = t.cap + 1;
-    const u64 per = (n_slots + FIN_NT - 1) / FIN_NT;
+    const u32 per = (u32)((n_slots + FIN_NT - 1) / FIN_NT);  // <= FIN_MAXPER (host checks cap)
     const u64 base = (u64)threadIdx.x * per;
     const bool ref_strings = S.has_strings && !S.inline_keys;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    u64 cnt = 0, sb[DBG_MAX_KEYS];
-    for (int c = 0; c < DBG_MAX_KEYS; ++c) sb[c] = 0;
-    for (u64 k = 0; k < per; ++k) {
+    if (threadIdx.x == 0)
+        do_recycle = recycle && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+    u64 ent[FIN_MAXPER];
+#pragma unroll
+    for (u32 k = 0; k < FIN_MAXPER; ++k) {
         u64 s = base + k;
-        if (s >= n_slots) break;
-        u64 e = t.slots[s * t.stride_words];
-        if (e == SLOT_EMPTY) continue;
+        ent[k] = (k < per && s < n_slots) ? gld<u64>(t.slots + s * t.stride_words) : SLOT_EMPTY;
+    }
+    u64 cnt = 0, sb[DBG_MAX_KEYS];
+    u32 occ = 0;  // occupied owned slots (bit k = slot base + k)
+    for (int c = 0; c < DBG_MAX_KEYS; ++c) sb[c] = 0;
+#pragma unroll
+    for (u32 k = 0; k < FIN_MAXPER; ++k) {
+        if (ent[k] == SLOT_EMPTY) continue;
         cnt++;
+        occ |= 1u << k;
         if (ref_strings)
             for (int c = 0; c < S.n_keys; ++c)
-                if (S.key_types[c].type == DBG_STRING) sb[c] += key_str_len(S, batches, e, c);
+                if (S.key_types[c].type == DBG_STRING) sb[c] += key_str_len(S, batches, ent[k], c);
     }
     // block exclusive scan of cnt (and of the string bytes of each key column)
     auto wave_incl = [&](u64 v) {
@@ -1493,17 +1515,17 @@ __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __re
         if (ref_strings)
             for (int w = 0; w < FIN_NT / 64; ++w) stot[c] += wsum[w][1 + c];
     }
-    for (u64 k = 0; k < per; ++k) {
-        u64 s = base + k;
-        if (s >= n_slots) break;
+    // write pass over the occupied slots only (one write_group instance in the code; the entry
+    // is re-read from the cache rather than indexed out of the register array)
+    while (occ && p < out.cap_groups) {
+        const u32 k = __builtin_ctz(occ);
+        occ &= occ - 1;
+        const u64 s = base + k;
         const u64* st = t.slots + s * t.stride_words;
-        u64 e = st[0];
-        if (e == SLOT_EMPTY) continue;
-        if (p >= out.cap_groups) break;
-        write_group(S, batches, t, s, st, e, p, sp, out);
+        write_group(S, batches, t, s, st, gld<u64>(st), p, sp, out);
         p++;
     }
-    __syncthreads();  // validity bytes of every row are written
+    __syncthreads();  // validity bytes of every row are written; every state word has been read
     u64 n = total < out.cap_groups ? total : out.cap_groups;
     for (u64 k = threadIdx.x; k < (n + 7) / 8; k += FIN_NT)
         for (int c = 0; c < S.n_keys + S.n_aggs; ++c) {
@@ -1524,19 +1546,51 @@ __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __re
             if (out.key_offsets[c] && total <= out.cap_groups) out.key_offsets[c][total] = stot[c];
         }
     }
+    __syncthreads();  // decimal-overflow bits of write_group are in the counters
+    // recycle only when the caller got every group (short buffers: the table must stay intact
+    // for the retry with larger ones)
+    bool rc = do_recycle != 0 && total <= out.cap_groups;
+    for (int c = 0; c < S.n_keys; ++c)
+        if (ref_strings && S.key_types[c].type == DBG_STRING && stot[c] > out.cap_str[c]) rc = false;
     // zero-copy read-back: the table counters and the totals go straight to mapped pinned host
     // memory ([0, CNT_WORDS) counters, then totals), so finalize needs no copy launches
+    // (system-scope stores: written through to host memory, never parked in the L2)
+    auto put = [&](int w, u64 v) { __hip_atomic_store(host_mirror + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    __shared__ u64 cnts[CNT_WORDS];
+    if (threadIdx.x < CNT_WORDS) {  // one load per thread, all in flight together
+        cnts[threadIdx.x] = ld_sc1(t.counters + threadIdx.x);
+        if (rc) t.counters[threadIdx.x] = 0;  // dbg_agg_reset
+    }
     __syncthreads();
-    if (host_mirror && threadIdx.x < CNT_WORDS) host_mirror[threadIdx.x] = ld_sc1(t.counters + threadIdx.x);
+    if (threadIdx.x == 0) {
+        if (host_mirror) {
+            for (int w = 0; w < CNT_WORDS; ++w) put(w, cnts[w]);
+            put(CNT_WORDS, total);
+            for (int c = 0; c < S.n_keys; ++c) put(CNT_WORDS + 1 + c, stot[c]);
+            put(CNT_WORDS + 1 + DBG_MAX_KEYS, rc ? 1 : 0);  // recycled
+        }
+    }
+    if (rc) {  // table_init of the owned slots
+        const u32 sw = (u32)t.stride_words;
+        for (u32 k = 0; k < per; ++k) {
+            u64 s = base + k;
+            if (s >= n_slots) break;
+            u64* d = t.slots + s * sw;
+            for (u32 w = 0; w < sw; ++w) d[w] = S.slot_init[w];
+        }
+    }
+    // `seq` last: thread 0 waits for its write-through mirror stores to complete before posting it.  No system-scope release: that would write
+    // back the whole L2; the output columns are consumed in stream order on the device.
     if (host_mirror && threadIdx.x == 0) {
-        host_mirror[CNT_WORDS] = total;
-        for (int c = 0; c < S.n_keys; ++c) host_mirror[CNT_WORDS + 1 + c] = stot[c];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(host_mirror + CNT_WORDS + 2 + DBG_MAX_KEYS, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
-                           u64* totals, u64* host_mirror) {
-    hipLaunchKernelGGL(finalize_small_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, out, totals, host_mirror);
+                           u64* totals, u64* host_mirror, int recycle, u64 seq) {
+    hipLaunchKernelGGL(finalize_small_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, out, totals, host_mirror, recycle,
+                       seq);
 }
 
 // Fused finalize tail: bit-pack every nullable output's validity and close the string offsets,
@@ -1600,6 +1654,17 @@ void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits) {
 // ------------------------------------------------------------------------------------------
 // Export partial-state records: [hash][key part][state words], partition-major.
 // ------------------------------------------------------------------------------------------
+// Key part of a record from an inline (packed) entry.
+__device__ __forceinline__ void write_inline_key_part(const Spec& S, u64 key, u8* rec) {
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& ty = S.key_types[c];
+        u32 w = type_width(ty.type);
+        u64 b = (key >> (8 * S.koff[c])) & width_mask(w);
+        if (ty.nullable) rec[S.rec_val_off[c]] = ((key >> (8 * S.voff[c])) & 0xff) != 0;
+        for (u32 j = 0; j < w; ++j) rec[S.rec_key_off[c] + j] = (u8)(b >> (8 * j));
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) export_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                       TableDesc t, u32 n_parts, int scheme, const u64* pos, const u64* str_pos,
                                                       u64 nblocks, u8* rec_out, u8* str_out, const u64* part_str_base) {
@@ -1626,14 +1691,7 @@ __global__ void __launch_bounds__(BLOCK) export_kernel(const Spec* __restrict__ 
         u8* rec = rec_out + r * S.rec_width;
         *(u64*)rec = h;
         if (S.inline_keys) {
-            u64 key = s == t.cap ? SLOT_EMPTY : e;
-            for (int c = 0; c < S.n_keys; ++c) {
-                const dbg_datatype& ty = S.key_types[c];
-                u32 w = type_width(ty.type);
-                u64 b = (key >> (8 * S.koff[c])) & width_mask(w);
-                if (ty.nullable) rec[S.rec_val_off[c]] = ((key >> (8 * S.voff[c])) & 0xff) != 0;
-                for (u32 j = 0; j < w; ++j) rec[S.rec_key_off[c] + j] = (u8)(b >> (8 * j));
-            }
+            write_inline_key_part(S, s == t.cap ? SLOT_EMPTY : e, rec);
         } else {
             const BatchDesc& RB = batches[ref_bid(e)];
             u64 row = ref_row(e);
@@ -1669,3 +1727,83 @@ void launch_export(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
                        rec_out, str_out, part_str_base);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// export_fixed: the groups of a small inline-key table as records in a fixed-capacity buffer
+// whose record 0 is the header [count][flags] — replicas + gather for low cardinality
+// (SURVEY.md §8e): the count never leaves the device, so the exchange that follows (an RCCL
+// all-gather of equal-size buffers) and the merge need no host round trip.  One workgroup, the
+// same owned-slot scan as finalize_small.  flags = 1: incomplete (more groups than capacity, or
+// inserts still deferred in the overflow lists); the merge turns that into a finalize error.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(FIN_NT) export_fixed_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                              TableDesc t, u8* buf, u64 cap_records, int recycle) {
+    const Spec& S = *spec;
+    __shared__ u64 wsum[FIN_NT / 64];
+    const u64 n_slots = t.cap + 1;
+    const u32 per = (u32)((n_slots + FIN_NT - 1) / FIN_NT);
+    const u64 base = (u64)threadIdx.x * per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 ent[FIN_MAXPER];
+    u32 occ = 0, cnt = 0;
+#pragma unroll
+    for (u32 k = 0; k < FIN_MAXPER; ++k) {
+        u64 s = base + k;
+        ent[k] = (k < per && s < n_slots) ? gld<u64>(t.slots + s * t.stride_words) : SLOT_EMPTY;
+    }
+#pragma unroll
+    for (u32 k = 0; k < FIN_MAXPER; ++k)
+        if (ent[k] != SLOT_EMPTY) {
+            occ |= 1u << k;
+            cnt++;
+        }
+    u64 ic = cnt;
+    for (int off = 1; off < 64; off <<= 1) {
+        u64 o = __shfl_up(ic, off, 64);
+        if (lane >= off) ic += o;
+    }
+    if (lane == 63) wsum[wave] = ic;
+    __syncthreads();
+    u64 p = ic - cnt, total = 0;
+    for (int w = 0; w < FIN_NT / 64; ++w) {
+        if (w < wave) p += wsum[w];
+        total += wsum[w];
+    }
+    const u32 rw = S.rec_width;
+    while (occ && p < cap_records) {
+        const u32 k = __builtin_ctz(occ);
+        occ &= occ - 1;
+        const u64 s = base + k;
+        const u64* st = t.slots + s * t.stride_words;
+        const u64 e = gld<u64>(st);
+        u8* rec = buf + (1 + p) * rw;
+        const u64 key = s == t.cap ? SLOT_EMPTY : e;
+        *(u64*)rec = hash_packed(S, key);
+        write_inline_key_part(S, key, rec);
+        u64* sw = (u64*)(rec + S.rec_state_off);
+        for (int w = 1; w <= S.n_words; ++w) sw[w - 1] = gld<u64>(st + w);
+        p++;
+    }
+    if (threadIdx.x == 0) {
+        const bool pending = ld_sc1(t.counters + CNT_OVF_ROWS) != 0 || ld_sc1(t.counters + CNT_OVF_RECS) != 0;
+        ((u64*)buf)[0] = total < cap_records ? total : cap_records;
+        ((u64*)buf)[1] = (total > cap_records || pending) ? 1 : 0;
+    }
+    if (recycle) {  // dbg_agg_set_recycle: table_init of the owned slots + counter reset (an
+                    // incomplete export is flagged above, so nothing is lost silently)
+        __syncthreads();  // every state word has been read
+        if (threadIdx.x < CNT_WORDS) t.counters[threadIdx.x] = 0;
+        const u32 sw = (u32)t.stride_words;
+        for (u32 k = 0; k < per; ++k) {
+            u64 s = base + k;
+            if (s >= n_slots) break;
+            u64* d = t.slots + s * sw;
+            for (u32 w = 0; w < sw; ++w) d[w] = S.slot_init[w];
+        }
+    }
+}
+
+void launch_export_fixed(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, u8* buf, u64 cap_records,
+                         int recycle) {
+    hipLaunchKernelGGL(export_fixed_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, buf, cap_records, recycle);
+}

@@ -38,6 +38,9 @@ struct BatchDesc {
     int32_t is_records;
     uint32_t rec_width;
     const u8* rec_base;
+    // fixed-capacity record segments (dbg_agg_merge_fixed): record i belongs to segment
+    // i / seg_records; its record 0 holds [count u64][flags u64], records 1..count are groups
+    u64 seg_records;
     DCol keys[DBG_MAX_KEYS];
     DCol args[DBG_MAX_AGGS];
     DCol fcols[DBG_MAX_FCOLS];
@@ -65,7 +68,7 @@ struct TableDesc {
 #define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
 enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_WORDS = 8 };
-enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2 };
+enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4 };
 
 // ---- launch wrappers (agg.hip) ----
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
@@ -93,11 +96,14 @@ struct OutDesc {
 };
 #define FIN_SMALL_SLOTS 16384  // tables up to this many slots finalize in one workgroup
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
-                           u64* totals, u64* host_mirror /* mapped pinned: counters, then totals */);
+                           u64* totals, u64* host_mirror /* mapped pinned: counters, totals, recycled, seq */,
+                           int recycle, u64 seq);
 void launch_finish_outputs(hipStream_t s, const OutDesc& out, const u64* totals, int n_keys, int n_aggs);
 void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                           const u64* pos /* scanned hist */, const u64* str_pos, const OutDesc& out);
 void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);
+void launch_export_fixed(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, u8* buf, u64 cap_records,
+                         int recycle);
 void launch_export(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                    u32 n_parts, int scheme, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out,
                    const u64* part_str_base);

@@ -13,6 +13,12 @@ Here each rank exports its partial table as fixed-width records partitioned by t
 Group sets of the ranks are disjoint afterwards (like the reference's per-node finals).  One
 process per GPU; `backend="nccl"` is RCCL on ROCm.  `all_to_all_bytes` is backend-agnostic and
 is exercised with gloo on CPU by the tests.
+
+Low cardinality (a partial table of a few thousand slots at most, fixed-width keys) takes the
+replicas + gather route of SURVEY.md §8e instead (`gather_small`): every rank writes its groups
+into an equal-size buffer whose group count stays on the device (dbg_agg_export_fixed), one RCCL
+all-gather moves the buffers, and the root merges them (dbg_agg_merge_fixed) — no host round
+trip and no size exchange, which at these sizes would cost more than the data.
 """
 from __future__ import annotations
 
@@ -66,3 +72,45 @@ def exchange_partial(partial, final, device) -> dict:
     sent = sum(c * w for c in counts) + sum(sbytes)
     return dict(sent_bytes=sent, remote_bytes=sent - counts[dist.get_rank()] * w - sbytes[dist.get_rank()],
                 received_records=sum(seg_records))
+
+
+_FIXED_BUFS = {}
+
+
+def _fixed_buffer(key, nbytes, device):
+    """Persistent exchange buffers: a stable address keeps the merge's batch descriptor cached
+    on the device (no upload, so the next reset needs no stream synchronisation)."""
+    import torch
+    b = _FIXED_BUFS.get(key)
+    if b is None or b.numel() != nbytes or b.device != torch.device(device):
+        b = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _FIXED_BUFS[key] = b
+    return b
+
+
+def all_gather_fixed(buf, out):
+    """All-gather of equal-size uint8 buffers (out holds world * buf.numel() bytes, rank order)."""
+    _dist().all_gather_into_tensor(out, buf)
+    return out
+
+
+def fixed_capacity(partial) -> int:
+    """Records per fixed buffer: every group a table of this capacity can hold (cap + sentinel)."""
+    return partial.capacity + 1
+
+
+def gather_small(partial, final, device, root: int = 0, cap_records: int = 0):
+    """Replicas + gather: merge every rank's `partial` groups into `final` on rank `root`.
+    Returns the bytes each rank sent."""
+    dist = _dist()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    cap = cap_records or fixed_capacity(partial)
+    w = partial.record_width()
+    nbytes = (cap + 1) * w
+    buf = _fixed_buffer(("send", str(device)), nbytes, device)
+    out = _fixed_buffer(("recv", str(device)), world * nbytes, device)
+    partial.export_fixed(buf, cap)
+    all_gather_fixed(buf, out)
+    if rank == root:
+        final.merge_fixed(out, world, cap)
+    return nbytes

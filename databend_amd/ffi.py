@@ -18,8 +18,8 @@ _LIB = None
 EXPORTED = [
     "dbg_version", "dbg_last_error", "dbg_device_count", "dbg_agg_result_type", "dbg_agg_create",
     "dbg_agg_destroy", "dbg_agg_set_stream", "dbg_agg_reset", "dbg_agg_add_groups", "dbg_agg_finalize",
-    "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
-    "dbg_agg_merge_records", "dbg_filter_select", "dbg_take_fixed", "dbg_prof_enable", "dbg_prof_reset",
+    "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_set_recycle", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
+    "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_prof_enable", "dbg_prof_reset",
     "dbg_prof_get", "dbg_datagen",
 ]
 
@@ -69,10 +69,14 @@ def lib():
         L.dbg_agg_finalize.argtypes = [VP, P(U64), P(U64)]
         L.dbg_agg_result.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), C.c_int]
         L.dbg_agg_finalize_into.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), U64, P(U64), P(U64), P(U64)]
+        L.dbg_agg_set_recycle.argtypes = [VP, C.c_int]
         L.dbg_agg_record_width.argtypes = [VP, P(C.c_uint32)]
         L.dbg_agg_partition.argtypes = [VP, C.c_uint32, C.c_int, P(U64), P(U64)]
         L.dbg_agg_export_records.argtypes = [VP, VP, VP]
         L.dbg_agg_merge_records.argtypes = [VP, VP, VP, I32, P(U64), P(U64)]
+        L.dbg_agg_export_fixed.argtypes = [VP, VP, U64]
+        L.dbg_agg_capacity.argtypes = [VP, P(U64)]
+        L.dbg_agg_merge_fixed.argtypes = [VP, VP, I32, U64]
         L.dbg_filter_select.argtypes = [P(abi.dbg_filter), U64, VP, P(U64), VP]
         L.dbg_take_fixed.argtypes = [P(abi.dbg_column), VP, U64, VP, VP, VP]
         L.dbg_prof_enable.argtypes = [C.c_int]

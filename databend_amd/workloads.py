@@ -192,6 +192,8 @@ class ConfigRunner:
         self.params = params_for(cfg, types)
         self.result_types = [f.return_type() for f in self.params.aggregate_functions]
         self.table = AggregateHashTable(self.params, HashTableConfig(True, capacity_hint))
+        # one table per batch stream: a small table is re-initialised by the fused finalize
+        check(lib().dbg_agg_set_recycle(self.table.h, 1))
         self.programs = []
         for inp in self.inputs:
             if self.shape.predicate:
@@ -229,12 +231,21 @@ class ConfigRunner:
         """One pass of the hot path over one batch; results land in HBM (self.out_*).
         reset -> fused filter + GROUP BY insert -> fused finalize (count, scan, write) with one
         host round trip (dbg_agg_finalize_into)."""
+        self.insert(k)
+        return self.finalize_into(self.table.h)
+
+    def insert(self, k: int = 0):
+        """reset -> fused filter + GROUP BY insert of input copy k into the partial table."""
         i = k % len(self.inputs)
         L = lib()
         h = self.table.h
         keys, args, fp = self._prepared(i)
         check(L.dbg_agg_reset(h))
         check(L.dbg_agg_add_groups(h, keys, args, fp, self.rows, 1))
+
+    def finalize_into(self, h):
+        """Fused finalize of table handle h into this runner's device output columns."""
+        L = lib()
         n = C.c_uint64()
         sb = (C.c_uint64 * len(self.shape.keys))()
         if not hasattr(self, "_out_structs"):

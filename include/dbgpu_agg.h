@@ -205,6 +205,14 @@ int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_c
                           uint64_t max_groups, const uint64_t* max_string_bytes, uint64_t* n_groups,
                           uint64_t* string_bytes);
 
+/* Recycle mode (default off): a dbg_agg_finalize_into that delivers every group of a small table
+ * (low cardinality, finalized in one workgroup) also re-initialises the table in that same
+ * launch, leaving the handle as dbg_agg_reset would — the result columns are then the only copy
+ * of the groups, and the next dbg_agg_reset costs no launch.  The partial table of
+ * TransformPartialAggregate is dropped after on_finish (transform_aggregate_partial.rs:449-465),
+ * so a processor that reuses one handle per batch stream loses nothing. */
+int dbg_agg_set_recycle(dbg_agg_handle* h, int on);
+
 /* ---- partial-state records: exchange / partition bucket (EAGG/payload.rs:356-391,
  *      EAGG/partitioned_payload.rs:100-143, AGG/aggregate_exchange_injector.rs:154-235) ----
  * A record = [hash u64][group keys, fixed part][state words]; string keys are (u64 offset, u64 len)
@@ -227,6 +235,26 @@ int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strin
 int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void* dev_strings,
                           int32_t n_segments, const uint64_t* seg_records,
                           const uint64_t* seg_string_bytes);
+
+/* ---- fixed-capacity exchange: replicas + gather for low-cardinality tables ----
+ * Replaces, for small inline-key partial tables, the Serialized/Flight hand-off of
+ * TransformPartialAggregate::on_finish (AGG/transform_aggregate_partial.rs:449-465) to the final
+ * node's TransformFinalAggregate (AGG/transform_aggregate_final.rs:71-156).  A buffer holds
+ * (cap_records + 1) records of dbg_agg_record_width bytes: record 0 = [u64 group count][u64 flags],
+ * records 1..count = the groups ([hash][keys][state words]).  The count stays on the device, so
+ * an all-gather of equal-size buffers (RCCL) and the merge run without a host round trip.
+ * Inline (fixed-width, <= 8 byte) keys and tables of at most 8192 slots only
+ * (DBG_ERR_UNSUPPORTED otherwise: use dbg_agg_partition + dbg_agg_export_records).  A partial
+ * with more groups than cap_records, or with unresolved overflow, marks its buffer incomplete;
+ * the merging handle's finalize then fails with DBG_ERR_INVALID. */
+/* Current slot capacity of the table (a table holds at most capacity + 1 groups). */
+int dbg_agg_capacity(dbg_agg_handle* h, uint64_t* slots);
+/* In recycle mode (dbg_agg_set_recycle) the export also leaves the table empty, as
+ * dbg_agg_reset would. */
+int dbg_agg_export_fixed(dbg_agg_handle* h, void* dev_buf, uint64_t cap_records);
+/* Merge n_bufs fixed buffers laid end to end (an all-gather output) into h; the buffers are
+ * retained until dbg_agg_reset like on_device inputs. */
+int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs, uint64_t cap_records);
 
 /* ---- standalone filter (FilterExecutor::select + take, EXP/filter/filter_executor.rs:73-128) ----
  * sel_out (device) receives the ascending u32 row indices where the predicate is TRUE;

@@ -122,3 +122,83 @@ def test_exchange_partials_gloo(world):
     exp = {(s, i): [c, sm] for s, i, c, sm in zip(gk[0].values(), gk[1].values(), ga[0].values(), ga[1].values())}
     got = {k: v for m in results.values() for k, v in m.items()}
     assert got == exp
+
+
+def _worker_fixed(rank, world, port, q):
+    """Replicas + gather (the low-cardinality route of bench.py / exchange.gather_small): each
+    rank packs its partial groups into an equal-size buffer with the group count in record 0,
+    one all-gather moves them, the root merges."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from databend_amd import column as col
+    from databend_amd.aggregates import AggregateFunctionFactory
+    from databend_amd.column import Column
+    from databend_amd.exchange import all_gather_fixed
+    from oracle import oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(7)
+        n = 50_000
+        adv = np.where(rng.random(n) < 0.99, 0, rng.integers(1, 33, n)).astype(np.int16)
+        lo, hi = n * rank // world, n * (rank + 1) // world
+        F = AggregateFunctionFactory.instance()
+        pk, pa = oracle.aggregate([Column.from_numbers(col.Int16, adv[lo:hi])], [(F.get("count").to_abi(), None)])
+        h = oracle.group_hash(pk)
+        cap, w = 64, 24
+        buf = bytearray((cap + 1) * w)
+        g = len(pk[0])
+        struct.pack_into("<QQ", buf, 0, g, 0)
+        for j, (k, c) in enumerate(zip(pk[0].values(), pa[0].values())):
+            struct.pack_into("<QqQ", buf, (1 + j) * w, int(h[j]), int(k), int(c))
+        send = torch.frombuffer(buf, dtype=torch.uint8)
+        out = torch.empty(world * len(buf), dtype=torch.uint8)
+        all_gather_fixed(send, out)
+        merged = {}
+        if rank == 0:
+            ob = bytes(out.numpy())
+            for r in range(world):
+                base = r * len(buf)
+                cnt, flags = struct.unpack_from("<QQ", ob, base)
+                assert flags == 0 and cnt <= cap
+                for j in range(cnt):
+                    hh, k, c = struct.unpack_from("<QqQ", ob, base + (1 + j) * w)
+                    merged[k] = merged.get(k, 0) + c
+        q.put((rank, merged))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fixed_gather_gloo(world):
+    import torch.multiprocessing as mp
+    from databend_amd import column as col
+    from databend_amd.aggregates import AggregateFunctionFactory
+    from databend_amd.column import Column
+    from oracle import oracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_fixed, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, m = q.get(timeout=240)
+        results[r] = m
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(7)
+    n = 50_000
+    adv = np.where(rng.random(n) < 0.99, 0, rng.integers(1, 33, n)).astype(np.int16)
+    F = AggregateFunctionFactory.instance()
+    gk, ga = oracle.aggregate([Column.from_numbers(col.Int16, adv)], [(F.get("count").to_abi(), None)])
+    exp = {int(k): int(c) for k, c in zip(gk[0].values(), ga[0].values())}
+    assert results[0] == exp
+    assert all(results[r] == {} for r in range(1, world))

@@ -406,3 +406,67 @@ def test_benchmark_configs_match_oracle(cfg, n):
         filt = (cmp(0, op, const), [cols[name]])
     ok, oa = oracle_aggregate(keys, aggs, filt, threads=8)
     assert_results_equal(res["keys"], res["aggs"], ok, oa)
+
+
+def test_recycling_finalize_two_batches_and_short_buffers():
+    """dbg_agg_set_recycle: the fused small-table finalize re-initialises the table, so each
+    reset -> add_groups -> finalize_into cycle sees only its own batch; a finalize into buffers
+    that are too short must leave the table intact for the retry (no recycle)."""
+    from databend_amd import workloads
+    n = 2_000_000
+    r = workloads.ConfigRunner(2, n, copies=2)
+    try:
+        r._alloc_out(4, [1])  # 32 groups do not fit: first finalize fails, runner retries larger
+        for k in range(2):
+            r.step(k)
+            keys, aggs = r.results_host()
+            cols = oracle.datagen(2, n, start=k * n)
+            ok, oa = oracle_aggregate([cols["AdvEngineID"]], [("count", None)],
+                                      (cmp(0, "<>", 0), [cols["AdvEngineID"]]), threads=8)
+            assert_results_equal(keys, aggs, ok, oa)
+            r._alloc_out(4, [1])
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("cfg_rows", [(2, 3_000_000)])
+def test_fixed_exchange_two_partials_merge(cfg_rows):
+    """dbg_agg_export_fixed -> concatenated buffers (what the RCCL all-gather produces) ->
+    dbg_agg_merge_fixed -> finalize: equals one aggregation over both partials' rows.  Also an
+    undersized buffer must make the merging finalize fail (never a silent partial result)."""
+    import torch
+    from databend_amd import workloads
+    from databend_amd.exchange import fixed_capacity
+    cfg, n = cfg_rows
+    runners = [workloads.ConfigRunner(cfg, n, start=r * n) for r in range(2)]
+    final = AggregateHashTable(runners[0].params, HashTableConfig(False))
+    try:
+        cap = fixed_capacity(runners[0].table)
+        w = runners[0].table.record_width()
+        out = torch.empty(2 * (cap + 1) * w, dtype=torch.uint8, device="cuda")
+        for r, rn in enumerate(runners):
+            rn.insert(0)
+            rn.table.export_fixed(out[r * (cap + 1) * w:(r + 1) * (cap + 1) * w], cap)
+        final.merge_fixed(out, 2, cap)
+        blk = final.merge_result()
+        cols = oracle.datagen(cfg, 2 * n)
+        shape = workloads.SHAPES[cfg]
+        name, op, const = shape.predicate
+        ok, oa = oracle_aggregate([cols[k] for k in shape.keys], [(f, cols[c] if c else None) for f, c in shape.aggs],
+                                  (cmp(0, op, const), [cols[name]]), threads=8)
+        na = len(shape.aggs)
+        assert_results_equal(blk.columns[na:], blk.columns[:na], ok, oa)
+        # 32 groups into 8-record buffers: flagged incomplete
+        final.reset()
+        small = torch.empty(2 * 9 * w, dtype=torch.uint8, device="cuda")
+        for r, rn in enumerate(runners):
+            rn.insert(0)
+            rn.table.export_fixed(small[r * 9 * w:(r + 1) * 9 * w], 8)
+        final.merge_fixed(small, 2, 8)
+        from databend_amd.ffi import DbgError
+        with pytest.raises(DbgError):
+            final.merge_result()
+    finally:
+        final.close()
+        for rn in runners:
+            rn.close()
