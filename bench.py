@@ -4,7 +4,10 @@ Default workload (BASELINE.json configs[1]): ClickBench Q8-style
     SELECT AdvEngineID, COUNT(*) FROM hits WHERE AdvEngineID <> 0 GROUP BY AdvEngineID
 over 100M synthetic rows per GPU (AdvEngineID Int16, P(0) = 0.9937).  One step = one pass of the
 hot path over one batch: fresh table -> fused filter + GROUP BY over every row -> (N > 1: partial
-states routed by hash % N over RCCL and merged) -> result columns resident in HBM.
+states gathered (low cardinality) or routed by hash % N (high) over RCCL and merged) -> result
+columns resident in HBM.  Consecutive batches are pipelined on two streams (batch k's finalize /
+exchange overlaps batch k+1's insert; two tables alternate); every batch's work completes inside
+the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..5] [--rows R]
 
@@ -91,7 +94,7 @@ def main():
     from databend_amd import ffi
     from databend_amd.aggregator import AggregateHashTable, HashTableConfig
     from databend_amd import abi
-    from databend_amd.exchange import exchange_partial, gather_small
+    from databend_amd.exchange import GatherPipeline, exchange_partial
     from databend_amd.workloads import DEFAULT_ROWS, SHAPES, ConfigRunner, algorithmic_bytes
 
     cfg = args.config
@@ -115,13 +118,27 @@ def main():
                                          runner.inputs[0][k].dtype.type_id != abi.STRING for k in shape.keys) \
             and len(shape.keys) == 1 and runner.table.capacity <= 8192
 
+    # Batches are pipelined: batch k's finalize (and, N > 1, its exchange and
+    # final merge) overlaps batch k+1's insert on a second stream; drain() completes the last
+    # one inside the timed region.
+    pipe = None
+    if world == 1:
+        runner.enable_pipeline()
+    elif small:
+        pipe = GatherPipeline(runner, final, dev, rank, world)
+
+    def drain():
+        if world == 1:
+            return runner.pipe_drain()
+        if pipe is not None:
+            return pipe.drain()
+        return 0
+
     def step(k):
         if world == 1:
-            return runner.step(k)
-        if small:
-            runner.insert(k)
-            gather_small(runner.table, final, dev, root=0)
-            return runner.finalize_into(final.h) if rank == 0 else 0
+            return runner.pipe_step(k)
+        if pipe is not None:
+            return pipe.step(k)
         i = k % len(runner.inputs)
         t = runner.table
         t.reset()
@@ -133,6 +150,7 @@ def main():
 
     for k in range(args.warmup):
         step(k)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -140,6 +158,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k)
+    drain()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -155,6 +174,7 @@ def main():
     ffi.prof_enable(True)
     for k in range(args.steps):
         step(args.warmup + args.steps + k)
+    drain()
     torch.cuda.synchronize()
     ffi.prof_enable(False)
     prof = ffi.prof_read()

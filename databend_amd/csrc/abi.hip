@@ -117,6 +117,17 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+struct FinState {
+    bool active = false;
+    std::vector<dbg_out_column> aggs, keys;
+    u64 max_groups = 0;
+    bool has_max_str = false;
+    std::vector<u64> max_str;
+    u64 cap_str[DBG_MAX_KEYS] = {};
+    bool zero_copy = false;
+    u64 seq = 0;
+};
+
 struct dbg_agg_handle {
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
@@ -171,6 +182,9 @@ struct dbg_agg_handle {
     // fused finalize: validity bytes staging
     u8* vbytes = nullptr;
     u64 vbytes_cap = 0;
+    // fused finalize in flight (dbg_agg_finalize_into_async)
+    FinState fin;
+    hipEvent_t switch_ev = nullptr;  // dbg_agg_set_stream hand-off
     // recycle mode (dbg_agg_set_recycle): a small-table finalize_into leaves the table empty
     int recycle = 0;
     bool clean = false;           // table already re-initialised by the last finalize
@@ -676,6 +690,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     for (void* p : bufs)
         if (p) hipFree(p);
     if (h->hcounters) hipHostFree(h->hcounters);
+    if (h->switch_ev) hipEventDestroy(h->switch_ev);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
 }
@@ -685,7 +700,11 @@ int dbg_agg_set_stream(dbg_agg_handle* h, void* s) {
     HIPCHECK(hipSetDevice(h->device));
     hipStream_t ns = s ? (hipStream_t)s : h->own_stream;
     if (ns != h->stream) {
-        HIPCHECK(hipStreamSynchronize(h->stream));
+        // device-side hand-off: work queued on the new stream waits for everything queued on the
+        // old one (no host synchronisation, so a caller can alternate streams per launch)
+        if (!h->switch_ev) HIPCHECK(hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(h->switch_ev, h->stream));
+        HIPCHECK(hipStreamWaitEvent(ns, h->switch_ev, 0));
         h->stream = ns;
     }
     return DBG_OK;
@@ -934,13 +953,148 @@ int dbg_agg_set_recycle(dbg_agg_handle* h, int on) {
     return DBG_OK;
 }
 
-int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, uint64_t max_groups,
-                          const uint64_t* max_string_bytes, uint64_t* n_groups, uint64_t* string_bytes) {
-    if (!h || !out_aggs || !out_keys || !n_groups) return fail(DBG_ERR_INVALID, "null argument");
-    HIPCHECK(hipSetDevice(h->device));
+// Fused finalize, split into launch and completion so a caller can overlap the device work with
+// other launches (dbg_agg_finalize_into_async / dbg_agg_finalize_wait).
+static int fin_launch(dbg_agg_handle* h) {
+    FinState& F = h->fin;
     const Spec& S = h->spec;
+    u64 nb = finalize_blocks(h->cap);
+    RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
+    RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
+    TableDesc t = table_desc(h);
+    const bool small = h->cap + 1 <= FIN_SMALL_SLOTS;
+    u64* totals = h->d_pos + nb;
+    if (!small) {
+        prof::Scope ps("count_groups", h->stream);
+        launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+        launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
+        if (S.has_strings && !S.inline_keys)
+            for (int c = 0; c < S.n_keys; ++c)
+                if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
+    }
+    OutDesc od;
+    memset(&od, 0, sizeof(od));
+    od.cap_groups = F.max_groups;
+    u8* vb = h->vbytes;
+    for (int c = 0; c < S.n_keys; ++c) {
+        od.key_data[c] = F.keys[c].data;
+        od.key_offsets[c] = S.key_types[c].type == DBG_STRING ? F.keys[c].offsets : nullptr;
+        od.cap_str[c] = (S.key_types[c].type == DBG_STRING && F.has_max_str) ? F.max_str[c] : 0;
+        F.cap_str[c] = od.cap_str[c];
+        if (S.key_types[c].nullable) {
+            od.key_valid[c] = vb;
+            od.key_bits[c] = F.keys[c].validity;
+            vb += F.max_groups + 1;
+        }
+    }
+    for (int a = 0; a < S.n_aggs; ++a) {
+        od.agg_data[a] = F.aggs[a].data;
+        if (h->result_types[a].nullable) {
+            od.agg_valid[a] = vb;
+            od.agg_bits[a] = F.aggs[a].validity;
+            vb += F.max_groups + 1;
+        }
+    }
+    F.zero_copy = small && h->hcounters_dev != nullptr;
+    F.seq = ++h->fin_seq;
+    if (small) {
+        prof::Scope ps("finalize_small", h->stream);
+        launch_finalize_small(h->stream, h->dspec, h->dbatches, t, od, totals, F.zero_copy ? h->hcounters_dev : nullptr,
+                              h->recycle && F.zero_copy, F.seq);
+    } else {
+        prof::Scope ps("write_results", h->stream);
+        launch_write_results(h->stream, h->dspec, S, h->dbatches, t, h->d_pos, h->d_str_pos, od);
+        launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);
+    }
+    if (!F.zero_copy) {
+        HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
+    }
+    F.active = true;
+    return DBG_OK;
+}
+
+// Wait for the launched round; *retry = the inserts had overflowed (now resolved: launch again).
+static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint64_t* string_bytes) {
+    FinState& F = h->fin;
+    const Spec& S = h->spec;
+    *retry = false;
+    F.active = false;
+    bool recycled = false;
+    if (!F.zero_copy) {
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    } else {
+        // the kernel posts `seq` last (after its write-through mirror stores): spin on it
+        // instead of a stream synchronisation (whose wake-up costs several microseconds); after
+        // ~20 ms fall back to the blocking wait (long queued inserts)
+        volatile u64* hseq = h->hcounters + CNT_WORDS + 2 + DBG_MAX_KEYS;
+        bool seen = false;
+        auto t0 = std::chrono::steady_clock::now();
+        for (u64 it = 0;; ++it) {
+            if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == F.seq) {
+                seen = true;
+                break;
+            }
+            if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+            __builtin_ia32_pause();
+        }
+        if (!seen) HIPCHECK(hipStreamSynchronize(h->stream));
+        HIPCHECK(hipGetLastError());
+        recycled = h->hcounters[CNT_WORDS + 1 + DBG_MAX_KEYS] != 0;
+    }
+    h->uploads_pending = false;
+    if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+    if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
+        return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
+                                     "buffer, or unresolved overflow): use dbg_agg_partition + export_records");
+    if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {
+        RETURN_IF(resolve_overflow(h));
+        *retry = true;
+        return DBG_OK;
+    }
+    h->pending_rows = h->pending_recs = 0;
+    const u64* tot = h->hcounters + CNT_WORDS;
+    h->n_groups = tot[0];
+    h->string_bytes.assign(S.n_keys, 0);
+    bool short_buf = h->n_groups > F.max_groups;
+    for (int c = 0; c < S.n_keys; ++c) {
+        h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? tot[1 + c] : 0;
+        if (S.key_types[c].type == DBG_STRING && h->string_bytes[c] > F.cap_str[c]) short_buf = true;
+    }
+    *n_groups = h->n_groups;
+    if (string_bytes)
+        for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
+    if (h->n_groups != h->hcounters[CNT_CLAIMS])
+        return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
+                                          std::to_string(h->hcounters[CNT_CLAIMS]));
+    h->finalized = true;
+    if (recycled) {  // the table was re-initialised by the kernel: dbg_agg_reset state
+        h->clean = true;
+        h->finalized = false;
+        h->n_batches = h->n_cached;
+        h->pending_rows = h->pending_recs = 0;
+    }
+    if (h->hcounters[CNT_ERR] & ERR_DEC_OVERFLOW) {
+        if (!recycled) HIPCHECK(hipMemsetAsync(h->counters + CNT_ERR, 0, 8, h->stream));
+        return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
+    }
+    if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
+    return DBG_OK;
+}
+
+static int fin_setup(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, uint64_t max_groups,
+                     const uint64_t* max_string_bytes) {
+    const Spec& S = h->spec;
+    FinState& F = h->fin;
     for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = h->result_types[a];
     for (int c = 0; c < S.n_keys; ++c) out_keys[c].dt = S.key_types[c];
+    F.aggs.assign(out_aggs, out_aggs + S.n_aggs);
+    F.keys.assign(out_keys, out_keys + S.n_keys);
+    F.max_groups = max_groups;
+    F.has_max_str = max_string_bytes != nullptr;
+    F.max_str.assign(S.n_keys, 0);
+    if (max_string_bytes)
+        for (int c = 0; c < S.n_keys; ++c) F.max_str[c] = max_string_bytes[c];
     // validity bytes staging (bit-packed into the caller's buffers by finish_outputs)
     int n_nullable = 0;
     for (int c = 0; c < S.n_keys; ++c) n_nullable += S.key_types[c].nullable ? 1 : 0;
@@ -951,115 +1105,33 @@ int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_c
         h->vbytes_cap = std::max<u64>(need, 4096);
         RETURN_IF(dev_alloc((void**)&h->vbytes, h->vbytes_cap));
     }
+    return DBG_OK;
+}
+
+int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, uint64_t max_groups,
+                          const uint64_t* max_string_bytes, uint64_t* n_groups, uint64_t* string_bytes) {
+    RETURN_IF(dbg_agg_finalize_into_async(h, out_aggs, out_keys, max_groups, max_string_bytes));
+    return dbg_agg_finalize_wait(h, n_groups, string_bytes);
+}
+
+int dbg_agg_finalize_into_async(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, uint64_t max_groups,
+                                const uint64_t* max_string_bytes) {
+    if (!h || !out_aggs || !out_keys) return fail(DBG_ERR_INVALID, "null argument");
+    if (h->fin.active) return fail(DBG_ERR_INVALID, "a finalize is already in flight: dbg_agg_finalize_wait first");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(fin_setup(h, out_aggs, out_keys, max_groups, max_string_bytes));
+    return fin_launch(h);
+}
+
+int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
+    if (!h || !n_groups) return fail(DBG_ERR_INVALID, "null argument");
+    if (!h->fin.active) return fail(DBG_ERR_INVALID, "no finalize in flight");
+    HIPCHECK(hipSetDevice(h->device));
     for (int round = 0; round < 3; ++round) {
-        u64 nb = finalize_blocks(h->cap);
-        RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
-        RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
-        TableDesc t = table_desc(h);
-        const bool small = h->cap + 1 <= FIN_SMALL_SLOTS;
-        u64* totals = h->d_pos + nb;
-        if (!small) {
-            prof::Scope ps("count_groups", h->stream);
-            launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
-            launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
-            if (S.has_strings && !S.inline_keys)
-                for (int c = 0; c < S.n_keys; ++c)
-                    if (S.key_types[c].type == DBG_STRING) launch_exclusive_scan(h->stream, h->d_str_pos + (u64)c * nb, nb, totals + 1 + c);
-        }
-        OutDesc od;
-        memset(&od, 0, sizeof(od));
-        od.cap_groups = max_groups;
-        u8* vb = h->vbytes;
-        for (int c = 0; c < S.n_keys; ++c) {
-            od.key_data[c] = out_keys[c].data;
-            od.key_offsets[c] = S.key_types[c].type == DBG_STRING ? out_keys[c].offsets : nullptr;
-            od.cap_str[c] = (S.key_types[c].type == DBG_STRING && max_string_bytes) ? max_string_bytes[c] : 0;
-            if (S.key_types[c].nullable) {
-                od.key_valid[c] = vb;
-                od.key_bits[c] = out_keys[c].validity;
-                vb += max_groups + 1;
-            }
-        }
-        for (int a = 0; a < S.n_aggs; ++a) {
-            od.agg_data[a] = out_aggs[a].data;
-            if (h->result_types[a].nullable) {
-                od.agg_valid[a] = vb;
-                od.agg_bits[a] = out_aggs[a].validity;
-                vb += max_groups + 1;
-            }
-        }
-        const bool zero_copy = small && h->hcounters_dev != nullptr;
-        const u64 seq = ++h->fin_seq;
-        volatile u64* hseq = h->hcounters + CNT_WORDS + 2 + DBG_MAX_KEYS;
-        if (small) {
-            prof::Scope ps("finalize_small", h->stream);
-            launch_finalize_small(h->stream, h->dspec, h->dbatches, t, od, totals, zero_copy ? h->hcounters_dev : nullptr,
-                                  h->recycle && zero_copy, seq);
-        } else {
-            prof::Scope ps("write_results", h->stream);
-            launch_write_results(h->stream, h->dspec, S, h->dbatches, t, h->d_pos, h->d_str_pos, od);
-            launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);
-        }
-        bool recycled = false;
-        if (!zero_copy) {
-            HIPCHECK(hipMemcpyAsync(h->hcounters, h->counters, CNT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
-            HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
-            HIPCHECK(hipStreamSynchronize(h->stream));
-        } else {
-            // the kernel posts `seq` last (system-scope release after every other write): spin
-            // on it instead of a stream synchronisation (whose wake-up costs several
-            // microseconds); after ~20 ms fall back to the blocking wait (long queued inserts)
-            bool seen = false;
-            auto t0 = std::chrono::steady_clock::now();
-            for (u64 it = 0;; ++it) {
-                if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == seq) {
-                    seen = true;
-                    break;
-                }
-                if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
-                __builtin_ia32_pause();
-            }
-            if (!seen) HIPCHECK(hipStreamSynchronize(h->stream));
-            HIPCHECK(hipGetLastError());
-            recycled = h->hcounters[CNT_WORDS + 1 + DBG_MAX_KEYS] != 0;
-        }
-        h->uploads_pending = false;
-        if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
-        if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
-            return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
-                                         "buffer, or unresolved overflow): use dbg_agg_partition + export_records");
-        if (h->hcounters[CNT_OVF_ROWS] || h->hcounters[CNT_OVF_RECS]) {
-            RETURN_IF(resolve_overflow(h));
-            continue;
-        }
-        h->pending_rows = h->pending_recs = 0;
-        const u64* tot = h->hcounters + CNT_WORDS;
-        h->n_groups = tot[0];
-        h->string_bytes.assign(S.n_keys, 0);
-        bool short_buf = h->n_groups > max_groups;
-        for (int c = 0; c < S.n_keys; ++c) {
-            h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? tot[1 + c] : 0;
-            if (S.key_types[c].type == DBG_STRING && h->string_bytes[c] > od.cap_str[c]) short_buf = true;
-        }
-        *n_groups = h->n_groups;
-        if (string_bytes)
-            for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
-        if (h->n_groups != h->hcounters[CNT_CLAIMS])
-            return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
-                                              std::to_string(h->hcounters[CNT_CLAIMS]));
-        h->finalized = true;
-        if (recycled) {  // the table was re-initialised by the kernel: dbg_agg_reset state
-            h->clean = true;
-            h->finalized = false;
-            h->n_batches = h->n_cached;
-            h->pending_rows = h->pending_recs = 0;
-        }
-        if (h->hcounters[CNT_ERR] & ERR_DEC_OVERFLOW) {
-            if (!recycled) HIPCHECK(hipMemsetAsync(h->counters + CNT_ERR, 0, 8, h->stream));
-            return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
-        }
-        if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
-        return DBG_OK;
+        if (round) RETURN_IF(fin_launch(h));
+        bool retry = false;
+        int rc = fin_complete(h, &retry, n_groups, string_bytes);
+        if (rc != DBG_OK || !retry) return rc;
     }
     return fail(DBG_ERR_INTERNAL, "finalize did not converge");
 }

@@ -114,3 +114,57 @@ def gather_small(partial, final, device, root: int = 0, cap_records: int = 0):
     if rank == root:
         final.merge_fixed(out, world, cap)
     return nbytes
+
+
+class GatherPipeline:
+    """Replicas + gather, pipelined over batches (bench.py, N > 1, low cardinality).
+
+    stream s1: insert(k) -> export_fixed(k) into send[k % 2]
+    stream s2: all-gather(k) -> (root) merge_fixed(k) -> fused finalize(k)
+    The host enqueues batch k+1's insert and all-gather before it waits for finalize(k), so the
+    exchange and final merge of one batch overlap the partial aggregation of the next.  Buffers
+    and events are per parity; export(k+2) waits for all-gather(k) to have read send[k % 2]."""
+
+    def __init__(self, runner, final, device, rank: int, world: int, root: int = 0):
+        import torch
+        self.runner, self.final, self.rank, self.world, self.root = runner, final, rank, world, root
+        self.s1 = torch.cuda.current_stream()
+        self.s2 = torch.cuda.Stream()
+        runner.table.set_stream(self.s1)
+        final.set_stream(self.s2)
+        self.cap = fixed_capacity(runner.table)
+        w = runner.table.record_width()
+        n = (self.cap + 1) * w
+        self.send = [torch.empty(n, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.recv = [torch.empty(world * n, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.ev_exp = [torch.cuda.Event() for _ in range(2)]
+        self.ev_gath = [torch.cuda.Event() for _ in range(2)]
+        self.used = [False, False]
+        self.pending = None  # parity whose merge + finalize is still to be enqueued / waited
+        self.bytes_per_rank = n
+
+    def step(self, k: int) -> int:
+        import torch
+        p = k % 2
+        r = self.runner
+        r.insert(k)
+        if self.used[p]:
+            self.s1.wait_event(self.ev_gath[p])
+        r.table.export_fixed(self.send[p], self.cap)
+        self.ev_exp[p].record(self.s1)
+        with torch.cuda.stream(self.s2):
+            self.s2.wait_event(self.ev_exp[p])
+            all_gather_fixed(self.send[p], self.recv[p])
+            self.ev_gath[p].record(self.s2)
+        self.used[p] = True
+        n = self.drain()
+        if self.rank == self.root:
+            self.final.merge_fixed(self.recv[p], self.world, self.cap)
+            r.finalize_async(self.final.h, p)
+            self.pending = p
+        return n
+
+    def drain(self) -> int:
+        """Wait for the finalize in flight (root only); returns its group count."""
+        p, self.pending = self.pending, None
+        return self.runner.finalize_wait(self.final.h, p) if p is not None else 0

@@ -174,7 +174,9 @@ int dbg_agg_result_type(const dbg_agg_spec* spec, dbg_datatype* out);
 /* AggregateHashTable::new + HashTableConfig (builder_aggregate.rs:132-164). */
 int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out);
 void dbg_agg_destroy(dbg_agg_handle* h);
-/* Launch on the caller's hipStream_t (NULL restores the handle's own stream). */
+/* Launch on the caller's hipStream_t (NULL restores the handle's own stream).  The switch is
+ * ordered on the device (work on the new stream waits for all work queued on the old one); the
+ * host does not block, so a caller may alternate streams per call to overlap handles. */
 int dbg_agg_set_stream(dbg_agg_handle* h, void* hip_stream);
 /* Drop all groups and retained inputs, keep device memory (a fresh table for the next query). */
 int dbg_agg_reset(dbg_agg_handle* h);
@@ -204,6 +206,14 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
 int dbg_agg_finalize_into(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys,
                           uint64_t max_groups, const uint64_t* max_string_bytes, uint64_t* n_groups,
                           uint64_t* string_bytes);
+
+/* The same in two halves: _async enqueues the finalize (the output columns fill in stream order)
+ * and returns; _wait delivers *n_groups / string_bytes (and any error) — other launches can be
+ * enqueued in between, e.g. the next batch's insert into another handle.  At most one finalize
+ * per handle is in flight; the out column structs are copied by _async. */
+int dbg_agg_finalize_into_async(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys,
+                                uint64_t max_groups, const uint64_t* max_string_bytes);
+int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes);
 
 /* Recycle mode (default off): a dbg_agg_finalize_into that delivers every group of a small table
  * (low cardinality, finalized in one workgroup) also re-initialises the table in that same

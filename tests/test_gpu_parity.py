@@ -470,3 +470,35 @@ def test_fixed_exchange_two_partials_merge(cfg_rows):
         final.close()
         for rn in runners:
             rn.close()
+
+
+@pytest.mark.parametrize("mode", ["single", "dual"])
+@pytest.mark.parametrize("cfg,n", [(2, 2_000_000), (3, 500_000), (5, 500_000)])
+def test_pipelined_batches_match_oracle(cfg, n, mode):
+    """ConfigRunner.pipe_step: batch k's finalize (dbg_agg_finalize_into_async) is still in flight
+    when batch k+1's insert is enqueued into the other table; each batch's published result,
+    delivered by the next pipe_step (or pipe_drain for the last), equals the oracle over that
+    batch's rows alone."""
+    from databend_amd import workloads
+    shape = workloads.SHAPES[cfg]
+    r = workloads.ConfigRunner(cfg, n, copies=3)
+    try:
+        r.enable_pipeline(mode)
+        got = []
+        for k in range(4):
+            r.pipe_step(k)
+            if k:
+                got.append(r.results_host())
+        r.pipe_drain()
+        got.append(r.results_host())
+        for k, (keys, aggs) in enumerate(got):
+            cols = oracle.datagen(cfg, n, start=(k % 3) * n)
+            filt = None
+            if shape.predicate:
+                name, op, const = shape.predicate
+                filt = (cmp(0, op, const), [cols[name]])
+            ok, oa = oracle_aggregate([cols[c] for c in shape.keys],
+                                      [(f, cols[c] if c else None) for f, c in shape.aggs], filt, threads=8)
+            assert_results_equal(keys, aggs, ok, oa)
+    finally:
+        r.close()
