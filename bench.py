@@ -121,22 +121,28 @@ def main():
     # Batches are pipelined: batch k's finalize (and, N > 1, its exchange and
     # final merge) overlaps batch k+1's insert on a second stream; drain() completes the last
     # one inside the timed region.
+    # Pipelining pays where a step is tens of microseconds (C1, C2).  A high-cardinality step is
+    # milliseconds of GPU work per launch, and a second table of its size (C4: 2^31 slots x 64 B)
+    # would not fit next to the first, so those run one table, step after step.
     pipe = None
-    if world == 1:
+    pipelined = world == 1 and cfg in (1, 2)
+    if pipelined:
         runner.enable_pipeline()
     elif small:
         pipe = GatherPipeline(runner, final, dev, rank, world)
 
     def drain():
-        if world == 1:
+        if pipelined:
             return runner.pipe_drain()
         if pipe is not None:
             return pipe.drain()
         return 0
 
     def step(k):
-        if world == 1:
+        if pipelined:
             return runner.pipe_step(k)
+        if world == 1:
+            return runner.step(k)
         if pipe is not None:
             return pipe.step(k)
         i = k % len(runner.inputs)

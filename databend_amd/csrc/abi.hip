@@ -139,6 +139,7 @@ struct dbg_agg_handle {
     // table
     u64* slots = nullptr;
     u64 cap = 0;
+    u64 init_cap = 0;  // from the capacity hint: the table never shrinks below it
     u64* counters = nullptr;   // device, CNT_WORDS
     u64* hcounters = nullptr;  // pinned
     u64* hcounters_dev = nullptr;  // its device mapping (finalize_small writes it directly)
@@ -190,6 +191,13 @@ struct dbg_agg_handle {
     bool clean = false;           // table already re-initialised by the last finalize
     u64 fin_seq = 0;              // sequence number the finalize kernel posts to host_mirror
     bool uploads_pending = false; // descriptor uploads from pinned staging since the last sync
+    // radix-partitioned insert (part.hip): sorted mixed keys, slice bounds, rocPRIM scratch
+    u64* part_sorted = nullptr;
+    u64 part_sorted_cap = 0;
+    u64* part_bounds = nullptr;
+    u64 part_bounds_cap = 0;
+    void* part_temp = nullptr;
+    size_t part_temp_cap = 0;
 };
 
 static int dev_alloc(void** p, size_t bytes) {
@@ -391,17 +399,26 @@ static int read_counters(dbg_agg_handle* h) {
 // Resolve deferred overflow: grow so that every pending group fits at <= 50% load, re-insert.
 static int resolve_overflow(dbg_agg_handle* h) {
     RETURN_IF(read_counters(h));
+    bool grew = false;  // sized by overflowed rows this call: shrink to the groups once known
     for (int round = 0; round < 4; ++round) {
         u64 claims = h->hcounters[CNT_CLAIMS], orows = h->hcounters[CNT_OVF_ROWS], orecs = h->hcounters[CNT_OVF_RECS];
         if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
         if (orows == 0 && orecs == 0) {
             h->pending_rows = h->pending_recs = 0;
             // keep the load factor sane for the next batch (the reference resizes at 1/1.5)
-            if ((double)claims * 1.5 > (double)h->cap) RETURN_IF(grow_table(h, pow2_at_least((u64)(claims * 2.0) + 1)));
+            const u64 fit = std::max<u64>(pow2_at_least((u64)(claims * 2.0) + 1), 1024);
+            if ((double)claims * 1.5 > (double)h->cap) RETURN_IF(grow_table(h, fit));
+            // overflow growth sizes by overflowed ROWS (an upper bound on the groups they hold):
+            // once the groups are known, give back a table more than 4x what they need, so scans
+            // (finalize, table_init) and partitioned inserts touch 2x the groups, not 30x
+            else if (grew && h->cap >= 4 * fit && fit >= h->init_cap) RETURN_IF(grow_table(h, fit));
             return DBG_OK;
         }
         u64 need = pow2_at_least(2 * (claims + orows + orecs) + 1);
-        if (need > h->cap) RETURN_IF(grow_table(h, need));
+        if (need > h->cap) {
+            RETURN_IF(grow_table(h, need));
+            grew = true;
+        }
         HIPCHECK(hipMemsetAsync(h->counters + CNT_OVF_ROWS, 0, 16, h->stream));
         {
             prof::Scope ps("agg_retry", h->stream);
@@ -663,6 +680,7 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     // small table keeps init / finalize scans short for low-cardinality queries)
     u64 hint = params->capacity_hint ? params->capacity_hint : 2048;
     h->cap = pow2_at_least(std::max<u64>(hint * 2, 1024));
+    h->init_cap = h->cap;
     if ((rc = alloc_table(h, h->cap, &h->slots)) != DBG_OK) return cleanup(rc);
     // parking rows for every workgroup of an insert launch (launch_insert caps its grid here)
     h->scr_blocks = DBG_INSERT_MAX_BLOCKS;
@@ -686,7 +704,8 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     for (auto& b : h->owned) hipFree(b.p);
     for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
-                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->vbytes};
+                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->vbytes, h->part_sorted, h->part_bounds,
+                    h->part_temp};
     for (void* p : bufs)
         if (p) hipFree(p);
     if (h->hcounters) hipHostFree(h->hcounters);
@@ -731,6 +750,31 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     return DBG_OK;
 }
 
+static int ensure_buf(u64** p, u64* cap, u64 n);
+
+// Radix-partitioned COUNT(*) insert of a high-cardinality batch (part.hip); buffers grow only.
+static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, u32 sb) {
+    (void)bid;
+    const int width = (int)st->keys[0].width;
+    size_t tb = part_temp_bytes(width, rows, sb, h->cap);
+    if (!tb) return fail(DBG_ERR_INTERNAL, "rocprim radix_sort_keys sizing failed");
+    if (tb > h->part_temp_cap) {
+        if (h->part_temp) HIPCHECK(hipFree(h->part_temp));
+        h->part_temp = nullptr;
+        h->part_temp_cap = 0;
+        RETURN_IF(dev_alloc(&h->part_temp, tb));
+        h->part_temp_cap = tb;
+    }
+    RETURN_IF(ensure_buf(&h->part_sorted, &h->part_sorted_cap, rows));
+    RETURN_IF(ensure_buf(&h->part_bounds, &h->part_bounds_cap, (h->cap >> sb) + 1));
+    prof::Scope ps("agg_insert", h->stream);
+    const char* step = "";
+    hipError_t e = launch_part_insert(h->stream, *st, rows, table_desc(h), sb, h->part_temp, h->part_temp_cap, h->part_sorted,
+                                      h->part_bounds, &step);
+    if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("partitioned insert (") + step + "): " + hipGetErrorString(e));
+    return DBG_OK;
+}
+
 int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols, const dbg_filter* filter,
                        uint64_t rows, int on_device) {
     if (!h || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
@@ -760,6 +804,16 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     RETURN_IF(submit_batch(h, &st, &bid, on_device && h->owned.size() == owned0));
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
     u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
+    if (part_slice_bits(S, *st, rows, h->cap)) {
+        // radix-partitioned insert: every row may become an overflow record (probe left its
+        // slice).  ensure_ovf may resolve pending overflow (and resize): shape after it.
+        RETURN_IF(ensure_ovf(h, 0, rows));
+    }
+    if (u32 sb = part_slice_bits(S, *st, rows, h->cap)) {
+        RETURN_IF(part_insert(h, st, bid, rows, sb));
+        if (!on_device) RETURN_IF(resolve_overflow(h));
+        return DBG_OK;
+    }
     RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
     {
         prof::Scope ps("agg_insert", h->stream);

@@ -25,9 +25,7 @@
 #define LDS_PROBE_CAP 64
 #define FLUSH_ROUND 16  // rounds of BLOCK rows between checks for a full LDS table
 
-// Slot placement for inline keys: any good mixer works (placement is not observable); the
-// reference hash is recomputed from the key wherever routing needs it.
-__device__ __forceinline__ u64 slot_mix(u64 x) { return hash_prim(x ^ 0x9E3779B97F4A7C15ULL); }
+// slot_mix (inline-key slot placement) lives in agg.hpp
 
 // ------------------------------------------------------------------------------------------
 // Key packing (inline mode): the row format of EAGG/payload.rs:100-129 in <= 8 bytes.
@@ -96,38 +94,7 @@ __device__ __forceinline__ u64 entry_hash(const Spec& S, const BatchDesc* batche
 // branch) compiles to FLAT atomics, which count against vmcnt as well as lgkmcnt — every LDS
 // wait then drains all global loads in flight and the streaming pipeline collapses.
 // ------------------------------------------------------------------------------------------
-#define AS_GLB 1
-#define AS_LDS 3
-template <int AS> using wptr = __attribute__((address_space(AS))) u64*;
-template <int AS> using sptr = __attribute__((address_space(AS))) long long*;
-template <int AS> using dptr = __attribute__((address_space(AS))) double*;
-template <int AS> using vwptr = volatile __attribute__((address_space(AS))) u64*;
-template <int AS> __device__ __forceinline__ wptr<AS> asp(u64* p) { return (wptr<AS>)p; }
-template <int AS> __device__ __forceinline__ wptr<AS> asp(const u64* p) { return (wptr<AS>)(u64*)p; }
-#define AT_SCOPE(AS) ((AS) == AS_LDS ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT)
-template <int AS> __device__ __forceinline__ u64 at_add(wptr<AS> p, u64 v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-}
-template <int AS> __device__ __forceinline__ void at_addf(wptr<AS> p, double v) {
-    __hip_atomic_fetch_add((dptr<AS>)p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-}
-template <int AS> __device__ __forceinline__ void at_or(wptr<AS> p, u64 v) {
-    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-}
-template <int AS> __device__ __forceinline__ void at_minmax(wptr<AS> p, u64 v, bool mn, bool sgn) {
-    if (sgn) {
-        if (mn) __hip_atomic_fetch_min((sptr<AS>)p, (long long)v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-        else __hip_atomic_fetch_max((sptr<AS>)p, (long long)v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-    } else {
-        if (mn) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-        else __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
-    }
-}
-template <int AS> __device__ __forceinline__ u64 at_cas(wptr<AS> p, u64 expected, u64 desired) {
-    __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AT_SCOPE(AS));
-    return expected;  // the old value (== the expected one iff the exchange happened)
-}
-template <int AS> __device__ __forceinline__ u64 vld(wptr<AS> p) { return *(vwptr<AS>)p; }
+// wptr / asp / at_* / vld live in agg.hpp (shared with part.hip)
 
 template <int AS>
 __device__ __forceinline__ void add128(wptr<AS> p, u64 lo, u64 hi) {
@@ -173,9 +140,6 @@ __device__ __forceinline__ void apply_row(const Spec& S, wptr<AS> st, const Batc
 
 // merge_states of a partial state (word array r, same layout) into st.  SC1: read r with sc1
 // loads (words parked by another workgroup in this launch, see block_flush).
-__device__ __forceinline__ u64 ld_sc1(const u64* p) {
-    return __hip_atomic_load((wptr<AS_GLB>)(u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // RAS: address space of r (LDS table rows being flushed, or global records / parked rows)
 template <bool SC1, int RAS>
 __device__ __forceinline__ u64 rdw(const u64* p) { return SC1 ? ld_sc1(p) : *asp<RAS>(p); }
@@ -1039,6 +1003,7 @@ __global__ void __launch_bounds__(BLOCK) agg_retry_kernel(const Spec* __restrict
         } else {
             const u64* r = recs_list + (k - n_rows) * t.stride_words;
             u64 key = r[0];
+            if (INLINE && key == SLOT_EMPTY) continue;  // consumed by part_fixup (never a record key)
             u64 h = 0;
             if (!INLINE) {
                 const BatchDesc& B = batches[ref_bid(key)];

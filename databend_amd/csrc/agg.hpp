@@ -67,10 +67,77 @@ struct TableDesc {
 #define SCR_GROUP 16
 #define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
-enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_WORDS = 8 };
+enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_WORDS = 8 };
 enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4 };
 
+// ---- device helpers shared by agg.hip and part.hip ----
+// Slot placement for inline keys: any good mixer works (placement is not observable); the
+// reference hash is recomputed from the key wherever routing needs it.  A bijection of u64
+// (xor-shift by 32 and odd multipliers are invertible), so part.hip can sort mixed keys and
+// recover the key with slot_unmix.
+__host__ __device__ __forceinline__ u64 slot_mix(u64 x) { return hash_prim(x ^ 0x9E3779B97F4A7C15ULL); }
+constexpr u64 mul_inverse_u64(u64 c) {
+    u64 x = c;  // c * c == 1 (mod 8); each Newton step doubles the correct low bits
+    for (int i = 0; i < 6; ++i) x *= 2 - c * x;
+    return x;
+}
+__host__ __device__ __forceinline__ u64 slot_unmix(u64 y) {
+    constexpr u64 CI = mul_inverse_u64(0xd6e8feb86659fd93ULL);
+    y ^= y >> 32;
+    y *= CI;
+    y ^= y >> 32;
+    y *= CI;
+    y ^= y >> 32;
+    return y ^ 0x9E3779B97F4A7C15ULL;
+}
+static_assert(0xd6e8feb86659fd93ULL * mul_inverse_u64(0xd6e8feb86659fd93ULL) == 1, "inverse");
+
+// State updates on an LDS (AS_LDS) or HBM (AS_GLB) slot; the address space is a template
+// parameter (see agg.hip: a generic pointer compiles to FLAT atomics).
+#define AS_GLB 1
+#define AS_LDS 3
+template <int AS> using wptr = __attribute__((address_space(AS))) u64*;
+template <int AS> using sptr = __attribute__((address_space(AS))) long long*;
+template <int AS> using dptr = __attribute__((address_space(AS))) double*;
+template <int AS> using vwptr = volatile __attribute__((address_space(AS))) u64*;
+template <int AS> __device__ __forceinline__ wptr<AS> asp(u64* p) { return (wptr<AS>)p; }
+template <int AS> __device__ __forceinline__ wptr<AS> asp(const u64* p) { return (wptr<AS>)(u64*)p; }
+#define AT_SCOPE(AS) ((AS) == AS_LDS ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT)
+template <int AS> __device__ __forceinline__ u64 at_add(wptr<AS> p, u64 v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+}
+template <int AS> __device__ __forceinline__ void at_addf(wptr<AS> p, double v) {
+    __hip_atomic_fetch_add((dptr<AS>)p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+}
+template <int AS> __device__ __forceinline__ void at_or(wptr<AS> p, u64 v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+}
+template <int AS> __device__ __forceinline__ void at_minmax(wptr<AS> p, u64 v, bool mn, bool sgn) {
+    if (sgn) {
+        if (mn) __hip_atomic_fetch_min((sptr<AS>)p, (long long)v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        else __hip_atomic_fetch_max((sptr<AS>)p, (long long)v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+    } else {
+        if (mn) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        else __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
+    }
+}
+template <int AS> __device__ __forceinline__ u64 at_cas(wptr<AS> p, u64 expected, u64 desired) {
+    __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AT_SCOPE(AS));
+    return expected;  // the old value (== the expected one iff the exchange happened)
+}
+template <int AS> __device__ __forceinline__ u64 vld(wptr<AS> p) { return *(vwptr<AS>)p; }
+
+// device-scope (L2-bypassing) load of a word another workgroup of this launch may write
+__device__ __forceinline__ u64 ld_sc1(const u64* p) {
+    return __hip_atomic_load((wptr<AS_GLB>)(u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- launch wrappers (agg.hip) ----
+// part.hip: radix-partitioned COUNT(*) insert for high-cardinality single integer keys
+u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap);  // 0 = not eligible
+size_t part_temp_bytes(int width, u64 rows, u32 sb, u64 cap);
+hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, const TableDesc& t, u32 sb, void* temp,
+                              size_t temp_bytes, u64* sorted, u64* bounds, const char** step);
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
                    bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr);

@@ -502,3 +502,39 @@ def test_pipelined_batches_match_oracle(cfg, n, mode):
             assert_results_equal(keys, aggs, ok, oa)
     finally:
         r.close()
+
+
+PART_CASES = [
+    # (key type, distinct keys, rows, capacity hint, batches)
+    ("i64", 600_000, 3_000_000, 1 << 20, 2),      # slices hold every group (load ~0.3)
+    ("i64", 1_500_000, 3_000_000, 1 << 19, 1),    # cap 2^20 too small: overflow records + growth
+    ("i32", 400_000, 2_000_000, 1 << 19, 3),
+    ("i16", 65_536, 2_000_000, 1 << 19, 1),       # every i16 value, including -1 (all-ones key)
+    ("u8", 256, 1_000_000, 1 << 19, 1),
+]
+
+
+@pytest.mark.parametrize("kind,distinct,n,hint,batches", PART_CASES, ids=lambda x: str(x))
+def test_partitioned_insert(kind, distinct, n, hint, batches, monkeypatch):
+    """part.hip: radix-partitioned COUNT(*) insert (rocPRIM sort of mixed keys + one workgroup per
+    64 KB table slice in LDS).  Thresholds lowered so test-sized batches take the path; the
+    sentinel key (all-ones), runs that leave a slice (overflow records -> agg_retry), growth,
+    and several batches into one table are all covered."""
+    monkeypatch.setenv("DBG_PART_MIN_ROWS", "1000")
+    monkeypatch.setenv("DBG_PART_MIN_CAP", str(1 << 20))
+    rng = np.random.default_rng(distinct)
+    t = {"i64": col.Int64, "i32": col.Int32, "i16": col.Int16, "u8": col.UInt8}[kind]
+    if kind == "i64":
+        pool = rng.integers(-2**63, 2**63 - 1, distinct, dtype=np.int64)
+        pool[0] = -1  # packs to the EMPTY entry: sentinel slot
+    elif kind == "i32":
+        pool = rng.integers(-2**31, 2**31 - 1, distinct, dtype=np.int64)
+        pool[0] = -1
+    elif kind == "i16":
+        pool = np.arange(-2**15, 2**15, dtype=np.int64)
+    else:
+        pool = np.arange(0, 256, dtype=np.int64)
+    vals = pool[rng.integers(0, len(pool), n)]
+    key = Column.from_numbers(t, vals.astype(t.np_dtype))
+    g = check_parity([key], [("count", None)], on_device=True, capacity_hint=hint, batches=batches)
+    assert g == len(np.unique(vals))
