@@ -28,7 +28,7 @@
 #include "agg.hpp"
 
 #define PART_NT 1024
-#define PART_LDS_BYTES (64 * 1024)
+#define PART_SB 12  // slice = 4096 slots x 16 B = 64 KB of LDS
 #define PART_PROBE_CAP 64
 
 namespace {
@@ -56,21 +56,31 @@ __global__ void __launch_bounds__(256) part_bounds_kernel(const u64* __restrict_
 
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 
-// One workgroup per table slice [b * S, (b + 1) * S).  COUNT(*) only: slot = [entry][count].
+// One workgroup per table slice [b * S, (b + 1) * S), S = 2^SB slots.  COUNT(*) only: slot =
+// [entry][count].  The slice size is a compile-time constant so that the slice's loads (S / NT
+// 16-byte vectors per lane) are all in flight together before the first LDS store waits on
+// them: one memory latency per workgroup, not one per load.
+template <int SB>
 __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restrict__ sorted, const u64* __restrict__ bounds,
-                                                             TableDesc t, u32 sb) {
+                                                             TableDesc t) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     __shared__ u32 lclaims;
-    const u64 S = 1ULL << sb;
+    constexpr u64 S = 1ULL << SB;
+    constexpr int PER = (int)(S / PART_NT);
+    static_assert(PER >= 1 && S % PART_NT == 0, "slice size");
     const u64 b = blockIdx.x;
     const u64 s0 = b * S;
     const u64 mask = t.cap - 1;
+    const u64 lo = bounds[b], hi = bounds[b + 1];
     // slice -> LDS (16-byte loads; the slot stride is 2 words)
     const v2u64 __attribute__((address_space(1)))* gsl = (const v2u64 __attribute__((address_space(1)))*)(t.slots + s0 * 2);
     v2u64* lsl = (v2u64*)lds;
-    for (u32 i = threadIdx.x; i < S; i += PART_NT) lsl[i] = gsl[i];
+    v2u64 sv[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) sv[k] = gsl[threadIdx.x + k * PART_NT];
     if (threadIdx.x == 0) lclaims = 0;
-    const u64 lo = bounds[b], hi = bounds[b + 1];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) lsl[threadIdx.x + k * PART_NT] = sv[k];
     __syncthreads();
     u32 my_claims = 0;
     auto one = [&](u64 m) {
@@ -125,7 +135,8 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     if (my_claims) atomicAdd(&lclaims, my_claims);
     __syncthreads();
     v2u64 __attribute__((address_space(1)))* osl = (v2u64 __attribute__((address_space(1)))*)(t.slots + s0 * 2);
-    for (u32 i = threadIdx.x; i < S; i += PART_NT) osl[i] = lsl[i];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) osl[threadIdx.x + k * PART_NT] = lsl[threadIdx.x + k * PART_NT];
     if (threadIdx.x == 0 && lclaims) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lclaims);
 }
 
@@ -226,9 +237,10 @@ u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap) {
     const u64 min_rows = getenv("DBG_PART_MIN_ROWS") ? strtoull(getenv("DBG_PART_MIN_ROWS"), nullptr, 10) : (1ULL << 22);
     const u64 min_cap = getenv("DBG_PART_MIN_CAP") ? strtoull(getenv("DBG_PART_MIN_CAP"), nullptr, 10) : (1ULL << 20);
     if (rows < min_rows || cap < min_cap) return 0;
-    u32 sb = log2u(PART_LDS_BYTES / 16);  // 4096 slots of 16 B
-    if ((1ULL << sb) > cap / 2) sb = log2u(cap / 2);
-    return sb;
+    // 4096 slots of 16 B per slice (the kernel is instantiated for this size only; at least two
+    // slices)
+    if (cap < (2ULL << PART_SB)) return 0;
+    return PART_SB;
 }
 
 size_t part_temp_bytes(int width, u64 rows, u32 sb, u64 cap) {
@@ -256,7 +268,9 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
                        n_slices, bounds);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_slice";
-    hipLaunchKernelGGL(part_slice_kernel, dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << sb), s, sorted, bounds, t, sb);
+    if (sb != PART_SB) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(part_slice_kernel<PART_SB>, dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << PART_SB), s, sorted, bounds,
+                       t);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_fixup";
     hipLaunchKernelGGL(part_fixup_kernel, dim3(512), dim3(256), 0, s, t);

@@ -20,7 +20,7 @@ cat gpurun_out/bench.json
 for c in ${CONFIGS:-2 1 3 4 5}; do
   step "rocprof config $c"
   st=20; [ "$c" != 2 ] && st=${STEPS:-3}
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c$c -o c$c --output-format csv -- python3 -u bench.py --config $c --steps $st --warmup 1 --no-cpu-baseline > gpurun_out/bench_c$c.json 2> gpurun_out/bench_c$c.err || { echo "config $c failed"; tail -20 gpurun_out/bench_c$c.err; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c$c -o c$c --output-format csv -- python3 -u bench.py --config $c --steps $st --warmup ${CWARM:-2} --no-cpu-baseline > gpurun_out/bench_c$c.json 2> gpurun_out/bench_c$c.err || { echo "config $c failed"; tail -20 gpurun_out/bench_c$c.err; exit 1; }
   grep '"metric"' gpurun_out/bench_c$c.json | cut -c1-300
 done
 if [ -z "$NO_PMC" ]; then
