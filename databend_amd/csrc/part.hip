@@ -30,6 +30,8 @@
 #define PART_NT 1024
 #define PART_SB 12  // slice = 4096 slots x 16 B = 64 KB of LDS
 #define PART_PROBE_CAP 64
+#define PART_OVF_LDS 512  // overflow keys gathered per workgroup before one device atomic
+#define RB 4  // sorted keys per lane per batch in the slice kernel
 
 namespace {
 
@@ -64,7 +66,9 @@ template <int SB>
 __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restrict__ sorted, const u64* __restrict__ bounds,
                                                              TableDesc t) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
-    __shared__ u32 lclaims;
+    __shared__ u32 lclaims, novf;
+    __shared__ u64 ovfq[PART_OVF_LDS];
+    __shared__ u64 ovf_base;
     constexpr u64 S = 1ULL << SB;
     constexpr int PER = (int)(S / PART_NT);
     static_assert(PER >= 1 && S % PART_NT == 0, "slice size");
@@ -78,62 +82,98 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     v2u64 sv[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) sv[k] = gsl[threadIdx.x + k * PART_NT];
-    if (threadIdx.x == 0) lclaims = 0;
+    // the slice's first sorted keys are loaded before the slice reaches LDS (independent loads,
+    // all in flight together); later batches are loaded one batch ahead of their processing
+    const u64 __attribute__((address_space(1)))* src = (const u64 __attribute__((address_space(1)))*)sorted;
+    const u64 last = hi > lo ? hi - 1 : 0;
+    u64 r = lo + threadIdx.x;
+    u64 cur[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) cur[k] = src[min<u64>(r + (u64)k * PART_NT, last)];
+    if (threadIdx.x == 0) lclaims = novf = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) lsl[threadIdx.x + k * PART_NT] = sv[k];
     __syncthreads();
     u32 my_claims = 0;
-    auto one = [&](u64 m) {
-        const u64 key = slot_unmix(m);
-        if (key == SLOT_EMPTY) {  // the sentinel slot (index cap) is outside every slice
-            wptr<AS_GLB> sent = asp<AS_GLB>(t.slots + t.cap * 2);
-            u64 old = at_cas<AS_GLB>(sent, SLOT_EMPTY, 0ULL);
-            if (old == SLOT_EMPTY) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), 1ULL);
-            at_add<AS_GLB>(sent + 1, 1ULL);
-            return;
-        }
-        u32 ls = (u32)((m & mask) - s0);
-        const u32 lim = (u32)min<u64>(S, (u64)ls + PART_PROBE_CAP);
-        for (; ls < lim; ++ls) {
-            wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)ls * 2);
-            u64 ev = vld<AS_LDS>(e);
-            if (ev == SLOT_EMPTY) {
-                u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
-                if (old == SLOT_EMPTY) {
-                    my_claims++;
-                    at_add<AS_LDS>(e + 1, 1ULL);
-                    return;
-                }
-                ev = old;
-            }
-            if (ev == key) {
-                at_add<AS_LDS>(e + 1, 1ULL);
-                return;
-            }
-        }
-        // the run leaves the slice (or is long): deferred, merged by agg_retry after this launch
+    auto push_rec = [&](u64 key) {
         u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), 1ULL);
         if (k < t.ovf_recs_cap) {
-            u64* r = t.ovf_recs + k * t.stride_words;
-            r[0] = key;
-            r[1] = 1;
+            u64* rec = t.ovf_recs + k * t.stride_words;
+            rec[0] = key;
+            rec[1] = 1;
         } else {
             atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
         }
     };
-    const u64 __attribute__((address_space(1)))* src = (const u64 __attribute__((address_space(1)))*)sorted;
-    u64 r = lo + threadIdx.x;
-    // four sorted keys in flight per lane
-    for (; r + 3 * PART_NT < hi; r += 4 * PART_NT) {
-        u64 m0 = src[r], m1 = src[r + PART_NT], m2 = src[r + 2 * PART_NT], m3 = src[r + 3 * PART_NT];
-        one(m0);
-        one(m1);
-        one(m2);
-        one(m3);
+    // Probe state machine with one loop exit (the SQ_INSTS_SALU count of a loop with several
+    // divergent returns was ~3x its VALU count: exec-mask bookkeeping per exit).  Plain LDS
+    // loads are enough: an entry, once set, never changes, and an EMPTY read that went stale is
+    // corrected by the CAS's return value.
+    auto one = [&](u64 m) {
+        const u64 key = slot_unmix(m);
+        u32 ls = (u32)((m & mask) - s0);
+        const u32 lim = (u32)min<u64>(S, (u64)ls + PART_PROBE_CAP);
+        int st = key == SLOT_EMPTY ? 2 : 0;  // 0 probing, 1 found at ls, 2 sentinel key, 3 overflow
+        while (st == 0) {
+            wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)ls * 2);
+            u64 ev = *e;
+            if (ev == SLOT_EMPTY) {
+                const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
+                my_claims += old == SLOT_EMPTY ? 1u : 0u;
+                ev = old == SLOT_EMPTY ? key : old;
+            }
+            if (ev == key) st = 1;
+            else if (++ls >= lim) st = 3;
+        }
+        if (st == 1) {
+            at_add<AS_LDS>(asp<AS_LDS>(lds + (u64)ls * 2 + 1), 1ULL);
+        } else if (st == 2) {  // the sentinel slot (index cap) is outside every slice
+            wptr<AS_GLB> sent = asp<AS_GLB>(t.slots + t.cap * 2);
+            u64 old = at_cas<AS_GLB>(sent, SLOT_EMPTY, 0ULL);
+            if (old == SLOT_EMPTY) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), 1ULL);
+            at_add<AS_GLB>(sent + 1, 1ULL);
+        } else {
+            // the run leaves the slice (or is long): an overflow record, merged by part_fixup.
+            // Gathered in LDS and reserved with one device atomic per workgroup, not one
+            // device-scope atomic per row on a single counter.
+            const u32 q = atomicAdd(&novf, 1u);
+            if (q < PART_OVF_LDS) ovfq[q] = key;
+            else push_rec(key);
+        }
+    };
+    // RB keys per lane in process, the next RB in flight
+    while (r < hi) {
+        const u64 rn = r + (u64)RB * PART_NT;
+        u64 nxt[RB];
+        if (rn < hi) {
+#pragma unroll
+            for (int k = 0; k < RB; ++k) nxt[k] = src[min<u64>(rn + (u64)k * PART_NT, last)];
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k)
+            if (r + (u64)k * PART_NT < hi) one(cur[k]);
+        if (rn >= hi) break;
+#pragma unroll
+        for (int k = 0; k < RB; ++k) cur[k] = nxt[k];
+        r = rn;
     }
-    for (; r < hi; r += PART_NT) one(src[r]);
     if (my_claims) atomicAdd(&lclaims, my_claims);
     __syncthreads();
+    const u32 nq = min<u32>(novf, PART_OVF_LDS);
+    if (nq) {
+        if (threadIdx.x == 0) ovf_base = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), (unsigned long long)nq);
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < nq; i += PART_NT) {
+            const u64 k = ovf_base + i;
+            if (k < t.ovf_recs_cap) {
+                u64* rec = t.ovf_recs + k * t.stride_words;
+                rec[0] = ovfq[i];
+                rec[1] = 1;
+            } else {
+                atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+            }
+        }
+    }
     v2u64 __attribute__((address_space(1)))* osl = (v2u64 __attribute__((address_space(1)))*)(t.slots + s0 * 2);
 #pragma unroll
     for (int k = 0; k < PER; ++k) osl[threadIdx.x + k * PART_NT] = lsl[threadIdx.x + k * PART_NT];
