@@ -579,6 +579,7 @@ __device__ __forceinline__ T vget(const v4u& y, int j) {
 // with every lane active: at low selectivity (Q8: 0.63 %) a lane-divergent insert per row would
 // leave 63 of 64 lanes idle on every LDS round trip.
 #define WQ 128  // queue entries per wave
+#define WQW 384  // u64 words of per-wave queue space: rows (2 x WQ) or candidate vectors (WQ x (16 + 8) B)
 
 template <typename T, bool PRED, int NT, bool CO>
 __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
@@ -595,8 +596,11 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     const u32 llimit = lds_slots - lds_slots / 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // per-wave queue (keys and rows) after the table and its 16 bytes of counters
-    u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * (2 * WQ);
+    u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * WQW;
     u64* qrow = qkey + WQ;
+    // candidate-vector queue (the `<> c` path below) over the same per-wave space
+    v4u* vq = (v4u*)qkey;
+    u64* vqb = qkey + 2 * WQ;
     lds_table_init(S, lds, lds_slots, sw, NT);
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
@@ -646,6 +650,68 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         process(k, r);
     };
 
+    // `key <> c` (ClickBench Q8: AdvEngineID <> 0) as a two-level compaction.  A row-level
+    // queue pays the per-row mask + ballot-prefix VALU work on every lane (SQ counters: ~350
+    // VALU per 32-row round, VALU ~60 % busy); instead each 16-byte vector is tested whole —
+    // "some element differs from c" is three ORs of XORs — and only candidate vectors (4.9 % at
+    // Q8's selectivity) are appended, whole, to a per-wave LDS queue; 64 at a time they are
+    // expanded with every lane busy.  ~10 VALU per 8-row vector instead of ~90.
+    const bool neq_fast = PRED && negate && lo == hi;
+    u32 cc_lo, cc_hi;
+    {
+        typedef typename std::make_unsigned<T>::type UT;
+        const u64 c = (u64)(UT)lo;
+        if (sizeof(T) == 8) { cc_lo = (u32)c; cc_hi = (u32)(c >> 32); }
+        else if (sizeof(T) == 4) { cc_lo = cc_hi = (u32)c; }
+        else if (sizeof(T) == 2) { cc_lo = cc_hi = (u32)(c | (c << 16)); }
+        else { cc_lo = cc_hi = (u32)(c * 0x01010101u); }
+    }
+    u32 vqn = 0;  // wave-uniform candidate count
+    // expand candidate vectors [0, n) (n <= 64, one per lane), shift [64, vqn) down
+    auto drain_vec = [&](u32 n) {
+        v4u v = {0, 0, 0, 0};
+        u64 bs = 0;
+        const bool have = lane < (int)n;
+        if (have) {
+            v = ((volatile v4u*)vq)[lane];
+            bs = ((volatile u64*)vqb)[lane];
+        }
+        const bool mv = lane + 64 < (int)vqn;
+        v4u v2 = {0, 0, 0, 0};
+        u64 b2 = 0;
+        if (mv) {
+            v2 = ((volatile v4u*)vq)[lane + 64];
+            b2 = ((volatile u64*)vqb)[lane + 64];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (mv) {
+            ((volatile v4u*)vq)[lane] = v2;
+            ((volatile u64*)vqb)[lane] = b2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        vqn -= n;
+        u32 mm = 0;
+        if (have)
+#pragma unroll
+            for (int j = 0; j < V; ++j) mm |= (pass(vget<T>(v, j)) ? 1u : 0u) << j;
+        while (mm) {
+            const int j = __builtin_ctz(mm);
+            mm &= mm - 1;
+            // element j of v from registers (j is lane-varying here): select over the dwords
+            const int W = (int)sizeof(T);
+            const int wi = (j * W) >> 2;
+            const u32 w0 = wi == 0 ? v.x : (wi == 1 ? v.y : (wi == 2 ? v.z : v.w));
+            u64 key;
+            if (W == 8) {
+                const u32 w1 = wi == 0 ? v.y : v.w;
+                key = ((u64)w1 << 32) | w0;
+            } else {
+                const u32 sh = (u32)((j * W) & 3) * 8;
+                key = (u64)((w0 >> sh) & (W == 4 ? 0xFFFFFFFFu : ((1u << (8 * W)) - 1u)));
+            }
+            process(key, bs + j);
+        }
+    };
     u32 sink = 0;  // experiment modes keep the loads alive through this
     const u64 ltmask = (1ULL << lane) - 1;
     auto key_of = [&](const v4u& y, int j) -> u64 { return (u64)(typename std::make_unsigned<T>::type)vget<T>(y, j); };
@@ -661,6 +727,26 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
                 if ((actm >> u) & 1)
 #pragma unroll
                     for (int j = 0; j < V; ++j) process(key_of(y[u], j), base[u] + j);
+            return;
+        }
+        if (neq_fast && xmode != 5) {
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                const v4u& v = y[u];
+                const bool any = (((v.x ^ cc_lo) | (v.y ^ cc_hi) | (v.z ^ cc_lo) | (v.w ^ cc_hi)) != 0) && ((actm >> u) & 1);
+                const u64 b = __ballot(any);
+                if (b == 0) continue;
+                if (any) {
+                    const u32 pos = vqn + (u32)__popcll(b & ltmask);
+                    vq[pos] = v;
+                    vqb[pos] = base[u];
+                }
+                vqn += (u32)__popcll(b);
+                if (vqn >= 64) {
+                    __builtin_amdgcn_wave_barrier();
+                    drain_vec(64);
+                }
+            }
             return;
         }
         u32 m[FAST_UNROLL];
@@ -768,6 +854,10 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
 #pragma unroll
         for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
         k = kn;
+    }
+    if (PRED && vqn) {
+        __builtin_amdgcn_wave_barrier();
+        drain_vec(vqn);
     }
     // drain the queue's rest (< 64 entries): lanes below qn take one each
     if (PRED && qn) {
@@ -899,7 +989,7 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     }
     const int nt = 1024;
     static const u64 max_blocks = getenv("DBG_FAST_MAXBLOCKS") ? strtoull(getenv("DBG_FAST_MAXBLOCKS"), nullptr, 10) : 256;
-    size_t shmem = table_bytes + (size_t)(nt / 64) * 2 * WQ * 8;
+    size_t shmem = table_bytes + (size_t)(nt / 64) * WQW * 8;
     u64 quantum = V * (u64)nt * FAST_UNROLL;
     u64 blocks = (rows + quantum - 1) / quantum;
     if (blocks > max_blocks) blocks = max_blocks;
