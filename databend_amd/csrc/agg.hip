@@ -439,6 +439,66 @@ void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64*
 // ------------------------------------------------------------------------------------------
 // agg_insert: one workgroup = one contiguous row range; LDS partial table, HBM fallback.
 // ------------------------------------------------------------------------------------------
+// One selected row (or partial record): group hash -> LDS table -> HBM table -> state update.
+template <bool INLINE, bool RECORDS>
+__device__ __forceinline__ void insert_one(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u32 bid, u64 i,
+                                           u64* lds, u32 lmask, u32 sw, u32* lcount, u32 llimit, const TableDesc& t,
+                                           u32& my_claims) {
+    u64 h, key;
+    if (RECORDS) {
+        h = gld<u64>(B.rec_base + i * (u64)B.rec_width);
+    } else if (INLINE) {
+        h = 0;
+    } else {
+        h = group_hash(B.keys, S.n_keys, i);
+    }
+    if (INLINE) key = pack_key(S, B.keys, i);
+    else key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+
+    int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
+    const u64* rec = RECORDS ? (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1 : nullptr;
+    if (ls >= 0) {
+        wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
+        if (RECORDS) apply_state<AS_LDS>(S, st, rec);
+        else apply_row<AS_LDS>(S, st, B, i);
+        return;
+    }
+    bool claimed;
+    u64 gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, t.probe_limit, claimed);
+    if (gs == ~0ULL) {
+        push_ovf_row(t, bid, i);
+        return;
+    }
+    my_claims += claimed ? 1 : 0;
+    wptr<AS_GLB> st = asp<AS_GLB>(t.slots + gs * t.stride_words);
+    if (RECORDS) apply_state<AS_GLB>(S, st, rec);
+    else apply_row<AS_GLB>(S, st, B, i);
+}
+
+// Every FLUSH_ROUND rounds: a full LDS table is flushed to HBM and started over (the
+// reference's clear_ht of a full partial table, aggregate_hashtable.rs:225-239), so hot keys of
+// a skewed stream keep being combined in LDS instead of hammering one HBM slot (not once the HBM
+// table overflows: the deferred-overflow lists are sized for two flushes of every workgroup's
+// table).  Thread 0 decides, so the branch is uniform.  Called by every thread.
+template <bool INLINE, bool RECORDS>
+__device__ __forceinline__ void maybe_flush(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds,
+                                            u32 lds_slots, u32 sw, u32* lcount, u32 llimit, const TableDesc& t,
+                                            u32& my_claims) {
+    __shared__ u32 do_flush;
+    if (threadIdx.x == 0)
+        do_flush = lcount[0] >= llimit && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+    __syncthreads();
+    const bool flush_now = do_flush;
+    __syncthreads();  // everyone has read the flag before thread 0 may rewrite it
+    if (flush_now) {
+        flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, BLOCK, t, my_claims);
+        __syncthreads();
+        lds_table_init(S, lds, lds_slots, sw, BLOCK);
+        if (threadIdx.x == 0) lcount[0] = 0;
+        __syncthreads();
+    }
+}
+
 template <bool INLINE, bool RECORDS>
 __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
@@ -459,68 +519,61 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
     u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
     u32 my_claims = 0;
     const u64 n_iter = r1 > r0 ? (r1 - r0 + BLOCK - 1) / BLOCK : 0;
-    for (u64 it = 0; it < n_iter; ++it) {
-        // Every FLUSH_ROUND rounds: a full LDS table is flushed to HBM and started over (the
-        // reference's clear_ht of a full partial table, aggregate_hashtable.rs:225-239), so hot
-        // keys of a skewed stream keep being combined here instead of hammering one HBM slot.
-        if (it && (it % FLUSH_ROUND) == 0) {
-            // (not once the HBM table overflows: the deferred-overflow lists are sized for two
-            // flushes of every workgroup's table).  Thread 0 decides, so the branch is uniform.
-            __shared__ u32 do_flush;
-            if (threadIdx.x == 0)
-                do_flush = lcount[0] >= llimit && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+    if (!RECORDS && B.n_nodes && rows_per_block < (1ULL << 32)) {
+        // Filtered input (FilterExecutor::select then take, EXP/filter/filter_executor.rs:73-128):
+        // every lane evaluates the predicate on its row, the selected rows are queued in LDS (wave
+        // ballot + one LDS add per wave), and the hash / probe / state update runs on BLOCK queued
+        // rows at a time with every lane busy — at 13% selectivity (ClickBench Q13) the
+        // row-per-lane loop would run the long dependent chain of a string key with 1 lane in 8.
+        __shared__ u32 selq[2 * BLOCK];
+        __shared__ u32 qn;
+        if (threadIdx.x == 0) qn = 0;
+        __syncthreads();
+        const u32 lane = __lane_id();
+        for (u64 it = 0; it < n_iter; ++it) {
+            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            const u64 i = r0 + it * BLOCK + threadIdx.x;
+            const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+            const u64 m = __ballot(sel);
+            if (m) {
+                u32 wbase = 0;
+                if (lane == 0) wbase = atomicAdd(&qn, (u32)__popcll(m));
+                wbase = __shfl(wbase, 0);
+                if (sel) selq[wbase + (u32)__popcll(m & ((1ULL << lane) - 1))] = (u32)(i - r0);
+            }
             __syncthreads();
-            const bool flush_now = do_flush;
-            __syncthreads();  // everyone has read the flag before thread 0 may rewrite it
-            if (flush_now) {
-                flush_lds_direct<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, BLOCK, t, my_claims);
+            const u32 n = qn;  // < 2 * BLOCK
+            if (n >= BLOCK) {
+                const u32 off = selq[threadIdx.x];
+                const u32 rem = n - BLOCK;  // < BLOCK
+                const u32 mv = threadIdx.x < rem ? selq[BLOCK + threadIdx.x] : 0u;
                 __syncthreads();
-                lds_table_init(S, lds, lds_slots, sw, BLOCK);
-                if (threadIdx.x == 0) lcount[0] = 0;
-                __syncthreads();
+                if (threadIdx.x < rem) selq[threadIdx.x] = mv;
+                if (threadIdx.x == 0) qn = rem;
+                insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + off, lds, lmask, sw, lcount, llimit, t, my_claims);
             }
+            __syncthreads();  // the queue is settled before the next round appends
         }
-        const u64 i = r0 + it * BLOCK + threadIdx.x;
-        if (i >= r1) continue;
-        if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
-        if (RECORDS && B.seg_records) {  // fixed-capacity segments: record 0 is [count][flags]
-            const u64 q = i % B.seg_records;
-            const u8* hdr = B.rec_base + (i - q) * (u64)B.rec_width;
-            if (q == 0) {
-                if (gld<u64>(hdr + 8)) atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_FIXED_INCOMPLETE);
-                continue;
+        const u32 n = qn;  // < BLOCK
+        if (threadIdx.x < n)
+            insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + selq[threadIdx.x], lds, lmask, sw, lcount, llimit, t, my_claims);
+    } else {
+        for (u64 it = 0; it < n_iter; ++it) {
+            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            const u64 i = r0 + it * BLOCK + threadIdx.x;
+            if (i >= r1) continue;
+            if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+            if (RECORDS && B.seg_records) {  // fixed-capacity segments: record 0 is [count][flags]
+                const u64 q = i % B.seg_records;
+                const u8* hdr = B.rec_base + (i - q) * (u64)B.rec_width;
+                if (q == 0) {
+                    if (gld<u64>(hdr + 8)) atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_FIXED_INCOMPLETE);
+                    continue;
+                }
+                if (q > gld<u64>(hdr)) continue;
             }
-            if (q > gld<u64>(hdr)) continue;
+            insert_one<INLINE, RECORDS>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
         }
-        u64 h, key;
-        if (RECORDS) {
-            h = gld<u64>(B.rec_base + i * (u64)B.rec_width);
-        } else if (INLINE) {
-            h = 0;
-        } else {
-            h = group_hash(B.keys, S.n_keys, i);
-        }
-        if (INLINE) key = pack_key(S, B.keys, i);
-        else key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
-
-        int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
-        const u64* rec = RECORDS ? (const u64*)(B.rec_base + i * (u64)B.rec_width + S.rec_state_off) - 1 : nullptr;
-        if (ls >= 0) {
-            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
-            if (RECORDS) apply_state<AS_LDS>(S, st, rec);
-            else apply_row<AS_LDS>(S, st, B, i);
-            continue;
-        }
-        bool claimed;
-        u64 gs = g_find<INLINE>(S, batches, B.keys, i, key, h, t, t.probe_limit, claimed);
-        if (gs == ~0ULL) {
-            push_ovf_row(t, bid, i);
-            continue;
-        }
-        my_claims += claimed ? 1 : 0;
-        wptr<AS_GLB> st = asp<AS_GLB>(t.slots + gs * t.stride_words);
-        if (RECORDS) apply_state<AS_GLB>(S, st, rec);
-        else apply_row<AS_GLB>(S, st, B, i);
     }
     __syncthreads();
     block_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);

@@ -142,6 +142,17 @@ __device__ __forceinline__ u64 load_u64_unaligned(const u8* p) {
     return (w0 >> (8 * off)) | (w1 << (64 - 8 * off));
 }
 
+// The first r (1..8) bytes at p as a little-endian word (upper bytes unspecified): aligned loads
+// only, and only of words that hold at least one of the r bytes (so never past the buffer's page).
+__device__ __forceinline__ u64 load_partial(const u8* p, u64 r) {
+    uintptr_t a = (uintptr_t)p;
+    u32 off = (u32)(a & 7);
+    const u8* base = (const u8*)(a & ~(uintptr_t)7);
+    u64 w = gld<u64>(base) >> (8 * off);
+    if (off + r > 8) w |= gld<u64>(base + 8) << (64 - 8 * off);
+    return w;
+}
+
 // impl AggHash for [u8] (group_hash.rs:161-192)
 __device__ __forceinline__ u64 hash_bytes(const u8* p, u64 len) {
     const u64 M = 0xc6a4a7935bd1e995ULL, R = 47;
@@ -156,8 +167,8 @@ __device__ __forceinline__ u64 hash_bytes(const u8* p, u64 len) {
         h *= M;
     }
     u64 tl = len & 7;
-    const u8* t = p + nb * 8;
-    for (u64 i = 0; i < tl; ++i) h ^= (u64)gld<u8>(t + i) << (8 * (tl - i - 1));
+    // tail: h ^= b[i] << 8 * (tl - 1 - i), i.e. the tail bytes big-endian
+    if (tl) h ^= __builtin_bswap64(load_partial(p + nb * 8, tl)) >> (8 * (8 - tl));
     h ^= h >> R;
     h *= M;
     h ^= h >> R;
@@ -227,9 +238,9 @@ __device__ __forceinline__ bool bytes_equal(const u8* a, const u8* b, u64 n) {
     u64 i = 0;
     for (; i + 8 <= n; i += 8)
         if (load_u64_unaligned(a + i) != load_u64_unaligned(b + i)) return false;
-    for (; i < n; ++i)
-        if (gld<u8>(a + i) != gld<u8>(b + i)) return false;
-    return true;
+    if (i == n) return true;
+    const u64 r = n - i;  // 1..7
+    return ((load_partial(a + i, r) ^ load_partial(b + i, r)) & ((1ULL << (8 * r)) - 1)) == 0;
 }
 
 __device__ __forceinline__ bool cell_equal(const DCol& a, u64 i, const DCol& b, u64 j) {
