@@ -17,6 +17,7 @@
 
 #include "agg.hpp"
 #include "filter.hpp"
+#include "sort.hpp"
 
 // ------------------------------------------------------------------------------------------
 // errors
@@ -1420,6 +1421,27 @@ int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, v
     HIPCHECK(hipStreamSynchronize(s));
     if (vbytes) hipFree(vbytes);
     return DBG_OK;
+}
+
+int dbg_sort_limit_indices(const dbg_column* col, uint64_t rows, int asc, int nulls_first, uint64_t limit,
+                           uint32_t* idx_out, uint64_t* n_out, void* stream) {
+    if (!col || !n_out || (!idx_out && limit && rows)) return fail(DBG_ERR_INVALID, "null argument");
+    const int t = col->dt.type;
+    if (t == DBG_STRING || t == DBG_DECIMAL128 || type_width(t) == 0)
+        return fail(DBG_ERR_UNSUPPORTED, "dbg_sort_limit_indices: fixed-width number columns only");
+    DCol d;
+    memset(&d, 0, sizeof(d));
+    d.type = t;
+    d.nullable = col->dt.nullable;
+    d.width = type_width(t);
+    d.stride = d.width;
+    d.data = (const u8*)col->data;
+    d.validity = col->validity;
+    d.validity_offset = col->validity_offset;
+    d.data_offset = col->data_offset;
+    std::string err;
+    int rc = sort_limit_run((hipStream_t)stream, d, rows, asc, nulls_first, limit, idx_out, n_out, err);
+    return rc == DBG_OK ? rc : fail(rc, err);
 }
 
 // ---- profiling ----

@@ -19,7 +19,7 @@ EXPORTED = [
     "dbg_version", "dbg_last_error", "dbg_device_count", "dbg_agg_result_type", "dbg_agg_create",
     "dbg_agg_destroy", "dbg_agg_set_stream", "dbg_agg_reset", "dbg_agg_add_groups", "dbg_agg_finalize",
     "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_set_recycle", "dbg_agg_finalize_into_async", "dbg_agg_finalize_wait", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
-    "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_prof_enable", "dbg_prof_reset",
+    "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_sort_limit_indices", "dbg_prof_enable", "dbg_prof_reset",
     "dbg_prof_get", "dbg_datagen",
 ]
 
@@ -81,6 +81,7 @@ def lib():
         L.dbg_agg_merge_fixed.argtypes = [VP, VP, I32, U64]
         L.dbg_filter_select.argtypes = [P(abi.dbg_filter), U64, VP, P(U64), VP]
         L.dbg_take_fixed.argtypes = [P(abi.dbg_column), VP, U64, VP, VP, VP]
+        L.dbg_sort_limit_indices.argtypes = [P(abi.dbg_column), U64, C.c_int, C.c_int, U64, VP, P(U64), VP]
         L.dbg_prof_enable.argtypes = [C.c_int]
         L.dbg_prof_get.argtypes = [C.c_int, P(C.c_char_p), P(C.c_double), P(U64)]
         L.dbg_datagen.argtypes = [C.c_int, U64, U64, U64, P(VP), C.c_int, VP, VP]

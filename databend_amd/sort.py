@@ -1,0 +1,65 @@
+"""ORDER BY <one column> [ASC|DESC] [NULLS FIRST|LAST] LIMIT k on device.
+
+Host mirror of `DataBlock::sort(block, descriptions, limit)` (EXP/kernels/sort.rs:79-107) for one
+sort column — the shape that ends every ClickBench GROUP BY query (`ORDER BY c DESC LIMIT 10`),
+run over the aggregate's result columns while they are still in HBM.  The indices come from
+`dbg_sort_limit_indices` (databend_amd/csrc/sort.hip: radix select + LDS bitonic sort); the
+columns are gathered with `dbg_take_fixed` (DataBlock::take, EXP/kernels/take.rs:56-91).
+
+Semantics follow arrow's sort_to_indices (src/common/arrow/src/arrow/compute/sort/common.rs:95-174):
+NULLs first or last in ascending row order, integer order / IEEE totalOrder for floats, DESC
+reverses the value order only.  Equal values come out in ascending row order (the reference's
+select_nth_unstable_by leaves them unspecified).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+from . import abi
+from .device import DeviceColumn, empty
+from .ffi import check, lib
+
+SORT_LIMIT_MAX = 2048  # SORT_CAP in csrc/sort.hpp
+
+
+@dataclass
+class SortColumnDescription:
+    """EXP/kernels/sort.rs:50-56."""
+    offset: int
+    asc: bool = True
+    nulls_first: bool = False
+    is_nullable: bool = False
+
+
+def sort_limit_indices(col: DeviceColumn, asc: bool, nulls_first: bool, limit: Optional[int]):
+    """Row indices (torch int32 on the column's device) of the first min(limit, rows) rows."""
+    import torch
+
+    n = len(col)
+    k = n if limit is None else min(int(limit), n)
+    out = torch.empty(max(1, k), dtype=torch.int32, device=col.data.device)
+    got = C.c_uint64()
+    check(lib().dbg_sort_limit_indices(C.byref(col.to_abi()), n, 1 if asc else 0, 1 if nulls_first else 0, k,
+                                       out.data_ptr(), C.byref(got), None))
+    return out[:got.value]
+
+
+def take(col: DeviceColumn, idx) -> DeviceColumn:
+    """DataBlock::take of one fixed-width column by device indices."""
+    n = int(idx.numel())
+    out = empty(col.dtype, n, device=col.data.device)
+    check(lib().dbg_take_fixed(C.byref(col.to_abi()), idx.data_ptr(), n, out.data.data_ptr(),
+                               out.validity.data_ptr() if out.validity is not None else None, None))
+    return out
+
+
+def sort(columns: Sequence[DeviceColumn], descriptions: Sequence[SortColumnDescription],
+         limit: Optional[int]) -> List[DeviceColumn]:
+    """DataBlock::sort for one sort description over fixed-width columns."""
+    if len(descriptions) != 1:
+        raise NotImplementedError("device sort: one sort column")
+    d = descriptions[0]
+    idx = sort_limit_indices(columns[d.offset], d.asc, d.nulls_first, limit)
+    return [take(c, idx) for c in columns]

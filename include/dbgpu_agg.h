@@ -276,6 +276,19 @@ int dbg_filter_select(const dbg_filter* filter, uint64_t rows, uint32_t* sel_out
 int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, void* out_data,
                    uint8_t* out_validity, void* hip_stream);
 
+/* ---- ORDER BY one column LIMIT k (DataBlock::sort, EXP/kernels/sort.rs:79-107 -> arrow
+ * sort_to_indices / indices_sorted_unstable_by, src/common/arrow/src/arrow/compute/sort/common.rs:95-174)
+ * over a device-resident fixed-width number column (ints, date, timestamp, float32/64, boolean) —
+ * the sort that ends every ClickBench GROUP BY, run on the aggregate result while it is in HBM.
+ * idx_out (device, >= min(limit, rows) u32) receives the row indices of the first
+ * min(limit, rows) rows in sort order: NULLs first or last (nulls_first) in ascending row order;
+ * values by ord::total_cmp (integers) / total_cmp_f32|f64 (floats, IEEE totalOrder), reversed when
+ * asc == 0; equal values in ascending row order (the reference leaves their order unspecified:
+ * select_nth_unstable_by).  *n_out = min(limit, rows).  limit > 2048, Decimal128 and STRING
+ * columns return DBG_ERR_UNSUPPORTED.  Synchronous on hip_stream. */
+int dbg_sort_limit_indices(const dbg_column* col, uint64_t rows, int asc, int nulls_first, uint64_t limit,
+                           uint32_t* idx_out, uint64_t* n_out, void* hip_stream);
+
 /* ---- in-library kernel timing (HIP events around each launch; off by default) ---- */
 int dbg_prof_enable(int on);
 int dbg_prof_reset(void);

@@ -202,3 +202,34 @@ def datagen(cfg: int, rows: int, start: int = 0, seed: Optional[int] = None, thr
         _check(L.orc_datagen_c5_bytes(seed, start, rows, offs.ctypes.data, data.ctypes.data, cdf.ctypes.data, threads))
         return {"SearchPhrase": Column(col.String, data[:int(offs[-1])], offs)}
     raise ValueError(cfg)
+
+
+def sort_limit_indices(col: Column, asc: bool, nulls_first: bool, limit) -> np.ndarray:
+    """DataBlock::sort with one column (EXP/kernels/sort.rs:79-107) -> arrow sort_to_indices ->
+    indices_sorted_unstable_by (src/common/arrow/src/arrow/compute/sort/common.rs:95-174):
+    NULL rows first/last in ascending row order; valid rows by ord::total_cmp / total_cmp_f32|f64
+    (array/ord.rs:36-56), reversed for DESC; equal values in ascending row order (one of the
+    orders select_nth_unstable_by may produce)."""
+    n = len(col)
+    k = n if limit is None else min(int(limit), n)
+    t = col.dtype.type_id
+    v = np.asarray(col.data)
+    if t == abi.FLOAT64:
+        b = v.astype(np.float64).view(np.uint64)
+        key = np.where(b >> np.uint64(63) != 0, ~b, b | np.uint64(1 << 63))
+    elif t == abi.FLOAT32:
+        b = v.astype(np.float32).view(np.uint32).astype(np.uint64)
+        key = np.where(b >> np.uint64(31) != 0, (~b) & np.uint64(0xFFFFFFFF), b | np.uint64(0x80000000))
+    elif t in (abi.UINT8, abi.UINT16, abi.UINT32, abi.UINT64, abi.BOOLEAN):
+        key = v.astype(np.uint64)
+    else:
+        key = v.astype(np.int64).view(np.uint64) ^ np.uint64(1 << 63)
+    if not asc:
+        key = ~key
+    valid = np.ones(n, dtype=bool) if col.validity is None or not col.dtype.nullable else np.asarray(col.validity, bool)
+    rows = np.arange(n, dtype=np.int64)
+    nulls = rows[~valid]
+    vrows = rows[valid]
+    vsorted = vrows[np.argsort(key[valid], kind="stable")]
+    order = np.concatenate([nulls, vsorted]) if nulls_first else np.concatenate([vsorted, nulls])
+    return order[:k]
