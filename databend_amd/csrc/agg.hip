@@ -502,7 +502,7 @@ __device__ __forceinline__ void maybe_flush(const Spec& S, const BatchDesc* batc
 template <bool INLINE, bool RECORDS>
 __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
-                                                          u32 lds_slots) {
+                                                          u32 lds_slots, int xmode) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
@@ -530,8 +530,9 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         if (threadIdx.x == 0) qn = 0;
         __syncthreads();
         const u32 lane = __lane_id();
+        u64 sink = 0;
         for (u64 it = 0; it < n_iter; ++it) {
-            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            if (it && (it % FLUSH_ROUND) == 0 && xmode != 5 && xmode != 3) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
             const u64 i = r0 + it * BLOCK + threadIdx.x;
             const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
             const u64 m = __ballot(sel);
@@ -550,12 +551,22 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
                 __syncthreads();
                 if (threadIdx.x < rem) selq[threadIdx.x] = mv;
                 if (threadIdx.x == 0) qn = rem;
-                insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + off, lds, lmask, sw, lcount, llimit, t, my_claims);
+                if (xmode == 0 || xmode == 5) insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + off, lds, lmask, sw, lcount, llimit, t, my_claims);
+                else if (xmode == 2) sink ^= group_hash(B.keys, S.n_keys, r0 + off);
+                else if (xmode == 3 || xmode == 4) {
+                    const u64 i = r0 + off;
+                    const u64 h = group_hash(B.keys, S.n_keys, i);
+                    const u64 key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+                    int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
+                    if (ls >= 0) apply_row<AS_LDS>(S, asp<AS_LDS>(lds + (u64)ls * sw), B, i);
+                    else if (xmode == 4) insert_one<INLINE, RECORDS>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+                }
             }
             __syncthreads();  // the queue is settled before the next round appends
         }
+        if (xmode) asm volatile("" ::"v"(sink));
         const u32 n = qn;  // < BLOCK
-        if (threadIdx.x < n)
+        if (threadIdx.x < n && xmode == 0)
             insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + selq[threadIdx.x], lds, lmask, sw, lcount, llimit, t, my_claims);
     } else {
         for (u64 it = 0; it < n_iter; ++it) {
@@ -1096,7 +1107,10 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
             case DBG_UINT64: launch_fast_t<uint64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
         }
     }
-    u32 lslots = use_lds ? lds_slots_for(S) : 1;
+    static const int gxmode = getenv("DBG_GEN_XMODE") ? atoi(getenv("DBG_GEN_XMODE")) : 0;  // timing experiments only
+    // LDS partial-table budget per workgroup (DBG_LDS_BYTES: A/B knob, default LDS_BUDGET_BYTES)
+    static const u32 lds_budget = getenv("DBG_LDS_BYTES") ? (u32)atoi(getenv("DBG_LDS_BYTES")) : (u32)LDS_BUDGET_BYTES;
+    u32 lslots = use_lds ? lds_slots_for(S, lds_budget) : 1;
     // enough workgroups to fill 256 CUs several times over, each a contiguous row range
     u64 min_rows_per_block = (u64)BLOCK * 16;
     u64 blocks = (rows + min_rows_per_block - 1) / min_rows_per_block;
@@ -1106,11 +1120,11 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     blocks = (rows + rpb - 1) / rpb;
     size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
     if (S.inline_keys) {
-        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
-        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
+        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
     } else {
-        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
-        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
+        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
     }
 }
 
