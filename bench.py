@@ -22,6 +22,8 @@ import statistics
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -243,6 +245,24 @@ def main():
             out["roofline"]["traffic_source"] = os.path.relpath(tf, ROOT)
         except Exception:
             pass
+    # The ORDER BY <count> DESC LIMIT 10 that ends the ClickBench query, on the device result
+    # (untimed leg, reported beside the step; dbg_sort_limit_indices).
+    if world == 1 and n_groups > 0:
+        ci_cnt = next((i for i, (f, c) in enumerate(shape.aggs) if f == "count" and c is None), None)
+        if ci_cnt is not None:
+            from databend_amd.sort import sort_limit_indices
+            dc = runner.out_aggs[ci_cnt]
+            sort_limit_indices(dc, False, False, 10)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                idx = sort_limit_indices(dc, False, False, 10)
+            torch.cuda.synchronize()
+            sort_ms = (time.perf_counter() - t0) / 5 * 1e3
+            top = np.asarray(aggs_h[ci_cnt].data)[idx.cpu().numpy()]
+            ok = top.tolist() == np.sort(np.asarray(aggs_h[ci_cnt].data))[::-1][: len(top)].tolist()
+            out["order_by_limit"] = {"sql": "ORDER BY count DESC LIMIT 10", "ms": sort_ms, "groups": n_groups,
+                                     "values_match_host_sort": ok}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sample = args.cpu_sample_rows or {1: 6_001_215, 2: 100_000_000, 3: 20_000_000, 4: 10_000_000, 5: 20_000_000}[cfg]
         sample = min(sample, rows)

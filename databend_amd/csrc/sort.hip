@@ -13,9 +13,10 @@
 // MI355X shape: an MSD radix select over the composite key (null rank 1 bit | order key 64 bits |
 // row 32 bits), one 8-bit digit per pass: each pass is one streaming read of the column with an
 // LDS histogram per workgroup (HBM-bound, 8 B/row for 64-bit columns), and the host picks the
-// digit bucket holding the limit-th row.  Passes stop as soon as that bucket is taken whole, so a
-// LIMIT over distinct values usually needs 2-4 passes.  The <= limit selected rows are then
-// compacted and ordered by one workgroup's bitonic sort in LDS.
+// digit bucket holding the limit-th row.  Passes stop as soon as that bucket is taken whole, and
+// one AND/OR reduction pass finds the key bytes every row shares (the high bytes of a COUNT
+// column), whose passes are skipped.  The <= limit selected rows are then compacted and ordered by
+// one workgroup's bitonic sort in LDS; inputs of <= 2048 rows go straight to that sort.
 #include <cstring>
 #include <string>
 
@@ -86,6 +87,29 @@ __global__ void __launch_bounds__(SBLOCK) sort_hist_kernel(DCol c, u64 rows, int
         if (h[t]) atomicAdd(&hist[t], h[t]);
 }
 
+// Bitwise AND / OR of the order keys of the rows in play: a byte on which they agree is common
+// to every row in play (and to every subset of them), so its radix pass can be skipped.
+__global__ void __launch_bounds__(SBLOCK) sort_andor_kernel(DCol c, u64 rows, int desc, int nulls_first, SortSel s,
+                                                            u64* andor) {
+    u64 a = ~0ULL, o = 0ULL;
+    for (u64 i = blockIdx.x * (u64)SBLOCK + threadIdx.x; i < rows; i += (u64)gridDim.x * SBLOCK) {
+        u32 nr;
+        u64 ok;
+        row_key(c, i, desc, nulls_first, nr, ok);
+        if (!in_play(s, nr, ok, (u32)i)) continue;
+        a &= ok;
+        o |= ok;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        a &= __shfl_xor(a, off);
+        o |= __shfl_xor(o, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAnd((unsigned long long*)andor, (unsigned long long)a);
+        atomicOr((unsigned long long*)(andor + 1), (unsigned long long)o);
+    }
+}
+
 // Rows whose masked composite key is <= the threshold: exactly the first `limit` rows.
 __global__ void __launch_bounds__(SBLOCK) sort_select_kernel(DCol c, u64 rows, int desc, int nulls_first, SortSel s,
                                                              u64* cand_ok, u64* cand_lo, u32* counter, u32 cap) {
@@ -115,7 +139,8 @@ __device__ __forceinline__ bool sort_less(u64 ao, u64 al, u64 bo, u64 bl) {
     return (u32)al < (u32)bl;
 }
 
-__global__ void __launch_bounds__(SORT_NT) sort_small_kernel(const u64* cand_ok, const u64* cand_lo, u32 n, u32* idx_out) {
+__global__ void __launch_bounds__(SORT_NT) sort_small_kernel(const u64* cand_ok, const u64* cand_lo, u32 n, u32 n_out,
+                                                            u32* idx_out) {
     __shared__ u64 ko[SORT_CAP], kl[SORT_CAP];
     u32 m = 1;
     while (m < n) m <<= 1;
@@ -143,7 +168,7 @@ __global__ void __launch_bounds__(SORT_NT) sort_small_kernel(const u64* cand_ok,
             __syncthreads();
         }
     }
-    for (u32 t = threadIdx.x; t < n; t += SORT_NT) idx_out[t] = (u32)kl[t];
+    for (u32 t = threadIdx.x; t < n_out; t += SORT_NT) idx_out[t] = (u32)kl[t];
 }
 
 int sort_limit_run(hipStream_t s, const DCol& c, u64 rows, int asc, int nulls_first, u64 limit, u32* idx_out,
@@ -159,9 +184,9 @@ int sort_limit_run(hipStream_t s, const DCol& c, u64 rows, int asc, int nulls_fi
         err = "sort limit: row indices are u32";
         return DBG_ERR_UNSUPPORTED;
     }
-    // one allocation: hist[256] u32 | counter u32 (+pad) | cand_ok | cand_lo
+    // one allocation: hist[256] u32 | counter u32 (+pad) | cand_ok | cand_lo | and/or u64 x 2
     char* buf = nullptr;
-    const size_t bytes = 256 * 4 + 16 + 2 * (size_t)SORT_CAP * 8;
+    const size_t bytes = 256 * 4 + 16 + 2 * (size_t)SORT_CAP * 8 + 16;
     if (hipMalloc((void**)&buf, bytes) != hipSuccess) {
         err = "sort limit: device allocation failed";
         return DBG_ERR_OOM;
@@ -170,6 +195,7 @@ int sort_limit_run(hipStream_t s, const DCol& c, u64 rows, int asc, int nulls_fi
     u32* counter = (u32*)(buf + 1024);
     u64* cand_ok = (u64*)(buf + 1024 + 16);
     u64* cand_lo = cand_ok + SORT_CAP;
+    u64* andor = cand_lo + SORT_CAP;
     const int desc = asc ? 0 : 1;
     const bool has_nulls = c.nullable && c.validity != nullptr;
     u64 blocks = (rows + SBLOCK * 8 - 1) / (SBLOCK * 8);
@@ -187,7 +213,33 @@ int sort_limit_run(hipStream_t s, const DCol& c, u64 rows, int asc, int nulls_fi
     int rc = DBG_OK;
     u64 need = need_total;
     u32 h[256];
+    u64 common = 0, common_val = 0;  // order-key bits shared by every row in play
+    bool have_common = false;
+    if (rows <= SORT_CAP) level = 13;  // every row is a candidate: no select passes
     for (; level <= 12; ++level) {
+        if (level >= 1 && level <= 8 && !have_common) {
+            const u64 init[2] = {~0ULL, 0ULL};
+            hipMemcpyAsync(andor, init, 16, hipMemcpyHostToDevice, s);
+            hipLaunchKernelGGL(sort_andor_kernel, dim3((u32)blocks), dim3(SBLOCK), 0, s, c, rows, desc, nulls_first, sel, andor);
+            u64 ao[2];
+            hipMemcpyAsync(ao, andor, 16, hipMemcpyDeviceToHost, s);
+            if (hipStreamSynchronize(s) != hipSuccess) {
+                err = "sort limit: and/or pass failed";
+                rc = DBG_ERR_DEVICE;
+                break;
+            }
+            common = ~(ao[0] ^ ao[1]);
+            common_val = ao[0];
+            have_common = true;
+        }
+        if (level >= 1 && level <= 8) {
+            const int sh = 8 * (8 - level);
+            if (((common >> sh) & 255ULL) == 255ULL) {  // one bucket holds every row in play
+                sel.ok_mask |= 255ULL << sh;
+                sel.ok_val |= common_val & (255ULL << sh);
+                continue;
+            }
+        }
         hipMemsetAsync(hist, 0, 1024, s);
         hipLaunchKernelGGL(sort_hist_kernel, dim3((u32)blocks), dim3(SBLOCK), 0, s, c, rows, desc, nulls_first, sel, level, hist);
         hipMemcpyAsync(h, hist, sizeof(h), hipMemcpyDeviceToHost, s);
@@ -227,15 +279,16 @@ int sort_limit_run(hipStream_t s, const DCol& c, u64 rows, int asc, int nulls_fi
         hipMemsetAsync(counter, 0, 4, s);
         hipLaunchKernelGGL(sort_select_kernel, dim3((u32)blocks), dim3(SBLOCK), 0, s, c, rows, desc, nulls_first, sel,
                            cand_ok, cand_lo, counter, (u32)SORT_CAP);
-        hipLaunchKernelGGL(sort_small_kernel, dim3(1), dim3(SORT_NT), 0, s, cand_ok, cand_lo, (u32)need_total, idx_out);
+        const u64 n_cand = rows <= SORT_CAP ? rows : need_total;
+        hipLaunchKernelGGL(sort_small_kernel, dim3(1), dim3(SORT_NT), 0, s, cand_ok, cand_lo, (u32)n_cand, (u32)need_total, idx_out);
         u32 got = 0;
         hipMemcpyAsync(&got, counter, 4, hipMemcpyDeviceToHost, s);
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
             err = std::string("sort limit: ") + hipGetErrorString(e);
             rc = DBG_ERR_DEVICE;
-        } else if (got != need_total) {
-            err = "sort limit: selected " + std::to_string(got) + " rows, expected " + std::to_string(need_total);
+        } else if (got != n_cand) {
+            err = "sort limit: selected " + std::to_string(got) + " rows, expected " + std::to_string(n_cand);
             rc = DBG_ERR_INTERNAL;
         } else {
             *n_out = need_total;
