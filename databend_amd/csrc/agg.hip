@@ -1639,6 +1639,7 @@ __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __re
     }
     // write pass over the occupied slots only (one write_group instance in the code; the entry
     // is re-read from the cache rather than indexed out of the register array)
+    const u32 occ_all = occ;
     while (occ && p < out.cap_groups) {
         const u32 k = __builtin_ctz(occ);
         occ &= occ - 1;
@@ -1692,12 +1693,14 @@ __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __re
             put(CNT_WORDS + 1 + DBG_MAX_KEYS, rc ? 1 : 0);  // recycled
         }
     }
-    if (rc) {  // table_init of the owned slots
+    if (rc) {  // table_init of the owned slots that were claimed (an EMPTY slot is still in its
+               // initial state: state words are only written after the entry is claimed)
         const u32 sw = (u32)t.stride_words;
-        for (u32 k = 0; k < per; ++k) {
-            u64 s = base + k;
-            if (s >= n_slots) break;
-            u64* d = t.slots + s * sw;
+        u32 o = occ_all;
+        while (o) {
+            const u32 k = __builtin_ctz(o);
+            o &= o - 1;
+            u64* d = t.slots + (base + k) * sw;
             for (u32 w = 0; w < sw; ++w) d[w] = S.slot_init[w];
         }
     }
