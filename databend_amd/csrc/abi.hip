@@ -675,7 +675,6 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
     if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
     if (hipHostGetDevicePointer((void**)&h->hcounters_dev, h->hcounters, 0) != hipSuccess) h->hcounters_dev = nullptr;
-    // initial capacity: AggregateHashTable::initial_capacity() = 32768, or 2x the hint
     // initial capacity: 2x the hint, or 4096 slots (the CPU table starts at 32768 =
     // AggregateHashTable::initial_capacity(); on the GPU growth is a cheap rehash kernel and a
     // small table keeps init / finalize scans short for low-cardinality queries)
