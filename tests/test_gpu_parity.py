@@ -389,7 +389,10 @@ def test_fast_path_predicates(t, lo, hi):
     check_parity([key], [("count", None), ("sum", v), ("min", v)], filt=(cmp(0, "<>", c), [key]), on_device=True)
 
 
-@pytest.mark.parametrize("cfg,n", [(1, 6_001_215), (2, 10_000_000), (3, 3_000_000), (4, 2_000_000), (5, 3_000_000)])
+# (5, 20M): > 2048 x 4096 rows, so each workgroup of the queued filtered insert runs past the
+# periodic LDS-flush checks (FLUSH_ROUND) with a full table of Zipf string keys.
+@pytest.mark.parametrize("cfg,n", [(1, 6_001_215), (2, 10_000_000), (3, 3_000_000), (4, 2_000_000), (5, 3_000_000),
+                                   (5, 20_000_000)])
 def test_benchmark_configs_match_oracle(cfg, n):
     """Each BASELINE.json config through the bench's own runner (device datagen, fused
     finalize into device buffers, growth from the 4096-slot initial table) vs the oracle on the
