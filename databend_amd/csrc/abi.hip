@@ -675,10 +675,11 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
     if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
     if (hipHostGetDevicePointer((void**)&h->hcounters_dev, h->hcounters, 0) != hipSuccess) h->hcounters_dev = nullptr;
-    // initial capacity: 2x the hint, or 4096 slots (the CPU table starts at 32768 =
+    // initial capacity: 2x the hint, or 1024 slots (the CPU table starts at 32768 =
     // AggregateHashTable::initial_capacity(); on the GPU growth is a cheap rehash kernel and a
-    // small table keeps init / finalize scans short for low-cardinality queries)
-    u64 hint = params->capacity_hint ? params->capacity_hint : 2048;
+    // small table keeps init / finalize scans short for low-cardinality queries: 4096 -> 1024
+    // slots took C2's fused finalize from 13.3 to 11.4 us and C1's from 58 to 50 us)
+    u64 hint = params->capacity_hint ? params->capacity_hint : 512;
     h->cap = pow2_at_least(std::max<u64>(hint * 2, 1024));
     h->init_cap = h->cap;
     if ((rc = alloc_table(h, h->cap, &h->slots)) != DBG_OK) return cleanup(rc);
