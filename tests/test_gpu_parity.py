@@ -395,7 +395,7 @@ def test_fast_path_predicates(t, lo, hi):
                                    (5, 20_000_000)])
 def test_benchmark_configs_match_oracle(cfg, n):
     """Each BASELINE.json config through the bench's own runner (device datagen, fused
-    finalize into device buffers, growth from the 4096-slot initial table) vs the oracle on the
+    finalize into device buffers, growth from the 1024-slot initial table) vs the oracle on the
     same rows generated on the host."""
     from databend_amd import workloads
     res = workloads.run_config(cfg, n, steps=2)
