@@ -20,6 +20,9 @@ FLOAT32, FLOAT64, DECIMAL128, DATE, TIMESTAMP, STRING, BOOLEAN = range(8, 15)
 # dbg_agg_kind
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = range(5)
 
+# dbg_agg_set_strategy
+STRATEGY_AUTO, STRATEGY_TABLE, STRATEGY_PARTITIONED = range(3)
+
 # dbg_cmp
 CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
 

@@ -136,7 +136,16 @@ class AggregateHashTable:
         # retained device inputs may go: later reuse of their memory is stream-ordered after
         # every launch that reads them (the handle runs on torch's current stream)
         self._retained.clear()
-        self._retained.clear()
+
+    def set_strategy(self, strategy: int):
+        """abi.STRATEGY_AUTO / STRATEGY_TABLE / STRATEGY_PARTITIONED (include/dbgpu_agg.h)."""
+        check(lib().dbg_agg_set_strategy(self.h, strategy))
+
+    def strategy(self):
+        """(partitioned?, partitions of the last finalize that needed extra LDS rounds)."""
+        p, r = C.c_int(), C.c_uint64()
+        check(lib().dbg_agg_get_strategy(self.h, C.byref(p), C.byref(r)))
+        return bool(p.value), r.value
 
     # ---- AggregateHashTable::add_groups (+ fused filter)
     def add_groups(self, group_columns: Sequence[ColumnLike], params: Sequence[Optional[ColumnLike]],

@@ -176,6 +176,7 @@ struct dbg_agg_handle {
     // partition state
     u32 part_n = 0;
     int part_scheme = 0;
+    u64 part_nb = 0;  // blocks of the partition histogram
     u64* d_part_pos = nullptr;
     u64* d_part_str_pos = nullptr;
     u64* d_part_str_base = nullptr;
@@ -199,6 +200,56 @@ struct dbg_agg_handle {
     u64 part_bounds_cap = 0;
     void* part_temp = nullptr;
     size_t part_temp_cap = 0;
+    u64 table_rows = 0;  // rows / records inserted into the HBM table since the last reset
+    int strategy = DBG_STRATEGY_AUTO;
+    u64 hint_groups = 0;  // dbg_agg_params.capacity_hint
+
+    // ---- partitioned payload (pp.hip): high-cardinality mode ----
+    bool pp = false;          // batches go to the radix-partitioned payload, not the HBM table
+    double pp_ratio = 1.0;    // estimated groups per selected row (cardinality probe)
+    struct Seg {
+        u64 base, n;
+        std::vector<u64> off;  // level-1 partition offsets (257), relative to base
+    };
+    struct Kind {  // 0: raw records (add_groups), 1: state records (merge_records)
+        u8* l1 = nullptr;
+        u64 l1_cap = 0, l1_n = 0;  // records
+        std::vector<Seg> segs;
+        u8* a = nullptr;  // finalize levels: ping-pong buffers, l1_n records each
+        u8* b = nullptr;
+        u64 ab_cap = 0;
+        u64* part = nullptr;  // final partition offsets (device)
+        u64 part_cap = 0;
+        u8* fin = nullptr;    // final-level buffer and its alternate (the aggregate's overflow)
+        u8* alt = nullptr;
+    } ppk[2];
+    u32 pp_bits = 0;  // final partition bits
+    u32* pp_cnt = nullptr;
+    u64 pp_cnt_cap = 0;
+    u64* pp_off = nullptr;
+    u64 pp_off_cap = 0;
+    u64* pp_mid = nullptr;  // intermediate partition offsets (device)
+    u64 pp_mid_cap = 0;
+    PPChunk* pp_dchunks = nullptr;
+    u64 pp_dchunks_cap = 0;
+    PPChunk* pp_hchunks = nullptr;  // pinned staging
+    u64 pp_hchunks_cap = 0;
+    u32* pp_dc0 = nullptr;
+    u64 pp_dc0_cap = 0;
+    u32* pp_hc0 = nullptr;
+    u64 pp_hc0_cap = 0;
+    u64* pp_hpart = nullptr;  // pinned read-back of partition offsets
+    u64 pp_hpart_cap = 0;
+    u64* pp_tot = nullptr;    // PPT_* (device)
+    u64* pp_htot = nullptr;   // pinned
+    u64* pp_set = nullptr;    // cardinality probe hash set
+    u8* pp_grec = nullptr;    // group records (state record format)
+    u64 pp_grec_cap = 0;      // bytes
+    u64* pp_blk = nullptr;    // per-block string lengths, scanned
+    u64 pp_blk_cap = 0;
+    bool pp_grec_ready = false;
+    u64 pp_nb = 0;            // blocks of the grec passes
+    u64 pp_stat_rounds = 0;   // partitions that took more than one LDS round (last finalize)
 };
 
 static int dev_alloc(void** p, size_t bytes) {
@@ -339,6 +390,31 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
         if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) S.slot_init[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
     S.rec_state_off = off;
     S.rec_width = off + 8 * (u32)S.n_words;
+    // partitioned payload record formats (pp.hip): key part, then each argument value aligned to
+    // its width, then one validity bit per nullable argument
+    S.pp_str = S.has_strings;
+    S.pp_kw = S.has_strings ? 48 : (u32)((S.inline_width + 7) & ~7);
+    u32 po = S.pp_kw;
+    int vbits = 0;
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        S.pp_avbit[a] = -1;
+        S.pp_aoff[a] = 0;
+        if (A.arg_type < 0) continue;
+        const u32 aw = A.arg_type == DBG_BOOLEAN ? 1 : type_width(A.arg_type);
+        const u32 al = aw >= 8 ? 8 : aw;
+        po = (po + al - 1) & ~(al - 1);
+        S.pp_aoff[a] = (uint16_t)po;
+        po += aw;
+        if (A.arg_nullable) S.pp_avbit[a] = (int16_t)vbits++;
+    }
+    S.pp_avoff = po;
+    po += (u32)(vbits + 7) / 8;
+    S.pp_rw_raw = (po + 7) & ~7u;
+    if (!vbits) S.pp_avoff = S.pp_rw_raw;
+    S.pp_rw_state = S.pp_kw + 8 * (u32)S.n_words;
+    S.pp_sw = 1 + S.pp_kw / 8 + (u32)S.n_words;
+    S.pp_ok = S.pp_rw_raw <= 256 && S.pp_rw_state <= 512 && vbits <= 64 && S.pp_sw <= 64;
     return DBG_OK;
 }
 
@@ -679,6 +755,7 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     // AggregateHashTable::initial_capacity(); on the GPU growth is a cheap rehash kernel and a
     // small table keeps init / finalize scans short for low-cardinality queries: 4096 -> 1024
     // slots took C2's fused finalize from 13.3 to 11.4 us and C1's from 58 to 50 us)
+    h->hint_groups = params->capacity_hint;
     u64 hint = params->capacity_hint ? params->capacity_hint : 512;
     h->cap = pow2_at_least(std::max<u64>(hint * 2, 1024));
     h->init_cap = h->cap;
@@ -709,6 +786,17 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
                     h->part_temp};
     for (void* p : bufs)
         if (p) hipFree(p);
+    for (auto& K : h->ppk) {
+        void* kb[] = {K.l1, K.a, K.b, K.part};
+        for (void* q : kb)
+            if (q) hipFree(q);
+    }
+    void* pb[] = {h->pp_cnt, h->pp_off, h->pp_mid, h->pp_dchunks, h->pp_dc0, h->pp_tot, h->pp_set, h->pp_grec, h->pp_blk};
+    for (void* q : pb)
+        if (q) hipFree(q);
+    void* ph[] = {h->pp_hchunks, h->pp_hc0, h->pp_hpart, h->pp_htot};
+    for (void* q : ph)
+        if (q) hipHostFree(q);
     if (h->hcounters) hipHostFree(h->hcounters);
     if (h->switch_ev) hipEventDestroy(h->switch_ev);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
@@ -744,6 +832,12 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     h->n_batches = h->n_cached;  // cached descriptors stay valid (immutable)
     h->pending_rows = h->pending_recs = 0;
     h->finalized = false;
+    h->table_rows = 0;
+    for (auto& K : h->ppk) {  // partitioned payload: records dropped, buffers kept (the mode too)
+        K.l1_n = 0;
+        K.segs.clear();
+    }
+    h->pp_grec_ready = false;
     if (h->clean) return DBG_OK;  // the recycling finalize already re-initialised table + counters
     prof::Scope ps("table_init", h->stream);
     launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap, h->counters);
@@ -776,6 +870,308 @@ static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows
     return DBG_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// partitioned payload (pp.hip), host side
+// ------------------------------------------------------------------------------------------
+}  // extern "C" (templates need C++ linkage)
+template <typename T>
+static int ensure_dev(T** p, u64* cap, u64 n) {
+    if (n <= *cap && *p) return DBG_OK;
+    if (*p) HIPCHECK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    const u64 c = std::max<u64>(n, 64);
+    RETURN_IF(dev_alloc((void**)p, c * sizeof(T)));
+    *cap = c;
+    return DBG_OK;
+}
+template <typename T>
+static int ensure_pinned(dbg_agg_handle* h, T** p, u64* cap, u64 n) {
+    if (n <= *cap && *p) return DBG_OK;
+    if (*p) {
+        HIPCHECK(hipStreamSynchronize(h->stream));  // a queued copy may still read it
+        HIPCHECK(hipHostFree(*p));
+    }
+    *p = nullptr;
+    *cap = 0;
+    const u64 c = std::max<u64>(n, 1024);
+    HIPCHECK(hipHostMalloc((void**)p, c * sizeof(T), hipHostMallocDefault));
+    *cap = c;
+    return DBG_OK;
+}
+
+extern "C" {
+
+#define PP_MIN_ROWS (1ULL << 22)
+#define PP_MIN_GROUPS (1ULL << 20)
+#define PP_SET_CAP (1ULL << 22)
+
+// Cardinality probe of the first batch into an empty handle (AggregateHashTable decides its
+// partial strategy by observed cardinality too: clear_ht / maybe_repartition,
+// EAGG/aggregate_hashtable.rs:225-239, 453-503).  Distinct group hashes among 2^20 evenly spaced
+// selected rows give the estimate: the larger of twice the uniform-frequency solution of
+// D = G (1 - exp(-s / G)) and Haas's GEE sqrt(N / s) f1 + (D - f1), capped at the selected rows.
+static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
+    const Spec& S = h->spec;
+    const int mode = h->strategy == DBG_STRATEGY_TABLE ? 0 : (h->strategy == DBG_STRATEGY_PARTITIONED ? 2 : 1);
+    if (h->pp || !mode || !S.pp_ok || h->table_rows) return DBG_OK;
+    if (mode == 1 && (rows < PP_MIN_ROWS || (!S.has_strings && S.inline_width <= 2))) return DBG_OK;
+    if (!h->pp_set) RETURN_IF(dev_alloc((void**)&h->pp_set, PP_SET_CAP * 16 + 64));
+    u64* out = h->pp_set + 2 * PP_SET_CAP;
+    const u64 ns = std::min<u64>(rows, 1ULL << 20);
+    {
+        prof::Scope ps("pp_probe", h->stream);
+        launch_pp_sample(h->stream, h->dspec, h->dbatches, bid, rows, ns, h->pp_set, PP_SET_CAP, out);
+    }
+    HIPCHECK(hipGetLastError());
+    RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, 1024));
+    HIPCHECK(hipMemcpyAsync(h->pp_hpart, out, 32, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    const double sel = (double)h->pp_hpart[0], D = (double)h->pp_hpart[1], f1 = (double)h->pp_hpart[2];
+    if (sel <= 0) return DBG_OK;
+    const double nsel = (double)rows * sel / (double)ns;
+    double gu = nsel;
+    if (D < sel - 0.5) {  // bisection on G >= D of G (1 - exp(-sel / G)) = D (increasing in G)
+        double lo = D, hi = 1e15;
+        for (int it = 0; it < 200; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            if (mid * -std::expm1(-sel / mid) < D) lo = mid;
+            else hi = mid;
+        }
+        gu = lo;
+    }
+    const double gee = std::sqrt(nsel / sel) * f1 + (D - f1);
+    const double g = std::min(nsel, std::max(2.0 * gu, gee));
+    h->pp_ratio = std::min(1.0, std::max(g / nsel, 1e-9));
+    if (mode == 2 || g > (double)PP_MIN_GROUPS) h->pp = true;
+    return DBG_OK;
+}
+
+// The pinned chunk staging is rewritten only after the stream has drained its last upload.
+static int pp_upload_chunks(dbg_agg_handle* h, const std::vector<PPChunk>& ch, const std::vector<u32>& c0) {
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    RETURN_IF(ensure_pinned(h, &h->pp_hchunks, &h->pp_hchunks_cap, ch.size()));
+    RETURN_IF(ensure_pinned(h, &h->pp_hc0, &h->pp_hc0_cap, c0.size()));
+    RETURN_IF(ensure_dev(&h->pp_dchunks, &h->pp_dchunks_cap, ch.size()));
+    RETURN_IF(ensure_dev(&h->pp_dc0, &h->pp_dc0_cap, c0.size()));
+    memcpy(h->pp_hchunks, ch.data(), ch.size() * sizeof(PPChunk));
+    memcpy(h->pp_hc0, c0.data(), c0.size() * sizeof(u32));
+    HIPCHECK(hipMemcpyAsync(h->pp_dchunks, h->pp_hchunks, ch.size() * sizeof(PPChunk), hipMemcpyHostToDevice, h->stream));
+    HIPCHECK(hipMemcpyAsync(h->pp_dc0, h->pp_hc0, c0.size() * sizeof(u32), hipMemcpyHostToDevice, h->stream));
+    return DBG_OK;
+}
+
+// count + scan of one level: part_out receives G * K + 1 partition offsets
+static int pp_count_scan(dbg_agg_handle* h, int src, int kind, const u8* recs, const std::vector<PPChunk>& ch,
+                         const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out) {
+    const u64 K = 1ULL << kbits;
+    RETURN_IF(pp_upload_chunks(h, ch, c0));
+    RETURN_IF(ensure_dev(&h->pp_cnt, &h->pp_cnt_cap, ch.size() * K));
+    RETURN_IF(ensure_dev(&h->pp_off, &h->pp_off_cap, ch.size() * K));
+    {
+        prof::Scope ps("pp_count", h->stream);
+        launch_pp_count(h->stream, h->dspec, h->dbatches, src, kind, recs, h->pp_dchunks, (u32)ch.size(), shift, kbits, h->pp_cnt);
+    }
+    launch_pp_scan(h->stream, h->pp_cnt, (u32)ch.size(), kbits, h->pp_dc0, (u32)(c0.size() - 1), h->pp_off, part_out);
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+static int pp_scatter(dbg_agg_handle* h, int src, int kind, const u8* recs, u32 n_chunks, u32 shift, u32 kbits, u8* dst) {
+    prof::Scope ps("pp_scatter", h->stream);
+    launch_pp_scatter(h->stream, h->dspec, h->spec, h->dbatches, src, kind, recs, h->pp_dchunks, n_chunks, shift, kbits, h->pp_off, dst);
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+// Level 1 (TransformPartialAggregate::transform in partitioned mode): the batch's selected rows
+// become records appended to the payload, grouped into 256 partitions (PartitionedPayload::
+// append_rows, EAGG/partitioned_payload.rs:100-143).
+static int pp_add_batch(dbg_agg_handle* h, u32 bid, u64 rows, int kind) {
+    const Spec& S = h->spec;
+    auto& K = h->ppk[kind];
+    const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
+    std::vector<PPChunk> ch;
+    for (u64 s = 0; s < rows; s += PP_CHUNK) ch.push_back(PPChunk{s, std::min<u64>(PP_CHUNK, rows - s), bid, 0});
+    std::vector<u32> c0{0, (u32)ch.size()};
+    RETURN_IF(ensure_dev(&h->pp_mid, &h->pp_mid_cap, 257));
+    RETURN_IF(pp_count_scan(h, 0, kind, nullptr, ch, c0, 64 - PP_L1_BITS, PP_L1_BITS, h->pp_mid));
+    RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, 1024));
+    HIPCHECK(hipMemcpyAsync(h->pp_hpart, h->pp_mid, 257 * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    const u64 total = h->pp_hpart[256];
+    if (!total) return DBG_OK;
+    if (K.l1_n + total > K.l1_cap) {  // grow (x2), keeping the records already appended
+        const u64 ncap = std::max<u64>(K.l1_n + total, K.l1_n ? 2 * K.l1_cap : 0);
+        u8* nb = nullptr;
+        RETURN_IF(dev_alloc((void**)&nb, ncap * rw));
+        if (K.l1) {
+            if (K.l1_n) HIPCHECK(hipMemcpyAsync(nb, K.l1, K.l1_n * rw, hipMemcpyDeviceToDevice, h->stream));
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipFree(K.l1));
+        }
+        K.l1 = nb;
+        K.l1_cap = ncap;
+    }
+    RETURN_IF(pp_scatter(h, 0, kind, nullptr, (u32)ch.size(), 64 - PP_L1_BITS, PP_L1_BITS, K.l1 + K.l1_n * rw));
+    K.segs.push_back(dbg_agg_handle::Seg{K.l1_n, total, std::vector<u64>(h->pp_hpart, h->pp_hpart + 257)});
+    K.l1_n += total;
+    h->pp_grec_ready = false;
+    return DBG_OK;
+}
+
+// Levels 2 and 3 (NewTransformPartitionBucket + the final bucket split): every level-1 partition
+// of both record kinds is re-scattered by the next hash bits until the estimated groups of a
+// final partition fit half a workgroup's LDS table.
+static int pp_prepare(dbg_agg_handle* h) {
+    const Spec& S = h->spec;
+    const u64 nr = h->ppk[0].l1_n, nsr = h->ppk[1].l1_n;
+    // estimated groups: the capacity hint when the caller gave one, else the probe's ratio
+    const double est = h->hint_groups ? (double)h->hint_groups : h->pp_ratio * (double)nr + (double)nsr;
+    const double g = std::min((double)(nr + nsr), est);
+    const double target = std::max(64.0, 0.5 * (double)pp_agg_slots(S));
+    const double need = std::max(1.0, std::ceil(g / target));
+    u32 B = PP_L1_BITS + 1;
+    while ((double)(1ULL << B) < need && B < PP_L1_BITS + 16) ++B;
+    const u32 k2 = std::min<u32>(8, B - PP_L1_BITS), k3 = B - PP_L1_BITS - k2;
+    h->pp_bits = B;
+    for (int kind = 0; kind < 2; ++kind) {
+        auto& K = h->ppk[kind];
+        if (!K.l1_n) continue;
+        const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
+        if (K.ab_cap < K.l1_n) {
+            if (K.a) HIPCHECK(hipFree(K.a));
+            if (K.b) HIPCHECK(hipFree(K.b));
+            K.a = K.b = nullptr;
+            K.ab_cap = 0;
+            RETURN_IF(dev_alloc((void**)&K.a, K.l1_n * rw));
+            RETURN_IF(dev_alloc((void**)&K.b, K.l1_n * rw));
+            K.ab_cap = K.l1_n;
+        }
+        RETURN_IF(ensure_dev(&K.part, &K.part_cap, (1ULL << B) + 1));
+        // level 2: units never straddle a level-1 partition (group = partition index)
+        std::vector<PPChunk> ch;
+        std::vector<u32> c0;
+        for (u32 g1 = 0; g1 < (1u << PP_L1_BITS); ++g1) {
+            c0.push_back((u32)ch.size());
+            for (const auto& sg : K.segs) {
+                const u64 lo = sg.base + sg.off[g1], hi = sg.base + sg.off[g1 + 1];
+                for (u64 x = lo; x < hi; x += PP_CHUNK) ch.push_back(PPChunk{x, std::min<u64>(PP_CHUNK, hi - x), 0, g1});
+            }
+            if (c0.back() == ch.size()) ch.push_back(PPChunk{0, 0, 0, g1});
+        }
+        c0.push_back((u32)ch.size());
+        const u32 sh2 = 64 - PP_L1_BITS - k2;
+        u64* p2 = k3 ? nullptr : K.part;
+        if (k3) {
+            RETURN_IF(ensure_dev(&h->pp_mid, &h->pp_mid_cap, (256ULL << k2) + 1));
+            p2 = h->pp_mid;
+        }
+        RETURN_IF(pp_count_scan(h, 1, kind, K.l1, ch, c0, sh2, k2, p2));
+        RETURN_IF(pp_scatter(h, 1, kind, K.l1, (u32)ch.size(), sh2, k2, K.a));
+        K.fin = K.a;
+        K.alt = K.b;
+        if (!k3) continue;
+        // level 3: units inside level-2 partitions
+        const u64 G2 = 256ULL << k2;
+        RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, G2 + 1));
+        HIPCHECK(hipMemcpyAsync(h->pp_hpart, p2, (G2 + 1) * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        ch.clear();
+        c0.clear();
+        for (u64 g2 = 0; g2 < G2; ++g2) {
+            c0.push_back((u32)ch.size());
+            const u64 lo = h->pp_hpart[g2], hi = h->pp_hpart[g2 + 1];
+            for (u64 x = lo; x < hi; x += PP_CHUNK) ch.push_back(PPChunk{x, std::min<u64>(PP_CHUNK, hi - x), 0, (u32)g2});
+            if (c0.back() == ch.size()) ch.push_back(PPChunk{0, 0, 0, (u32)g2});
+        }
+        c0.push_back((u32)ch.size());
+        const u32 sh3 = sh2 - k3;
+        RETURN_IF(pp_count_scan(h, 1, kind, K.a, ch, c0, sh3, k3, K.part));
+        RETURN_IF(pp_scatter(h, 1, kind, K.a, (u32)ch.size(), sh3, k3, K.b));
+        K.fin = K.b;
+        K.alt = K.a;
+    }
+    return DBG_OK;
+}
+
+static u64 pp_records(const dbg_agg_handle* h) { return h->ppk[0].l1_n + h->ppk[1].l1_n; }
+
+// The LDS aggregation of every final partition: mode 0 writes the result columns of `od` (fixed-width
+// keys), mode 1 the group records (state record format) into pp_grec.  Totals land in pp_tot.
+static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
+    const Spec& S = h->spec;
+    if (!h->pp_tot) RETURN_IF(dev_alloc((void**)&h->pp_tot, PPT_WORDS * 8));
+    HIPCHECK(hipMemsetAsync(h->pp_tot, 0, PPT_WORDS * 8, h->stream));
+    const u64 N = pp_records(h);
+    if (!N) return DBG_OK;
+    RETURN_IF(pp_prepare(h));
+    PPAggOut o;
+    memset(&o, 0, sizeof(o));
+    o.tot = h->pp_tot;
+    if (mode == 0) {
+        o.cols = *od;
+    } else {
+        RETURN_IF(ensure_dev(&h->pp_grec, &h->pp_grec_cap, N * S.pp_rw_state));
+        o.grec = h->pp_grec;
+        o.grec_cap = N;
+    }
+    auto& R = h->ppk[0];
+    auto& T = h->ppk[1];
+    {
+        prof::Scope ps("pp_agg", h->stream);
+        launch_pp_agg(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.l1_n ? R.part : nullptr,
+                      T.l1_n ? T.part : nullptr, R.fin, R.alt, T.fin, T.alt, o);
+    }
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+// Group records + per-block string lengths (scanned; totals in pp_tot[PPT_STR + c]).  Async.
+static int pp_grec_build(dbg_agg_handle* h) {
+    const Spec& S = h->spec;
+    RETURN_IF(pp_agg(h, 1, nullptr));
+    const u64 N = std::max<u64>(pp_records(h), 1);
+    h->pp_nb = pp_grec_blocks(N);
+    RETURN_IF(ensure_dev(&h->pp_blk, &h->pp_blk_cap, (u64)S.n_keys * h->pp_nb + 8));
+    if (S.has_strings && pp_records(h)) {
+        launch_pp_grec_lengths(h->stream, h->dspec, h->pp_grec, h->pp_tot, h->pp_blk, h->pp_nb, h->dbatches);
+        for (int c = 0; c < S.n_keys; ++c)
+            if (S.key_types[c].type == DBG_STRING)
+                launch_exclusive_scan(h->stream, h->pp_blk + (u64)c * h->pp_nb, h->pp_nb, h->pp_tot + PPT_STR + c);
+    }
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+static int pp_read_tot(dbg_agg_handle* h) {
+    if (!h->pp_htot) HIPCHECK(hipHostMalloc((void**)&h->pp_htot, PPT_WORDS * 8, hipHostMallocDefault));
+    HIPCHECK(hipMemcpyAsync(h->pp_htot, h->pp_tot, PPT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    h->pp_stat_rounds = h->pp_htot[PPT_ROUNDS];
+    return DBG_OK;
+}
+
+// dbg_agg_finalize in partitioned mode: group records built, sizes known.
+static int pp_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
+    const Spec& S = h->spec;
+    if (!h->pp_grec_ready) {
+        RETURN_IF(pp_grec_build(h));
+        RETURN_IF(pp_read_tot(h));
+        if (h->pp_htot[PPT_GROUPS] > pp_records(h)) return fail(DBG_ERR_INTERNAL, "partitioned aggregate: more groups than records");
+        h->pp_grec_ready = true;
+    }
+    h->n_groups = h->pp_htot[PPT_GROUPS];
+    h->string_bytes.assign(S.n_keys, 0);
+    for (int c = 0; c < S.n_keys; ++c)
+        h->string_bytes[c] = S.key_types[c].type == DBG_STRING ? h->pp_htot[PPT_STR + c] : 0;
+    h->finalized = true;
+    if (n_groups) *n_groups = h->n_groups;
+    if (string_bytes)
+        for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
+    return DBG_OK;
+}
+
 int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols, const dbg_filter* filter,
                        uint64_t rows, int on_device) {
     if (!h || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
@@ -783,7 +1179,6 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     HIPCHECK(hipSetDevice(h->device));
     h->finalized = false;
     if (rows == 0) return DBG_OK;
-    h->clean = false;
     const Spec& S = h->spec;
     BatchDesc* st;
     u32 bid;
@@ -803,6 +1198,11 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     }
     if (filter && filter->n_nodes) RETURN_IF(fill_filter(h, filter, on_device, st->fcols, &st->n_fcols, st->nodes, &st->n_nodes));
     RETURN_IF(submit_batch(h, &st, &bid, on_device && h->owned.size() == owned0));
+    // high cardinality: the radix-partitioned payload instead of the HBM table (pp.hip)
+    if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, rows));
+    if (h->pp) return pp_add_batch(h, bid, rows, 0);
+    h->table_rows += rows;
+    h->clean = false;
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
     u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
     if (part_slice_bits(S, *st, rows, h->cap)) {
@@ -835,6 +1235,7 @@ static int ensure_buf(u64** p, u64* cap, u64 n) {
 int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
+    if (h->pp) return pp_finalize(h, n_groups, string_bytes);
     const Spec& S = h->spec;
     // Optimistic single round trip: count + scan are enqueued behind the inserts and read back
     // together with the overflow counters; only when an insert overflowed does the table grow
@@ -940,7 +1341,11 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
         free_temps();
         return rc;
     }
-    {
+    if (h->pp) {
+        prof::Scope ps("pp_write", h->stream);
+        launch_pp_grec_write(h->stream, h->dspec, h->dbatches, h->pp_grec, h->pp_tot, h->pp_blk, h->pp_nb, od,
+                             h->counters + CNT_ERR);
+    } else {
         prof::Scope ps("write_results", h->stream);
         launch_write_results(h->stream, h->dspec, S, h->dbatches, table_desc(h), h->d_pos, h->d_str_pos, od);
     }
@@ -1002,9 +1407,71 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
 }
 
 
+int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    if (strategy < DBG_STRATEGY_AUTO || strategy > DBG_STRATEGY_PARTITIONED) return fail(DBG_ERR_INVALID, "unknown strategy");
+    if (h->table_rows || h->ppk[0].l1_n || h->ppk[1].l1_n)
+        return fail(DBG_ERR_INVALID, "dbg_agg_set_strategy: the handle holds groups (call it after create or reset)");
+    h->strategy = strategy;
+    h->pp = strategy == DBG_STRATEGY_PARTITIONED;
+    return DBG_OK;
+}
+
+int dbg_agg_get_strategy(dbg_agg_handle* h, int* partitioned, uint64_t* extra_rounds) {
+    if (!h || !partitioned) return fail(DBG_ERR_INVALID, "null argument");
+    *partitioned = h->pp ? 1 : 0;
+    if (extra_rounds) *extra_rounds = h->pp_stat_rounds;
+    return DBG_OK;
+}
+
 int dbg_agg_set_recycle(dbg_agg_handle* h, int on) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     h->recycle = on ? 1 : 0;
+    return DBG_OK;
+}
+
+// Fused finalize in partitioned mode: the LDS aggregation writes the result columns directly
+// (fixed-width keys) or through group records (string keys: offsets need the scanned lengths).
+static int pp_fin_launch(dbg_agg_handle* h, const OutDesc& od) {
+    const Spec& S = h->spec;
+    if (!S.has_strings) {
+        RETURN_IF(pp_agg(h, 0, &od));
+    } else {
+        RETURN_IF(pp_grec_build(h));
+        if (pp_records(h)) {
+            prof::Scope ps("pp_write", h->stream);
+            launch_pp_grec_write(h->stream, h->dspec, h->dbatches, h->pp_grec, h->pp_tot, h->pp_blk, h->pp_nb, od,
+                                 h->pp_tot + PPT_ERR);
+        }
+    }
+    launch_finish_outputs(h->stream, od, h->pp_tot, S.n_keys, S.n_aggs);
+    if (!h->pp_htot) HIPCHECK(hipHostMalloc((void**)&h->pp_htot, PPT_WORDS * 8, hipHostMallocDefault));
+    HIPCHECK(hipMemcpyAsync(h->pp_htot, h->pp_tot, PPT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+static int pp_fin_complete(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
+    const Spec& S = h->spec;
+    FinState& F = h->fin;
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    h->uploads_pending = false;
+    const u64* t = h->pp_htot;
+    h->pp_stat_rounds = t[PPT_ROUNDS];
+    h->n_groups = t[PPT_GROUPS];
+    h->string_bytes.assign(S.n_keys, 0);
+    bool short_buf = h->n_groups > F.max_groups;
+    for (int c = 0; c < S.n_keys; ++c) {
+        h->string_bytes[c] = S.key_types[c].type == DBG_STRING ? t[PPT_STR + c] : 0;
+        if (S.key_types[c].type == DBG_STRING && h->string_bytes[c] > F.cap_str[c]) short_buf = true;
+    }
+    *n_groups = h->n_groups;
+    if (string_bytes)
+        for (int c = 0; c < S.n_keys; ++c) string_bytes[c] = h->string_bytes[c];
+    h->pp_grec_ready = S.has_strings != 0;
+    h->finalized = h->pp_grec_ready;
+    if (t[PPT_ERR] & ERR_DEC_OVERFLOW) return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
+    if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
     return DBG_OK;
 }
 
@@ -1019,7 +1486,7 @@ static int fin_launch(dbg_agg_handle* h) {
     TableDesc t = table_desc(h);
     const bool small = h->cap + 1 <= FIN_SMALL_SLOTS;
     u64* totals = h->d_pos + nb;
-    if (!small) {
+    if (!small && !h->pp) {
         prof::Scope ps("count_groups", h->stream);
         launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
         launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
@@ -1050,6 +1517,13 @@ static int fin_launch(dbg_agg_handle* h) {
             vb += F.max_groups + 1;
         }
     }
+    if (h->pp) {
+        F.zero_copy = false;
+        F.seq = ++h->fin_seq;
+        RETURN_IF(pp_fin_launch(h, od));
+        F.active = true;
+        return DBG_OK;
+    }
     F.zero_copy = small && h->hcounters_dev != nullptr;
     F.seq = ++h->fin_seq;
     if (small) {
@@ -1075,6 +1549,7 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
     const Spec& S = h->spec;
     *retry = false;
     F.active = false;
+    if (h->pp) return pp_fin_complete(h, n_groups, string_bytes);
     bool recycled = false;
     if (!F.zero_copy) {
         HIPCHECK(hipStreamSynchronize(h->stream));
@@ -1203,9 +1678,10 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
     if (n_parts < 1 || n_parts > 256) return fail(DBG_ERR_UNSUPPORTED, "1..256 partitions");
     if (scheme == 1 && (n_parts & (n_parts - 1))) return fail(DBG_ERR_INVALID, "radix partitions must be a power of two");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(resolve_overflow(h));
+    if (h->pp) RETURN_IF(pp_finalize(h, nullptr, nullptr));
+    else RETURN_IF(resolve_overflow(h));
     const Spec& S = h->spec;
-    u64 nb = finalize_blocks(h->cap);
+    u64 nb = h->pp ? pp_grec_blocks(std::max<u64>(h->n_groups, 1)) : finalize_blocks(h->cap);
     u64 nflat = (u64)n_parts * nb;
     RETURN_IF(ensure_buf(&h->d_part_pos, &h->part_cap, nflat + 8));
     RETURN_IF(ensure_buf(&h->d_part_str_pos, &h->part_str_cap, nflat * S.n_keys + 8));
@@ -1213,8 +1689,14 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
     HIPCHECK(hipMemsetAsync(h->d_part_str_pos, 0, (nflat * S.n_keys + 8) * 8, h->stream));
     {
         prof::Scope ps("count_groups", h->stream);
-        launch_count_groups(h->stream, h->dspec, S, h->dbatches, table_desc(h), n_parts, scheme, h->d_part_pos, h->d_part_str_pos);
+        if (h->pp)
+            launch_pp_grec_count_parts(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, n_parts, scheme, h->d_part_pos,
+                                       h->d_part_str_pos, nb);
+        else
+            launch_count_groups(h->stream, h->dspec, S, h->dbatches, table_desc(h), n_parts, scheme, h->d_part_pos,
+                                h->d_part_str_pos);
     }
+    h->part_nb = nb;
     std::vector<u64> hist(nflat), shist(nflat * S.n_keys);
     HIPCHECK(hipMemcpyAsync(hist.data(), h->d_part_pos, nflat * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCHECK(hipMemcpyAsync(shist.data(), h->d_part_str_pos, nflat * S.n_keys * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1245,8 +1727,12 @@ int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strin
     if (!h->part_n) return fail(DBG_ERR_INVALID, "dbg_agg_partition must precede dbg_agg_export_records");
     HIPCHECK(hipSetDevice(h->device));
     prof::Scope ps("export_records", h->stream);
-    launch_export(h->stream, h->dspec, h->spec, h->dbatches, table_desc(h), h->part_n, h->part_scheme, h->d_part_pos,
-                  h->d_part_str_pos, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
+    if (h->pp)
+        launch_pp_grec_export(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, h->part_n, h->part_scheme, h->d_part_pos,
+                              h->d_part_str_pos, h->part_nb, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
+    else
+        launch_export(h->stream, h->dspec, h->spec, h->dbatches, table_desc(h), h->part_n, h->part_scheme, h->d_part_pos,
+                      h->d_part_str_pos, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
     HIPCHECK(hipGetLastError());
     return DBG_OK;
 }
@@ -1262,7 +1748,7 @@ int dbg_agg_export_fixed(dbg_agg_handle* h, void* dev_buf, uint64_t cap_records)
     if (!h || !dev_buf) return fail(DBG_ERR_INVALID, "null argument");
     const Spec& S = h->spec;
     if (!S.inline_keys) return fail(DBG_ERR_UNSUPPORTED, "fixed export needs fixed-width (inline) group keys");
-    if (h->cap + 1 > FIN_SMALL_SLOTS) return fail(DBG_ERR_UNSUPPORTED, "fixed export is for small tables");
+    if (h->cap + 1 > FIN_SMALL_SLOTS || h->pp) return fail(DBG_ERR_UNSUPPORTED, "fixed export is for small tables");
     if (S.rec_width < 16) return fail(DBG_ERR_INTERNAL, "record narrower than the fixed header");
     HIPCHECK(hipSetDevice(h->device));
     prof::Scope ps("export_fixed", h->stream);
@@ -1281,6 +1767,7 @@ int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs,
     if (!h || !dev_bufs || n_bufs < 1) return fail(DBG_ERR_INVALID, "bad argument");
     const Spec& S = h->spec;
     if (!S.inline_keys) return fail(DBG_ERR_UNSUPPORTED, "fixed merge needs fixed-width (inline) group keys");
+    if (h->pp) return fail(DBG_ERR_UNSUPPORTED, "fixed merge: the handle runs partitioned (high cardinality)");
     const u64 n = (u64)n_bufs * (cap_records + 1);
     if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
     HIPCHECK(hipSetDevice(h->device));
@@ -1289,6 +1776,7 @@ int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs,
     BatchDesc* st;
     u32 bid;
     RETURN_IF(new_batch(h, &st, &bid));
+    h->table_rows += n;
     const u8* base = (const u8*)dev_bufs;
     st->rows = n;
     st->is_records = 1;
@@ -1355,6 +1843,12 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
             d.strings = strs;
         }
         RETURN_IF(upload_batch(h, st, bid));
+        if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, n));
+        if (h->pp) {
+            RETURN_IF(pp_add_batch(h, bid, n, 1));
+            continue;
+        }
+        h->table_rows += n;
         u64 blocks = std::min<u64>(2048, (n + 4095) / 4096) + 1;
         RETURN_IF(ensure_ovf(h, n, blocks * 4096));
         prof::Scope ps("agg_merge", h->stream);

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "agg.hpp"
+#include "agg_dev.hpp"
 
 #define BLOCK 256
 #define SLOTS_PER_THREAD 8
@@ -30,7 +31,6 @@
 // ------------------------------------------------------------------------------------------
 // Key packing (inline mode): the row format of EAGG/payload.rs:100-129 in <= 8 bytes.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ u64 width_mask(u32 w) { return w >= 8 ? ~0ULL : ((1ULL << (8 * w)) - 1); }
 
 __device__ __forceinline__ u64 pack_key(const Spec& S, const DCol* keys, u64 i) {
     u64 k = 0;
@@ -47,17 +47,6 @@ __device__ __forceinline__ u64 pack_key(const Spec& S, const DCol* keys, u64 i) 
     return k;
 }
 
-// AggHash of a cell from its raw bits (inline keys / records).
-__device__ __forceinline__ u64 hash_bits(int type, u64 b) {
-    switch (type) {
-        case DBG_BOOLEAN: return b & 1;
-        case DBG_FLOAT32: case DBG_FLOAT64: return hash_prim(canon_float_bits(type, b));
-        case DBG_INT8: return hash_prim((u64)(i64)(int8_t)b);
-        case DBG_INT16: return hash_prim((u64)(i64)(int16_t)b);
-        case DBG_INT32: case DBG_DATE: return hash_prim((u64)(i64)(int32_t)b);
-        default: return hash_prim(b);
-    }
-}
 
 __device__ __forceinline__ u64 hash_packed(const Spec& S, u64 key) {
     u64 h = 0;
@@ -71,8 +60,6 @@ __device__ __forceinline__ u64 hash_packed(const Spec& S, u64 key) {
     return h;
 }
 
-__device__ __forceinline__ u32 ref_bid(u64 e) { return (u32)((e >> 32) & 0xFFFF); }
-__device__ __forceinline__ u32 ref_row(u64 e) { return (u32)e; }
 
 __device__ __forceinline__ bool ref_equal(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 e) {
     const DCol* other = batches[ref_bid(e)].keys;
@@ -88,91 +75,6 @@ __device__ __forceinline__ u64 entry_hash(const Spec& S, const BatchDesc* batche
     return group_hash(batches[ref_bid(e)].keys, S.n_keys, ref_row(e));
 }
 
-// ------------------------------------------------------------------------------------------
-// State updates on an LDS (AS_LDS) or HBM (AS_GLB) slot.  The address space is a template
-// parameter, never inferred: a slot pointer that may be either (a phi of the LDS and the HBM
-// branch) compiles to FLAT atomics, which count against vmcnt as well as lgkmcnt — every LDS
-// wait then drains all global loads in flight and the streaming pipeline collapses.
-// ------------------------------------------------------------------------------------------
-// wptr / asp / at_* / vld live in agg.hpp (shared with part.hip)
-
-template <int AS>
-__device__ __forceinline__ void add128(wptr<AS> p, u64 lo, u64 hi) {
-    u64 old = at_add<AS>(p, lo);
-    u64 carry = (old + lo) < old ? 1ULL : 0ULL;
-    u64 h = hi + carry;
-    if (h) at_add<AS>(p + 1, h);
-}
-
-template <int AS>
-__device__ __forceinline__ void set_flag(wptr<AS> st, int fw, int bit) {
-    u64 m = 1ULL << bit;
-    if (!(st[fw] & m)) at_or<AS>(st + fw, m);
-}
-
-// accumulate_keys of every aggregate for input row i into the slot at st (word 0 = entry).
-template <int AS>
-__device__ __forceinline__ void apply_row(const Spec& S, wptr<AS> st, const BatchDesc& B, u64 i) {
-    for (int a = 0; a < S.n_aggs; ++a) {
-        const DAgg& A = S.aggs[a];
-        const DCol& c = B.args[a];
-        if (A.arg_type >= 0 && A.arg_nullable && !dcol_valid(c, i)) continue;
-        wptr<AS> w = st + A.w0;
-        switch (A.kind) {
-            case DBG_AGG_COUNT: at_add<AS>(w, 1ULL); break;
-            case DBG_AGG_SUM: case DBG_AGG_AVG: {
-                if (A.sumk == SUMK_I64) at_add<AS>(w, (u64)dcol_i64(c, i));
-                else if (A.sumk == SUMK_F64) at_addf<AS>(w, dcol_f64(c, i));
-                else add128<AS>(w, dcol_bits(c, i), dcol_hi(c, i));
-                if (A.kind == DBG_AGG_AVG) at_add<AS>(w + (A.sumk == SUMK_I128 ? 2 : 1), 1ULL);
-                break;
-            }
-            case DBG_AGG_MIN: case DBG_AGG_MAX: {
-                bool mn = A.kind == DBG_AGG_MIN;
-                if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)dcol_i64(c, i), mn, true);
-                else at_minmax<AS>(w, A.mmk == MMK_U64 ? dcol_bits(c, i) : f64_order_key(dcol_f64(c, i)), mn, false);
-                break;
-            }
-        }
-        if (A.flag_bit >= 0) set_flag<AS>(st, S.flags_word, A.flag_bit);
-    }
-}
-
-// merge_states of a partial state (word array r, same layout) into st.  SC1: read r with sc1
-// loads (words parked by another workgroup in this launch, see block_flush).
-// RAS: address space of r (LDS table rows being flushed, or global records / parked rows)
-template <bool SC1, int RAS>
-__device__ __forceinline__ u64 rdw(const u64* p) { return SC1 ? ld_sc1(p) : *asp<RAS>(p); }
-
-template <int AS, bool SC1 = false, int RAS = AS_GLB>
-__device__ __forceinline__ void apply_state(const Spec& S, wptr<AS> st, const u64* r) {
-    for (int a = 0; a < S.n_aggs; ++a) {
-        const DAgg& A = S.aggs[a];
-        wptr<AS> w = st + A.w0;
-        const u64* x = r + A.w0;
-        const u64 x0 = rdw<SC1, RAS>(x);
-        switch (A.kind) {
-            case DBG_AGG_COUNT: if (x0) at_add<AS>(w, x0); break;
-            case DBG_AGG_SUM: case DBG_AGG_AVG: {
-                if (A.sumk == SUMK_I64) { if (x0) at_add<AS>(w, x0); }
-                else if (A.sumk == SUMK_F64) at_addf<AS>(w, __longlong_as_double((long long)x0));
-                else add128<AS>(w, x0, rdw<SC1, RAS>(x + 1));
-                if (A.kind == DBG_AGG_AVG) {
-                    int k = A.sumk == SUMK_I128 ? 2 : 1;
-                    u64 xk = rdw<SC1, RAS>(x + k);
-                    if (xk) at_add<AS>(w + k, xk);
-                }
-                break;
-            }
-            case DBG_AGG_MIN: at_minmax<AS>(w, x0, true, A.mmk == MMK_I64); break;
-            case DBG_AGG_MAX: at_minmax<AS>(w, x0, false, A.mmk == MMK_I64); break;
-        }
-    }
-    if (S.flags_word >= 0) {
-        u64 f = rdw<SC1, RAS>(r + S.flags_word);
-        if (f) at_or<AS>(st + S.flags_word, f);
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // Probing
@@ -1323,133 +1225,6 @@ void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total) {
 // ------------------------------------------------------------------------------------------
 // Results (merge_result + flush_column): deterministic order inside a workgroup via block scan.
 // ------------------------------------------------------------------------------------------
-struct U128 {
-    u64 lo, hi;
-};
-__device__ __forceinline__ U128 u128_neg(U128 a) {
-    U128 r;
-    r.lo = ~a.lo + 1;
-    r.hi = ~a.hi + (r.lo == 0 ? 1 : 0);
-    return r;
-}
-// magnitude * 10 with overflow detection (> limit)
-__device__ __forceinline__ bool u128_mul10(U128& a) {
-    u64 lo_hi = __umul64hi(a.lo, 10ULL);
-    u64 lo = a.lo * 10ULL;
-    u64 hi_hi = __umul64hi(a.hi, 10ULL);
-    u64 hi = a.hi * 10ULL;
-    u64 nhi = hi + lo_hi;
-    bool ovf = hi_hi != 0 || nhi < hi;
-    a.lo = lo;
-    a.hi = nhi;
-    return ovf;
-}
-// (a / d) truncating, d > 0
-__device__ __forceinline__ U128 u128_div_u64(U128 a, u64 d) {
-    U128 q{0, 0};
-    q.hi = a.hi / d;
-    u64 r = a.hi % d;
-    u64 lo = 0;
-    for (int b = 63; b >= 0; --b) {
-        u64 top = r >> 63;
-        r = (r << 1) | ((a.lo >> b) & 1);
-        if (top || r >= d) {
-            r -= d;
-            lo |= 1ULL << b;
-        }
-    }
-    q.lo = lo;
-    return q;
-}
-// 10^38 - 1 = 0x4B3B4CA85A86C47A_098A223FFFFFFFFF
-#define DEC38_MAX_HI 0x4B3B4CA85A86C47AULL
-#define DEC38_MAX_LO 0x098A223FFFFFFFFFULL
-__device__ __forceinline__ bool dec38_out_of_range(u64 lo, u64 hi) {
-    U128 m{lo, hi};
-    if ((i64)hi < 0) m = u128_neg(m);
-    if (m.hi != DEC38_MAX_HI) return m.hi > DEC38_MAX_HI;
-    return m.lo > DEC38_MAX_LO;
-}
-
-__device__ __forceinline__ void write_bytes(void* dst, u64 pos, u32 w, u64 lo, u64 hi) {
-    u8* p = (u8*)dst + pos * w;
-    switch (w) {
-        case 1: *p = (u8)lo; break;
-        case 2: *(uint16_t*)p = (uint16_t)lo; break;
-        case 4: *(u32*)p = (u32)lo; break;
-        case 8: *(u64*)p = lo; break;
-        default: ((u64*)p)[0] = lo; ((u64*)p)[1] = hi; break;
-    }
-}
-
-// Result value of aggregate A from its state words; returns validity.
-__device__ __forceinline__ bool agg_result(const Spec& S, const DAgg& A, const u64* st, u64& lo, u64& hi, u64* err) {
-    const u64* w = st + A.w0;
-    bool valid = true;
-    if (A.res_nullable) {
-        if (A.kind == DBG_AGG_AVG) valid = w[A.sumk == SUMK_I128 ? 2 : 1] != 0;
-        else if (A.flag_bit >= 0) valid = (st[S.flags_word] >> A.flag_bit) & 1;
-    }
-    hi = 0;
-    switch (A.kind) {
-        case DBG_AGG_COUNT: lo = w[0]; break;
-        case DBG_AGG_SUM:
-            lo = w[0];
-            if (A.sumk == SUMK_I128) {
-                hi = w[1];
-                if (valid && A.dec_check && dec38_out_of_range(lo, hi)) atomicOr((unsigned long long*)err, (unsigned long long)ERR_DEC_OVERFLOW);
-            }
-            if (!valid) lo = hi = 0;
-            break;
-        case DBG_AGG_AVG: {
-            u64 cnt = w[A.sumk == SUMK_I128 ? 2 : 1];
-            if (!valid || cnt == 0) {
-                lo = hi = 0;
-                break;
-            }
-            if (A.sumk == SUMK_I128) {
-                U128 m{w[0], w[1]};
-                bool neg = (i64)w[1] < 0;
-                if (neg) m = u128_neg(m);
-                bool ovf = false;
-                for (int k = 0; k < A.scale_add; ++k) ovf |= u128_mul10(m);
-                // checked_mul fits i128 iff magnitude <= 2^127 - 1 (+1 when negative)
-                if (m.hi >> 63) ovf |= !(neg && m.hi == 0x8000000000000000ULL && m.lo == 0);
-                if (ovf) atomicOr((unsigned long long*)err, (unsigned long long)ERR_DEC_OVERFLOW);
-                U128 q = u128_div_u64(m, cnt);
-                if (neg) q = u128_neg(q);
-                lo = q.lo;
-                hi = q.hi;
-            } else {
-                double sum;
-                if (A.sumk == SUMK_F64) sum = __longlong_as_double((long long)w[0]);
-                else if (A.arg_type == DBG_UINT8 || A.arg_type == DBG_UINT16 || A.arg_type == DBG_UINT32 || A.arg_type == DBG_UINT64)
-                    sum = (double)w[0];
-                else sum = (double)(i64)w[0];
-                double r = sum / (double)cnt;
-                lo = (u64)__double_as_longlong(r);
-            }
-            break;
-        }
-        case DBG_AGG_MIN: case DBG_AGG_MAX: {
-            if (!valid) {
-                lo = hi = 0;
-                break;
-            }
-            u64 v = w[0];
-            if (A.mmk == MMK_F64) {
-                double d = f64_from_order_key(v);
-                if (A.res_type == DBG_FLOAT32) lo = (u64)__float_as_uint((float)d);
-                else lo = (u64)__double_as_longlong(d);
-            } else {
-                lo = v;
-                if (A.res_type == DBG_DECIMAL128) hi = (i64)v < 0 ? ~0ULL : 0ULL;
-            }
-            break;
-        }
-    }
-    return valid;
-}
 
 // flush_column of one group (slot s, entry e, state words st) into output row p; sp[c] = string
 // write cursor of key column c (advanced).

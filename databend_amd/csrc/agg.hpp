@@ -30,7 +30,25 @@ struct Spec {
     uint32_t rec_state_off;
     DAgg aggs[DBG_MAX_AGGS];
     u64 slot_init[DBG_MAX_WORDS];  // initial value of every slot word (EMPTY entry, MIN/MAX identities)
+    // partitioned payload (pp.hip): record formats of the radix-partitioned row store
+    //   key part: fixed-width keys -> the row format of EAGG/payload.rs:100-129 ([validity bytes]
+    //             [values]) padded to 8 bytes; string keys -> [group hash u64][klen u8][blob 39 B]
+    //             (blob = per column [validity u8][value | u8 len + bytes]; klen 0xFF = long key,
+    //             blob[0..8) = (bid << 32 | row) reference into the retained input)
+    //   raw record   = [key part][arg values, each aligned to its width][arg validity bits]
+    //   state record = [key part][state words 1..n_words]
+    int32_t pp_ok;          // the spec can run partitioned (record widths within bounds)
+    int32_t pp_str;         // key part is [hash][klen][blob]
+    uint32_t pp_kw;         // key part bytes (multiple of 8)
+    uint32_t pp_rw_raw;     // raw record bytes (multiple of 8)
+    uint32_t pp_rw_state;   // state record bytes
+    uint32_t pp_avoff;      // byte offset of the arg validity bits
+    uint32_t pp_sw;         // LDS slot words: [tag][key part][state words]
+    uint16_t pp_aoff[DBG_MAX_AGGS];  // raw arg value offset (0: the aggregate takes no argument)
+    int16_t pp_avbit[DBG_MAX_AGGS];  // raw arg validity bit (-1: always valid)
 };
+#define PP_BLOB 39        // inline blob bytes of a string key part
+#define PP_KLEN_LONG 0xFF  // key too long for the blob: reference into the retained input
 
 struct BatchDesc {
     u64 rows;
@@ -174,3 +192,53 @@ void launch_export_fixed(hipStream_t s, const Spec* dspec, const BatchDesc* batc
 void launch_export(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                    u32 n_parts, int scheme, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out,
                    const u64* part_str_base);
+
+// ---- partitioned payload (pp.hip) ----
+// A scatter/count work unit: `n` rows of batch `bid` from row `start` (raw input, level 1) or `n`
+// records of a record buffer from index `start` (levels >= 2); `group` = the source partition.
+struct PPChunk {
+    u64 start;
+    u64 n;
+    u32 bid;
+    u32 group;
+};
+#define PP_L1_BITS 8
+#define PP_CHUNK 262144  // rows / records per scatter work unit
+// sample probe: distinct group hashes among sampled selected rows -> out[0] selected, [1] distinct,
+// [2] singletons (f1), [3] doubletons (f2)
+void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches, u32 bid, u64 rows, u64 n_sample,
+                      u64* set, u64 set_cap, u64* out);
+// level scatter: src = 0 raw batch rows (records built from the batch), 1 records of `src_recs`
+void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches, int src, int kind, const u8* src_recs,
+                     const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt);
+void launch_pp_scan(hipStream_t s, const u32* cnt, u32 n_chunks, u32 kbits, const u32* group_c0, u32 n_groups, u64* off,
+                    u64* part_off);
+void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
+                       const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
+                       u8* dst);
+// aggregation of the final partitions in LDS; mode 0: result columns (fixed-width keys), mode 1:
+// group records (state record format) in `grec`.  counters: [0] row cursor, [1] overflow records
+struct PPAggOut {
+    OutDesc cols;   // mode 0
+    u8* grec;       // mode 1
+    u64 grec_cap;
+    u64* tot;       // PPT_* words (device)
+};
+// device totals of one partitioned finalize: groups, string bytes per key column, extra rounds, errors
+enum { PPT_GROUPS = 0, PPT_STR = 1, PPT_ROUNDS = 1 + DBG_MAX_KEYS, PPT_ERR = 2 + DBG_MAX_KEYS, PPT_WORDS = 4 + DBG_MAX_KEYS };
+u32 pp_agg_slots(const Spec& hspec);
+void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
+                   const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out);
+// group records -> result columns (deterministic positions: block sums, scan, write)
+void launch_pp_grec_lengths(hipStream_t s, const Spec* dspec, const u8* grec, const u64* n_dev, u64* blk_len /* [n_keys][blocks] */,
+                            u64 nblocks, const BatchDesc* batches);
+u64 pp_grec_blocks(u64 n);
+void launch_pp_grec_write(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, const u64* n_dev,
+                          const u64* str_pos /* [n_keys][blocks] scanned */, u64 nblocks, const OutDesc& out, u64* err);
+// group records -> exchange records partitioned by hash % n (scheme 0) or radix bits (scheme 1)
+void launch_pp_grec_count_parts(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n,
+                                u32 n_parts, int scheme, u64* hist /* [n_parts][blocks] */,
+                                u64* str_hist /* [n_parts][n_keys][blocks] */, u64 nblocks);
+void launch_pp_grec_export(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n, u32 n_parts,
+                           int scheme, const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out, u8* str_out,
+                           const u64* part_str_base);

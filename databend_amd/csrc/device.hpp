@@ -22,6 +22,7 @@ typedef uint64_t u64;
 typedef int64_t i64;
 typedef uint32_t u32;
 typedef uint8_t u8;
+typedef uint16_t u16;
 
 // ------------------------------------------------------------------------------------------
 // Column descriptor

@@ -1,0 +1,1018 @@
+// pp.hip — the radix-partitioned payload: high-cardinality GROUP BY without an HBM hash table.
+//
+// The reference's own design at high cardinality: TransformPartialAggregate's table keeps being
+// cleared (clear_ht, EAGG/aggregate_hashtable.rs:225-239) so partial aggregation degenerates into
+// appending rows to a radix-PartitionedPayload (EAGG/partitioned_payload.rs:100-143), and the final
+// stage aggregates bucket by bucket on cache-sized tables (AGG/transform_aggregate_final.rs:71-156).
+// On MI355X the same shape is one streaming pass per level plus one LDS pass:
+//
+//   level 1 (add_groups):   predicate -> group hash -> raw record [key part][args] scattered into
+//                           256 partitions by the top bits of mix(hash)       (count, scan, scatter)
+//   level 2..3 (finalize):  every partition re-scattered by the next hash bits until a partition's
+//                           groups fit one workgroup's LDS table                (count, scan, scatter)
+//   aggregate (finalize):   one workgroup per final partition: LDS hash table, LDS atomics,
+//                           groups written straight to the result columns (or as state records)
+//
+// Every scatter is a stable-by-tile counting sort: a count pass writes per-(work unit, bucket)
+// histograms, one workgroup scans them in (source partition, bucket, unit) order, and the scatter
+// pass stages records in LDS, sorts each tile by bucket and writes whole runs.  No device-scope
+// atomics touch the data: HBM traffic is record streams only.
+#include "agg.hpp"
+#include "agg_dev.hpp"
+
+#define PP_NT 512
+#define PP_AGG_NT 1024
+#define PP_AGG_LDS (144 * 1024)
+#define PP_STAGE_BYTES (32 * 1024)
+#define PP_MAXK 1024
+#define PP_WINDOW 96
+
+typedef __attribute__((address_space(3))) u8 l8;
+typedef __attribute__((address_space(3))) u16 l16;
+typedef __attribute__((address_space(3))) u32 l32;
+typedef __attribute__((address_space(3))) u64 l64;
+
+// Partition bits come from a remix of the reference group hash (a bool-only key hashes to 0/1):
+// level-local bucket = (pp_mix(h) >> shift) & (K - 1); the LDS slot uses the low 32 bits.
+__device__ __forceinline__ u64 pp_mix(u64 h) { return hash_prim(h ^ 0x2545F4914F6CDD1DULL); }
+
+// little-endian value of w (1..8) bytes at p (global memory, any alignment)
+__device__ __forceinline__ u64 ld_le(const u8* p, u32 w) { return load_partial(p, w) & width_mask(w); }
+
+// group_hash_columns of a packed fixed-width key (row format, Spec koff/voff).
+__device__ __forceinline__ u64 pp_fixed_hash(const Spec& S, const u8* k) {
+    u64 h = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        u64 x;
+        const bool v = !t.nullable || gld<u8>(k + S.voff[c]) != 0;
+        if (!v) x = NULL_HASH_VAL;
+        else if (t.type == DBG_DECIMAL128) x = hash_i128(ld_le(k + S.koff[c], 8), ld_le(k + S.koff[c] + 8, 8));
+        else x = hash_bits(t.type, ld_le(k + S.koff[c], type_width(t.type)));
+        h = c == 0 ? x : (h * NULL_HASH_VAL) ^ x;
+    }
+    return h;
+}
+__device__ __forceinline__ u64 pp_rec_hash(const Spec& S, const u8* rec) { return S.pp_str ? gld<u64>(rec) : pp_fixed_hash(S, rec); }
+
+// hash of input row i of a batch (raw rows or exchange records, which carry it)
+__device__ __forceinline__ u64 pp_row_hash(const Spec& S, const BatchDesc& B, u64 i) {
+    if (B.is_records) return gld<u64>(B.rec_base + i * (u64)B.rec_width);
+    return group_hash(B.keys, S.n_keys, i);
+}
+
+// ---- LDS byte helpers ----
+__device__ __forceinline__ void lput(l8* d, u32 off, u64 v, u32 w) {
+    if (w == 8 && !(off & 7)) { *(l64*)(d + off) = v; return; }
+    if (w == 4 && !(off & 3)) { *(l32*)(d + off) = (u32)v; return; }
+    if (w == 2 && !(off & 1)) { *(l16*)(d + off) = (u16)v; return; }
+    for (u32 j = 0; j < w; ++j) d[off + j] = (u8)(v >> (8 * j));
+}
+__device__ __forceinline__ u64 lget(const l8* d, u32 off, u32 w) {
+    if (w == 8 && !(off & 7)) return *(const l64*)(d + off);
+    if (w == 4 && !(off & 3)) return *(const l32*)(d + off);
+    if (w == 2 && !(off & 1)) return *(const l16*)(d + off);
+    u64 v = 0;
+    for (u32 j = 0; j < w; ++j) v |= (u64)d[off + j] << (8 * j);
+    return v;
+}
+
+// Key part of row i into d (LDS, zeroed): packed row format or [hash][klen][blob].
+__device__ __forceinline__ void pp_put_key(const Spec& S, const DCol* keys, u32 bid, u64 i, u64 h, l8* d) {
+    if (!S.pp_str) {
+        for (int c = 0; c < S.n_keys; ++c) {
+            const DCol& col = keys[c];
+            const bool v = dcol_valid(col, i);
+            if (S.key_types[c].nullable) d[S.voff[c]] = v ? 1 : 0;
+            if (!v) continue;
+            const u32 w = type_width(col.type);
+            if (col.type == DBG_DECIMAL128) {
+                lput(d, S.koff[c], dcol_bits(col, i), 8);
+                lput(d, S.koff[c] + 8, dcol_hi(col, i), 8);
+            } else {
+                u64 b = dcol_bits(col, i);
+                if (col.type == DBG_FLOAT32 || col.type == DBG_FLOAT64) b = canon_float_bits(col.type, b);
+                lput(d, S.koff[c], b, w);
+            }
+        }
+        return;
+    }
+    *(l64*)d = h;
+    u32 len = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const DCol& col = keys[c];
+        const bool v = dcol_valid(col, i);
+        len += S.key_types[c].nullable ? 1 : 0;
+        if (col.type == DBG_STRING) len += 1 + (v ? (u32)min<u64>(dcol_str(col, i).len, 256) : 0);
+        else len += type_width(col.type);
+    }
+    if (len > PP_BLOB) {
+        d[8] = PP_KLEN_LONG;
+        *(l64*)(d + 16) = ((u64)bid << 32) | (u64)(u32)i;
+        return;
+    }
+    d[8] = (u8)len;
+    u32 o = 9;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const DCol& col = keys[c];
+        const bool v = dcol_valid(col, i);
+        if (S.key_types[c].nullable) d[o++] = v ? 1 : 0;
+        if (col.type == DBG_STRING) {
+            StrRef s = v ? dcol_str(col, i) : StrRef{nullptr, 0};
+            d[o++] = (u8)s.len;
+            for (u64 j = 0; j < s.len; ++j) d[o + j] = gld<u8>(s.p + j);
+            o += (u32)s.len;
+        } else {
+            const u32 w = type_width(col.type);
+            if (v) {
+                if (col.type == DBG_DECIMAL128) {
+                    lput(d, o, dcol_bits(col, i), 8);
+                    lput(d, o + 8, dcol_hi(col, i), 8);
+                } else {
+                    u64 b = dcol_bits(col, i);
+                    if (col.type == DBG_FLOAT32 || col.type == DBG_FLOAT64) b = canon_float_bits(col.type, b);
+                    lput(d, o, b, w);
+                }
+            }
+            o += w;
+        }
+    }
+}
+
+// Raw record of row i: key part + argument values + argument validity bits (d zeroed).
+__device__ __forceinline__ void pp_put_raw(const Spec& S, const BatchDesc& B, u32 bid, u64 i, u64 h, l8* d) {
+    pp_put_key(S, B.keys, bid, i, h, d);
+    u64 vm = 0;
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        if (A.arg_type < 0) continue;
+        const DCol& c = B.args[a];
+        const bool v = dcol_valid(c, i);
+        if (S.pp_avbit[a] >= 0 && v) vm |= 1ULL << S.pp_avbit[a];
+        if (!v) continue;
+        const u32 w = A.arg_type == DBG_BOOLEAN ? 1 : type_width(A.arg_type);
+        if (A.arg_type == DBG_DECIMAL128) {
+            lput(d, S.pp_aoff[a], dcol_bits(c, i), 8);
+            lput(d, S.pp_aoff[a] + 8, dcol_hi(c, i), 8);
+        } else {
+            lput(d, S.pp_aoff[a], dcol_bits(c, i), w);
+        }
+    }
+    if (vm) {
+        const u32 nb = (S.pp_rw_raw - S.pp_avoff) < 8 ? (S.pp_rw_raw - S.pp_avoff) : 8;
+        lput(d, S.pp_avoff, vm, nb);
+    }
+}
+
+// State record of exchange record i (LAYOUT_RECORD batch): key part + the record's state words.
+__device__ __forceinline__ void pp_put_state(const Spec& S, const BatchDesc& B, u32 bid, u64 i, u64 h, l8* d) {
+    pp_put_key(S, B.keys, bid, i, h, d);
+    const u8* src = B.rec_base + i * (u64)B.rec_width + S.rec_state_off;
+    for (int w = 0; w < S.n_words; ++w) *(l64*)(d + S.pp_kw + 8 * w) = load_u64_unaligned(src + 8 * w);
+}
+
+// ---- argument values of a raw record (global) ----
+__device__ __forceinline__ i64 pp_sext(int t, u64 b) {
+    switch (t) {
+        case DBG_INT8: return (i64)(int8_t)b;
+        case DBG_INT16: return (i64)(int16_t)b;
+        case DBG_INT32: case DBG_DATE: return (i64)(int32_t)b;
+        case DBG_BOOLEAN: return (i64)(b & 1);
+        default: return (i64)b;
+    }
+}
+
+// accumulate_keys of one raw record into the slot states st (st[A.w0] = first word).
+template <int AS>
+__device__ __forceinline__ void pp_apply_raw(const Spec& S, wptr<AS> st, const u8* rec) {
+    u64 vm = ~0ULL;
+    if (S.pp_avoff < S.pp_rw_raw) vm = ld_le(rec + S.pp_avoff, min(8u, S.pp_rw_raw - S.pp_avoff));
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        if (A.arg_type >= 0 && S.pp_avbit[a] >= 0 && !((vm >> S.pp_avbit[a]) & 1)) continue;
+        wptr<AS> w = st + A.w0;
+        const u8* p = rec + S.pp_aoff[a];
+        const u32 aw = A.arg_type == DBG_BOOLEAN ? 1 : (A.arg_type >= 0 ? type_width(A.arg_type) : 0);
+        switch (A.kind) {
+            case DBG_AGG_COUNT: at_add<AS>(w, 1ULL); break;
+            case DBG_AGG_SUM: case DBG_AGG_AVG: {
+                if (A.sumk == SUMK_I64) at_add<AS>(w, (u64)pp_sext(A.arg_type, ld_le(p, aw)));
+                else if (A.sumk == SUMK_F64) {
+                    const u64 b = ld_le(p, aw);
+                    at_addf<AS>(w, A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)b) : __longlong_as_double((long long)b));
+                } else {
+                    add128<AS>(w, ld_le(p, 8), ld_le(p + 8, 8));
+                }
+                if (A.kind == DBG_AGG_AVG) at_add<AS>(w + (A.sumk == SUMK_I128 ? 2 : 1), 1ULL);
+                break;
+            }
+            case DBG_AGG_MIN: case DBG_AGG_MAX: {
+                const bool mn = A.kind == DBG_AGG_MIN;
+                const u64 b = ld_le(p, aw);
+                if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
+                else if (A.mmk == MMK_U64) at_minmax<AS>(w, b, mn, false);
+                else
+                    at_minmax<AS>(w, f64_order_key(A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)b)
+                                                                          : __longlong_as_double((long long)b)),
+                                  mn, false);
+                break;
+            }
+        }
+        if (A.flag_bit >= 0) set_flag<AS>(st, S.flags_word, A.flag_bit);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Cardinality probe: distinct group hashes among n_sample evenly spaced (selected) rows.
+// set: 2 * set_cap words [hash | count]; out: [0] selected, [1] distinct, [2] f1, [3] f2.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pp_sample_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                       u32 bid, u64 rows, u64 n_sample, u64* set, u64 set_cap, u64* out) {
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    for (u64 k = blockIdx.x * 256ULL + threadIdx.x; k < n_sample; k += (u64)gridDim.x * 256) {
+        const u64 i = (k * rows) / n_sample;
+        if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+        atomicAdd((unsigned long long*)out, 1ULL);
+        u64 h = pp_row_hash(S, B, i);
+        h = h ? h : 1;
+        u64 s = slot_mix(h) & (set_cap - 1);
+        for (u64 p = 0; p < set_cap; ++p) {
+            u64 old = atomicCAS((unsigned long long*)(set + 2 * s), 0ULL, (unsigned long long)h);
+            if (old == 0) atomicAdd((unsigned long long*)(out + 1), 1ULL);
+            if (old == 0 || old == h) {
+                atomicAdd((unsigned long long*)(set + 2 * s + 1), 1ULL);
+                break;
+            }
+            s = (s + 1) & (set_cap - 1);
+        }
+    }
+}
+__global__ void __launch_bounds__(256) pp_sample_stats_kernel(const u64* set, u64 set_cap, u64* out) {
+    u32 f1 = 0, f2 = 0;
+    for (u64 s = blockIdx.x * 256ULL + threadIdx.x; s < set_cap; s += (u64)gridDim.x * 256) {
+        const u64 c = set[2 * s + 1];
+        f1 += c == 1;
+        f2 += c == 2;
+    }
+    if (f1) atomicAdd((unsigned long long*)(out + 2), (unsigned long long)f1);
+    if (f2) atomicAdd((unsigned long long*)(out + 3), (unsigned long long)f2);
+}
+
+void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches, u32 bid, u64 rows, u64 n_sample, u64* set,
+                      u64 set_cap, u64* out) {
+    hipMemsetAsync(set, 0, set_cap * 16, s);
+    hipMemsetAsync(out, 0, 32, s);
+    hipLaunchKernelGGL(pp_sample_kernel, dim3(1024), dim3(256), 0, s, dspec, batches, bid, rows, n_sample, set, set_cap, out);
+    hipLaunchKernelGGL(pp_sample_stats_kernel, dim3(1024), dim3(256), 0, s, set, set_cap, out);
+}
+
+// ------------------------------------------------------------------------------------------
+// count: per work unit, a histogram of the level's local bucket over its (selected) rows/records
+// ------------------------------------------------------------------------------------------
+template <int SRC>
+__global__ void __launch_bounds__(PP_NT) pp_count_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                        int kind, const u8* __restrict__ recs, const PPChunk* __restrict__ chunks,
+                                                        u32 shift, u32 kbits, u32* __restrict__ cnt) {
+    const Spec& S = *spec;
+    __shared__ u32 hist[PP_MAXK];
+    const u32 K = 1u << kbits;
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) hist[b] = 0;
+    __syncthreads();
+    const PPChunk ch = chunks[blockIdx.x];
+    const u64 end = ch.start + ch.n;
+    if (SRC == 0) {
+        const BatchDesc& B = batches[ch.bid];
+        for (u64 i = ch.start + threadIdx.x; i < end; i += PP_NT) {
+            if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+            const u64 pm = pp_mix(pp_row_hash(S, B, i));
+            atomicAdd(&hist[(u32)(pm >> shift) & (K - 1)], 1u);
+        }
+    } else {
+        const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
+        for (u64 i = ch.start + threadIdx.x; i < end; i += PP_NT) {
+            const u64 pm = pp_mix(pp_rec_hash(S, recs + i * rw));
+            atomicAdd(&hist[(u32)(pm >> shift) & (K - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) cnt[(u64)blockIdx.x * K + b] = hist[b];
+}
+
+void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches, int src, int kind, const u8* src_recs,
+                     const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt) {
+    if (!n_chunks) return;
+    if (src == 0)
+        hipLaunchKernelGGL(pp_count_kernel<0>, dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
+    else
+        hipLaunchKernelGGL(pp_count_kernel<1>, dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
+}
+
+// ------------------------------------------------------------------------------------------
+// scan: exclusive prefix of cnt in (source group, bucket, unit) order — units of one group are
+// consecutive (group_c0[g] .. group_c0[g + 1]; every group has at least one unit).
+// off[unit][bucket] = destination of the unit's first record in that bucket;
+// part_off[g * K + b] = start of destination partition (g, b); part_off[G * K] = total.
+// ------------------------------------------------------------------------------------------
+#define SCAN_NT 1024
+__device__ __forceinline__ void scan_locate(u64 j, u32 K, const u32* c0, u32 G, u32& g, u32& b, u32& ci) {
+    u32 lo = 0, hi = G;  // largest g with c0[g] * K <= j
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if ((u64)c0[mid] * K <= j) lo = mid;
+        else hi = mid;
+    }
+    g = lo;
+    const u64 local = j - (u64)c0[g] * K;
+    const u32 nc = c0[g + 1] - c0[g];
+    b = (u32)(local / nc);
+    ci = (u32)(local % nc);
+}
+
+__global__ void __launch_bounds__(SCAN_NT) pp_scan_kernel(const u32* __restrict__ cnt, u32 n_chunks, u32 kbits,
+                                                         const u32* __restrict__ c0, u32 G, u64* __restrict__ off,
+                                                         u64* __restrict__ part_off) {
+    __shared__ u64 sums[SCAN_NT];
+    const u32 K = 1u << kbits;
+    const u64 E = (u64)n_chunks * K;
+    const u64 per = (E + SCAN_NT - 1) / SCAN_NT;
+    const u64 a = threadIdx.x * per, e = a + per < E ? a + per : E;
+    u64 acc = 0;
+    if (a < e) {
+        u32 g, b, ci;
+        scan_locate(a, K, c0, G, g, b, ci);
+        for (u64 j = a; j < e; ++j) {
+            acc += cnt[(u64)(c0[g] + ci) * K + b];
+            if (++ci == c0[g + 1] - c0[g]) {
+                ci = 0;
+                if (++b == K) { b = 0; ++g; }
+            }
+        }
+    }
+    sums[threadIdx.x] = acc;
+    __syncthreads();
+    for (u32 o = 1; o < SCAN_NT; o <<= 1) {
+        const u64 v = threadIdx.x >= o ? sums[threadIdx.x - o] : 0;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    u64 run = threadIdx.x ? sums[threadIdx.x - 1] : 0;
+    if (a < e) {
+        u32 g, b, ci;
+        scan_locate(a, K, c0, G, g, b, ci);
+        for (u64 j = a; j < e; ++j) {
+            const u64 idx = (u64)(c0[g] + ci) * K + b;
+            if (ci == 0) part_off[(u64)g * K + b] = run;
+            off[idx] = run;
+            run += cnt[idx];
+            if (++ci == c0[g + 1] - c0[g]) {
+                ci = 0;
+                if (++b == K) { b = 0; ++g; }
+            }
+        }
+    }
+    if (threadIdx.x == SCAN_NT - 1) part_off[(u64)G * K] = sums[SCAN_NT - 1];
+}
+
+void launch_pp_scan(hipStream_t s, const u32* cnt, u32 n_chunks, u32 kbits, const u32* group_c0, u32 n_groups, u64* off,
+                    u64* part_off) {
+    hipLaunchKernelGGL(pp_scan_kernel, dim3(1), dim3(SCAN_NT), 0, s, cnt, n_chunks, kbits, group_c0, n_groups, off, part_off);
+}
+
+// ------------------------------------------------------------------------------------------
+// scatter: records staged in LDS, counting-sorted by bucket per tile, written as runs.
+// LDS: stage [cap * rw] | bkt u16 [cap] | rank u16 [cap] | sidx u16 [cap] | hist u32 [K] |
+//      scan u32 [K] | run u64 [K]
+// ------------------------------------------------------------------------------------------
+// LDS carve-up of the scatter kernel (byte offsets, every array 16-byte aligned)
+struct PPStageLayout {
+    u32 cap, bkt, rank, sidx, hist, scn, run, bytes;
+};
+__host__ __device__ __forceinline__ u32 pp_al16(u32 x) { return (x + 15) & ~15u; }
+__host__ __device__ __forceinline__ PPStageLayout pp_stage_layout(u32 rw, u32 K) {
+    PPStageLayout L;
+    L.cap = PP_STAGE_BYTES / rw;
+    if (L.cap > 4096) L.cap = 4096;
+    L.bkt = pp_al16(L.cap * rw);
+    L.rank = pp_al16(L.bkt + 2 * L.cap);
+    L.sidx = pp_al16(L.rank + 2 * L.cap);
+    L.hist = pp_al16(L.sidx + 2 * L.cap);
+    L.scn = pp_al16(L.hist + 4 * K);
+    L.run = pp_al16(L.scn + 4 * K);
+    L.bytes = pp_al16(L.run + 8 * K);
+    return L;
+}
+static size_t pp_scatter_lds(u32 rw, u32 K) { return pp_stage_layout(rw, K).bytes; }
+
+// block-wide exclusive scan of one u32 per thread (PP_NT threads); returns the total
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* wtot, u32& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    u32 pre = 0, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wave) pre += wtot[w];
+        tot += wtot[w];
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+template <int SRC>
+__global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                          int kind, const u8* __restrict__ recs, const PPChunk* __restrict__ chunks,
+                                                          u32 shift, u32 kbits, const u64* __restrict__ off, u8* __restrict__ dst) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    const Spec& S = *spec;
+    const u32 K = 1u << kbits;
+    const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
+    const u32 wpr = rw / 8;
+    const PPStageLayout LY = pp_stage_layout(rw, K);
+    const u32 cap = LY.cap;
+    l8* stage = (l8*)lds_raw;
+    l16* bkt = (l16*)(stage + LY.bkt);
+    l16* rank = (l16*)(stage + LY.rank);
+    l16* sidx = (l16*)(stage + LY.sidx);
+    l32* hist = (l32*)(stage + LY.hist);
+    l32* scn = (l32*)(stage + LY.scn);
+    l64* run = (l64*)(stage + LY.run);
+    __shared__ u32 wtot[PP_NT / 64], wcnt[PP_NT / 64];
+
+    const PPChunk ch = chunks[blockIdx.x];
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) run[b] = off[(u64)blockIdx.x * K + b];
+    u32 qn = 0;  // staged records: kept in registers, identical in every thread (no shared counter)
+    __syncthreads();
+
+    auto flush = [&]() {
+        const u32 n = qn;
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) hist[b] = 0;
+        __syncthreads();
+        for (u32 q = threadIdx.x; q < n; q += PP_NT)
+            rank[q] = (u16)__hip_atomic_fetch_add(&hist[bkt[q]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        // exclusive scan of hist (K <= 1024 = 2 per thread)
+        {
+            const u32 b0 = threadIdx.x * 2;
+            const u32 h0 = b0 < K ? hist[b0] : 0, h1 = b0 + 1 < K ? hist[b0 + 1] : 0;
+            u32 tot;
+            const u32 pre = block_excl_scan(h0 + h1, wtot, tot);
+            if (b0 < K) scn[b0] = pre;
+            if (b0 + 1 < K) scn[b0 + 1] = pre + h0;
+        }
+        __syncthreads();
+        for (u32 q = threadIdx.x; q < n; q += PP_NT) sidx[scn[bkt[q]] + rank[q]] = (u16)q;
+        __syncthreads();
+        const u32 nw = n * wpr;
+        for (u32 j = threadIdx.x; j < nw; j += PP_NT) {
+            const u32 t = j / wpr, w = j - t * wpr;
+            const u32 q = sidx[t];
+            const u32 b = bkt[q];
+            const u64 di = run[b] + (t - scn[b]);
+            ((u64 __attribute__((address_space(1)))*)dst)[di * wpr + w] = *(const l64*)(stage + (size_t)q * rw + 8 * w);
+        }
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) run[b] += hist[b];
+        qn = 0;
+        __syncthreads();
+    };
+
+    const u64 end = ch.start + ch.n;
+    const BatchDesc& B = batches[ch.bid];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u64 base = ch.start; base < end; base += PP_NT) {
+        const u64 i = base + threadIdx.x;
+        bool sel = i < end;
+        if (SRC == 0 && sel && !B.is_records && B.n_nodes) sel = eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+        const u64 m = __ballot(sel);
+        if (lane == 0) wcnt[wave] = (u32)__popcll(m);
+        __syncthreads();
+        u32 wb = qn, tot = 0;
+        for (int w = 0; w < PP_NT / 64; ++w) {
+            if (w < wave) wb += wcnt[w];
+            tot += wcnt[w];
+        }
+        qn += tot;
+        if (sel) {
+            const u32 q = wb + (u32)__popcll(m & ((1ULL << lane) - 1));
+            l8* d = stage + (size_t)q * rw;
+            if (SRC == 0) {
+                for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = 0;
+                const u64 h = pp_row_hash(S, B, i);
+                if (kind) pp_put_state(S, B, ch.bid, i, h, d);
+                else pp_put_raw(S, B, ch.bid, i, h, d);
+                bkt[q] = (u16)((u32)(pp_mix(h) >> shift) & (K - 1));
+            } else {
+                const u8* r = recs + i * rw;
+                for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = gld<u64>(r + 8 * w);
+                bkt[q] = (u16)((u32)(pp_mix(pp_rec_hash(S, r)) >> shift) & (K - 1));
+            }
+        }
+        __syncthreads();
+        if (qn + PP_NT > cap) flush();
+    }
+    if (qn) flush();
+}
+
+void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
+                       const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
+                       u8* dst) {
+    if (!n_chunks) return;
+    const u32 rw = kind ? hspec.pp_rw_state : hspec.pp_rw_raw;
+    const size_t lds = pp_scatter_lds(rw, 1u << kbits);
+    if (src == 0)
+        hipLaunchKernelGGL(pp_scatter_kernel<0>, dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, chunks, shift,
+                           kbits, off, dst);
+    else
+        hipLaunchKernelGGL(pp_scatter_kernel<1>, dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, chunks, shift,
+                           kbits, off, dst);
+}
+
+// ------------------------------------------------------------------------------------------
+// aggregate: one workgroup per final partition, an LDS table of `cap` slots
+// [tag][key part][state words].  tag 0 = empty, 1 = being claimed, else (mix | 2).  A key whose
+// probe window is full in this round overflows — consistently for all its records, since slots
+// only ever fill — into the partition's region of the alternate buffer, aggregated in a further
+// round once this round's groups are written.
+// ------------------------------------------------------------------------------------------
+u32 pp_agg_slots(const Spec& S) { return (u32)((PP_AGG_LDS - 256) / (8 * S.pp_sw)); }
+
+__device__ __forceinline__ u64 lds_ld_acq(l64* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+__device__ __forceinline__ bool pp_long_equal(const Spec& S, const BatchDesc* batches, u64 ra, u64 rb) {
+    const DCol* ka = batches[ref_bid(ra)].keys;
+    const DCol* kb = batches[ref_bid(rb)].keys;
+    for (int c = 0; c < S.n_keys; ++c)
+        if (!cell_equal(ka[c], ref_row(ra), kb[c], ref_row(rb))) return false;
+    return true;
+}
+
+// key part of a record (global) == key part of a slot (LDS)
+__device__ __forceinline__ bool pp_key_equal(const Spec& S, const BatchDesc* batches, const l64* sk, const u8* rk) {
+    const u32 kw8 = S.pp_kw / 8;
+    if (!S.pp_str) {
+        for (u32 w = 0; w < kw8; ++w)
+            if (sk[w] != gld<u64>(rk + 8 * w)) return false;
+        return true;
+    }
+    if (sk[0] != gld<u64>(rk)) return false;  // group hash
+    const u64 w1 = gld<u64>(rk + 8);
+    const bool rl = (w1 & 0xff) == PP_KLEN_LONG, sl = (sk[1] & 0xff) == PP_KLEN_LONG;
+    if (rl || sl) return rl && sl && pp_long_equal(S, batches, sk[2], gld<u64>(rk + 16));
+    if (sk[1] != w1) return false;
+    for (u32 w = 2; w < kw8; ++w)
+        if (sk[w] != gld<u64>(rk + 8 * w)) return false;
+    return true;
+}
+
+// find or claim the slot of record rk; -1 = no room in its probe window (overflow)
+__device__ __forceinline__ int pp_find(const Spec& S, const BatchDesc* batches, l64* slots, u32 cap, u32 sw, const u8* rk,
+                                       u64 pm) {
+    const u32 kw8 = S.pp_kw / 8;
+    const u64 tag = pm | 2;
+    u32 pos = (u32)(((u64)(u32)pm * cap) >> 32);
+    const u32 win = cap < PP_WINDOW ? cap : PP_WINDOW;
+    for (u32 n = 0; n < win; ++n) {
+        l64* e = slots + (size_t)pos * sw;
+        u64 t = lds_ld_acq(e);
+        if (t == 0) {
+            u64 old = 0;
+            __hip_atomic_compare_exchange_strong(e, &old, 1ULL, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old == 0) {  // claimed: key, initial states, then publish the tag
+                for (u32 w = 0; w < kw8; ++w) e[1 + w] = gld<u64>(rk + 8 * w);
+                for (int w = 1; w <= S.n_words; ++w) e[kw8 + w] = S.slot_init[w];
+                __hip_atomic_store(e, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return (int)pos;
+            }
+            t = old;
+        }
+        while (t == 1) t = lds_ld_acq(e);  // the claimer publishes in straight-line code
+        if (t == tag && pp_key_equal(S, batches, e + 1, rk)) return (int)pos;
+        pos = pos + 1 == cap ? 0 : pos + 1;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void pp_copy_rec(u8* dst, const u8* src, u32 rw) {
+    for (u32 w = 0; w < rw / 8; ++w) ((u64*)dst)[w] = gld<u64>(src + 8 * w);
+}
+
+// write one group (slot key part + states) as output row `row` (fixed-width keys only)
+__device__ __forceinline__ void pp_write_fixed_row(const Spec& S, const l64* e, u64 row, const OutDesc& out, u64* err) {
+    const u32 kw8 = S.pp_kw / 8;
+    const l8* k = (const l8*)(e + 1);
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        const u32 w = type_width(t.type);
+        const bool v = !t.nullable || k[S.voff[c]] != 0;
+        u64 lo = 0, hi = 0;
+        if (t.type == DBG_DECIMAL128) {
+            lo = lget(k, S.koff[c], 8);
+            hi = lget(k, S.koff[c] + 8, 8);
+        } else {
+            lo = lget(k, S.koff[c], w);
+        }
+        write_bytes(out.key_data[c], row, w, lo, hi);
+        if (out.key_valid[c]) out.key_valid[c][row] = v ? 1 : 0;
+    }
+    const u64* st = (const u64*)(e + kw8);
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        u64 lo, hi;
+        const bool v = agg_result(S, A, st, lo, hi, err);
+        write_bytes(out.agg_data[a], row, A.res_width, lo, hi);
+        if (out.agg_valid[a]) out.agg_valid[a][row] = v ? 1 : 0;
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                          u32 n_parts, const u64* __restrict__ raw_off, const u64* __restrict__ st_off,
+                                                          u8* raw, u8* raw_alt, u8* st, u8* st_alt, u32 cap, PPAggOut out) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    const Spec& S = *spec;
+    l64* slots = (l64*)lds_raw;
+    const u32 sw = S.pp_sw, kw8 = S.pp_kw / 8;
+    __shared__ u32 novf[2], wsum[PP_AGG_NT / 64];
+    __shared__ u64 gbase;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
+        u64 r0 = raw_off ? raw_off[p] : 0, nr = raw_off ? raw_off[p + 1] - r0 : 0;
+        u64 s0 = st_off ? st_off[p] : 0, ns = st_off ? st_off[p + 1] - s0 : 0;
+        u8 *rin = raw, *rout = raw_alt, *sin = st, *sout = st_alt;
+        for (int round = 0;; ++round) {
+            for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) slots[(size_t)s * sw] = 0;
+            if (threadIdx.x < 2) novf[threadIdx.x] = 0;
+            __syncthreads();
+            for (u64 i = threadIdx.x; i < nr; i += PP_AGG_NT) {
+                const u8* rk = rin + (r0 + i) * S.pp_rw_raw;
+                const u64 pm = pp_mix(pp_rec_hash(S, rk));
+                const int ls = pp_find(S, batches, slots, cap, sw, rk, pm);
+                if (ls >= 0) {
+                    pp_apply_raw<AS_LDS>(S, (wptr<AS_LDS>)(slots + (size_t)ls * sw + kw8), rk);
+                } else {
+                    const u32 q = atomicAdd(&novf[0], 1u);
+                    pp_copy_rec(rout + (r0 + q) * S.pp_rw_raw, rk, S.pp_rw_raw);
+                }
+            }
+            for (u64 i = threadIdx.x; i < ns; i += PP_AGG_NT) {
+                const u8* rk = sin + (s0 + i) * S.pp_rw_state;
+                const u64 pm = pp_mix(pp_rec_hash(S, rk));
+                const int ls = pp_find(S, batches, slots, cap, sw, rk, pm);
+                if (ls >= 0) {
+                    apply_state<AS_LDS, false, AS_GLB>(S, (wptr<AS_LDS>)(slots + (size_t)ls * sw + kw8),
+                                                       (const u64*)(rk + S.pp_kw) - 1);
+                } else {
+                    const u32 q = atomicAdd(&novf[1], 1u);
+                    pp_copy_rec(sout + (s0 + q) * S.pp_rw_state, rk, S.pp_rw_state);
+                }
+            }
+            __syncthreads();
+            // emit: slot order per round of PP_AGG_NT slots, positions by block scan
+            u32 total = 0;
+            for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) total += slots[(size_t)s * sw] >= 2 ? 1 : 0;
+            {
+                u32 x = total;
+                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+                if (lane == 0) wsum[wave] = x;
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    u32 t = 0;
+                    for (int w = 0; w < PP_AGG_NT / 64; ++w) t += wsum[w];
+                    gbase = t ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)t) : 0;
+                }
+                __syncthreads();
+            }
+            u64 run = gbase;
+            for (u32 s0r = 0; s0r < cap; s0r += PP_AGG_NT) {
+                const u32 s = s0r + threadIdx.x;
+                const bool occ = s < cap && slots[(size_t)s * sw] >= 2;
+                const u64 m = __ballot(occ);
+                if (lane == 0) wsum[wave] = (u32)__popcll(m);
+                __syncthreads();
+                u32 pre = 0, tot = 0;
+                for (int w = 0; w < PP_AGG_NT / 64; ++w) {
+                    if (w < wave) pre += wsum[w];
+                    tot += wsum[w];
+                }
+                __syncthreads();
+                if (occ) {
+                    const u64 row = run + pre + (u32)__popcll(m & ((1ULL << lane) - 1));
+                    const l64* e = slots + (size_t)s * sw;
+                    if (MODE == 0) {
+                        if (row < out.cols.cap_groups) pp_write_fixed_row(S, e, row, out.cols, out.tot + PPT_ERR);
+                    } else if (row < out.grec_cap) {
+                        u64* d = (u64*)(out.grec + row * S.pp_rw_state);
+                        for (u32 w = 0; w < kw8; ++w) d[w] = e[1 + w];
+                        for (int w = 0; w < S.n_words; ++w) d[kw8 + w] = e[1 + kw8 + w];
+                    }
+                }
+                run += tot;
+            }
+            const u32 o0 = novf[0], o1 = novf[1];
+            __syncthreads();
+            if (o0 == 0 && o1 == 0) break;
+            if (threadIdx.x == 0) atomicAdd((unsigned long long*)(out.tot + PPT_ROUNDS), 1ULL);
+            // the overflow, written to this partition's region of the alternate buffers, is the
+            // next round's input; the consumed input region takes the round after's overflow
+            u8* t0 = rin; rin = rout; rout = t0;
+            u8* t1 = sin; sin = sout; sout = t1;
+            nr = o0;
+            ns = o1;
+            __threadfence_block();
+            (void)round;
+        }
+    }
+}
+
+void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
+                   const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out) {
+    if (!n_parts) return;
+    const u32 cap = pp_agg_slots(hspec);
+    const size_t lds = (size_t)cap * hspec.pp_sw * 8;
+    const u32 grid = n_parts < 4096 ? n_parts : 4096;
+    if (mode == 0)
+        hipLaunchKernelGGL(pp_agg_kernel<0>, dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, st_off, raw, raw_alt, st,
+                           st_alt, cap, out);
+    else
+        hipLaunchKernelGGL(pp_agg_kernel<1>, dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, st_off, raw, raw_alt, st,
+                           st_alt, cap, out);
+}
+
+// ------------------------------------------------------------------------------------------
+// group records -> result columns: per block of PP_GB rows, string bytes per key column; the
+// host scans them; the write pass places rows at their index and strings at scanned offsets.
+// ------------------------------------------------------------------------------------------
+#define PP_GB 2048
+#define PP_GNT 256
+u64 pp_grec_blocks(u64 n) { return (n + PP_GB - 1) / PP_GB; }
+
+// length of string key column c of a group record's key part (global)
+__device__ __forceinline__ StrRef pp_key_str(const Spec& S, const BatchDesc* batches, const u8* k, int c, bool& valid) {
+    const u8 klen = gld<u8>(k + 8);
+    if (klen == PP_KLEN_LONG) {
+        const u64 ref = gld<u64>(k + 16);
+        const DCol& col = batches[ref_bid(ref)].keys[c];
+        valid = dcol_valid(col, ref_row(ref));
+        return valid ? dcol_str(col, ref_row(ref)) : StrRef{nullptr, 0};
+    }
+    u32 o = 9;
+    for (int j = 0; j < S.n_keys; ++j) {
+        bool v = true;
+        if (S.key_types[j].nullable) v = gld<u8>(k + o++) != 0;
+        if (S.key_types[j].type == DBG_STRING) {
+            const u32 n = gld<u8>(k + o++);
+            if (j == c) {
+                valid = v;
+                return StrRef{k + o, n};
+            }
+            o += n;
+        } else {
+            o += type_width(S.key_types[j].type);
+        }
+    }
+    valid = false;
+    return StrRef{nullptr, 0};
+}
+// fixed-width key column c of a blob key part (global): value bits
+__device__ __forceinline__ bool pp_key_fixed(const Spec& S, const BatchDesc* batches, const u8* k, int c, u64& lo, u64& hi) {
+    lo = hi = 0;
+    if (!S.pp_str) {
+        const dbg_datatype& t = S.key_types[c];
+        const bool v = !t.nullable || gld<u8>(k + S.voff[c]) != 0;
+        if (t.type == DBG_DECIMAL128) {
+            lo = ld_le(k + S.koff[c], 8);
+            hi = ld_le(k + S.koff[c] + 8, 8);
+        } else {
+            lo = ld_le(k + S.koff[c], type_width(t.type));
+        }
+        return v;
+    }
+    const u8 klen = gld<u8>(k + 8);
+    if (klen == PP_KLEN_LONG) {
+        const u64 ref = gld<u64>(k + 16);
+        const DCol& col = batches[ref_bid(ref)].keys[c];
+        const bool v = dcol_valid(col, ref_row(ref));
+        if (v) {
+            lo = dcol_bits(col, ref_row(ref));
+            if (col.type == DBG_DECIMAL128) hi = dcol_hi(col, ref_row(ref));
+            else if (col.type == DBG_FLOAT32 || col.type == DBG_FLOAT64) lo = canon_float_bits(col.type, lo);
+        }
+        return v;
+    }
+    u32 o = 9;
+    for (int j = 0; j < S.n_keys; ++j) {
+        bool v = true;
+        if (S.key_types[j].nullable) v = gld<u8>(k + o++) != 0;
+        const int ty = S.key_types[j].type;
+        if (ty == DBG_STRING) {
+            o += 1 + gld<u8>(k + o);
+            continue;
+        }
+        const u32 w = type_width(ty);
+        if (j == c) {
+            if (ty == DBG_DECIMAL128) {
+                lo = ld_le(k + o, 8);
+                hi = ld_le(k + o + 8, 8);
+            } else {
+                lo = ld_le(k + o, w);
+            }
+            return v;
+        }
+        o += w;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(PP_GNT) pp_grec_len_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                            const u8* __restrict__ grec, const u64* __restrict__ np, u64* __restrict__ blk_len, u64 nblocks) {
+    const Spec& S = *spec;
+    const u64 n = *np;
+    __shared__ unsigned long long acc[DBG_MAX_KEYS];
+    if (threadIdx.x < DBG_MAX_KEYS) acc[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 r0 = (u64)blockIdx.x * PP_GB;
+    for (u64 r = r0 + threadIdx.x; r < r0 + PP_GB && r < n; r += PP_GNT) {
+        const u8* k = grec + r * S.pp_rw_state;
+        for (int c = 0; c < S.n_keys; ++c)
+            if (S.key_types[c].type == DBG_STRING) {
+                bool v;
+                atomicAdd(&acc[c], (unsigned long long)pp_key_str(S, batches, k, c, v).len);
+            }
+    }
+    __syncthreads();
+    if (threadIdx.x < (u32)S.n_keys) blk_len[(u64)threadIdx.x * nblocks + blockIdx.x] = acc[threadIdx.x];
+}
+
+void launch_pp_grec_lengths(hipStream_t s, const Spec* dspec, const u8* grec, const u64* np, u64* blk_len, u64 nblocks,
+                            const BatchDesc* batches) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(pp_grec_len_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, np, blk_len, nblocks);
+}
+
+__global__ void __launch_bounds__(PP_GNT) pp_grec_write_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                              const u8* __restrict__ grec, const u64* __restrict__ np, const u64* __restrict__ str_pos,
+                                                              u64 nblocks, OutDesc out, u64* err) {
+    const Spec& S = *spec;
+    const u64 n = *np;
+    __shared__ u32 wtot[PP_GNT / 64];
+    u64 srun[DBG_MAX_KEYS];
+    for (int c = 0; c < S.n_keys; ++c) srun[c] = S.key_types[c].type == DBG_STRING ? str_pos[(u64)c * nblocks + blockIdx.x] : 0;
+    const u64 r0 = (u64)blockIdx.x * PP_GB;
+    for (u64 rb = r0; rb < r0 + PP_GB && rb < n; rb += PP_GNT) {  // uniform
+        const u64 r = rb + threadIdx.x;
+        const bool in = r < n && r < r0 + PP_GB;
+        const u8* k = grec + (in ? r : rb) * S.pp_rw_state;
+        for (int c = 0; c < S.n_keys; ++c) {
+            const dbg_datatype& t = S.key_types[c];
+            if (t.type == DBG_STRING) {
+                bool v = false;
+                StrRef sr = in ? pp_key_str(S, batches, k, c, v) : StrRef{nullptr, 0};
+                u32 tot;
+                const u32 pre = block_excl_scan((u32)sr.len, wtot, tot);
+                if (in && r < out.cap_groups) {
+                    const u64 pos = srun[c] + pre;
+                    out.key_offsets[c][r] = pos;
+                    if (pos + sr.len <= out.cap_str[c]) {
+                        u8* d = (u8*)out.key_data[c] + pos;
+                        for (u64 j = 0; j < sr.len; ++j) d[j] = gld<u8>(sr.p + j);
+                    }
+                    if (out.key_valid[c]) out.key_valid[c][r] = v ? 1 : 0;
+                }
+                srun[c] += tot;
+            } else if (in && r < out.cap_groups) {
+                u64 lo, hi;
+                const bool v = pp_key_fixed(S, batches, k, c, lo, hi);
+                write_bytes(out.key_data[c], r, type_width(t.type), lo, hi);
+                if (out.key_valid[c]) out.key_valid[c][r] = v ? 1 : 0;
+            }
+        }
+        if (in && r < out.cap_groups) {
+            const u64* st = (const u64*)(k + S.pp_kw) - 1;
+            for (int a = 0; a < S.n_aggs; ++a) {
+                const DAgg& A = S.aggs[a];
+                u64 lo, hi;
+                const bool v = agg_result(S, A, st, lo, hi, err);
+                write_bytes(out.agg_data[a], r, A.res_width, lo, hi);
+                if (out.agg_valid[a]) out.agg_valid[a][r] = v ? 1 : 0;
+            }
+        }
+    }
+}
+
+void launch_pp_grec_write(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, const u64* np, const u64* str_pos,
+                          u64 nblocks, const OutDesc& out, u64* err) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(pp_grec_write_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, np, str_pos, nblocks, out, err);
+}
+
+// ------------------------------------------------------------------------------------------
+// group records -> exchange records ([hash][validity][keys][state words], strings into
+// per-partition blobs) partitioned by hash % n (Payload::scatter) or radix bits [48 - r, 48)
+// (PartitionedPayload) — the same record format as the HBM table's export.
+// ------------------------------------------------------------------------------------------
+#define PP_MAX_PARTS 256
+__device__ __forceinline__ u32 pp_part_of(u64 h, u32 n_parts, int scheme) {
+    if (n_parts <= 1) return 0;
+    if (scheme == 0) return (u32)(h % n_parts);
+    const u32 rb = 31 - __clz(n_parts);
+    return (u32)((h >> (48 - rb)) & (n_parts - 1));
+}
+__device__ __forceinline__ u64 pp_grec_hash(const Spec& S, const u8* k) { return S.pp_str ? gld<u64>(k) : pp_fixed_hash(S, k); }
+
+__global__ void __launch_bounds__(PP_GNT) pp_grec_count_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                              const u8* __restrict__ grec, u64 n, u32 n_parts, int scheme,
+                                                              u64* __restrict__ hist, u64* __restrict__ str_hist, u64 nblocks) {
+    const Spec& S = *spec;
+    __shared__ unsigned long long lh[PP_MAX_PARTS];
+    __shared__ unsigned long long ls[DBG_MAX_KEYS][PP_MAX_PARTS];
+    for (u32 p = threadIdx.x; p < n_parts; p += PP_GNT) {
+        lh[p] = 0;
+        for (int c = 0; c < S.n_keys; ++c) ls[c][p] = 0;
+    }
+    __syncthreads();
+    const u64 r0 = (u64)blockIdx.x * PP_GB;
+    for (u64 r = r0 + threadIdx.x; r < r0 + PP_GB && r < n; r += PP_GNT) {
+        const u8* k = grec + r * S.pp_rw_state;
+        const u32 p = pp_part_of(pp_grec_hash(S, k), n_parts, scheme);
+        atomicAdd(&lh[p], 1ULL);
+        for (int c = 0; c < S.n_keys; ++c)
+            if (S.key_types[c].type == DBG_STRING) {
+                bool v;
+                atomicAdd(&ls[c][p], (unsigned long long)pp_key_str(S, batches, k, c, v).len);
+            }
+    }
+    __syncthreads();
+    for (u32 p = threadIdx.x; p < n_parts; p += PP_GNT) {
+        hist[(u64)p * nblocks + blockIdx.x] = lh[p];
+        for (int c = 0; c < S.n_keys; ++c) str_hist[((u64)p * S.n_keys + c) * nblocks + blockIdx.x] = ls[c][p];
+    }
+}
+
+void launch_pp_grec_count_parts(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n, u32 n_parts,
+                                int scheme, u64* hist, u64* str_hist, u64 nblocks) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(pp_grec_count_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, hist,
+                       str_hist, nblocks);
+}
+
+__global__ void __launch_bounds__(PP_GNT) pp_grec_export_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                               const u8* __restrict__ grec, u64 n, u32 n_parts, int scheme,
+                                                               const u64* __restrict__ pos, const u64* __restrict__ str_pos,
+                                                               u64 nblocks, u8* rec_out, u8* str_out,
+                                                               const u64* __restrict__ part_str_base) {
+    const Spec& S = *spec;
+    __shared__ unsigned long long cur[PP_MAX_PARTS];
+    __shared__ unsigned long long scur[DBG_MAX_KEYS][PP_MAX_PARTS];
+    for (u32 p = threadIdx.x; p < n_parts; p += PP_GNT) {
+        cur[p] = pos[(u64)p * nblocks + blockIdx.x];
+        for (int c = 0; c < S.n_keys; ++c) scur[c][p] = str_pos[((u64)p * S.n_keys + c) * nblocks + blockIdx.x];
+    }
+    __syncthreads();
+    const u64 r0 = (u64)blockIdx.x * PP_GB;
+    for (u64 r = r0 + threadIdx.x; r < r0 + PP_GB && r < n; r += PP_GNT) {
+        const u8* k = grec + r * S.pp_rw_state;
+        const u64 h = pp_grec_hash(S, k);
+        const u32 p = pp_part_of(h, n_parts, scheme);
+        const u64 ri = atomicAdd(&cur[p], 1ULL);
+        u8* rec = rec_out + ri * S.rec_width;
+        *(u64*)rec = h;
+        for (int c = 0; c < S.n_keys; ++c) {
+            const dbg_datatype& t = S.key_types[c];
+            u8* kd = rec + S.rec_key_off[c];
+            if (t.type == DBG_STRING) {
+                bool v = false;
+                StrRef sr = pp_key_str(S, batches, k, c, v);
+                if (t.nullable) rec[S.rec_val_off[c]] = v ? 1 : 0;
+                const u64 o = atomicAdd(&scur[c][p], (unsigned long long)sr.len);
+                for (u64 j = 0; j < sr.len; ++j) str_out[o + j] = gld<u8>(sr.p + j);
+                ((u64*)kd)[0] = o - part_str_base[p];
+                ((u64*)kd)[1] = sr.len;
+            } else {
+                u64 lo, hi;
+                const bool v = pp_key_fixed(S, batches, k, c, lo, hi);
+                if (t.nullable) rec[S.rec_val_off[c]] = v ? 1 : 0;
+                const u32 w = type_width(t.type);
+                for (u32 j = 0; j < w && j < 8; ++j) kd[j] = (u8)(lo >> (8 * j));
+                for (u32 j = 8; j < w; ++j) kd[j] = (u8)(hi >> (8 * (j - 8)));
+            }
+        }
+        u64* sw = (u64*)(rec + S.rec_state_off);
+        const u64* st = (const u64*)(k + S.pp_kw);
+        for (int w = 0; w < S.n_words; ++w) sw[w] = st[w];
+    }
+}
+
+void launch_pp_grec_export(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n, u32 n_parts,
+                           int scheme, const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out, u8* str_out,
+                           const u64* part_str_base) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(pp_grec_export_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, pos,
+                       str_pos, nblocks, rec_out, str_out, part_str_base);
+}

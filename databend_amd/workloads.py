@@ -182,7 +182,7 @@ class ConfigRunner:
     256 MiB Infinity Cache) and one reusable GPU table for config cfg."""
 
     def __init__(self, cfg: int, rows: int, copies: int = 1, capacity_hint: int = 0, seed: Optional[int] = None,
-                 start: int = 0):
+                 start: int = 0, strategy: int = abi.STRATEGY_AUTO):
         torch = _torch()
         self.cfg, self.rows = cfg, rows
         self.shape = SHAPES[cfg]
@@ -193,6 +193,7 @@ class ConfigRunner:
         self.result_types = [f.return_type() for f in self.params.aggregate_functions]
         self._capacity_hint = capacity_hint
         self.table = AggregateHashTable(self.params, HashTableConfig(True, capacity_hint))
+        self.table.set_strategy(strategy)
         # one table per batch stream: a small table is re-initialised by the fused finalize
         check(lib().dbg_agg_set_recycle(self.table.h, 1))
         self.programs = []
@@ -374,9 +375,10 @@ def _dev_to_host(c: DeviceColumn, n: int) -> Column:
     return Column(t, data, offs, val)
 
 
-def run_config(cfg: int, rows: int, steps: int = 1, copies: int = 1, capacity_hint: int = 0) -> dict:
+def run_config(cfg: int, rows: int, steps: int = 1, copies: int = 1, capacity_hint: int = 0,
+               strategy: int = abi.STRATEGY_AUTO) -> dict:
     torch = _torch()
-    r = ConfigRunner(cfg, rows, copies=copies, capacity_hint=capacity_hint)
+    r = ConfigRunner(cfg, rows, copies=copies, capacity_hint=capacity_hint, strategy=strategy)
     try:
         times = []
         for k in range(steps):
@@ -386,6 +388,7 @@ def run_config(cfg: int, rows: int, steps: int = 1, copies: int = 1, capacity_hi
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
         keys, aggs = r.results_host()
-        return dict(keys=keys, aggs=aggs, n_groups=r.n_groups, times=times)
+        part, rounds = r.table.strategy()
+        return dict(keys=keys, aggs=aggs, n_groups=r.n_groups, times=times, partitioned=part, extra_rounds=rounds)
     finally:
         r.close()

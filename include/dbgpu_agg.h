@@ -223,6 +223,25 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
  * so a processor that reuses one handle per batch stream loses nothing. */
 int dbg_agg_set_recycle(dbg_agg_handle* h, int on);
 
+/* Aggregation strategy of a handle (set after create or reset, before any batch):
+ *   DBG_STRATEGY_AUTO        — the first large batch (>= 4M rows) into an empty handle is probed
+ *                              (distinct group hashes of 2^20 sampled rows); an estimated > 1M groups
+ *                              selects the partitioned payload, otherwise the HBM table.  The
+ *                              reference adapts the same way at run time (clear_ht / radix
+ *                              repartition of a partial table, EAGG/aggregate_hashtable.rs:225-239,
+ *                              453-503).
+ *   DBG_STRATEGY_TABLE       — always the HBM hash table with LDS staging (low / mid cardinality).
+ *   DBG_STRATEGY_PARTITIONED — always the radix-partitioned payload (PartitionedPayload,
+ *                              EAGG/partitioned_payload.rs:100-143): batches are scattered into
+ *                              hash partitions, finalize aggregates each partition in LDS.
+ * In partitioned mode a capacity_hint (dbg_agg_params) is the expected group count that sizes the
+ * final partitions; dbg_agg_export_fixed / dbg_agg_merge_fixed return DBG_ERR_UNSUPPORTED. */
+enum { DBG_STRATEGY_AUTO = 0, DBG_STRATEGY_TABLE = 1, DBG_STRATEGY_PARTITIONED = 2 };
+int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy);
+/* *partitioned = the handle's current mode; *extra_rounds (may be NULL) = partitions of the last
+ * partitioned finalize whose groups needed more than one LDS round. */
+int dbg_agg_get_strategy(dbg_agg_handle* h, int* partitioned, uint64_t* extra_rounds);
+
 /* ---- partial-state records: exchange / partition bucket (EAGG/payload.rs:356-391,
  *      EAGG/partitioned_payload.rs:100-143, AGG/aggregate_exchange_injector.rs:154-235) ----
  * A record = [hash u64][group keys, fixed part][state words]; string keys are (u64 offset, u64 len)

@@ -29,11 +29,13 @@ def _torch():
     return torch
 
 
-def gpu_aggregate(keys, aggs, filt=None, on_device=False, capacity_hint=0, batches=1):
-    """aggs: list of (name, Column|None).  filt: (pred, [Columns]) or None."""
+def gpu_aggregate(keys, aggs, filt=None, on_device=False, capacity_hint=0, batches=1, strategy=abi.STRATEGY_AUTO, info=None):
+    """aggs: list of (name, Column|None).  filt: (pred, [Columns]) or None.  info (dict, optional)
+    receives the handle's strategy after the run."""
     fns = [F.get(n, [], [c.dtype] if c is not None else []) for n, c in aggs]
     params = AggregatorParams([k.dtype for k in keys], fns)
     ht = AggregateHashTable(params, HashTableConfig(True, capacity_hint))
+    ht.set_strategy(strategy)
     try:
         n = len(keys[0])
         bounds = np.linspace(0, n, batches + 1).astype(int)
@@ -55,6 +57,8 @@ def gpu_aggregate(keys, aggs, filt=None, on_device=False, capacity_hint=0, batch
                 fp = FilterProgram(filt[0], [c.to_abi() for c in fcols])
             ht.add_groups(ks, ars, rows=hi - lo, filter_program=fp, on_device=on_device)
         block = ht.merge_result()
+        if info is not None:
+            info["partitioned"], info["extra_rounds"] = ht.strategy()
     finally:
         ht.close()
     na = len(aggs)
