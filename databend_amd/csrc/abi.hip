@@ -414,7 +414,7 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     if (!vbits) S.pp_avoff = S.pp_rw_raw;
     S.pp_rw_state = S.pp_kw + 8 * (u32)S.n_words;
     S.pp_sw = 1 + S.pp_kw / 8 + (u32)S.n_words;
-    S.pp_ok = S.pp_rw_raw <= 256 && S.pp_rw_state <= 512 && vbits <= 64 && S.pp_sw <= 64;
+    S.pp_ok = S.pp_rw_raw <= 256 && S.pp_rw_state <= 256 && vbits <= 64 && S.pp_sw <= 64;
     return DBG_OK;
 }
 

@@ -208,7 +208,7 @@ __device__ __forceinline__ void pp_apply_raw(const Spec& S, wptr<AS> st, const u
             }
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 const bool mn = A.kind == DBG_AGG_MIN;
-                const u64 b = ld_le(p, aw);
+                const u64 b = ld_le(p, aw < 8 ? aw : 8);  // Decimal128 (p <= 18): the low word
                 if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
                 else if (A.mmk == MMK_U64) at_minmax<AS>(w, b, mn, false);
                 else
@@ -392,7 +392,7 @@ struct PPStageLayout {
 __host__ __device__ __forceinline__ u32 pp_al16(u32 x) { return (x + 15) & ~15u; }
 __host__ __device__ __forceinline__ PPStageLayout pp_stage_layout(u32 rw, u32 K) {
     PPStageLayout L;
-    L.cap = PP_STAGE_BYTES / rw;
+    L.cap = PP_STAGE_BYTES / rw;  // >= 128 for records up to 256 bytes
     if (L.cap > 4096) L.cap = 4096;
     L.bkt = pp_al16(L.cap * rw);
     L.rank = pp_al16(L.bkt + 2 * L.cap);
@@ -486,9 +486,11 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restric
     const u64 end = ch.start + ch.n;
     const BatchDesc& B = batches[ch.bid];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (u64 base = ch.start; base < end; base += PP_NT) {
+    // rows staged per fill step: at most half the stage (wide records hold fewer than PP_NT)
+    const u32 T = cap >= 2 * PP_NT ? PP_NT : ((cap / 2) & ~63u);
+    for (u64 base = ch.start; base < end; base += T) {
         const u64 i = base + threadIdx.x;
-        bool sel = i < end;
+        bool sel = threadIdx.x < T && i < end;
         if (SRC == 0 && sel && !B.is_records && B.n_nodes) sel = eval_pred(B.nodes, B.n_nodes, B.fcols, i);
         const u64 m = __ballot(sel);
         if (lane == 0) wcnt[wave] = (u32)__popcll(m);
@@ -515,7 +517,7 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restric
             }
         }
         __syncthreads();
-        if (qn + PP_NT > cap) flush();
+        if (qn + T > cap) flush();
     }
     if (qn) flush();
 }
