@@ -41,6 +41,11 @@ def parse():
     p.add_argument("--cpu-sample-rows", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capacity-hint", type=int, default=0)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher plumbing only: every rank joins a gloo group, rank 0 prints n_gpus (no GPU work)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                   help="weak: every GPU aggregates the config's rows; strong: the config's rows are split over "
+                        "the GPUs (default: strong for the 1B-row configs 3-5, weak for 1-2)")
     return p.parse_args()
 
 
@@ -79,10 +84,44 @@ def cpu_baseline(cfg, sample_rows, gpu_check=None):
                 seconds_per_run=med), result, cols
 
 
+def spawn_ranks(args) -> int:
+    """`--gpus N` without a launcher: start `torch.distributed.run` with N ranks (one per GPU) as a
+    child process before this process touches the GPU (never exec), relay its output (rank 0 prints
+    the JSON line) and return its exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
+
+    if args.dry_run:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        if world > 1:
+            dist.init_process_group("gloo")
+            seen = torch.tensor([1])
+            dist.all_reduce(seen)
+            world_seen = int(seen.item())
+            dist.destroy_process_group()
+        else:
+            world_seen = 1
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world_seen, "gpus_requested": args.gpus}), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -100,7 +139,10 @@ def main():
     from databend_amd.workloads import DEFAULT_ROWS, SHAPES, ConfigRunner, algorithmic_bytes
 
     cfg = args.config
-    rows = args.rows or DEFAULT_ROWS[cfg]
+    scaling = args.scaling or ("strong" if cfg in (3, 4, 5) else "weak")
+    total_rows = args.rows or DEFAULT_ROWS[cfg]
+    # strong scaling: the config's rows split over the ranks; weak: every rank its own full batch
+    rows = total_rows // world if scaling == "strong" else total_rows
     shape = SHAPES[cfg]
     in_bytes_per_row = {1: 100, 2: 2, 3: 8, 4: 16, 5: 27}[cfg]
     copies = args.copies or max(1, min(4, -(-768 * 2**20 // max(1, rows * in_bytes_per_row))))
@@ -109,6 +151,8 @@ def main():
     # rank r aggregates its own disjoint rows of the synthetic table (weak scaling)
     # every rank aggregates disjoint row ranges of the same generator
     runner = ConfigRunner(cfg, rows, copies=copies, capacity_hint=args.capacity_hint, start=rank * copies * rows)
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     final = None
     small = False
     if world > 1:
@@ -187,8 +231,18 @@ def main():
     ffi.prof_enable(False)
     prof = ffi.prof_read()
 
-    # dominant kernel = the fused filter + GROUP BY insert
-    ins_ms, ins_n = prof.get("agg_insert", (0.0, 0))
+    # dominant kernel: the fused filter + GROUP BY insert (HBM-table strategy), or — radix-
+    # partitioned strategy (pp.hip, high cardinality) — the whole step's level passes + LDS
+    # aggregation, whose launches together touch the §8d bytes once
+    partitioned = runner.table.strategy()[0]
+    if partitioned:
+        pp_names = [k for k in prof if k.startswith("pp_") and k != "pp_probe"]
+        ins_ms = sum(prof[k][0] for k in pp_names)
+        ins_n = args.steps
+        kernel_name = "+".join(sorted(pp_names)) + " (one step)"
+    else:
+        ins_ms, ins_n = prof.get("agg_insert", (0.0, 0))
+        kernel_name = "agg_insert"
     avg_ms = ins_ms / max(1, ins_n)
     # algorithmic bytes of one insert launch
     if world == 1:
@@ -213,8 +267,7 @@ def main():
     alg_bytes = algorithmic_bytes(cfg, runner.inputs[0], rows, sel, n_groups, runner.result_types, kstr)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
 
-    total_rows = rows * world * args.steps
-    value = total_rows / elapsed
+    value = rows * world * args.steps / elapsed
     out = {
         "metric": "input rows/sec aggregated (filter + hash GROUP BY), % HBM roofline",
         "value": value,
@@ -224,15 +277,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int16 key / u64 count" if cfg == 2 else "int64/decimal128/u64",
         "data": "synthetic (device-generated, seeded splitmix64; SURVEY.md §8d)",
-        "config": {"workload": shape.name, "query": shape.sql, "rows_per_gpu": rows, "input_copies": copies,
-                   "groups": n_groups, "selected_rows": sel, "parallelism": f"dp{world}" if world > 1 else "single"},
+        "config": {"workload": shape.name + ("" if scaling == "weak" or world == 1 else f"_strong_{total_rows}_rows"),
+                   "query": shape.sql, "rows_per_gpu": rows, "input_copies": copies,
+                   "groups": n_groups, "selected_rows": sel, "parallelism": f"dp{world}" if world > 1 else "single",
+                   "strategy": "partitioned" if partitioned else "hbm_table"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "agg_insert", "kernel_avg_ms": avg_ms, "kernel_launches": ins_n,
+                     "kernel": kernel_name, "kernel_avg_ms": avg_ms, "kernel_launches": ins_n,
                      "algorithmic_bytes_per_launch": alg_bytes},
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
     }

@@ -68,7 +68,13 @@ class dbg_agg_params(C.Structure):
                 ("partial", C.c_int32), ("capacity_hint", C.c_uint64)]
 
 
+class dbg_record_layout(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("state_off", C.c_uint32), ("key_off", C.c_uint32 * 8),
+                ("validity_off", C.c_uint32 * 8), ("agg_w0", C.c_int32 * 32), ("agg_words", C.c_int32 * 32),
+                ("flags_word", C.c_int32), ("n_words", C.c_int32)]
+
+
 EXPECTED_SIZES = {
     "dbg_datatype": 8, "dbg_column": 56, "dbg_out_column": 32, "dbg_agg_spec": 16,
-    "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 48,
+    "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 48, "dbg_record_layout": 328,
 }

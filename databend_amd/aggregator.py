@@ -42,6 +42,14 @@ class AggregatorParams:
                                1 if partial else 0, capacity_hint)
         return p, (gt, ag)
 
+    def record_layout(self) -> "abi.dbg_record_layout":
+        """The exchange-record layout of a table with these params (dbg_agg_record_layout), computed on
+        the host: no device needed."""
+        p, keep = self.to_abi(True, 0, -1)
+        out = abi.dbg_record_layout()
+        check(lib().dbg_agg_record_layout(C.byref(p), C.byref(out)))
+        return out
+
     def empty_result_block(self) -> DataBlock:
         """AggregatorParams::empty_result_block (:103-115): [agg results..., group cols...]."""
         cols = []

@@ -1004,7 +1004,7 @@ static int pp_add_batch(dbg_agg_handle* h, u32 bid, u64 rows, int kind) {
     if (K.l1_n + total > K.l1_cap) {  // grow (x2), keeping the records already appended
         const u64 ncap = std::max<u64>(K.l1_n + total, K.l1_n ? 2 * K.l1_cap : 0);
         u8* nb = nullptr;
-        RETURN_IF(dev_alloc((void**)&nb, ncap * rw));
+        RETURN_IF(dev_alloc((void**)&nb, ncap * rw + 64));  // slack: the aggregation reads whole words
         if (K.l1) {
             if (K.l1_n) HIPCHECK(hipMemcpyAsync(nb, K.l1, K.l1_n * rw, hipMemcpyDeviceToDevice, h->stream));
             HIPCHECK(hipStreamSynchronize(h->stream));
@@ -1029,10 +1029,13 @@ static int pp_prepare(dbg_agg_handle* h) {
     // estimated groups: the capacity hint when the caller gave one, else the probe's ratio
     const double est = h->hint_groups ? (double)h->hint_groups : h->pp_ratio * (double)nr + (double)nsr;
     const double g = std::min((double)(nr + nsr), est);
-    const double target = std::max(64.0, 0.5 * (double)pp_agg_slots(S));
+    const double target = std::max(64.0, 0.6 * (double)pp_agg_slots(S));
     const double need = std::max(1.0, std::ceil(g / target));
     u32 B = PP_L1_BITS + 1;
     while ((double)(1ULL << B) < need && B < PP_L1_BITS + 16) ++B;
+    // a level of one bit costs a full pass to halve partitions that still have headroom
+    // (the target is 60 % of the table): keep them, the next level starts at two bits
+    if (B == 2 * PP_L1_BITS + 1) B = 2 * PP_L1_BITS;
     const u32 k2 = std::min<u32>(8, B - PP_L1_BITS), k3 = B - PP_L1_BITS - k2;
     h->pp_bits = B;
     for (int kind = 0; kind < 2; ++kind) {
@@ -1044,8 +1047,8 @@ static int pp_prepare(dbg_agg_handle* h) {
             if (K.b) HIPCHECK(hipFree(K.b));
             K.a = K.b = nullptr;
             K.ab_cap = 0;
-            RETURN_IF(dev_alloc((void**)&K.a, K.l1_n * rw));
-            RETURN_IF(dev_alloc((void**)&K.b, K.l1_n * rw));
+            RETURN_IF(dev_alloc((void**)&K.a, K.l1_n * rw + 64));
+            RETURN_IF(dev_alloc((void**)&K.b, K.l1_n * rw + 64));
             K.ab_cap = K.l1_n;
         }
         RETURN_IF(ensure_dev(&K.part, &K.part_cap, (1ULL << B) + 1));
@@ -1670,6 +1673,27 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
 int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width) {
     if (!h || !width) return fail(DBG_ERR_INVALID, "null argument");
     *width = h->spec.rec_width;
+    return DBG_OK;
+}
+
+int dbg_agg_record_layout(const dbg_agg_params* params, dbg_record_layout* out) {
+    if (!params || !out) return fail(DBG_ERR_INVALID, "null argument");
+    Spec S;
+    std::vector<dbg_datatype> rt;
+    RETURN_IF(build_spec(params, S, rt));
+    memset(out, 0, sizeof(*out));
+    out->width = S.rec_width;
+    out->state_off = S.rec_state_off;
+    for (int c = 0; c < S.n_keys; ++c) {
+        out->key_off[c] = S.rec_key_off[c];
+        out->validity_off[c] = S.key_types[c].nullable ? S.rec_val_off[c] : 0;
+    }
+    for (int a = 0; a < S.n_aggs; ++a) {
+        out->agg_w0[a] = S.aggs[a].w0;
+        out->agg_words[a] = S.aggs[a].nwords;
+    }
+    out->flags_word = S.flags_word;
+    out->n_words = S.n_words;
     return DBG_OK;
 }
 

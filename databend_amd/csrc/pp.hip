@@ -21,9 +21,10 @@
 #include "agg_dev.hpp"
 
 #define PP_NT 512
-#define PP_AGG_NT 1024
-#define PP_AGG_LDS (144 * 1024)
-#define PP_STAGE_BYTES (32 * 1024)
+#define PP_AGG_NT 512
+#define PP_AGG_LDS (72 * 1024)  // two workgroups per CU
+#define PP_AU 4                  // raw records per thread in flight (aggregation)
+#define PP_STAGE_BYTES (48 * 1024)
 #define PP_MAXK 1024
 #define PP_WINDOW 96
 
@@ -270,6 +271,7 @@ void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches
 // ------------------------------------------------------------------------------------------
 // count: per work unit, a histogram of the level's local bucket over its (selected) rows/records
 // ------------------------------------------------------------------------------------------
+#define PP_CU 8  // rows / records per thread in flight (count)
 template <int SRC>
 __global__ void __launch_bounds__(PP_NT) pp_count_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                         int kind, const u8* __restrict__ recs, const PPChunk* __restrict__ chunks,
@@ -281,19 +283,25 @@ __global__ void __launch_bounds__(PP_NT) pp_count_kernel(const Spec* __restrict_
     __syncthreads();
     const PPChunk ch = chunks[blockIdx.x];
     const u64 end = ch.start + ch.n;
-    if (SRC == 0) {
-        const BatchDesc& B = batches[ch.bid];
-        for (u64 i = ch.start + threadIdx.x; i < end; i += PP_NT) {
-            if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
-            const u64 pm = pp_mix(pp_row_hash(S, B, i));
-            atomicAdd(&hist[(u32)(pm >> shift) & (K - 1)], 1u);
+    const BatchDesc& B = batches[ch.bid];
+    const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
+    for (u64 i0 = ch.start + threadIdx.x; i0 < end; i0 += (u64)PP_NT * PP_CU) {
+        u32 bk[PP_CU];
+#pragma unroll
+        for (int u = 0; u < PP_CU; ++u) {  // hashes of PP_CU rows, loads independent of each other
+            const u64 i = i0 + (u64)u * PP_NT;
+            bk[u] = ~0u;
+            if (i >= end) continue;
+            if (SRC == 0) {
+                if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+                bk[u] = (u32)(pp_mix(pp_row_hash(S, B, i)) >> shift) & (K - 1);
+            } else {
+                bk[u] = (u32)(pp_mix(pp_rec_hash(S, recs + i * rw)) >> shift) & (K - 1);
+            }
         }
-    } else {
-        const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
-        for (u64 i = ch.start + threadIdx.x; i < end; i += PP_NT) {
-            const u64 pm = pp_mix(pp_rec_hash(S, recs + i * rw));
-            atomicAdd(&hist[(u32)(pm >> shift) & (K - 1)], 1u);
-        }
+#pragma unroll
+        for (int u = 0; u < PP_CU; ++u)
+            if (bk[u] != ~0u) atomicAdd(&hist[bk[u]], 1u);
     }
     __syncthreads();
     for (u32 b = threadIdx.x; b < K; b += PP_NT) cnt[(u64)blockIdx.x * K + b] = hist[b];
@@ -443,7 +451,7 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restric
     l32* hist = (l32*)(stage + LY.hist);
     l32* scn = (l32*)(stage + LY.scn);
     l64* run = (l64*)(stage + LY.run);
-    __shared__ u32 wtot[PP_NT / 64], wcnt[PP_NT / 64];
+    __shared__ u32 wtot[PP_NT / 64];
 
     const PPChunk ch = chunks[blockIdx.x];
     for (u32 b = threadIdx.x; b < K; b += PP_NT) run[b] = off[(u64)blockIdx.x * K + b];
@@ -470,8 +478,9 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restric
         for (u32 q = threadIdx.x; q < n; q += PP_NT) sidx[scn[bkt[q]] + rank[q]] = (u16)q;
         __syncthreads();
         const u32 nw = n * wpr;
+        const u64 rcp = ((1ULL << 32) + wpr - 1) / wpr;  // exact for j < 2^32 / wpr^2 (j < 2^17 here)
         for (u32 j = threadIdx.x; j < nw; j += PP_NT) {
-            const u32 t = j / wpr, w = j - t * wpr;
+            const u32 t = (u32)(((u64)j * rcp) >> 32), w = j - t * wpr;
             const u32 q = sidx[t];
             const u32 b = bkt[q];
             const u64 di = run[b] + (t - scn[b]);
@@ -485,24 +494,32 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restric
 
     const u64 end = ch.start + ch.n;
     const BatchDesc& B = batches[ch.bid];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // rows staged per fill step: at most half the stage (wide records hold fewer than PP_NT)
+    // rows per fill step: U per thread (all threads) while that is at most half the stage; wide
+    // records: one row on each of the first T threads
+    const u32 U = cap >= 8 * PP_NT ? 4 : (cap >= 4 * PP_NT ? 2 : 1);
     const u32 T = cap >= 2 * PP_NT ? PP_NT : ((cap / 2) & ~63u);
-    for (u64 base = ch.start; base < end; base += T) {
-        const u64 i = base + threadIdx.x;
-        bool sel = threadIdx.x < T && i < end;
-        if (SRC == 0 && sel && !B.is_records && B.n_nodes) sel = eval_pred(B.nodes, B.n_nodes, B.fcols, i);
-        const u64 m = __ballot(sel);
-        if (lane == 0) wcnt[wave] = (u32)__popcll(m);
-        __syncthreads();
-        u32 wb = qn, tot = 0;
-        for (int w = 0; w < PP_NT / 64; ++w) {
-            if (w < wave) wb += wcnt[w];
-            tot += wcnt[w];
+    const u32 step = T * U;
+    for (u64 base = ch.start; base < end; base += step) {
+        u32 m = 0;
+        u16 bk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // selection (and, for records, the bucket) of my rows
+            bk[u] = 0;
+            const u64 i = base + (u64)u * T + threadIdx.x;
+            if ((u32)u >= U || threadIdx.x >= T || i >= end) continue;
+            if (SRC == 0) {
+                if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
+            } else {
+                bk[u] = (u16)((u32)(pp_mix(pp_rec_hash(S, recs + i * rw)) >> shift) & (K - 1));
+            }
+            m |= 1u << u;
         }
-        qn += tot;
-        if (sel) {
-            const u32 q = wb + (u32)__popcll(m & ((1ULL << lane) - 1));
+        u32 tot;
+        u32 q = qn + block_excl_scan((u32)__popc(m), wtot, tot);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!((m >> u) & 1)) continue;
+            const u64 i = base + (u64)u * T + threadIdx.x;
             l8* d = stage + (size_t)q * rw;
             if (SRC == 0) {
                 for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = 0;
@@ -513,11 +530,13 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restric
             } else {
                 const u8* r = recs + i * rw;
                 for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = gld<u64>(r + 8 * w);
-                bkt[q] = (u16)((u32)(pp_mix(pp_rec_hash(S, r)) >> shift) & (K - 1));
+                bkt[q] = bk[u];
             }
+            ++q;
         }
+        qn += tot;
         __syncthreads();
-        if (qn + T > cap) flush();
+        if (qn + step > cap) flush();
     }
     if (qn) flush();
 }
@@ -543,7 +562,7 @@ void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, cons
 // only ever fill — into the partition's region of the alternate buffer, aggregated in a further
 // round once this round's groups are written.
 // ------------------------------------------------------------------------------------------
-u32 pp_agg_slots(const Spec& S) { return (u32)((PP_AGG_LDS - 256) / (8 * S.pp_sw)); }
+u32 pp_agg_slots(const Spec& S) { return (u32)((PP_AGG_LDS - 256) / (8 * S.pp_sw + 2)); }
 
 __device__ __forceinline__ u64 lds_ld_acq(l64* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
@@ -555,27 +574,72 @@ __device__ __forceinline__ bool pp_long_equal(const Spec& S, const BatchDesc* ba
     return true;
 }
 
-// key part of a record (global) == key part of a slot (LDS)
-__device__ __forceinline__ bool pp_key_equal(const Spec& S, const BatchDesc* batches, const l64* sk, const u8* rk) {
+// A record as the aggregation reads it: W words held in registers (raw records of up to 64 bytes,
+// loaded PP_AU per thread before any LDS work so the loads overlap), or read from global memory
+// (wide raw records, state records).  word(w) / le(off, bytes) give little-endian fields.
+template <int W>
+struct RegRec {
+    u64 r[W];
+    __device__ __forceinline__ u64 word(u32 w) const {
+        u64 v = r[0];
+#pragma unroll
+        for (int k = 1; k < W; ++k)
+            if (w == (u32)k) v = r[k];
+        return v;
+    }
+    __device__ __forceinline__ u64 le(u32 off, u32 nb) const {
+        const u32 wi = off >> 3, sh = (off & 7) * 8;
+        u64 v = word(wi) >> sh;
+        if (sh && (off & 7) + nb > 8) v |= word(wi + 1) << (64 - sh);
+        return v & width_mask(nb);
+    }
+};
+struct GlbRec {
+    const u8* p;
+    __device__ __forceinline__ u64 word(u32 w) const { return gld<u64>(p + 8 * w); }
+    __device__ __forceinline__ u64 le(u32 off, u32 nb) const { return ld_le(p + off, nb); }
+};
+
+template <typename R>
+__device__ __forceinline__ u64 pp_hash_of(const Spec& S, const R& rk) {
+    if (S.pp_str) return rk.word(0);
+    u64 h = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        u64 x;
+        const bool v = !t.nullable || rk.le(S.voff[c], 1) != 0;
+        if (!v) x = NULL_HASH_VAL;
+        else if (t.type == DBG_DECIMAL128) x = hash_i128(rk.le(S.koff[c], 8), rk.le(S.koff[c] + 8, 8));
+        else x = hash_bits(t.type, rk.le(S.koff[c], type_width(t.type)));
+        h = c == 0 ? x : (h * NULL_HASH_VAL) ^ x;
+    }
+    return h;
+}
+
+// key part of a record == key part of a slot (LDS)
+template <typename R>
+__device__ __forceinline__ bool pp_key_eq(const Spec& S, const BatchDesc* batches, const l64* sk, const R& rk) {
     const u32 kw8 = S.pp_kw / 8;
     if (!S.pp_str) {
         for (u32 w = 0; w < kw8; ++w)
-            if (sk[w] != gld<u64>(rk + 8 * w)) return false;
+            if (sk[w] != rk.word(w)) return false;
         return true;
     }
-    if (sk[0] != gld<u64>(rk)) return false;  // group hash
-    const u64 w1 = gld<u64>(rk + 8);
+    if (sk[0] != rk.word(0)) return false;  // group hash
+    const u64 w1 = rk.word(1);
     const bool rl = (w1 & 0xff) == PP_KLEN_LONG, sl = (sk[1] & 0xff) == PP_KLEN_LONG;
-    if (rl || sl) return rl && sl && pp_long_equal(S, batches, sk[2], gld<u64>(rk + 16));
+    if (rl || sl) return rl && sl && pp_long_equal(S, batches, sk[2], rk.word(2));
     if (sk[1] != w1) return false;
     for (u32 w = 2; w < kw8; ++w)
-        if (sk[w] != gld<u64>(rk + 8 * w)) return false;
+        if (sk[w] != rk.word(w)) return false;
     return true;
 }
 
-// find or claim the slot of record rk; -1 = no room in its probe window (overflow)
-__device__ __forceinline__ int pp_find(const Spec& S, const BatchDesc* batches, l64* slots, u32 cap, u32 sw, const u8* rk,
-                                       u64 pm) {
+// find or claim the slot of a record; -1 = no room in its probe window (overflow).  A claimed
+// slot is appended to the partition's group list.
+template <typename R>
+__device__ __forceinline__ int pp_find(const Spec& S, const BatchDesc* batches, l64* slots, u32 cap, u32 sw, const R& rk, u64 pm,
+                                       l16* list, u32* nlist) {
     const u32 kw8 = S.pp_kw / 8;
     const u64 tag = pm | 2;
     u32 pos = (u32)(((u64)(u32)pm * cap) >> 32);
@@ -587,22 +651,59 @@ __device__ __forceinline__ int pp_find(const Spec& S, const BatchDesc* batches, 
             u64 old = 0;
             __hip_atomic_compare_exchange_strong(e, &old, 1ULL, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == 0) {  // claimed: key, initial states, then publish the tag
-                for (u32 w = 0; w < kw8; ++w) e[1 + w] = gld<u64>(rk + 8 * w);
+                for (u32 w = 0; w < kw8; ++w) e[1 + w] = rk.word(w);
                 for (int w = 1; w <= S.n_words; ++w) e[kw8 + w] = S.slot_init[w];
                 __hip_atomic_store(e, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                list[atomicAdd(nlist, 1u)] = (u16)pos;
                 return (int)pos;
             }
             t = old;
         }
         while (t == 1) t = lds_ld_acq(e);  // the claimer publishes in straight-line code
-        if (t == tag && pp_key_equal(S, batches, e + 1, rk)) return (int)pos;
+        if (t == tag && pp_key_eq(S, batches, e + 1, rk)) return (int)pos;
         pos = pos + 1 == cap ? 0 : pos + 1;
     }
     return -1;
 }
 
-__device__ __forceinline__ void pp_copy_rec(u8* dst, const u8* src, u32 rw) {
-    for (u32 w = 0; w < rw / 8; ++w) ((u64*)dst)[w] = gld<u64>(src + 8 * w);
+// accumulate_keys of one raw record into the slot states st (st[A.w0] = first word)
+template <typename R>
+__device__ __forceinline__ void pp_apply_rec(const Spec& S, wptr<AS_LDS> st, const R& rk) {
+    u64 vm = ~0ULL;
+    if (S.pp_avoff < S.pp_rw_raw) vm = rk.le(S.pp_avoff, min(8u, S.pp_rw_raw - S.pp_avoff));
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        if (A.arg_type >= 0 && S.pp_avbit[a] >= 0 && !((vm >> S.pp_avbit[a]) & 1)) continue;
+        wptr<AS_LDS> w = st + A.w0;
+        const u32 off = S.pp_aoff[a];
+        const u32 aw = A.arg_type == DBG_BOOLEAN ? 1 : (A.arg_type >= 0 ? type_width(A.arg_type) : 0);
+        switch (A.kind) {
+            case DBG_AGG_COUNT: at_add<AS_LDS>(w, 1ULL); break;
+            case DBG_AGG_SUM: case DBG_AGG_AVG: {
+                if (A.sumk == SUMK_I64) at_add<AS_LDS>(w, (u64)pp_sext(A.arg_type, rk.le(off, aw)));
+                else if (A.sumk == SUMK_F64) {
+                    const u64 b = rk.le(off, aw);
+                    at_addf<AS_LDS>(w, A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)b) : __longlong_as_double((long long)b));
+                } else {
+                    add128<AS_LDS>(w, rk.le(off, 8), rk.le(off + 8, 8));
+                }
+                if (A.kind == DBG_AGG_AVG) at_add<AS_LDS>(w + (A.sumk == SUMK_I128 ? 2 : 1), 1ULL);
+                break;
+            }
+            case DBG_AGG_MIN: case DBG_AGG_MAX: {
+                const bool mn = A.kind == DBG_AGG_MIN;
+                const u64 b = rk.le(off, aw < 8 ? aw : 8);  // Decimal128 (p <= 18): the low word
+                if (A.mmk == MMK_I64) at_minmax<AS_LDS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
+                else if (A.mmk == MMK_U64) at_minmax<AS_LDS>(w, b, mn, false);
+                else
+                    at_minmax<AS_LDS>(w, f64_order_key(A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)b)
+                                                                              : __longlong_as_double((long long)b)),
+                                      mn, false);
+                break;
+            }
+        }
+        if (A.flag_bit >= 0) set_flag<AS_LDS>(st, S.flags_word, A.flag_bit);
+    }
 }
 
 // write one group (slot key part + states) as output row `row` (fixed-width keys only)
@@ -633,91 +734,92 @@ __device__ __forceinline__ void pp_write_fixed_row(const Spec& S, const l64* e, 
     }
 }
 
-template <int MODE>
+template <typename R>
+__device__ __forceinline__ void pp_store_rec(u8* dst, const R& rk, u32 rw) {
+    for (u32 w = 0; w < rw / 8; ++w) ((u64*)dst)[w] = rk.word(w);
+}
+
+// One workgroup per final partition (grid-strided), an LDS table of `cap` slots
+// [tag][key part][state words] plus the list of claimed slots.  tag 0 = empty, 1 = being claimed,
+// else (mix | 2).  A key whose probe window is full in this round overflows — consistently for all
+// its records, since slots only fill within a round — into the partition's region of the alternate
+// buffer and is aggregated in a further round, after this round's groups are written.  W > 0: raw
+// records of W words are held in registers, PP_AU per thread loaded together.
+template <int MODE, int W>
 __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 n_parts, const u64* __restrict__ raw_off, const u64* __restrict__ st_off,
                                                           u8* raw, u8* raw_alt, u8* st, u8* st_alt, u32 cap, PPAggOut out) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     const Spec& S = *spec;
+    const u32 sw = S.pp_sw, kw8 = S.pp_kw / 8, rwr = S.pp_rw_raw, rws = S.pp_rw_state;
     l64* slots = (l64*)lds_raw;
-    const u32 sw = S.pp_sw, kw8 = S.pp_kw / 8;
-    __shared__ u32 novf[2], wsum[PP_AGG_NT / 64];
+    l16* list = (l16*)(slots + (size_t)cap * sw);
+    __shared__ u32 nlist, novf[2];
     __shared__ u64 gbase;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) slots[(size_t)s * sw] = 0;
+    if (threadIdx.x == 0) nlist = novf[0] = novf[1] = 0;
+    __syncthreads();
     for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
-        u64 r0 = raw_off ? raw_off[p] : 0, nr = raw_off ? raw_off[p + 1] - r0 : 0;
-        u64 s0 = st_off ? st_off[p] : 0, ns = st_off ? st_off[p + 1] - s0 : 0;
+        const u64 r0 = raw_off ? raw_off[p] : 0, s0 = st_off ? st_off[p] : 0;
+        u64 nr = raw_off ? raw_off[p + 1] - r0 : 0, ns = st_off ? st_off[p + 1] - s0 : 0;
         u8 *rin = raw, *rout = raw_alt, *sin = st, *sout = st_alt;
-        for (int round = 0;; ++round) {
-            for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) slots[(size_t)s * sw] = 0;
-            if (threadIdx.x < 2) novf[threadIdx.x] = 0;
-            __syncthreads();
-            for (u64 i = threadIdx.x; i < nr; i += PP_AGG_NT) {
-                const u8* rk = rin + (r0 + i) * S.pp_rw_raw;
-                const u64 pm = pp_mix(pp_rec_hash(S, rk));
-                const int ls = pp_find(S, batches, slots, cap, sw, rk, pm);
-                if (ls >= 0) {
-                    pp_apply_raw<AS_LDS>(S, (wptr<AS_LDS>)(slots + (size_t)ls * sw + kw8), rk);
-                } else {
-                    const u32 q = atomicAdd(&novf[0], 1u);
-                    pp_copy_rec(rout + (r0 + q) * S.pp_rw_raw, rk, S.pp_rw_raw);
+        for (;;) {
+            auto raw_one = [&](const auto& rk) {
+                const u64 pm = pp_mix(pp_hash_of(S, rk));
+                const int ls = pp_find(S, batches, slots, cap, sw, rk, pm, list, &nlist);
+                if (ls >= 0) pp_apply_rec(S, (wptr<AS_LDS>)(slots + (size_t)ls * sw + kw8), rk);
+                else pp_store_rec(rout + (r0 + atomicAdd(&novf[0], 1u)) * rwr, rk, rwr);
+            };
+            if constexpr (W > 0) {
+                constexpr int AU = W <= 2 ? PP_AU : (W <= 4 ? 2 : 1);  // records in flight within 128 VGPRs
+                for (u64 base = 0; base < nr; base += (u64)PP_AGG_NT * AU) {
+                    RegRec<W> rr[AU];
+#pragma unroll
+                    for (int u = 0; u < AU; ++u) {
+                        const u64 i = base + (u64)u * PP_AGG_NT + threadIdx.x;
+                        if (i < nr) {
+                            const u8* rk = rin + (r0 + i) * rwr;
+#pragma unroll
+                            for (int w = 0; w < W; ++w) rr[u].r[w] = gld<u64>(rk + 8 * w);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < AU; ++u)
+                        if (base + (u64)u * PP_AGG_NT + threadIdx.x < nr) raw_one(rr[u]);
                 }
+            } else {
+                for (u64 i = threadIdx.x; i < nr; i += PP_AGG_NT) raw_one(GlbRec{rin + (r0 + i) * rwr});
             }
             for (u64 i = threadIdx.x; i < ns; i += PP_AGG_NT) {
-                const u8* rk = sin + (s0 + i) * S.pp_rw_state;
-                const u64 pm = pp_mix(pp_rec_hash(S, rk));
-                const int ls = pp_find(S, batches, slots, cap, sw, rk, pm);
-                if (ls >= 0) {
+                const GlbRec rk{sin + (s0 + i) * rws};
+                const u64 pm = pp_mix(pp_hash_of(S, rk));
+                const int ls = pp_find(S, batches, slots, cap, sw, rk, pm, list, &nlist);
+                if (ls >= 0)
                     apply_state<AS_LDS, false, AS_GLB>(S, (wptr<AS_LDS>)(slots + (size_t)ls * sw + kw8),
-                                                       (const u64*)(rk + S.pp_kw) - 1);
-                } else {
-                    const u32 q = atomicAdd(&novf[1], 1u);
-                    pp_copy_rec(sout + (s0 + q) * S.pp_rw_state, rk, S.pp_rw_state);
-                }
+                                                       (const u64*)(rk.p + S.pp_kw) - 1);
+                else
+                    pp_store_rec(sout + (s0 + atomicAdd(&novf[1], 1u)) * rws, rk, rws);
             }
             __syncthreads();
-            // emit: slot order per round of PP_AGG_NT slots, positions by block scan
-            u32 total = 0;
-            for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) total += slots[(size_t)s * sw] >= 2 ? 1 : 0;
-            {
-                u32 x = total;
-                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-                if (lane == 0) wsum[wave] = x;
-                __syncthreads();
-                if (threadIdx.x == 0) {
-                    u32 t = 0;
-                    for (int w = 0; w < PP_AGG_NT / 64; ++w) t += wsum[w];
-                    gbase = t ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)t) : 0;
+            if (threadIdx.x == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
+            __syncthreads();
+            // emit the claimed slots in claim order, clearing their tags for the next table
+            const u32 ng = nlist;
+            for (u32 k = threadIdx.x; k < ng; k += PP_AGG_NT) {
+                l64* e = slots + (size_t)list[k] * sw;
+                const u64 row = gbase + k;
+                if (MODE == 0) {
+                    if (row < out.cols.cap_groups) pp_write_fixed_row(S, e, row, out.cols, out.tot + PPT_ERR);
+                } else if (row < out.grec_cap) {
+                    u64* d = (u64*)(out.grec + row * rws);
+                    for (u32 w = 0; w < kw8; ++w) d[w] = e[1 + w];
+                    for (int w = 0; w < S.n_words; ++w) d[kw8 + w] = e[1 + kw8 + w];
                 }
-                __syncthreads();
-            }
-            u64 run = gbase;
-            for (u32 s0r = 0; s0r < cap; s0r += PP_AGG_NT) {
-                const u32 s = s0r + threadIdx.x;
-                const bool occ = s < cap && slots[(size_t)s * sw] >= 2;
-                const u64 m = __ballot(occ);
-                if (lane == 0) wsum[wave] = (u32)__popcll(m);
-                __syncthreads();
-                u32 pre = 0, tot = 0;
-                for (int w = 0; w < PP_AGG_NT / 64; ++w) {
-                    if (w < wave) pre += wsum[w];
-                    tot += wsum[w];
-                }
-                __syncthreads();
-                if (occ) {
-                    const u64 row = run + pre + (u32)__popcll(m & ((1ULL << lane) - 1));
-                    const l64* e = slots + (size_t)s * sw;
-                    if (MODE == 0) {
-                        if (row < out.cols.cap_groups) pp_write_fixed_row(S, e, row, out.cols, out.tot + PPT_ERR);
-                    } else if (row < out.grec_cap) {
-                        u64* d = (u64*)(out.grec + row * S.pp_rw_state);
-                        for (u32 w = 0; w < kw8; ++w) d[w] = e[1 + w];
-                        for (int w = 0; w < S.n_words; ++w) d[kw8 + w] = e[1 + kw8 + w];
-                    }
-                }
-                run += tot;
+                e[0] = 0;
             }
             const u32 o0 = novf[0], o1 = novf[1];
+            __syncthreads();
+            if (threadIdx.x == 0) nlist = novf[0] = novf[1] = 0;
             __syncthreads();
             if (o0 == 0 && o1 == 0) break;
             if (threadIdx.x == 0) atomicAdd((unsigned long long*)(out.tot + PPT_ROUNDS), 1ULL);
@@ -727,8 +829,6 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
             u8* t1 = sin; sin = sout; sout = t1;
             nr = o0;
             ns = o1;
-            __threadfence_block();
-            (void)round;
         }
     }
 }
@@ -737,14 +837,29 @@ void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
                    const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out) {
     if (!n_parts) return;
     const u32 cap = pp_agg_slots(hspec);
-    const size_t lds = (size_t)cap * hspec.pp_sw * 8;
-    const u32 grid = n_parts < 4096 ? n_parts : 4096;
-    if (mode == 0)
-        hipLaunchKernelGGL(pp_agg_kernel<0>, dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, st_off, raw, raw_alt, st,
-                           st_alt, cap, out);
-    else
-        hipLaunchKernelGGL(pp_agg_kernel<1>, dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, st_off, raw, raw_alt, st,
-                           st_alt, cap, out);
+    const size_t lds = (size_t)cap * (hspec.pp_sw * 8 + 2);
+    const u32 grid = n_parts < 8192 ? n_parts : 8192;
+    const u32 wpr = hspec.pp_rw_raw / 8;  // record buffers carry >= 64 bytes of slack: W may round up
+    const int W = wpr <= 1 ? 1 : wpr <= 2 ? 2 : wpr <= 4 ? 4 : wpr <= 6 ? 6 : wpr <= 8 ? 8 : 0;
+#define PP_AGG_LAUNCH(M, WW)                                                                                        \
+    hipLaunchKernelGGL((pp_agg_kernel<M, WW>), dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, \
+                       st_off, raw, raw_alt, st, st_alt, cap, out)
+#define PP_AGG_W(M)                                  \
+    switch (W) {                                     \
+        case 1: PP_AGG_LAUNCH(M, 1); break;          \
+        case 2: PP_AGG_LAUNCH(M, 2); break;          \
+        case 4: PP_AGG_LAUNCH(M, 4); break;          \
+        case 6: PP_AGG_LAUNCH(M, 6); break;          \
+        case 8: PP_AGG_LAUNCH(M, 8); break;          \
+        default: PP_AGG_LAUNCH(M, 0); break;         \
+    }
+    if (mode == 0) {
+        PP_AGG_W(0)
+    } else {
+        PP_AGG_W(1)
+    }
+#undef PP_AGG_W
+#undef PP_AGG_LAUNCH
 }
 
 // ------------------------------------------------------------------------------------------

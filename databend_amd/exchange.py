@@ -53,9 +53,42 @@ def all_to_all_bytes(send, send_splits: Sequence[int], device) -> Tuple["object"
     return recv, recv_splits
 
 
+def exchange_records(recs, strs, counts: Sequence[int], sbytes: Sequence[int], width: int, device):
+    """All-to-all of partition-major exchange records (dbg_agg_export_records layout) and their
+    string blobs: counts[d] records / sbytes[d] blob bytes go to rank d.  ONE collective carries
+    both size vectors (the only host round trip), then the record and blob bytes move with one
+    all_to_all_single each.  Returns (records, blobs, per-source record counts, per-source blob bytes)."""
+    world = _dist().get_world_size()
+    return _exchange_with_sizes(recs, strs, counts, sbytes, width, device, world)
+
+
+def _exchange_with_sizes(recs, strs, counts, sbytes, width, device, world):
+    import torch
+    dist = _dist()
+    # [c_0, s_0, c_1, s_1, ...]: the pair for destination d is contiguous, so an even all-to-all
+    # (2 int64 per peer) delivers each source's pair
+    pairs = torch.tensor([x for d in range(world) for x in (counts[d], sbytes[d])], dtype=torch.int64, device=device)
+    got = torch.empty_like(pairs)
+    dist.all_to_all_single(got, pairs)
+    got = got.view(world, 2).tolist()
+    seg_records = [int(c) for c, _ in got]
+    seg_strings = [int(s) for _, s in got]
+    rrecv = torch.empty(max(1, sum(seg_records) * width), dtype=torch.uint8, device=device)
+    srecv = torch.empty(max(1, sum(seg_strings)), dtype=torch.uint8, device=device)
+    nsend = sum(counts) * width
+    dist.all_to_all_single(rrecv[:sum(seg_records) * width], recs[:nsend],
+                           output_split_sizes=[c * width for c in seg_records],
+                           input_split_sizes=[c * width for c in counts])
+    dist.all_to_all_single(srecv[:sum(seg_strings)], strs[:sum(sbytes)],
+                           output_split_sizes=seg_strings, input_split_sizes=list(sbytes))
+    return rrecv[:max(0, sum(seg_records) * width)], srecv[:sum(seg_strings)], seg_records, seg_strings
+
+
 def exchange_partial(partial, final, device) -> dict:
     """Route `partial`'s groups to rank hash % world and merge what arrives into `final`
-    (both AggregateHashTable).  Returns byte counts for reporting xGMI traffic."""
+    (both AggregateHashTable).  The export and the collectives run in stream order on the current
+    stream (no stream synchronisation); the host waits once, for the exchanged sizes.  Returns
+    byte counts for reporting xGMI traffic."""
     import torch
     dist = _dist()
     world = dist.get_world_size()
@@ -64,14 +97,11 @@ def exchange_partial(partial, final, device) -> dict:
     recs = torch.empty(max(1, sum(counts) * w), dtype=torch.uint8, device=device)
     strs = torch.empty(max(1, sum(sbytes)), dtype=torch.uint8, device=device)
     partial.export_records(recs, strs)
-    torch.cuda.current_stream().synchronize()
-    rrecs, rsplits = all_to_all_bytes(recs, [c * w for c in counts], device)
-    rstrs, rssplits = all_to_all_bytes(strs, list(sbytes), device)
-    seg_records = [s // w for s in rsplits]
-    final.merge_records(rrecs, rstrs, seg_records, rssplits)
+    rrecs, rstrs, seg_records, seg_strings = _exchange_with_sizes(recs, strs, counts, sbytes, w, device, world)
+    final.merge_records(rrecs if rrecs.numel() else recs[:1], rstrs if rstrs.numel() else strs[:1], seg_records, seg_strings)
+    me = dist.get_rank()
     sent = sum(c * w for c in counts) + sum(sbytes)
-    return dict(sent_bytes=sent, remote_bytes=sent - counts[dist.get_rank()] * w - sbytes[dist.get_rank()],
-                received_records=sum(seg_records))
+    return dict(sent_bytes=sent, remote_bytes=sent - counts[me] * w - sbytes[me], received_records=sum(seg_records))
 
 
 _FIXED_BUFS = {}

@@ -249,6 +249,22 @@ int dbg_agg_get_strategy(dbg_agg_handle* h, int* partitioned, uint64_t* extra_ro
  * StrengthReducedU64); scheme 1: partition = (hash & mask) >> (48 - r) with n_parts = 2^r
  * (radix buckets). */
 int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width);
+/* The record layout of a handle built from `params`, computed on the host (no device needed): a
+ * mixed CPU/GPU exchange or a test packs and unpacks records with it.  Offsets are in bytes from
+ * the record start; the group hash (u64) is at 0; a string key's (offset u64, len u64) pair is at
+ * key_off; state word j (1-based, as agg_w0 / flags_word count them) is the u64 at
+ * state_off + 8 * (j - 1).  SUM/AVG of Decimal128 hold (lo, hi) words, AVG appends its count. */
+typedef struct dbg_record_layout {
+    uint32_t width;
+    uint32_t state_off;
+    uint32_t key_off[8];
+    uint32_t validity_off[8]; /* nullable key columns only */
+    int32_t agg_w0[32];       /* first state word of each aggregate */
+    int32_t agg_words[32];
+    int32_t flags_word;       /* -1: no "has input" flags word (OrNull of nullable arguments) */
+    int32_t n_words;
+} dbg_record_layout;
+int dbg_agg_record_layout(const dbg_agg_params* params, dbg_record_layout* out);
 int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t* rec_counts,
                       uint64_t* string_bytes);
 /* Write every partition's records, partition-major and contiguous, into dev_records

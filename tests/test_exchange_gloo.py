@@ -33,7 +33,19 @@ def _data(n=20_000):
     return keys_s, keys_i, vals
 
 
+def _params():
+    from databend_amd import column as col
+    from databend_amd.aggregates import AggregateFunctionFactory
+    from databend_amd.aggregator import AggregatorParams
+    F = AggregateFunctionFactory.instance()
+    return AggregatorParams([col.String, col.Int64], [F.get("count"), F.get("sum", [], [col.Int64])])
+
+
 def _worker(rank, world, port, q):
+    """Each rank: oracle partial aggregate of its slice -> records in the library's exchange layout
+    (dbg_agg_record_layout: what dbg_agg_export_records writes and dbg_agg_merge_records reads)
+    partitioned by hash % world -> exchange_records (the RCCL path's code, here over gloo) ->
+    merge of the received records, decoded with the same layout."""
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -41,50 +53,63 @@ def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
     from databend_amd import column as col
-    from databend_amd.aggregates import AggregateFunctionFactory
     from databend_amd.column import Column
-    from databend_amd.exchange import all_to_all_bytes
+    from databend_amd.exchange import exchange_records
     from oracle import oracle
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        params = _params()
+        L = params.record_layout()
+        W, so = L.width, L.state_off
         ks, ki, vals = _data()
         n = len(ki)
         lo, hi = n * rank // world, n * (rank + 1) // world
-        F = AggregateFunctionFactory.instance()
         keys = [Column.from_strings(ks[lo:hi]), Column.from_numbers(col.Int64, ki[lo:hi])]
         v = Column.from_numbers(col.Int64, vals[lo:hi])
-        pk, pa = oracle.aggregate(keys, [(F.get("count").to_abi(), None), (F.get("sum", [], [col.Int64]).to_abi(), v)])
+        fns = params.aggregate_functions
+        pk, pa = oracle.aggregate(keys, [(fns[0].to_abi(), None), (fns[1].to_abi(), v)])
         h = oracle.group_hash(pk)
         dest = (h % np.uint64(world)).astype(np.int64)
         s_vals, i_vals = pk[0].values(), pk[1].values()
         c_vals, sum_vals = pa[0].values(), pa[1].values()
-        # records: [hash u64][i64 key][u64 count][i64 sum][u64 len] + blob
         rec_parts, blob_parts = [[] for _ in range(world)], [[] for _ in range(world)]
         for g in range(len(i_vals)):
             d = int(dest[g])
             off = sum(len(b) for b in blob_parts[d])
-            rec_parts[d].append(struct.pack("<QqQqQQ", int(h[g]), i_vals[g], c_vals[g], sum_vals[g], off, len(s_vals[g])))
+            r = bytearray(W)
+            struct.pack_into("<Q", r, 0, int(h[g]))
+            struct.pack_into("<QQ", r, L.key_off[0], off, len(s_vals[g]))
+            struct.pack_into("<q", r, L.key_off[1], i_vals[g])
+            struct.pack_into("<Q", r, so + 8 * (L.agg_w0[0] - 1), c_vals[g])
+            struct.pack_into("<q", r, so + 8 * (L.agg_w0[1] - 1), sum_vals[g])
+            rec_parts[d].append(bytes(r))
             blob_parts[d].append(s_vals[g])
         recs = b"".join(b"".join(p) for p in rec_parts)
         blobs = b"".join(b"".join(p) for p in blob_parts)
         rsend = torch.frombuffer(bytearray(recs or b"\0"), dtype=torch.uint8)
         bsend = torch.frombuffer(bytearray(blobs or b"\0"), dtype=torch.uint8)
-        rrecv, rsplits = all_to_all_bytes(rsend, [sum(len(r) for r in p) for p in rec_parts], "cpu")
-        brecv, bsplits = all_to_all_bytes(bsend, [sum(len(b) for b in p) for p in blob_parts], "cpu")
-        rb, bb = bytes(rrecv.numpy()[:sum(rsplits)]), bytes(brecv.numpy()[:sum(bsplits)])
+        counts = [len(p) for p in rec_parts]
+        sbytes = [sum(len(b) for b in p) for p in blob_parts]
+        rrecv, brecv, seg_records, seg_strings = exchange_records(rsend, bsend, counts, sbytes, W, "cpu")
+        rb, bb = bytes(rrecv.numpy()), bytes(brecv.numpy())
         merged = {}
         ro = bo = 0
         for src in range(world):
-            for k in range(rsplits[src] // 48):
-                hh, ik, cnt, sm, off, ln = struct.unpack_from("<QqQqQQ", rb, ro + k * 48)
+            for k in range(seg_records[src]):
+                base = ro + k * W
+                hh, = struct.unpack_from("<Q", rb, base)
+                off, ln = struct.unpack_from("<QQ", rb, base + L.key_off[0])
+                ik, = struct.unpack_from("<q", rb, base + L.key_off[1])
+                cnt, = struct.unpack_from("<Q", rb, base + so + 8 * (L.agg_w0[0] - 1))
+                sm, = struct.unpack_from("<q", rb, base + so + 8 * (L.agg_w0[1] - 1))
                 sk = bb[bo + off:bo + off + ln]
                 assert hh % world == rank
                 e = merged.setdefault((sk, ik), [0, 0])
                 e[0] += cnt
                 e[1] += sm
-            ro += rsplits[src]
-            bo += bsplits[src]
+            ro += seg_records[src] * W
+            bo += seg_strings[src]
         q.put((rank, merged))
     finally:
         dist.destroy_process_group()
