@@ -228,6 +228,9 @@ struct dbg_agg_handle {
     u64 pp_cnt_cap = 0;
     u64* pp_off = nullptr;
     u64 pp_off_cap = 0;
+    u64* pp_scan_tmp = nullptr;  // scan scratch (group totals, block sums)
+    u64 pp_scan_tmp_cap = 0;
+    u64* pp_last_part = nullptr;  // partition offsets of the last count_scan (read by its scatter)
     u64* pp_mid = nullptr;  // intermediate partition offsets (device)
     u64 pp_mid_cap = 0;
     PPChunk* pp_dchunks = nullptr;
@@ -791,7 +794,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
         for (void* q : kb)
             if (q) hipFree(q);
     }
-    void* pb[] = {h->pp_cnt, h->pp_off, h->pp_mid, h->pp_dchunks, h->pp_dc0, h->pp_tot, h->pp_set, h->pp_grec, h->pp_blk};
+    void* pb[] = {h->pp_cnt, h->pp_off, h->pp_scan_tmp, h->pp_mid, h->pp_dchunks, h->pp_dc0, h->pp_tot, h->pp_set, h->pp_grec, h->pp_blk};
     for (void* q : pb)
         if (q) hipFree(q);
     void* ph[] = {h->pp_hchunks, h->pp_hc0, h->pp_hpart, h->pp_htot};
@@ -941,7 +944,7 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
         gu = lo;
     }
     const double gee = std::sqrt(nsel / sel) * f1 + (D - f1);
-    const double g = std::min(nsel, std::max(2.0 * gu, gee));
+    const double g = std::min(nsel, std::max(1.25 * gu, gee));
     h->pp_ratio = std::min(1.0, std::max(g / nsel, 1e-9));
     if (mode == 2 || g > (double)PP_MIN_GROUPS) h->pp = true;
     return DBG_OK;
@@ -962,24 +965,114 @@ static int pp_upload_chunks(dbg_agg_handle* h, const std::vector<PPChunk>& ch, c
 }
 
 // count + scan of one level: part_out receives G * K + 1 partition offsets
-static int pp_count_scan(dbg_agg_handle* h, int src, int kind, const u8* recs, const std::vector<PPChunk>& ch,
-                         const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out) {
+static const char* const PP_COUNT_NAME[4] = {"", "pp_count_l1", "pp_count_l2", "pp_count_l3"};
+static const char* const PP_SCAN_NAME[4] = {"", "pp_scan_l1", "pp_scan_l2", "pp_scan_l3"};
+static const char* const PP_SCATTER_NAME[4] = {"", "pp_scatter_l1", "pp_scatter_l2", "pp_scatter_l3"};
+
+// The specialised level-1 form of a raw batch (pp.hip pp_l1_*), or kind 0 for the generic kernels.
+static PPFast pp_fast_desc(const Spec& S, const BatchDesc& B, u32 bid, int kind) {
+    PPFast F;
+    memset(&F, 0, sizeof(F));
+    if (kind != 0 || B.is_records || B.n_nodes > 1) return F;
+    const DNode* nd = B.n_nodes ? &B.nodes[0] : nullptr;
+    if (nd && nd->op != DBG_PRED_CMP_CONST) return F;
+    const DCol* pc = nd ? &B.fcols[nd->col] : nullptr;
+    if (pc && (pc->nullable || pc->layout != LAYOUT_ARROW)) return F;
+    auto fixed_ok = [](int t) { return t != DBG_STRING && t != DBG_DECIMAL128 && t != DBG_BOOLEAN && type_width(t) > 0; };
+    if (!S.has_strings) {
+        if (S.pp_rw_raw > 64) return F;
+        u32 n = 0;
+        for (int c = 0; c < S.n_keys; ++c) {
+            const dbg_datatype& t = S.key_types[c];
+            const DCol& d = B.keys[c];
+            if (t.nullable || !fixed_ok(t.type) || d.layout != LAYOUT_ARROW) return F;
+            F.ptr[n] = d.data;
+            F.width[n] = (u8)type_width(t.type);
+            F.type[n] = (u8)t.type;
+            F.off[n] = S.koff[c];
+            ++n;
+        }
+        F.nk = n;
+        for (int a = 0; a < S.n_aggs; ++a) {
+            const DAgg& A = S.aggs[a];
+            if (A.arg_type < 0) continue;
+            const DCol& d = B.args[a];
+            if (A.arg_nullable || !fixed_ok(A.arg_type) || d.layout != LAYOUT_ARROW || n >= 8) return F;
+            F.ptr[n] = d.data;
+            F.width[n] = (u8)type_width(A.arg_type);
+            F.type[n] = (u8)A.arg_type;
+            F.off[n] = S.pp_aoff[a];
+            ++n;
+        }
+        F.ncol = n;
+        if (pc) {
+            const int t = pc->type;
+            if (!fixed_ok(t) || t == DBG_FLOAT32 || t == DBG_FLOAT64) return F;
+            F.has_pred = 1;
+            F.pcmp = nd->cmp;
+            F.ptype = t;
+            F.pwidth = type_width(t);
+            F.pptr = pc->data;
+            F.pconst = nd->i64v;
+        }
+        F.wpr = S.pp_rw_raw / 8;
+        F.kind = 1;
+        return F;
+    }
+    if (S.n_keys != 1 || S.key_types[0].type != DBG_STRING || S.key_types[0].nullable || S.pp_rw_raw != 48) return F;
+    for (int a = 0; a < S.n_aggs; ++a)
+        if (S.aggs[a].arg_type >= 0) return F;
+    const DCol& k = B.keys[0];
+    if (k.layout != LAYOUT_ARROW) return F;
+    if (pc) {
+        if (pc->type != DBG_STRING || pc->data != k.data || pc->offsets != k.offsets) return F;
+        F.has_pred = 1;
+        F.pcmp = nd->cmp;
+        F.pstr = nd->str;
+        F.pstr_len = nd->str_len;
+    }
+    F.soffs = k.offsets;
+    F.sdata = k.data;
+    F.bid = bid;
+    F.wpr = 6;
+    F.kind = 2;
+    return F;
+}
+
+static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const u8* recs, const std::vector<PPChunk>& ch,
+                         const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out, const PPFast* F = nullptr) {
     const u64 K = 1ULL << kbits;
     RETURN_IF(pp_upload_chunks(h, ch, c0));
     RETURN_IF(ensure_dev(&h->pp_cnt, &h->pp_cnt_cap, ch.size() * K));
     RETURN_IF(ensure_dev(&h->pp_off, &h->pp_off_cap, ch.size() * K));
     {
-        prof::Scope ps("pp_count", h->stream);
-        launch_pp_count(h->stream, h->dspec, h->dbatches, src, kind, recs, h->pp_dchunks, (u32)ch.size(), shift, kbits, h->pp_cnt);
+        prof::Scope ps(PP_COUNT_NAME[level], h->stream);
+        if (F && F->kind)
+            launch_pp_l1_fast(h->stream, *F, 1, h->pp_dchunks, (u32)ch.size(), h->pp_cnt, nullptr, nullptr, nullptr);
+        else
+            launch_pp_count(h->stream, h->dspec, h->dbatches, src, kind, recs, h->pp_dchunks, (u32)ch.size(), shift, kbits, h->pp_cnt);
     }
-    launch_pp_scan(h->stream, h->pp_cnt, (u32)ch.size(), kbits, h->pp_dc0, (u32)(c0.size() - 1), h->pp_off, part_out);
+    RETURN_IF(ensure_dev(&h->pp_scan_tmp, &h->pp_scan_tmp_cap, pp_scan_scratch_words((u32)(c0.size() - 1), kbits)));
+    {
+        prof::Scope ps(PP_SCAN_NAME[level], h->stream);
+        launch_pp_scan(h->stream, h->pp_cnt, (u32)ch.size(), kbits, h->pp_dc0, (u32)(c0.size() - 1), h->pp_off, part_out,
+                       h->pp_scan_tmp);
+    }
+    h->pp_last_part = part_out;
     HIPCHECK(hipGetLastError());
     return DBG_OK;
 }
 
-static int pp_scatter(dbg_agg_handle* h, int src, int kind, const u8* recs, u32 n_chunks, u32 shift, u32 kbits, u8* dst) {
-    prof::Scope ps("pp_scatter", h->stream);
-    launch_pp_scatter(h->stream, h->dspec, h->spec, h->dbatches, src, kind, recs, h->pp_dchunks, n_chunks, shift, kbits, h->pp_off, dst);
+static int pp_scatter(dbg_agg_handle* h, int level, int src, int kind, const u8* recs, u32 n_chunks, u32 shift, u32 kbits,
+                      u8* dst, const PPFast* F = nullptr) {
+    prof::Scope ps(PP_SCATTER_NAME[level], h->stream);
+    if (F && F->kind) {
+        launch_pp_l1_fast(h->stream, *F, 0, h->pp_dchunks, n_chunks, nullptr, h->pp_off, h->pp_last_part, dst);
+        HIPCHECK(hipGetLastError());
+        return DBG_OK;
+    }
+    launch_pp_scatter(h->stream, h->dspec, h->spec, h->dbatches, src, kind, recs, h->pp_dchunks, n_chunks, shift, kbits, h->pp_off,
+                      h->pp_last_part, dst);
     HIPCHECK(hipGetLastError());
     return DBG_OK;
 }
@@ -987,15 +1080,16 @@ static int pp_scatter(dbg_agg_handle* h, int src, int kind, const u8* recs, u32 
 // Level 1 (TransformPartialAggregate::transform in partitioned mode): the batch's selected rows
 // become records appended to the payload, grouped into 256 partitions (PartitionedPayload::
 // append_rows, EAGG/partitioned_payload.rs:100-143).
-static int pp_add_batch(dbg_agg_handle* h, u32 bid, u64 rows, int kind) {
+static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, int kind) {
     const Spec& S = h->spec;
     auto& K = h->ppk[kind];
+    const PPFast F = pp_fast_desc(S, *st, bid, kind);
     const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
     std::vector<PPChunk> ch;
     for (u64 s = 0; s < rows; s += PP_CHUNK) ch.push_back(PPChunk{s, std::min<u64>(PP_CHUNK, rows - s), bid, 0});
     std::vector<u32> c0{0, (u32)ch.size()};
     RETURN_IF(ensure_dev(&h->pp_mid, &h->pp_mid_cap, 257));
-    RETURN_IF(pp_count_scan(h, 0, kind, nullptr, ch, c0, 64 - PP_L1_BITS, PP_L1_BITS, h->pp_mid));
+    RETURN_IF(pp_count_scan(h, 1, 0, kind, nullptr, ch, c0, 64 - PP_L1_BITS, PP_L1_BITS, h->pp_mid, &F));
     RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, 1024));
     HIPCHECK(hipMemcpyAsync(h->pp_hpart, h->pp_mid, 257 * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));
@@ -1013,7 +1107,7 @@ static int pp_add_batch(dbg_agg_handle* h, u32 bid, u64 rows, int kind) {
         K.l1 = nb;
         K.l1_cap = ncap;
     }
-    RETURN_IF(pp_scatter(h, 0, kind, nullptr, (u32)ch.size(), 64 - PP_L1_BITS, PP_L1_BITS, K.l1 + K.l1_n * rw));
+    RETURN_IF(pp_scatter(h, 1, 0, kind, nullptr, (u32)ch.size(), 64 - PP_L1_BITS, PP_L1_BITS, K.l1 + K.l1_n * rw, &F));
     K.segs.push_back(dbg_agg_handle::Seg{K.l1_n, total, std::vector<u64>(h->pp_hpart, h->pp_hpart + 257)});
     K.l1_n += total;
     h->pp_grec_ready = false;
@@ -1070,8 +1164,8 @@ static int pp_prepare(dbg_agg_handle* h) {
             RETURN_IF(ensure_dev(&h->pp_mid, &h->pp_mid_cap, (256ULL << k2) + 1));
             p2 = h->pp_mid;
         }
-        RETURN_IF(pp_count_scan(h, 1, kind, K.l1, ch, c0, sh2, k2, p2));
-        RETURN_IF(pp_scatter(h, 1, kind, K.l1, (u32)ch.size(), sh2, k2, K.a));
+        RETURN_IF(pp_count_scan(h, 2, 1, kind, K.l1, ch, c0, sh2, k2, p2));
+        RETURN_IF(pp_scatter(h, 2, 1, kind, K.l1, (u32)ch.size(), sh2, k2, K.a));
         K.fin = K.a;
         K.alt = K.b;
         if (!k3) continue;
@@ -1090,8 +1184,8 @@ static int pp_prepare(dbg_agg_handle* h) {
         }
         c0.push_back((u32)ch.size());
         const u32 sh3 = sh2 - k3;
-        RETURN_IF(pp_count_scan(h, 1, kind, K.a, ch, c0, sh3, k3, K.part));
-        RETURN_IF(pp_scatter(h, 1, kind, K.a, (u32)ch.size(), sh3, k3, K.b));
+        RETURN_IF(pp_count_scan(h, 3, 1, kind, K.a, ch, c0, sh3, k3, K.part));
+        RETURN_IF(pp_scatter(h, 3, 1, kind, K.a, (u32)ch.size(), sh3, k3, K.b));
         K.fin = K.b;
         K.alt = K.a;
     }
@@ -1203,7 +1297,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     RETURN_IF(submit_batch(h, &st, &bid, on_device && h->owned.size() == owned0));
     // high cardinality: the radix-partitioned payload instead of the HBM table (pp.hip)
     if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, rows));
-    if (h->pp) return pp_add_batch(h, bid, rows, 0);
+    if (h->pp) return pp_add_batch(h, st, bid, rows, 0);
     h->table_rows += rows;
     h->clean = false;
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
@@ -1869,7 +1963,7 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
         RETURN_IF(upload_batch(h, st, bid));
         if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, n));
         if (h->pp) {
-            RETURN_IF(pp_add_batch(h, bid, n, 1));
+            RETURN_IF(pp_add_batch(h, st, bid, n, 1));
             continue;
         }
         h->table_rows += n;

@@ -211,11 +211,38 @@ void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches
 // level scatter: src = 0 raw batch rows (records built from the batch), 1 records of `src_recs`
 void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches, int src, int kind, const u8* src_recs,
                      const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt);
+// off[unit][bucket]: relative start of the unit's run inside partition (group, bucket);
+// part_off[g * K + b]: partition starts (G * K + 1 words); scratch: pp_scan_scratch_words
+u64 pp_scan_scratch_words(u32 n_groups, u32 kbits);
 void launch_pp_scan(hipStream_t s, const u32* cnt, u32 n_chunks, u32 kbits, const u32* group_c0, u32 n_groups, u64* off,
-                    u64* part_off);
+                    u64* part_off, u64* scratch);
 void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
                        const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
-                       u8* dst);
+                       const u64* part_off, u8* dst);
+// Level 1 from raw columns, specialised (pp.hip): kind 1 = fixed-width non-null keys and
+// arguments (<= 8 columns, records <= 64 bytes) with an optional `column <cmp> constant` on a
+// fixed-width non-null integer column; kind 2 = one non-null String key, no arguments, optional
+// `key <cmp> 'constant'`.
+struct PPFast {
+    int32_t kind;   // 0 none (generic kernels), 1 fixed, 2 one string key
+    u32 ncol, nk;   // loaded columns (keys first), keys
+    u32 wpr;        // raw record words
+    u32 bid;
+    const u8* ptr[8];
+    u8 width[8];
+    u8 type[8];
+    u16 off[8];     // byte offset of the value in the record
+    int32_t has_pred, pcmp, ptype;
+    u32 pwidth;
+    const u8* pptr;
+    i64 pconst;
+    const u64* soffs;  // kind 2
+    const u8* sdata;
+    const u8* pstr;
+    u64 pstr_len;
+};
+int launch_pp_l1_fast(hipStream_t s, const PPFast& F, int count, const PPChunk* chunks, u32 n_chunks, u32* cnt, const u64* off,
+                      const u64* part_off, u8* dst);
 // aggregation of the final partitions in LDS; mode 0: result columns (fixed-width keys), mode 1:
 // group records (state record format) in `grec`.  counters: [0] row cursor, [1] overflow records
 struct PPAggOut {

@@ -24,7 +24,6 @@
 #define PP_AGG_NT 512
 #define PP_AGG_LDS (72 * 1024)  // two workgroups per CU
 #define PP_AU 4                  // raw records per thread in flight (aggregation)
-#define PP_STAGE_BYTES (48 * 1024)
 #define PP_MAXK 1024
 #define PP_WINDOW 96
 
@@ -33,9 +32,10 @@ typedef __attribute__((address_space(3))) u16 l16;
 typedef __attribute__((address_space(3))) u32 l32;
 typedef __attribute__((address_space(3))) u64 l64;
 
-// Partition bits come from a remix of the reference group hash (a bool-only key hashes to 0/1):
-// level-local bucket = (pp_mix(h) >> shift) & (K - 1); the LDS slot uses the low 32 bits.
-__device__ __forceinline__ u64 pp_mix(u64 h) { return hash_prim(h ^ 0x2545F4914F6CDD1DULL); }
+// Partition bits are the top bits of the reference group hash itself (its murmur finalizer mixes
+// every input bit into them; only a Boolean-only key, <= 3 groups, never partitioned, hashes to
+// 0/1): level-local bucket = (h >> shift) & (K - 1); the LDS slot uses the low 32 bits.
+__device__ __forceinline__ u64 pp_mix(u64 h) { return h; }
 
 // little-endian value of w (1..8) bytes at p (global memory, any alignment)
 __device__ __forceinline__ u64 ld_le(const u8* p, u32 w) { return load_partial(p, w) & width_mask(w); }
@@ -317,102 +317,128 @@ void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches,
 }
 
 // ------------------------------------------------------------------------------------------
-// scan: exclusive prefix of cnt in (source group, bucket, unit) order — units of one group are
-// consecutive (group_c0[g] .. group_c0[g + 1]; every group has at least one unit).
-// off[unit][bucket] = destination of the unit's first record in that bucket;
-// part_off[g * K + b] = start of destination partition (g, b); part_off[G * K] = total.
+// scan: destinations of every (unit, bucket) run, all parallel.
+//   within:  one thread per (group g, bucket b): exclusive prefix over the group's units
+//            -> off[unit][b] (relative to the partition start), tot[g * K + b]
+//   blocks:  tot scanned in blocks of SCAN_ITEMS -> part_off (block-relative) + block sums
+//   sums:    one workgroup scans the block sums; fixup adds them -> part_off[g * K + b] = start
+//            of destination partition (g, b), part_off[G * K] = total.
+// A scatter unit starts its bucket-b run at part_off[group * K + b] + off[unit][b].
 // ------------------------------------------------------------------------------------------
-#define SCAN_NT 1024
-__device__ __forceinline__ void scan_locate(u64 j, u32 K, const u32* c0, u32 G, u32& g, u32& b, u32& ci) {
-    u32 lo = 0, hi = G;  // largest g with c0[g] * K <= j
-    while (hi - lo > 1) {
-        const u32 mid = (lo + hi) >> 1;
-        if ((u64)c0[mid] * K <= j) lo = mid;
-        else hi = mid;
+#define SCAN_NT 256
+#define SCAN_PER 16
+#define SCAN_ITEMS (SCAN_NT * SCAN_PER)
+
+__global__ void __launch_bounds__(SCAN_NT) pp_scan_within_kernel(const u32* __restrict__ cnt, u32 kbits, const u32* __restrict__ c0,
+                                                                u32 G, u64* __restrict__ off, u64* __restrict__ tot) {
+    const u32 K = 1u << kbits;
+    const u64 j = blockIdx.x * (u64)SCAN_NT + threadIdx.x;
+    if (j >= (u64)G * K) return;
+    const u32 g = (u32)(j >> kbits), b = (u32)(j & (K - 1));
+    u64 run = 0;
+    for (u32 c = c0[g]; c < c0[g + 1]; ++c) {
+        const u64 idx = (u64)c * K + b;
+        off[idx] = run;
+        run += cnt[idx];
     }
-    g = lo;
-    const u64 local = j - (u64)c0[g] * K;
-    const u32 nc = c0[g + 1] - c0[g];
-    b = (u32)(local / nc);
-    ci = (u32)(local % nc);
+    tot[j] = run;
 }
 
-__global__ void __launch_bounds__(SCAN_NT) pp_scan_kernel(const u32* __restrict__ cnt, u32 n_chunks, u32 kbits,
-                                                         const u32* __restrict__ c0, u32 G, u64* __restrict__ off,
-                                                         u64* __restrict__ part_off) {
-    __shared__ u64 sums[SCAN_NT];
+// the same for groups of many units (level 1: one group): one workgroup per (group, bucket)
+__global__ void __launch_bounds__(SCAN_NT) pp_scan_within_wg_kernel(const u32* __restrict__ cnt, u32 kbits, const u32* __restrict__ c0,
+                                                                   u32 G, u64* __restrict__ off, u64* __restrict__ tot) {
+    __shared__ u64 ws[SCAN_NT / 64];
     const u32 K = 1u << kbits;
-    const u64 E = (u64)n_chunks * K;
-    const u64 per = (E + SCAN_NT - 1) / SCAN_NT;
-    const u64 a = threadIdx.x * per, e = a + per < E ? a + per : E;
-    u64 acc = 0;
-    if (a < e) {
-        u32 g, b, ci;
-        scan_locate(a, K, c0, G, g, b, ci);
-        for (u64 j = a; j < e; ++j) {
-            acc += cnt[(u64)(c0[g] + ci) * K + b];
-            if (++ci == c0[g + 1] - c0[g]) {
-                ci = 0;
-                if (++b == K) { b = 0; ++g; }
-            }
+    const u64 j = blockIdx.x;
+    const u32 g = (u32)(j >> kbits), b = (u32)(j & (K - 1));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 run = 0;
+    for (u32 cb = c0[g]; cb < c0[g + 1]; cb += SCAN_NT) {
+        const u32 c = cb + threadIdx.x;
+        const u64 v = c < c0[g + 1] ? cnt[(u64)c * K + b] : 0;
+        u64 x = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u64 y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        u64 pre = x - v, all = 0;
+        for (int w = 0; w < SCAN_NT / 64; ++w) {
+            if (w < wave) pre += ws[w];
+            all += ws[w];
+        }
+        if (c < c0[g + 1]) off[(u64)c * K + b] = run + pre;
+        run += all;
+        __syncthreads();
     }
-    sums[threadIdx.x] = acc;
+    if (threadIdx.x == 0) tot[j] = run;
+}
+
+__global__ void __launch_bounds__(SCAN_NT) pp_scan_blocks_kernel(const u64* __restrict__ tot, u64 E, u64* __restrict__ part_off,
+                                                                u64* __restrict__ bsum) {
+    __shared__ u64 ws[SCAN_NT / 64];
+    const u64 base = (u64)blockIdx.x * SCAN_ITEMS + (u64)threadIdx.x * SCAN_PER;
+    u64 v[SCAN_PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        v[k] = base + k < E ? tot[base + k] : 0;
+        s += v[k];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const u64 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
     __syncthreads();
-    for (u32 o = 1; o < SCAN_NT; o <<= 1) {
-        const u64 v = threadIdx.x >= o ? sums[threadIdx.x - o] : 0;
-        __syncthreads();
-        sums[threadIdx.x] += v;
-        __syncthreads();
+    u64 pre = x - s, all = 0;
+    for (int w = 0; w < SCAN_NT / 64; ++w) {
+        if (w < wave) pre += ws[w];
+        all += ws[w];
     }
-    u64 run = threadIdx.x ? sums[threadIdx.x - 1] : 0;
-    if (a < e) {
-        u32 g, b, ci;
-        scan_locate(a, K, c0, G, g, b, ci);
-        for (u64 j = a; j < e; ++j) {
-            const u64 idx = (u64)(c0[g] + ci) * K + b;
-            if (ci == 0) part_off[(u64)g * K + b] = run;
-            off[idx] = run;
-            run += cnt[idx];
-            if (++ci == c0[g + 1] - c0[g]) {
-                ci = 0;
-                if (++b == K) { b = 0; ++g; }
-            }
-        }
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        if (base + k < E) part_off[base + k] = pre;
+        pre += v[k];
     }
-    if (threadIdx.x == SCAN_NT - 1) part_off[(u64)G * K] = sums[SCAN_NT - 1];
+    if (threadIdx.x == 0) bsum[blockIdx.x] = all;
+}
+
+__global__ void __launch_bounds__(SCAN_NT) pp_scan_fixup_kernel(u64* __restrict__ part_off, u64 E, const u64* __restrict__ bsum,
+                                                               u64 nb) {
+    const u64 i = blockIdx.x * (u64)SCAN_NT + threadIdx.x;
+    if (i < E) part_off[i] += bsum[i / SCAN_ITEMS];
+    if (i == 0) part_off[E] = bsum[nb];  // the total (exclusive scan of nb sums writes it at [nb])
+}
+
+void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total);
+
+u64 pp_scan_scratch_words(u32 n_groups, u32 kbits) {
+    const u64 E = (u64)n_groups << kbits;
+    return E + (E + SCAN_ITEMS - 1) / SCAN_ITEMS + 2;
 }
 
 void launch_pp_scan(hipStream_t s, const u32* cnt, u32 n_chunks, u32 kbits, const u32* group_c0, u32 n_groups, u64* off,
-                    u64* part_off) {
-    hipLaunchKernelGGL(pp_scan_kernel, dim3(1), dim3(SCAN_NT), 0, s, cnt, n_chunks, kbits, group_c0, n_groups, off, part_off);
+                    u64* part_off, u64* scratch) {
+    const u64 E = (u64)n_groups << kbits;
+    const u64 nb = (E + SCAN_ITEMS - 1) / SCAN_ITEMS;
+    u64* tot = scratch;
+    u64* bsum = scratch + E;
+    if (n_chunks >= 64 * (u64)n_groups)  // many units per group: a workgroup per (group, bucket)
+        hipLaunchKernelGGL(pp_scan_within_wg_kernel, dim3((u32)E), dim3(SCAN_NT), 0, s, cnt, kbits, group_c0, n_groups, off, tot);
+    else
+        hipLaunchKernelGGL(pp_scan_within_kernel, dim3((u32)((E + SCAN_NT - 1) / SCAN_NT)), dim3(SCAN_NT), 0, s, cnt, kbits,
+                           group_c0, n_groups, off, tot);
+    hipLaunchKernelGGL(pp_scan_blocks_kernel, dim3((u32)nb), dim3(SCAN_NT), 0, s, tot, E, part_off, bsum);
+    launch_exclusive_scan(s, bsum, nb, bsum + nb);
+    hipLaunchKernelGGL(pp_scan_fixup_kernel, dim3((u32)((E + SCAN_NT - 1) / SCAN_NT)), dim3(SCAN_NT), 0, s, part_off, E, bsum, nb);
 }
 
 // ------------------------------------------------------------------------------------------
-// scatter: records staged in LDS, counting-sorted by bucket per tile, written as runs.
-// LDS: stage [cap * rw] | bkt u16 [cap] | rank u16 [cap] | sidx u16 [cap] | hist u32 [K] |
-//      scan u32 [K] | run u64 [K]
+// scatter
 // ------------------------------------------------------------------------------------------
-// LDS carve-up of the scatter kernel (byte offsets, every array 16-byte aligned)
-struct PPStageLayout {
-    u32 cap, bkt, rank, sidx, hist, scn, run, bytes;
-};
-__host__ __device__ __forceinline__ u32 pp_al16(u32 x) { return (x + 15) & ~15u; }
-__host__ __device__ __forceinline__ PPStageLayout pp_stage_layout(u32 rw, u32 K) {
-    PPStageLayout L;
-    L.cap = PP_STAGE_BYTES / rw;  // >= 128 for records up to 256 bytes
-    if (L.cap > 4096) L.cap = 4096;
-    L.bkt = pp_al16(L.cap * rw);
-    L.rank = pp_al16(L.bkt + 2 * L.cap);
-    L.sidx = pp_al16(L.rank + 2 * L.cap);
-    L.hist = pp_al16(L.sidx + 2 * L.cap);
-    L.scn = pp_al16(L.hist + 4 * K);
-    L.run = pp_al16(L.scn + 4 * K);
-    L.bytes = pp_al16(L.run + 8 * K);
-    return L;
-}
-static size_t pp_scatter_lds(u32 rw, u32 K) { return pp_stage_layout(rw, K).bytes; }
-
 // block-wide exclusive scan of one u32 per thread (PP_NT threads); returns the total
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* wtot, u32& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -431,147 +457,6 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* wtot, u32& total) {
     __syncthreads();
     total = tot;
     return pre + x - v;
-}
-
-template <int SRC>
-__global__ void __launch_bounds__(PP_NT) pp_scatter_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                          int kind, const u8* __restrict__ recs, const PPChunk* __restrict__ chunks,
-                                                          u32 shift, u32 kbits, const u64* __restrict__ off, u8* __restrict__ dst) {
-    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
-    const Spec& S = *spec;
-    const u32 K = 1u << kbits;
-    const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
-    const u32 wpr = rw / 8;
-    const PPStageLayout LY = pp_stage_layout(rw, K);
-    const u32 cap = LY.cap;
-    l8* stage = (l8*)lds_raw;
-    l16* bkt = (l16*)(stage + LY.bkt);
-    l16* rank = (l16*)(stage + LY.rank);
-    l16* sidx = (l16*)(stage + LY.sidx);
-    l32* hist = (l32*)(stage + LY.hist);
-    l32* scn = (l32*)(stage + LY.scn);
-    l64* run = (l64*)(stage + LY.run);
-    __shared__ u32 wtot[PP_NT / 64];
-
-    const PPChunk ch = chunks[blockIdx.x];
-    for (u32 b = threadIdx.x; b < K; b += PP_NT) run[b] = off[(u64)blockIdx.x * K + b];
-    u32 qn = 0;  // staged records: kept in registers, identical in every thread (no shared counter)
-    __syncthreads();
-
-    auto flush = [&]() {
-        const u32 n = qn;
-        for (u32 b = threadIdx.x; b < K; b += PP_NT) hist[b] = 0;
-        __syncthreads();
-        for (u32 q = threadIdx.x; q < n; q += PP_NT)
-            rank[q] = (u16)__hip_atomic_fetch_add(&hist[bkt[q]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __syncthreads();
-        // exclusive scan of hist (K <= 1024 = 2 per thread)
-        {
-            const u32 b0 = threadIdx.x * 2;
-            const u32 h0 = b0 < K ? hist[b0] : 0, h1 = b0 + 1 < K ? hist[b0 + 1] : 0;
-            u32 tot;
-            const u32 pre = block_excl_scan(h0 + h1, wtot, tot);
-            if (b0 < K) scn[b0] = pre;
-            if (b0 + 1 < K) scn[b0 + 1] = pre + h0;
-        }
-        __syncthreads();
-        for (u32 q = threadIdx.x; q < n; q += PP_NT) sidx[scn[bkt[q]] + rank[q]] = (u16)q;
-        __syncthreads();
-        const u32 nw = n * wpr;
-        const u64 rcp = ((1ULL << 32) + wpr - 1) / wpr;  // exact for j < 2^32 / wpr^2 (j < 2^17 here)
-        for (u32 j = threadIdx.x; j < nw; j += PP_NT) {
-            const u32 t = (u32)(((u64)j * rcp) >> 32), w = j - t * wpr;
-            const u32 q = sidx[t];
-            const u32 b = bkt[q];
-            const u64 di = run[b] + (t - scn[b]);
-            ((u64 __attribute__((address_space(1)))*)dst)[di * wpr + w] = *(const l64*)(stage + (size_t)q * rw + 8 * w);
-        }
-        __syncthreads();
-        for (u32 b = threadIdx.x; b < K; b += PP_NT) run[b] += hist[b];
-        qn = 0;
-        __syncthreads();
-    };
-
-    const u64 end = ch.start + ch.n;
-    const BatchDesc& B = batches[ch.bid];
-    // rows per fill step: U per thread (all threads) while that is at most half the stage; wide
-    // records: one row on each of the first T threads
-    const u32 U = cap >= 8 * PP_NT ? 4 : (cap >= 4 * PP_NT ? 2 : 1);
-    const u32 T = cap >= 2 * PP_NT ? PP_NT : ((cap / 2) & ~63u);
-    const u32 step = T * U;
-    for (u64 base = ch.start; base < end; base += step) {
-        u32 m = 0;
-        u16 bk[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {  // selection (and, for records, the bucket) of my rows
-            bk[u] = 0;
-            const u64 i = base + (u64)u * T + threadIdx.x;
-            if ((u32)u >= U || threadIdx.x >= T || i >= end) continue;
-            if (SRC == 0) {
-                if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
-            } else {
-                bk[u] = (u16)((u32)(pp_mix(pp_rec_hash(S, recs + i * rw)) >> shift) & (K - 1));
-            }
-            m |= 1u << u;
-        }
-        u32 tot;
-        u32 q = qn + block_excl_scan((u32)__popc(m), wtot, tot);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (!((m >> u) & 1)) continue;
-            const u64 i = base + (u64)u * T + threadIdx.x;
-            l8* d = stage + (size_t)q * rw;
-            if (SRC == 0) {
-                for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = 0;
-                const u64 h = pp_row_hash(S, B, i);
-                if (kind) pp_put_state(S, B, ch.bid, i, h, d);
-                else pp_put_raw(S, B, ch.bid, i, h, d);
-                bkt[q] = (u16)((u32)(pp_mix(h) >> shift) & (K - 1));
-            } else {
-                const u8* r = recs + i * rw;
-                for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = gld<u64>(r + 8 * w);
-                bkt[q] = bk[u];
-            }
-            ++q;
-        }
-        qn += tot;
-        __syncthreads();
-        if (qn + step > cap) flush();
-    }
-    if (qn) flush();
-}
-
-void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
-                       const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
-                       u8* dst) {
-    if (!n_chunks) return;
-    const u32 rw = kind ? hspec.pp_rw_state : hspec.pp_rw_raw;
-    const size_t lds = pp_scatter_lds(rw, 1u << kbits);
-    if (src == 0)
-        hipLaunchKernelGGL(pp_scatter_kernel<0>, dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, chunks, shift,
-                           kbits, off, dst);
-    else
-        hipLaunchKernelGGL(pp_scatter_kernel<1>, dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, chunks, shift,
-                           kbits, off, dst);
-}
-
-// ------------------------------------------------------------------------------------------
-// aggregate: one workgroup per final partition, an LDS table of `cap` slots
-// [tag][key part][state words].  tag 0 = empty, 1 = being claimed, else (mix | 2).  A key whose
-// probe window is full in this round overflows — consistently for all its records, since slots
-// only ever fill — into the partition's region of the alternate buffer, aggregated in a further
-// round once this round's groups are written.
-// ------------------------------------------------------------------------------------------
-u32 pp_agg_slots(const Spec& S) { return (u32)((PP_AGG_LDS - 256) / (8 * S.pp_sw + 2)); }
-
-__device__ __forceinline__ u64 lds_ld_acq(l64* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-
-__device__ __forceinline__ bool pp_long_equal(const Spec& S, const BatchDesc* batches, u64 ra, u64 rb) {
-    const DCol* ka = batches[ref_bid(ra)].keys;
-    const DCol* kb = batches[ref_bid(rb)].keys;
-    for (int c = 0; c < S.n_keys; ++c)
-        if (!cell_equal(ka[c], ref_row(ra), kb[c], ref_row(rb))) return false;
-    return true;
 }
 
 // A record as the aggregation reads it: W words held in registers (raw records of up to 64 bytes,
@@ -614,6 +499,394 @@ __device__ __forceinline__ u64 pp_hash_of(const Spec& S, const R& rk) {
         h = c == 0 ? x : (h * NULL_HASH_VAL) ^ x;
     }
     return h;
+}
+
+// Direct scatter (the form every level runs): per tile of T x U rows, each selected row's bucket
+// and its rank in the bucket (one LDS atomic) give its destination run[bucket] + rank, and the
+// record is stored straight there — from registers (records of W words, W > 0) or from a
+// per-thread LDS scratch slot where a raw row's record is built (W == 0).  Three barriers per tile;
+// the records of one bucket land contiguously within the tile, so the XCD's L2 merges them into
+// whole lines.  LDS: hist u32 [K] | run u64 [K] | scratch [T * U * rw] (W == 0).
+#define PP_SCRATCH_BYTES (32 * 1024)
+__host__ __device__ __forceinline__ u32 pp_direct_t(u32 rw) {  // threads with a row per step
+    const u32 t = PP_SCRATCH_BYTES / rw;
+    return t >= PP_NT ? PP_NT : (t & ~63u);
+}
+__host__ __device__ __forceinline__ u32 pp_direct_u(int W, u32 rw) {  // rows per thread per step
+    if (W > 0) return W <= 2 ? 4 : (W <= 4 ? 2 : 1);
+    const u32 u = PP_SCRATCH_BYTES / (PP_NT * rw);
+    return u >= 4 ? 4 : (u >= 1 ? u : 1);
+}
+
+template <int SRC, int W>
+__global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                 int kind, const u8* __restrict__ recs,
+                                                                 const PPChunk* __restrict__ chunks, u32 shift, u32 kbits,
+                                                                 const u64* __restrict__ off, const u64* __restrict__ part_off,
+                                                                 u8* __restrict__ dst) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    const Spec& S = *spec;
+    const u32 K = 1u << kbits;
+    const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
+    const u32 wpr = rw / 8;
+    l32* hist = (l32*)lds_raw;
+    l64* run = (l64*)(hist + K + (K & 1));
+    l8* scratch = (l8*)(run + K);
+    constexpr u32 UMAX = 4;
+    const u32 U = pp_direct_u(W, rw);
+    const u32 T = W > 0 ? PP_NT : pp_direct_t(rw);
+    const PPChunk ch = chunks[blockIdx.x];
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+        hist[b] = 0;
+        run[b] = part_off[(u64)ch.group * K + b] + off[(u64)blockIdx.x * K + b];
+    }
+    __syncthreads();
+    const u64 end = ch.start + ch.n;
+    const BatchDesc& B = batches[ch.bid];
+    const u64 step = (u64)T * U;
+    for (u64 base = ch.start; base < end; base += step) {
+        u32 bk[UMAX], rk[UMAX];
+        RegRec<(W > 0 ? W : 1)> rr[UMAX];
+        u32 m = 0;
+#pragma unroll
+        for (u32 u = 0; u < UMAX; ++u) {
+            const u64 i = base + (u64)u * T + threadIdx.x;
+            if (u >= U || threadIdx.x >= T || i >= end) continue;
+            if constexpr (SRC == 1 && W > 0) {
+                const u8* r = recs + i * rw;
+#pragma unroll
+                for (int w = 0; w < (W > 0 ? W : 1); ++w) rr[u].r[w] = gld<u64>(r + 8 * w);
+            }
+            m |= 1u << u;
+        }
+#pragma unroll
+        for (u32 u = 0; u < UMAX; ++u) {
+            if (!((m >> u) & 1)) continue;
+            const u64 i = base + (u64)u * T + threadIdx.x;
+            u64 h;
+            if constexpr (SRC == 1 && W > 0) {
+                h = pp_hash_of(S, rr[u]);
+            } else {
+                l8* d = scratch + ((size_t)threadIdx.x * U + u) * rw;
+                if (SRC == 0) {
+                    if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) {
+                        m &= ~(1u << u);
+                        continue;
+                    }
+                    for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = 0;
+                    h = pp_row_hash(S, B, i);
+                    if (kind) pp_put_state(S, B, ch.bid, i, h, d);
+                    else pp_put_raw(S, B, ch.bid, i, h, d);
+                } else {
+                    const u8* r = recs + i * rw;
+                    for (u32 w = 0; w < wpr; ++w) ((l64*)d)[w] = gld<u64>(r + 8 * w);
+                    h = pp_rec_hash(S, r);
+                }
+            }
+            bk[u] = (u32)(pp_mix(h) >> shift) & (K - 1);
+            rk[u] = __hip_atomic_fetch_add(&hist[bk[u]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+#pragma unroll
+        for (u32 u = 0; u < UMAX; ++u) {
+            if (!((m >> u) & 1)) continue;
+            const u64 di = run[bk[u]] + rk[u];
+            u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + di * rw);
+            if constexpr (SRC == 1 && W > 0) {
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if ((u32)w < wpr) o[w] = rr[u].r[w];
+            } else {
+                const l64* s = (const l64*)(scratch + ((size_t)threadIdx.x * U + u) * rw);
+                for (u32 w = 0; w < wpr; ++w) o[w] = s[w];
+            }
+        }
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+            run[b] += hist[b];
+            hist[b] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
+                       const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
+                       const u64* part_off, u8* dst) {
+    if (!n_chunks) return;
+    const u32 rw = kind ? hspec.pp_rw_state : hspec.pp_rw_raw;
+    const u32 K = 1u << kbits;
+    const u32 wpr = rw / 8;
+    const int W = src == 0 ? 0 : (wpr == 1 ? 1 : wpr == 2 ? 2 : wpr == 4 ? 4 : wpr == 6 ? 6 : wpr == 8 ? 8 : 0);
+    const size_t lds = 4 * (size_t)(K + (K & 1)) + 8 * (size_t)K +
+                       (W == 0 ? (size_t)pp_direct_t(rw) * pp_direct_u(0, rw) * rw : 0);
+#define PP_SC(SR, WW)                                                                                                     \
+    hipLaunchKernelGGL((pp_scatter_direct_kernel<SR, WW>), dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, \
+                       chunks, shift, kbits, off, part_off, dst)
+    if (src == 0) {
+        PP_SC(0, 0);
+    } else {
+        switch (W) {
+            case 1: PP_SC(1, 1); break;
+            case 2: PP_SC(1, 2); break;
+            case 4: PP_SC(1, 4); break;
+            case 6: PP_SC(1, 6); break;
+            case 8: PP_SC(1, 8); break;
+            default: PP_SC(1, 0); break;
+        }
+    }
+#undef PP_SC
+}
+
+// ------------------------------------------------------------------------------------------
+// Level 1 from raw columns, specialised (count and scatter in one template): the shapes of the
+// high-cardinality benchmarks — fixed-width non-null keys and arguments with an optional
+// `column <cmp> constant` predicate (ClickBench Q16/Q33), or one non-null String key with an
+// optional string-constant predicate and COUNT(*) (Q13).  Every column value of U rows per thread
+// is loaded before any LDS work (the loads overlap), the record is assembled in registers and
+// stored straight to its run.  Same records, buckets and offsets as the generic kernels.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ u64 pp_ldw(const u8* base, u64 i) { return (u64)gld<T>(base + i * sizeof(T)); }
+__device__ __forceinline__ u64 pp_ld_width(const u8* base, u32 w, u64 i) {
+    switch (w) {
+        case 1: return pp_ldw<uint8_t>(base, i);
+        case 2: return pp_ldw<uint16_t>(base, i);
+        case 4: return pp_ldw<uint32_t>(base, i);
+        default: return pp_ldw<u64>(base, i);
+    }
+}
+__device__ __forceinline__ bool pp_fast_pred(const PPFast& F, u64 v) {
+    const int t = F.ptype;
+    int o;
+    if (is_unsigned_t(t)) o = cmp3_u64(v, (u64)F.pconst);
+    else o = cmp3_i64(pp_sext(t, v), F.pconst);
+    return apply_cmp(F.pcmp, o);
+}
+
+template <int COUNT, int W>
+__global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, const PPChunk* __restrict__ chunks, u32 shift,
+                                                           u32* __restrict__ cnt, const u64* __restrict__ off,
+                                                           const u64* __restrict__ part_off, u8* __restrict__ dst) {
+    constexpr u32 K = 1u << PP_L1_BITS;
+    constexpr int U = W <= 2 ? 4 : (W <= 4 ? 2 : 1);
+    __shared__ u32 hist[K];
+    __shared__ u64 run[K];
+    const PPChunk ch = chunks[blockIdx.x];
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+        hist[b] = 0;
+        if (!COUNT) run[b] = part_off[(u64)ch.group * K + b] + off[(u64)blockIdx.x * K + b];
+    }
+    __syncthreads();
+    const u64 end = ch.start + ch.n;
+    for (u64 base = ch.start; base < end; base += (u64)PP_NT * U) {
+        u64 v[U][8], pv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 i = base + (u64)u * PP_NT + threadIdx.x;
+            const u64 ii = i < end ? i : ch.start;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if ((u32)c < F.ncol) v[u][c] = pp_ld_width(F.ptr[c], F.width[c], ii);
+            pv[u] = F.has_pred ? pp_ld_width(F.pptr, F.pwidth, ii) : 0;
+        }
+        u32 bk[U], rk[U], m = 0;
+        RegRec<W> rec[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 i = base + (u64)u * PP_NT + threadIdx.x;
+            if (i >= end || (F.has_pred && !pp_fast_pred(F, pv[u]))) continue;
+            m |= 1u << u;
+            u64 h = 0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) rec[u].r[k] = 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                if ((u32)c >= F.ncol) continue;
+                u64 x = v[u][c];
+                if (F.type[c] == DBG_FLOAT32 || F.type[c] == DBG_FLOAT64) x = canon_float_bits(F.type[c], x);
+                if ((u32)c < F.nk) {
+                    const u64 hx = hash_bits(F.type[c], x);
+                    h = c == 0 ? hx : (h * NULL_HASH_VAL) ^ hx;
+                }
+                if (!COUNT) {  // place the value at its record offset (may straddle two words)
+                    const u32 o = F.off[c], wi = o >> 3, sh = (o & 7) * 8;
+#pragma unroll
+                    for (int k = 0; k < W; ++k) {
+                        if ((u32)k == wi) rec[u].r[k] |= x << sh;
+                        if (sh && (u32)k == wi + 1 && sh + 8 * F.width[c] > 64) rec[u].r[k] |= x >> (64 - sh);
+                    }
+                }
+            }
+            bk[u] = (u32)(pp_mix(h) >> shift) & (K - 1);
+        }
+        if (COUNT) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if ((m >> u) & 1) atomicAdd(&hist[bk[u]], 1u);
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if ((m >> u) & 1) rk[u] = atomicAdd(&hist[bk[u]], 1u);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!((m >> u) & 1)) continue;
+            u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[bk[u]] + rk[u]) * (8 * F.wpr));
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                if ((u32)k < F.wpr) o[k] = rec[u].r[k];
+        }
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+            run[b] += hist[b];
+            hist[b] = 0;
+        }
+        __syncthreads();
+    }
+    if (COUNT) {
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) cnt[(u64)blockIdx.x * K + b] = hist[b];
+    }
+}
+
+// One non-null String key, COUNT-only records: [hash][klen = 1 + len][len][bytes] (6 words).
+template <int COUNT>
+__global__ void __launch_bounds__(PP_NT) pp_l1_str1_kernel(const PPFast F, const PPChunk* __restrict__ chunks, u32 shift,
+                                                          u32* __restrict__ cnt, const u64* __restrict__ off,
+                                                          const u64* __restrict__ part_off, u8* __restrict__ dst) {
+    constexpr u32 K = 1u << PP_L1_BITS;
+    constexpr int U = 4;
+    __shared__ u32 hist[K];
+    __shared__ u64 run[K];
+    const PPChunk ch = chunks[blockIdx.x];
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+        hist[b] = 0;
+        if (!COUNT) run[b] = part_off[(u64)ch.group * K + b] + off[(u64)blockIdx.x * K + b];
+    }
+    __syncthreads();
+    const u64 end = ch.start + ch.n;
+    for (u64 base = ch.start; base < end; base += (u64)PP_NT * U) {
+        u64 a[U], e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 i = base + (u64)u * PP_NT + threadIdx.x;
+            const u64 ii = i < end ? i : ch.start;
+            a[u] = gld<u64>(F.soffs + ii);
+            e[u] = gld<u64>(F.soffs + ii + 1);
+        }
+        u32 m = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 i = base + (u64)u * PP_NT + threadIdx.x;
+            if (i >= end) continue;
+            if (F.has_pred && !apply_cmp(F.pcmp, cmp3_bytes(F.sdata + a[u], e[u] - a[u], F.pstr, F.pstr_len))) continue;
+            m |= 1u << u;
+        }
+        u32 bk[U], rk[U];
+        u64 h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!((m >> u) & 1)) continue;
+            h[u] = hash_bytes(F.sdata + a[u], e[u] - a[u]);
+            bk[u] = (u32)(pp_mix(h[u]) >> shift) & (K - 1);
+        }
+        if (COUNT) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if ((m >> u) & 1) atomicAdd(&hist[bk[u]], 1u);
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if ((m >> u) & 1) rk[u] = atomicAdd(&hist[bk[u]], 1u);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!((m >> u) & 1)) continue;
+            const u64 i = base + (u64)u * PP_NT + threadIdx.x;
+            const u8* s = F.sdata + a[u];
+            const u64 len = e[u] - a[u];
+            u64 w[6] = {h[u], 0, 0, 0, 0, 0};
+            if (1 + len > PP_BLOB) {
+                w[1] = PP_KLEN_LONG;
+                w[2] = ((u64)F.bid << 32) | (u64)(u32)i;
+            } else {
+                const u32 r1 = len < 6 ? (u32)len : 6;
+                w[1] = (1 + len) | (len << 8) | (r1 ? (load_partial(s, r1) & width_mask(r1)) << 16 : 0);
+#pragma unroll
+                for (int j = 2; j < 6; ++j) {
+                    const u64 q = 8 * j - 10;
+                    if (len > q) {
+                        const u32 r = len - q < 8 ? (u32)(len - q) : 8;
+                        w[j] = load_partial(s + q, r) & width_mask(r);
+                    }
+                }
+            }
+            u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[bk[u]] + rk[u]) * 48);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) o[j] = w[j];
+        }
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+            run[b] += hist[b];
+            hist[b] = 0;
+        }
+        __syncthreads();
+    }
+    if (COUNT) {
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < K; b += PP_NT) cnt[(u64)blockIdx.x * K + b] = hist[b];
+    }
+}
+
+int launch_pp_l1_fast(hipStream_t s, const PPFast& F, int count, const PPChunk* chunks, u32 n_chunks, u32* cnt, const u64* off,
+                      const u64* part_off, u8* dst) {
+    if (!n_chunks) return 0;
+    const u32 shift = 64 - PP_L1_BITS;
+    if (F.kind == 2) {
+        if (count) hipLaunchKernelGGL(pp_l1_str1_kernel<1>, dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, part_off, dst);
+        else hipLaunchKernelGGL(pp_l1_str1_kernel<0>, dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, part_off, dst);
+        return 0;
+    }
+    const int W = F.wpr <= 1 ? 1 : F.wpr <= 2 ? 2 : F.wpr <= 4 ? 4 : F.wpr <= 6 ? 6 : 8;
+#define PP_L1F(C, WW) hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW>), dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, part_off, dst)
+#define PP_L1F_W(C)                      \
+    switch (W) {                         \
+        case 1: PP_L1F(C, 1); break;     \
+        case 2: PP_L1F(C, 2); break;     \
+        case 4: PP_L1F(C, 4); break;     \
+        case 6: PP_L1F(C, 6); break;     \
+        default: PP_L1F(C, 8); break;    \
+    }
+    if (count) {
+        PP_L1F_W(1)
+    } else {
+        PP_L1F_W(0)
+    }
+#undef PP_L1F_W
+#undef PP_L1F
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// aggregate: one workgroup per final partition, an LDS table of `cap` slots
+// [tag][key part][state words].  tag 0 = empty, 1 = being claimed, else (mix | 2).  A key whose
+// probe window is full in this round overflows — consistently for all its records, since slots
+// only ever fill — into the partition's region of the alternate buffer, aggregated in a further
+// round once this round's groups are written.
+// ------------------------------------------------------------------------------------------
+u32 pp_agg_slots(const Spec& S) { return (u32)((PP_AGG_LDS - 256) / (8 * S.pp_sw + 2)); }
+
+__device__ __forceinline__ u64 lds_ld_acq(l64* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+__device__ __forceinline__ bool pp_long_equal(const Spec& S, const BatchDesc* batches, u64 ra, u64 rb) {
+    const DCol* ka = batches[ref_bid(ra)].keys;
+    const DCol* kb = batches[ref_bid(rb)].keys;
+    for (int c = 0; c < S.n_keys; ++c)
+        if (!cell_equal(ka[c], ref_row(ra), kb[c], ref_row(rb))) return false;
+    return true;
 }
 
 // key part of a record == key part of a slot (LDS)
@@ -758,12 +1031,42 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     __shared__ u64 gbase;
     for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) slots[(size_t)s * sw] = 0;
     if (threadIdx.x == 0) nlist = novf[0] = novf[1] = 0;
+    // Software pipeline over this workgroup's partitions p, p + G, p + 2G, ...: while partition p's
+    // group count is reserved and its groups are written, the first record tile of p + G is
+    // already being loaded into registers (its offsets were read one partition earlier, the
+    // offsets of p + 2G are read now), so a partition's inserts start on data in registers.
+    constexpr int AU = W > 0 ? (W <= 2 ? PP_AU : (W <= 4 ? 2 : 1)) : 1;  // records in flight within 128 VGPRs
+    RegRec<(W > 0 ? W : 1)> pre[AU];
+    auto part_range = [&](u32 q, u64& o0, u64& n) {
+        o0 = (raw_off && q < n_parts) ? raw_off[q] : 0;
+        n = (raw_off && q < n_parts) ? raw_off[q + 1] - o0 : 0;
+    };
+    auto load_tile = [&](RegRec<(W > 0 ? W : 1)>* rr, const u8* src, u64 o0, u64 n, u64 base) {
+        if constexpr (W > 0) {
+#pragma unroll
+            for (int u = 0; u < AU; ++u) {
+                const u64 i = base + (u64)u * PP_AGG_NT + threadIdx.x;
+                if (i < n) {
+                    const u8* rk = src + (o0 + i) * rwr;
+#pragma unroll
+                    for (int w = 0; w < W; ++w) rr[u].r[w] = gld<u64>(rk + 8 * w);
+                }
+            }
+        }
+    };
+    u64 nx_r0, nx_nr, nn_r0, nn_nr;
+    part_range(blockIdx.x, nx_r0, nx_nr);
+    load_tile(pre, raw, nx_r0, nx_nr, 0);
+    part_range(blockIdx.x + gridDim.x, nn_r0, nn_nr);
     __syncthreads();
     for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
-        const u64 r0 = raw_off ? raw_off[p] : 0, s0 = st_off ? st_off[p] : 0;
-        u64 nr = raw_off ? raw_off[p + 1] - r0 : 0, ns = st_off ? st_off[p + 1] - s0 : 0;
+        const u64 r0 = nx_r0, s0 = st_off ? st_off[p] : 0;
+        u64 nr = nx_nr, ns = st_off ? st_off[p + 1] - s0 : 0;
         u8 *rin = raw, *rout = raw_alt, *sin = st, *sout = st_alt;
-        for (;;) {
+        RegRec<(W > 0 ? W : 1)> cur[AU];
+#pragma unroll
+        for (int u = 0; u < AU; ++u) cur[u] = pre[u];
+        for (int round = 0;; ++round) {
             auto raw_one = [&](const auto& rk) {
                 const u64 pm = pp_mix(pp_hash_of(S, rk));
                 const int ls = pp_find(S, batches, slots, cap, sw, rk, pm, list, &nlist);
@@ -771,21 +1074,11 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
                 else pp_store_rec(rout + (r0 + atomicAdd(&novf[0], 1u)) * rwr, rk, rwr);
             };
             if constexpr (W > 0) {
-                constexpr int AU = W <= 2 ? PP_AU : (W <= 4 ? 2 : 1);  // records in flight within 128 VGPRs
                 for (u64 base = 0; base < nr; base += (u64)PP_AGG_NT * AU) {
-                    RegRec<W> rr[AU];
-#pragma unroll
-                    for (int u = 0; u < AU; ++u) {
-                        const u64 i = base + (u64)u * PP_AGG_NT + threadIdx.x;
-                        if (i < nr) {
-                            const u8* rk = rin + (r0 + i) * rwr;
-#pragma unroll
-                            for (int w = 0; w < W; ++w) rr[u].r[w] = gld<u64>(rk + 8 * w);
-                        }
-                    }
+                    if (round || base) load_tile(cur, rin, r0, nr, base);  // round 0's first tile: prefetched
 #pragma unroll
                     for (int u = 0; u < AU; ++u)
-                        if (base + (u64)u * PP_AGG_NT + threadIdx.x < nr) raw_one(rr[u]);
+                        if (base + (u64)u * PP_AGG_NT + threadIdx.x < nr) raw_one(cur[u]);
                 }
             } else {
                 for (u64 i = threadIdx.x; i < nr; i += PP_AGG_NT) raw_one(GlbRec{rin + (r0 + i) * rwr});
@@ -801,6 +1094,12 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
                     pp_store_rec(sout + (s0 + atomicAdd(&novf[1], 1u)) * rws, rk, rws);
             }
             __syncthreads();
+            if (round == 0) {  // prefetch: next partition's first tile, the one after's offsets
+                nx_r0 = nn_r0;
+                nx_nr = nn_nr;
+                load_tile(pre, raw, nx_r0, nx_nr, 0);
+                part_range(p + 2 * gridDim.x, nn_r0, nn_nr);
+            }
             if (threadIdx.x == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
             __syncthreads();
             // emit the claimed slots in claim order, clearing their tags for the next table
