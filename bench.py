@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--cpu-sample-rows", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capacity-hint", type=int, default=0)
+    p.add_argument("--strategy", choices=["auto", "table", "partitioned"], default="auto",
+                   help="aggregation strategy of the tables (dbg_agg_set_strategy); auto = the cardinality probe")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher plumbing only: every rank joins a gloo group, rank 0 prints n_gpus (no GPU work)")
     p.add_argument("--scaling", choices=["weak", "strong"], default=None,
@@ -150,13 +152,16 @@ def main():
         copies = args.copies or 1
     # rank r aggregates its own disjoint rows of the synthetic table (weak scaling)
     # every rank aggregates disjoint row ranges of the same generator
-    runner = ConfigRunner(cfg, rows, copies=copies, capacity_hint=args.capacity_hint, start=rank * copies * rows)
+    strategy = {"auto": abi.STRATEGY_AUTO, "table": abi.STRATEGY_TABLE, "partitioned": abi.STRATEGY_PARTITIONED}[args.strategy]
+    runner = ConfigRunner(cfg, rows, copies=copies, capacity_hint=args.capacity_hint, start=rank * copies * rows,
+                          strategy=strategy)
     if world != args.gpus and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     final = None
     small = False
     if world > 1:
         final = AggregateHashTable(runner.params, HashTableConfig(False, args.capacity_hint))
+        final.set_strategy(strategy)
         ffi.check(ffi.lib().dbg_agg_set_recycle(final.h, 1))
         # low cardinality: replicas + gather to rank 0 over one RCCL all-gather;
         # otherwise partial states routed by hash % N with all-to-all (exchange_partial)
@@ -245,8 +250,8 @@ def main():
         kernel_name = "agg_insert"
     avg_ms = ins_ms / max(1, ins_n)
     # algorithmic bytes of one insert launch
+    keys_h = aggs_h = None
     if world == 1:
-        keys_h, aggs_h = runner.results_host()
         n_groups = runner.n_groups
         kstr = runner.key_string_bytes
     else:
@@ -256,10 +261,9 @@ def main():
         keys_h, aggs_h = None, None
     # selected rows: SUM of COUNT(*) over the partial table of this rank
     sel = None
-    if world == 1:
-        ci = [f for f, _ in shape.aggs].index("count") if ("count", None) in shape.aggs else None
-        if ci is not None:
-            sel = int(sum(aggs_h[ci].values()))
+    ci_star = next((i for i, (f, c) in enumerate(shape.aggs) if f == "count" and c is None), None)
+    if world == 1 and ci_star is not None:  # on device: the result columns stay in HBM
+        sel = int(runner.out_aggs[ci_star].data[: 8 * n_groups].view(torch.int64).sum().item())
     if sel is None:
         blk = runner.table.merge_result()
         ci = [i for i, (f, c) in enumerate(shape.aggs) if f == "count" and c is None]
@@ -303,7 +307,7 @@ def main():
     # The ORDER BY <count> DESC LIMIT 10 that ends the ClickBench query, on the device result
     # (untimed leg, reported beside the step; dbg_sort_limit_indices).
     if world == 1 and n_groups > 0:
-        ci_cnt = next((i for i, (f, c) in enumerate(shape.aggs) if f == "count" and c is None), None)
+        ci_cnt = ci_star
         if ci_cnt is not None:
             from databend_amd.sort import sort_limit_indices
             dc = runner.out_aggs[ci_cnt]
@@ -314,8 +318,9 @@ def main():
                 idx = sort_limit_indices(dc, False, False, 10)
             torch.cuda.synchronize()
             sort_ms = (time.perf_counter() - t0) / 5 * 1e3
-            top = np.asarray(aggs_h[ci_cnt].data)[idx.cpu().numpy()]
-            ok = top.tolist() == np.sort(np.asarray(aggs_h[ci_cnt].data))[::-1][: len(top)].tolist()
+            counts = dc.data[: 8 * n_groups].view(torch.int64)  # check against torch's device top-k
+            top = counts[idx.long()].tolist()
+            ok = top == torch.topk(counts, min(10, n_groups)).values.tolist()
             out["order_by_limit"] = {"sql": "ORDER BY count DESC LIMIT 10", "ms": sort_ms, "groups": n_groups,
                                      "values_match_host_sort": ok}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -325,7 +330,7 @@ def main():
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         out["gpu_vs_cpu"] = value / cb["value"]
         # parity of this bench's own GPU result against the CPU run when they cover the same rows
-        if sample == rows and keys_h is not None and copies >= 1:
+        if sample == rows and copies >= 1:
             try:
                 from tests.parity import assert_results_equal
                 runner.step(0)  # copy 0 == rows [0, rows) == the CPU sample

@@ -397,7 +397,10 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     // its width, then one validity bit per nullable argument
     S.pp_str = S.has_strings;
     S.pp_kw = S.has_strings ? 48 : (u32)((S.inline_width + 7) & ~7);
-    u32 po = S.pp_kw;
+    // raw records pack the arguments right after the key bytes (a 12-byte key + two Int16 = 16 B);
+    // key words are compared / copied with the last one masked to the key bytes
+    S.pp_klast_mask = (S.has_strings || (S.inline_width & 7) == 0) ? ~0ULL : ((1ULL << (8 * (S.inline_width & 7))) - 1);
+    u32 po = S.has_strings ? S.pp_kw : (u32)S.inline_width;
     int vbits = 0;
     for (int a = 0; a < S.n_aggs; ++a) {
         const DAgg& A = S.aggs[a];
@@ -946,7 +949,9 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     const double gee = std::sqrt(nsel / sel) * f1 + (D - f1);
     const double g = std::min(nsel, std::max(1.25 * gu, gee));
     h->pp_ratio = std::min(1.0, std::max(g / nsel, 1e-9));
-    if (mode == 2 || g > (double)PP_MIN_GROUPS) h->pp = true;
+    // the partitioned payload beats the HBM table when keys are mostly unique (ClickBench Q33:
+    // 1e9 groups in 1e9 rows); moderate cardinality stays on the table
+    if (mode == 2 || (g > (double)PP_MIN_GROUPS && h->pp_ratio > 0.5)) h->pp = true;
     return DBG_OK;
 }
 
@@ -1123,14 +1128,13 @@ static int pp_prepare(dbg_agg_handle* h) {
     // estimated groups: the capacity hint when the caller gave one, else the probe's ratio
     const double est = h->hint_groups ? (double)h->hint_groups : h->pp_ratio * (double)nr + (double)nsr;
     const double g = std::min((double)(nr + nsr), est);
-    const double target = std::max(64.0, 0.6 * (double)pp_agg_slots(S));
+    // 45 % load: a wave's probe runs as long as its longest lane's (64 lanes in lockstep)
+    const double target = std::max(64.0, 0.45 * (double)pp_agg_slots(S));
     const double need = std::max(1.0, std::ceil(g / target));
     u32 B = PP_L1_BITS + 1;
     while ((double)(1ULL << B) < need && B < PP_L1_BITS + 16) ++B;
-    // a level of one bit costs a full pass to halve partitions that still have headroom
-    // (the target is 60 % of the table): keep them, the next level starts at two bits
-    if (B == 2 * PP_L1_BITS + 1) B = 2 * PP_L1_BITS;
-    const u32 k2 = std::min<u32>(8, B - PP_L1_BITS), k3 = B - PP_L1_BITS - k2;
+    // level 2 takes up to 10 bits (one pass instead of a 1-2 bit third level), level 3 the rest
+    const u32 k2 = std::min<u32>(B - PP_L1_BITS <= 10 ? 10 : 8, B - PP_L1_BITS), k3 = B - PP_L1_BITS - k2;
     h->pp_bits = B;
     for (int kind = 0; kind < 2; ++kind) {
         auto& K = h->ppk[kind];

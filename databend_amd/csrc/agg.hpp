@@ -44,6 +44,7 @@ struct Spec {
     uint32_t pp_rw_state;   // state record bytes
     uint32_t pp_avoff;      // byte offset of the arg validity bits
     uint32_t pp_sw;         // LDS slot words: [tag][key part][state words]
+    u64 pp_klast_mask;      // key bytes of the key part's last word (raw records put args after them)
     uint16_t pp_aoff[DBG_MAX_AGGS];  // raw arg value offset (0: the aggregate takes no argument)
     int16_t pp_avbit[DBG_MAX_AGGS];  // raw arg validity bit (-1: always valid)
 };

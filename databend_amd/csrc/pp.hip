@@ -894,9 +894,9 @@ template <typename R>
 __device__ __forceinline__ bool pp_key_eq(const Spec& S, const BatchDesc* batches, const l64* sk, const R& rk) {
     const u32 kw8 = S.pp_kw / 8;
     if (!S.pp_str) {
-        for (u32 w = 0; w < kw8; ++w)
+        for (u32 w = 0; w + 1 < kw8; ++w)
             if (sk[w] != rk.word(w)) return false;
-        return true;
+        return sk[kw8 - 1] == (rk.word(kw8 - 1) & S.pp_klast_mask);
     }
     if (sk[0] != rk.word(0)) return false;  // group hash
     const u64 w1 = rk.word(1);
@@ -924,7 +924,7 @@ __device__ __forceinline__ int pp_find(const Spec& S, const BatchDesc* batches, 
             u64 old = 0;
             __hip_atomic_compare_exchange_strong(e, &old, 1ULL, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == 0) {  // claimed: key, initial states, then publish the tag
-                for (u32 w = 0; w < kw8; ++w) e[1 + w] = rk.word(w);
+                for (u32 w = 0; w < kw8; ++w) e[1 + w] = rk.word(w) & (w + 1 == kw8 ? S.pp_klast_mask : ~0ULL);
                 for (int w = 1; w <= S.n_words; ++w) e[kw8 + w] = S.slot_init[w];
                 __hip_atomic_store(e, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 list[atomicAdd(nlist, 1u)] = (u16)pos;
