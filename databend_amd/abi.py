@@ -18,7 +18,7 @@ INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64 = range(8)
 FLOAT32, FLOAT64, DECIMAL128, DATE, TIMESTAMP, STRING, BOOLEAN = range(8, 15)
 
 # dbg_agg_kind
-AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = range(5)
+AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG, AGG_AVG_SQL = range(6)
 
 # dbg_agg_set_strategy
 STRATEGY_AUTO, STRATEGY_TABLE, STRATEGY_PARTITIONED = range(3)

@@ -16,8 +16,11 @@ from typing import Optional, Sequence
 from . import abi
 from .column import DataType
 
+# "sql_avg": SQL's avg(x), which the planner rewrites to sum(x) / if(count(x) = 0, 1, count(x))
+# (SQL/planner/semantic/aggregate_rewriter.rs:145-208), fused into one aggregate whose finalize
+# does the division (DBG_AGG_AVG_SQL); "avg" is AggregateAvgFunction itself (FUN/aggregate_avg.rs).
 _KINDS = {"count": abi.AGG_COUNT, "sum": abi.AGG_SUM, "min": abi.AGG_MIN, "max": abi.AGG_MAX,
-          "avg": abi.AGG_AVG}
+          "avg": abi.AGG_AVG, "sql_avg": abi.AGG_AVG_SQL}
 
 
 @dataclass(frozen=True)

@@ -141,6 +141,13 @@ struct dbg_agg_handle {
     u64* slots = nullptr;
     u64 cap = 0;
     u64 init_cap = 0;  // from the capacity hint: the table never shrinks below it
+    // An on-device fast-path insert whose launch is held back until the next call: a
+    // finalize_into_async of a small table then runs in the same launch (FusedFin); any other
+    // call launches it first (flush_deferred).
+    bool def_on = false;
+    u32 def_bid = 0;
+    u64 def_rows = 0;
+    BatchDesc def_hb;
     u64* counters = nullptr;   // device, CNT_WORDS
     u64* hcounters = nullptr;  // pinned
     u64* hcounters_dev = nullptr;  // its device mapping (finalize_small writes it directly)
@@ -301,6 +308,12 @@ static int result_type_of(const dbg_agg_spec& s, dbg_datatype* out) {
             else if (t == DBG_DECIMAL128) r = dbg_datatype{DBG_DECIMAL128, 38, (uint8_t)std::max<int>(s.arg.scale, 4), 0, 0};
             else return fail(DBG_ERR_UNSUPPORTED, "avg: unsupported argument type");
             break;
+        case DBG_AGG_AVG_SQL:  // divide's result type (EXP/types/decimal.rs:1015-1037; numbers: Float64)
+            if (is_signed_i(t) || is_unsigned_i(t) || is_float(t)) r.type = DBG_FLOAT64;
+            else if (t == DBG_DECIMAL128)
+                r = dbg_datatype{DBG_DECIMAL128, 38, (uint8_t)std::max<int>(s.arg.scale, std::min<int>(s.arg.scale + 6, 12)), 0, 0};
+            else return fail(DBG_ERR_UNSUPPORTED, "avg: unsupported argument type");
+            break;
         case DBG_AGG_MIN: case DBG_AGG_MAX:
             if (t == DBG_STRING || t == DBG_BOOLEAN) return fail(DBG_ERR_UNSUPPORTED, "min/max: String/Boolean arguments stay on the CPU path");
             if (t == DBG_DECIMAL128 && s.arg.precision > 18)
@@ -356,14 +369,15 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
         dbg_datatype rt;
         RETURN_IF(result_type_of(s, &rt));
         rtypes.push_back(rt);
-        A.kind = s.kind;
+        const bool sql_avg = s.kind == DBG_AGG_AVG_SQL;
+        A.kind = sql_avg ? DBG_AGG_AVG : s.kind;  // same state; only the result differs
         A.arg_type = s.kind == DBG_AGG_COUNT && s.arg.type < 0 ? -1 : s.arg.type;
         A.arg_nullable = A.arg_type >= 0 ? s.arg.nullable : 0;
         int t = A.arg_type;
         A.sumk = t == DBG_DECIMAL128 ? SUMK_I128 : (is_float(t) ? SUMK_F64 : SUMK_I64);
         A.mmk = is_unsigned_i(t) ? MMK_U64 : (is_float(t) ? MMK_F64 : MMK_I64);
         A.w0 = word;
-        switch (s.kind) {
+        switch (A.kind) {
             case DBG_AGG_COUNT: A.nwords = 1; break;
             case DBG_AGG_SUM: A.nwords = A.sumk == SUMK_I128 ? 2 : 1; break;
             case DBG_AGG_AVG: A.nwords = A.sumk == SUMK_I128 ? 3 : 2; break;
@@ -376,8 +390,10 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
         A.res_precision = rt.precision;
         A.res_scale = rt.scale;
         A.res_nullable = rt.nullable;
-        A.dec_check = (s.kind == DBG_AGG_SUM && t == DBG_DECIMAL128 && s.arg.precision <= 18) ? 1 : 0;
-        A.scale_add = (s.kind == DBG_AGG_AVG && t == DBG_DECIMAL128) ? (int)rt.scale - (int)s.arg.scale : 0;
+        // SUM's range check (DecimalSumState<OVERFLOW>, p <= 18) also guards AVG_SQL's sum
+        A.dec_check = ((s.kind == DBG_AGG_SUM || sql_avg) && t == DBG_DECIMAL128 && s.arg.precision <= 18) ? 1 : 0;
+        A.scale_add = (A.kind == DBG_AGG_AVG && t == DBG_DECIMAL128) ? (int)rt.scale - (int)s.arg.scale : 0;
+        A.avg_round = sql_avg && t == DBG_DECIMAL128;
         A.res_width = (int)type_width(rt.type);
     }
     if (flag_bits > 64) return fail(DBG_ERR_UNSUPPORTED, "too many nullable aggregates");
@@ -441,6 +457,17 @@ static TableDesc table_desc(dbg_agg_handle* h) {
     t.scratch = h->scratch;
     t.scr_blocks = h->scr_blocks;
     return t;
+}
+
+static int flush_deferred(dbg_agg_handle* h) {
+    if (!h->def_on) return DBG_OK;
+    h->def_on = false;
+    {
+        prof::Scope ps("agg_insert", h->stream);
+        launch_insert(h->stream, h->dspec, h->spec, h->dbatches, h->def_bid, h->def_rows, false, table_desc(h), true, &h->def_hb);
+    }
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
 }
 
 static u64 pow2_at_least(u64 x) {
@@ -812,6 +839,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
 int dbg_agg_set_stream(dbg_agg_handle* h, void* s) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     hipStream_t ns = s ? (hipStream_t)s : h->own_stream;
     if (ns != h->stream) {
         // device-side hand-off: work queued on the new stream waits for everything queued on the
@@ -827,6 +855,7 @@ int dbg_agg_set_stream(dbg_agg_handle* h, void* s) {
 int dbg_agg_reset(dbg_agg_handle* h) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
+    h->def_on = false;  // the held-back insert is discarded with the groups
     // inputs copied by earlier batches, and the pinned batch descriptors reused below, may still
     // be read by queued work: wait if any were queued since the last synchronisation
     if (!h->owned.empty() || h->uploads_pending) {
@@ -1278,6 +1307,7 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     if (!h || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
     if (rows >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "a batch holds fewer than 2^32 rows");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     h->finalized = false;
     if (rows == 0) return DBG_OK;
     const Spec& S = h->spec;
@@ -1317,6 +1347,13 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
         return DBG_OK;
     }
     RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
+    if (on_device && h->recycle && h->hcounters_dev && insert_can_fuse(S, *st, h->cap)) {  // held back: see def_on
+        h->def_on = true;
+        h->def_bid = bid;
+        h->def_rows = rows;
+        h->def_hb = *st;
+        return DBG_OK;
+    }
     {
         prof::Scope ps("agg_insert", h->stream);
         launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st);
@@ -1336,6 +1373,7 @@ static int ensure_buf(u64** p, u64* cap, u64 n) {
 int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     if (h->pp) return pp_finalize(h, n_groups, string_bytes);
     const Spec& S = h->spec;
     // Optimistic single round trip: count + scan are enqueued behind the inserts and read back
@@ -1393,6 +1431,7 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     if (!h->finalized) return fail(DBG_ERR_INVALID, "dbg_agg_finalize must precede dbg_agg_result");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     const Spec& S = h->spec;
     u64 n = h->n_groups;
     for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = h->result_types[a];
@@ -1586,6 +1625,8 @@ static int fin_launch(dbg_agg_handle* h) {
     RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
     TableDesc t = table_desc(h);
     const bool small = h->cap + 1 <= FIN_SMALL_SLOTS;
+    const bool fuse = h->def_on && !h->pp && small && h->hcounters_dev && insert_can_fuse(S, h->def_hb, h->cap);
+    if (!fuse) RETURN_IF(flush_deferred(h));
     u64* totals = h->d_pos + nb;
     if (!small && !h->pp) {
         prof::Scope ps("count_groups", h->stream);
@@ -1627,7 +1668,18 @@ static int fin_launch(dbg_agg_handle* h) {
     }
     F.zero_copy = small && h->hcounters_dev != nullptr;
     F.seq = ++h->fin_seq;
-    if (small) {
+    if (fuse) {  // the held-back insert and this finalize in one launch
+        FusedFin ff;
+        ff.out = od;
+        ff.totals = totals;
+        ff.host_mirror = h->hcounters_dev;
+        ff.seq = F.seq;
+        ff.recycle = h->recycle;
+        ff.on = 1;
+        h->def_on = false;
+        prof::Scope ps("agg_insert", h->stream);
+        launch_insert(h->stream, h->dspec, S, h->dbatches, h->def_bid, h->def_rows, false, t, true, &h->def_hb, &ff);
+    } else if (small) {
         prof::Scope ps("finalize_small", h->stream);
         launch_finalize_small(h->stream, h->dspec, h->dbatches, t, od, totals, F.zero_copy ? h->hcounters_dev : nullptr,
                               h->recycle && F.zero_copy, F.seq);
@@ -1758,6 +1810,7 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
     if (!h || !n_groups) return fail(DBG_ERR_INVALID, "null argument");
     if (!h->fin.active) return fail(DBG_ERR_INVALID, "no finalize in flight");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     for (int round = 0; round < 3; ++round) {
         if (round) RETURN_IF(fin_launch(h));
         bool retry = false;
@@ -1800,6 +1853,7 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
     if (n_parts < 1 || n_parts > 256) return fail(DBG_ERR_UNSUPPORTED, "1..256 partitions");
     if (scheme == 1 && (n_parts & (n_parts - 1))) return fail(DBG_ERR_INVALID, "radix partitions must be a power of two");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     if (h->pp) RETURN_IF(pp_finalize(h, nullptr, nullptr));
     else RETURN_IF(resolve_overflow(h));
     const Spec& S = h->spec;
@@ -1848,6 +1902,7 @@ int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strin
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     if (!h->part_n) return fail(DBG_ERR_INVALID, "dbg_agg_partition must precede dbg_agg_export_records");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     prof::Scope ps("export_records", h->stream);
     if (h->pp)
         launch_pp_grec_export(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, h->part_n, h->part_scheme, h->d_part_pos,
@@ -1873,6 +1928,7 @@ int dbg_agg_export_fixed(dbg_agg_handle* h, void* dev_buf, uint64_t cap_records)
     if (h->cap + 1 > FIN_SMALL_SLOTS || h->pp) return fail(DBG_ERR_UNSUPPORTED, "fixed export is for small tables");
     if (S.rec_width < 16) return fail(DBG_ERR_INTERNAL, "record narrower than the fixed header");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     prof::Scope ps("export_fixed", h->stream);
     launch_export_fixed(h->stream, h->dspec, h->dbatches, table_desc(h), (u8*)dev_buf, cap_records, h->recycle);
     HIPCHECK(hipGetLastError());
@@ -1893,6 +1949,7 @@ int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs,
     const u64 n = (u64)n_bufs * (cap_records + 1);
     if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     h->finalized = false;
     h->clean = false;
     BatchDesc* st;
@@ -1931,6 +1988,7 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
                           const uint64_t* seg_records, const uint64_t* seg_string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_deferred(h));
     h->finalized = false;
     h->clean = false;
     const Spec& S = h->spec;

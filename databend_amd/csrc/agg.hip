@@ -13,6 +13,7 @@
 // Bandwidth/atomic-bound integer work: no MFMA.  Every kernel is grid-strided over >= 2048
 // workgroups of 256 threads (64-wide waves) or over contiguous row ranges per workgroup.
 #include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <type_traits>
 
@@ -404,7 +405,7 @@ __device__ __forceinline__ void maybe_flush(const Spec& S, const BatchDesc* batc
 template <bool INLINE, bool RECORDS>
 __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
-                                                          u32 lds_slots, int xmode) {
+                                                          u32 lds_slots) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
@@ -432,9 +433,8 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         if (threadIdx.x == 0) qn = 0;
         __syncthreads();
         const u32 lane = __lane_id();
-        u64 sink = 0;
         for (u64 it = 0; it < n_iter; ++it) {
-            if (it && (it % FLUSH_ROUND) == 0 && xmode != 5 && xmode != 3) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
             const u64 i = r0 + it * BLOCK + threadIdx.x;
             const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
             const u64 m = __ballot(sel);
@@ -453,22 +453,12 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
                 __syncthreads();
                 if (threadIdx.x < rem) selq[threadIdx.x] = mv;
                 if (threadIdx.x == 0) qn = rem;
-                if (xmode == 0 || xmode == 5) insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + off, lds, lmask, sw, lcount, llimit, t, my_claims);
-                else if (xmode == 2) sink ^= group_hash(B.keys, S.n_keys, r0 + off);
-                else if (xmode == 3 || xmode == 4) {
-                    const u64 i = r0 + off;
-                    const u64 h = group_hash(B.keys, S.n_keys, i);
-                    const u64 key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
-                    int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
-                    if (ls >= 0) apply_row<AS_LDS>(S, asp<AS_LDS>(lds + (u64)ls * sw), B, i);
-                    else if (xmode == 4) insert_one<INLINE, RECORDS>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
-                }
+                insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + off, lds, lmask, sw, lcount, llimit, t, my_claims);
             }
             __syncthreads();  // the queue is settled before the next round appends
         }
-        if (xmode) asm volatile("" ::"v"(sink));
         const u32 n = qn;  // < BLOCK
-        if (threadIdx.x < n && xmode == 0)
+        if (threadIdx.x < n)
             insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + selq[threadIdx.x], lds, lmask, sw, lcount, llimit, t, my_claims);
     } else {
         for (u64 it = 0; it < n_iter; ++it) {
@@ -497,537 +487,6 @@ static u32 lds_slots_for(const Spec& S, u32 budget = LDS_BUDGET_BYTES) {
     u32 n = 1;
     while ((n * 2) * bytes_per + 16 <= budget) n *= 2;
     return n;
-}
-
-// ------------------------------------------------------------------------------------------
-// agg_insert_fast: one non-null integer key column, optional `key <cmp> constant` predicate on
-// that same column (GROUP BY x WHERE x <> c: ClickBench Q8; or no predicate: Q16).  Streams the
-// key column with 16-byte loads (4 in flight per lane), evaluates the predicate on every value,
-// and stages the selected rows in the LDS table exactly like agg_insert.
-// ------------------------------------------------------------------------------------------
-#define FAST_UNROLL 4
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-// Column data reached through a descriptor is a generic pointer to the compiler, which then
-// emits flat loads: those count against lgkmcnt too and retire out of order, so every LDS wait
-// (and every use of a loaded value) drains ALL loads in flight and the prefetch pipeline
-// collapses.  Streams read through this address-space-1 view compile to global_load.
-typedef const v4u __attribute__((address_space(1)))* gv4p;
-
-template <typename T>
-__device__ __forceinline__ bool fast_pred(T v, int op, i64 c) {
-    // the constant is in the column's domain (signed / unsigned by T)
-    T k = (T)c;
-    switch (op) {
-        case DBG_CMP_EQ: return v == k;
-        case DBG_CMP_NE: return v != k;
-        case DBG_CMP_LT: return v < k;
-        case DBG_CMP_LE: return v <= k;
-        case DBG_CMP_GT: return v > k;
-        default: return v >= k;
-    }
-}
-
-// Element j of a 16-byte vector viewed as T[16 / sizeof(T)], from registers (no address taken).
-template <typename T>
-__device__ __forceinline__ T vget(const v4u& y, int j) {
-    constexpr int W = sizeof(T);
-    if constexpr (W == 8) {
-        u32 lo = j ? y.z : y.x, hi = j ? y.w : y.y;
-        return (T)(((u64)hi << 32) | lo);
-    } else {
-        int wi = (j * W) >> 2;
-        u32 word = wi == 0 ? y.x : (wi == 1 ? y.y : (wi == 2 ? y.z : y.w));
-        return (T)(word >> (((j * W) & 3) * 8));
-    }
-}
-
-// Selected rows are appended to a per-wave LDS queue (ballot + mbcnt) and staged 64 at a time
-// with every lane active: at low selectivity (Q8: 0.63 %) a lane-divergent insert per row would
-// leave 63 of 64 lanes idle on every LDS round trip.
-#define WQ 128  // queue entries per wave
-#define WQW 384  // u64 words of per-wave queue space: rows (2 x WQ) or candidate vectors (WQ x (16 + 8) B)
-
-template <typename T, bool PRED, int NT, bool CO>
-__global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                               u32 bid, u64 rows, TableDesc t, u32 lds_slots,
-                                                               T lo, T hi, int negate, int xmode) {
-    extern __shared__ __attribute__((aligned(16))) u64 lds[];
-    constexpr int V = 16 / sizeof(T);
-    const Spec& S = *spec;
-    const BatchDesc& B = batches[bid];
-    const T* __restrict__ col = (const T*)B.keys[0].data;
-    const u32 sw = S.stride_words;
-    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);
-    const u32 lmask = lds_slots - 1;
-    const u32 llimit = lds_slots - lds_slots / 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // per-wave queue (keys and rows) after the table and its 16 bytes of counters
-    u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * WQW;
-    u64* qrow = qkey + WQ;
-    // candidate-vector queue (the `<> c` path below) over the same per-wave space
-    v4u* vq = (v4u*)qkey;
-    u64* vqb = qkey + 2 * WQ;
-    lds_table_init(S, lds, lds_slots, sw, NT);
-    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
-    __syncthreads();
-    u32 my_claims = 0;
-
-    // predicate in range form: lo <= v <= hi, xor negate (host maps =, <>, <, <=, >, >=)
-    auto pass = [&](T v) -> bool { return ((v >= lo) & (v <= hi)) ^ (negate != 0); };
-
-    // stage one selected row (key bits, row index) — all callers have full or near-full lanes
-    auto process = [&](u64 key, u64 i) {
-        int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
-        if (ls >= 0) {
-            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
-            if (CO) at_add<AS_LDS>(st + 1, 1ULL);
-            else apply_row<AS_LDS>(S, st, B, i);
-            return;
-        }
-        bool claimed;
-        u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
-        if (gs == ~0ULL) {
-            push_ovf_row(t, bid, i);
-            return;
-        }
-        my_claims += claimed ? 1 : 0;
-        wptr<AS_GLB> gst = asp<AS_GLB>(t.slots + gs * t.stride_words);
-        if (CO) at_add<AS_GLB>(gst + 1, 1ULL);
-        else apply_row<AS_GLB>(S, gst, B, i);
-    };
-
-    u32 qn = 0;  // wave-uniform queue length
-    auto drain64 = [&]() {  // process entries [0, 64), shift [64, qn) down
-        vwptr<AS_LDS> qk = (vwptr<AS_LDS>)qkey, qr = (vwptr<AS_LDS>)qrow;
-        u64 k = qk[lane], r = qr[lane];
-        u64 k2 = 0, r2 = 0;
-        bool mv = lane + 64 < (int)qn;
-        if (mv) {
-            k2 = qk[lane + 64];
-            r2 = qr[lane + 64];
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (mv) {
-            qk[lane] = k2;
-            qr[lane] = r2;
-        }
-        __builtin_amdgcn_wave_barrier();
-        qn -= 64;
-        process(k, r);
-    };
-
-    // `key <> c` (ClickBench Q8: AdvEngineID <> 0) as a two-level compaction.  A row-level
-    // queue pays the per-row mask + ballot-prefix VALU work on every lane (SQ counters: ~350
-    // VALU per 32-row round, VALU ~60 % busy); instead each 16-byte vector is tested whole —
-    // "some element differs from c" is three ORs of XORs — and only candidate vectors (4.9 % at
-    // Q8's selectivity) are appended, whole, to a per-wave LDS queue; 64 at a time they are
-    // expanded with every lane busy.  ~10 VALU per 8-row vector instead of ~90.
-    const bool neq_fast = PRED && negate && lo == hi;
-    u32 cc_lo, cc_hi;
-    {
-        typedef typename std::make_unsigned<T>::type UT;
-        const u64 c = (u64)(UT)lo;
-        if (sizeof(T) == 8) { cc_lo = (u32)c; cc_hi = (u32)(c >> 32); }
-        else if (sizeof(T) == 4) { cc_lo = cc_hi = (u32)c; }
-        else if (sizeof(T) == 2) { cc_lo = cc_hi = (u32)(c | (c << 16)); }
-        else { cc_lo = cc_hi = (u32)(c * 0x01010101u); }
-    }
-    u32 vqn = 0;  // wave-uniform candidate count
-    // expand candidate vectors [0, n) (n <= 64, one per lane), shift [64, vqn) down
-    auto drain_vec = [&](u32 n) {
-        v4u v = {0, 0, 0, 0};
-        u64 bs = 0;
-        const bool have = lane < (int)n;
-        if (have) {
-            v = ((volatile v4u*)vq)[lane];
-            bs = ((volatile u64*)vqb)[lane];
-        }
-        const bool mv = lane + 64 < (int)vqn;
-        v4u v2 = {0, 0, 0, 0};
-        u64 b2 = 0;
-        if (mv) {
-            v2 = ((volatile v4u*)vq)[lane + 64];
-            b2 = ((volatile u64*)vqb)[lane + 64];
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (mv) {
-            ((volatile v4u*)vq)[lane] = v2;
-            ((volatile u64*)vqb)[lane] = b2;
-        }
-        __builtin_amdgcn_wave_barrier();
-        vqn -= n;
-        u32 mm = 0;
-        if (have)
-#pragma unroll
-            for (int j = 0; j < V; ++j) mm |= (pass(vget<T>(v, j)) ? 1u : 0u) << j;
-        while (mm) {
-            const int j = __builtin_ctz(mm);
-            mm &= mm - 1;
-            // element j of v from registers (j is lane-varying here): select over the dwords
-            const int W = (int)sizeof(T);
-            const int wi = (j * W) >> 2;
-            const u32 w0 = wi == 0 ? v.x : (wi == 1 ? v.y : (wi == 2 ? v.z : v.w));
-            u64 key;
-            if (W == 8) {
-                const u32 w1 = wi == 0 ? v.y : v.w;
-                key = ((u64)w1 << 32) | w0;
-            } else {
-                const u32 sh = (u32)((j * W) & 3) * 8;
-                key = (u64)((w0 >> sh) & (W == 4 ? 0xFFFFFFFFu : ((1u << (8 * W)) - 1u)));
-            }
-            process(key, bs + j);
-        }
-    };
-    u32 sink = 0;  // experiment modes keep the loads alive through this
-    const u64 ltmask = (1ULL << lane) - 1;
-    auto key_of = [&](const v4u& y, int j) -> u64 { return (u64)(typename std::make_unsigned<T>::type)vget<T>(y, j); };
-    // Stage the selected rows of a group of NV vectors (one per lane and slot u), all lanes
-    // together.  A lane's vector slots hold rows base[u] .. base[u] + V - 1.
-    auto handle_group = [&](const v4u* y, const u64* base, int nv, u32 actm) {
-        if (xmode == 2) {
-            for (int u = 0; u < nv; ++u) sink ^= y[u].x ^ y[u].y ^ y[u].z ^ y[u].w;
-            return;
-        }
-        if (!PRED) {
-            for (int u = 0; u < nv; ++u)
-                if ((actm >> u) & 1)
-#pragma unroll
-                    for (int j = 0; j < V; ++j) process(key_of(y[u], j), base[u] + j);
-            return;
-        }
-        if (neq_fast && xmode != 5) {
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) {
-                const v4u& v = y[u];
-                const bool any = (((v.x ^ cc_lo) | (v.y ^ cc_hi) | (v.z ^ cc_lo) | (v.w ^ cc_hi)) != 0) && ((actm >> u) & 1);
-                const u64 b = __ballot(any);
-                if (b == 0) continue;
-                if (any) {
-                    const u32 pos = vqn + (u32)__popcll(b & ltmask);
-                    vq[pos] = v;
-                    vqb[pos] = base[u];
-                }
-                vqn += (u32)__popcll(b);
-                if (vqn >= 64) {
-                    __builtin_amdgcn_wave_barrier();
-                    drain_vec(64);
-                }
-            }
-            return;
-        }
-        u32 m[FAST_UNROLL];
-        u32 cnt = 0;
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) {
-            m[u] = 0;
-            if (u < nv) {
-#pragma unroll
-                for (int j = 0; j < V; ++j) m[u] |= (pass(vget<T>(y[u], j)) ? 1u : 0u) << j;
-            }
-            if (!((actm >> u) & 1)) m[u] = 0;
-            cnt += __popc(m[u]);
-        }
-        if (xmode == 1) {
-            sink ^= cnt;
-            return;
-        }
-        if (__ballot(cnt != 0) == 0) return;
-        // exclusive prefix and wave total of cnt (<= 32 = 6 bits) from one ballot per bit
-        u32 pre = 0, tot = 0;
-#pragma unroll
-        for (int bb = 0; bb < 6; ++bb) {
-            u64 bal = __ballot((cnt >> bb) & 1);
-            pre += (u32)__popcll(bal & ltmask) << bb;
-            tot += (u32)__popcll(bal) << bb;
-        }
-        if (xmode == 3) {  // timing experiment: ballots only
-            sink ^= pre;
-            qn = (qn + tot) & 63;
-            return;
-        }
-        if (qn + tot <= WQ) {
-            u32 pos = qn + pre;
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) {
-                u32 mm = m[u];
-                while (mm) {
-                    int j = __builtin_ctz(mm);
-                    mm &= mm - 1;
-                    qkey[pos] = key_of(y[u], j);
-                    qrow[pos] = base[u] + j;
-                    pos++;
-                }
-            }
-            qn += tot;
-            if (xmode == 4) {  // timing experiment: queue writes, no drain
-                qn &= 63;
-                return;
-            }
-            while (qn >= 64) {
-                __builtin_amdgcn_wave_barrier();
-                drain64();
-            }
-        } else {  // dense selection: lanes already busy, insert directly
-#pragma unroll
-            for (int u = 0; u < FAST_UNROLL; ++u) {
-                u32 mm = m[u];
-                while (mm) {
-                    int j = __builtin_ctz(mm);
-                    mm &= mm - 1;
-                    process(key_of(y[u], j), base[u] + j);
-                }
-            }
-        }
-    };
-
-    // Grid-strided stream (all waves of the chip sweep one window of the column together: DRAM
-    // rows stay open, scripts/micro/stream.hip): FAST_UNROLL unconditional 16-byte loads per lane
-    // per round (an index past the end is clamped and its lane-slot masked off), so no branch
-    // sits around the loads; other waves of the CU keep HBM busy while one filters.  The loop
-    // condition is wave-uniform (ballot) because the queue needs all 64 lanes.
-    const u64 nvec = rows / V;
-    gv4p vp = (gv4p)col;
-    const u64 gstride = (u64)gridDim.x * NT;
-    u64 k = (u64)blockIdx.x * NT + threadIdx.x;
-    const u64 step = (u64)FAST_UNROLL * gstride;
-    const u64 lastv = nvec ? nvec - 1 : 0;
-    // Software pipeline: the next round's FAST_UNROLL loads are issued before this round is
-    // filtered and queued, so a wave busy with its ballots and LDS queue writes still has
-    // 64 B/lane in flight (without it the per-round processing sits on the load critical path).
-    v4u y[FAST_UNROLL];
-#pragma unroll
-    for (int u = 0; u < FAST_UNROLL; ++u) {
-        u64 idx = k + u * gstride;
-        y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
-    }
-    while (__ballot(k < nvec) != 0) {
-        const u64 kn = k + step;
-        v4u yn[FAST_UNROLL];
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) {
-            u64 idx = kn + u * gstride;
-            yn[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
-        }
-        u64 bases[FAST_UNROLL];
-        u32 actm = 0;
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) {
-            u64 idx = k + u * gstride;
-            actm |= (idx < nvec ? 1u : 0u) << u;
-            bases[u] = idx * V;
-        }
-        handle_group(y, bases, FAST_UNROLL, actm);
-#pragma unroll
-        for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
-        k = kn;
-    }
-    if (PRED && vqn) {
-        __builtin_amdgcn_wave_barrier();
-        drain_vec(vqn);
-    }
-    // drain the queue's rest (< 64 entries): lanes below qn take one each
-    if (PRED && qn) {
-        __builtin_amdgcn_wave_barrier();
-        if (lane < (int)qn) process(((vwptr<AS_LDS>)qkey)[lane], ((vwptr<AS_LDS>)qrow)[lane]);
-        qn = 0;
-    }
-    for (u64 i = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; i < rows; i += gstride) {
-        T v = gld<T>(col + i);
-        if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
-    }
-    if (xmode) asm volatile("" ::"v"(sink));
-    __syncthreads();
-    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
-}
-
-
-// ------------------------------------------------------------------------------------------
-// agg_insert_sel: one non-null integer key column with a `key <op> c` predicate on itself
-// (ClickBench Q8: GROUP BY AdvEngineID WHERE AdvEngineID <> 0).  A grid-strided stream of
-// 16-byte nontemporal loads, SEL_UNROLL vectors in flight per lane (the shape that reads HBM
-// fastest, scripts/micro/stream.hip); the predicate is a branch-free range test on every value;
-// the few selected rows go straight into the workgroup's LDS table from their own lane (at 0.6 %
-// selectivity about one lane in six holds one selected row per round, so the divergent insert
-// costs a few hundred cycles per ~2k rows); block_flush merges the LDS tables at the end.
-// ------------------------------------------------------------------------------------------
-#define SEL_UNROLL 4
-template <typename T, int NT>
-__global__ void __launch_bounds__(NT) agg_insert_sel_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                           u32 bid, u64 rows, TableDesc t, u32 lds_slots, T lo, T hi, int negate,
-                                                           int count_only) {
-    extern __shared__ __attribute__((aligned(16))) u64 lds[];
-    constexpr int V = 16 / sizeof(T);
-    const Spec& S = *spec;
-    const BatchDesc& B = batches[bid];
-    const T* __restrict__ col = (const T*)B.keys[0].data;
-    const u32 sw = S.stride_words;
-    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);
-    const u32 lmask = lds_slots - 1;
-    const u32 llimit = lds_slots - lds_slots / 4;
-    lds_table_init(S, lds, lds_slots, sw, NT);
-    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
-    __syncthreads();
-    u32 my_claims = 0;
-    using UT = typename std::make_unsigned<T>::type;
-    auto process = [&](u64 key, u64 i) {
-        int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
-        if (ls >= 0) {
-            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
-            if (count_only) at_add<AS_LDS>(st + 1, 1ULL);
-            else apply_row<AS_LDS>(S, st, B, i);
-            return;
-        }
-        bool claimed;
-        u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
-        if (gs == ~0ULL) {
-            push_ovf_row(t, bid, i);
-            return;
-        }
-        my_claims += claimed ? 1 : 0;
-        apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
-    };
-    auto handle = [&](const v4u& y, u64 vi) {
-        u32 m = 0;
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            T v = vget<T>(y, j);
-            m |= (u32)(((v >= lo) & (v <= hi)) ^ (negate != 0)) << j;
-        }
-        while (m) {
-            int j = __builtin_ctz(m);
-            m &= m - 1;
-            process((u64)(UT)vget<T>(y, j), vi * V + j);
-        }
-    };
-    const u64 nvec = rows / V;
-    gv4p vp = (gv4p)col;
-    const u64 stride = (u64)gridDim.x * NT;
-    u64 i = (u64)blockIdx.x * NT + threadIdx.x;
-    for (; i + (SEL_UNROLL - 1) * stride < nvec; i += SEL_UNROLL * stride) {
-        v4u y[SEL_UNROLL];
-#pragma unroll
-        for (int u = 0; u < SEL_UNROLL; ++u) y[u] = __builtin_nontemporal_load(vp + i + u * stride);
-#pragma unroll
-        for (int u = 0; u < SEL_UNROLL; ++u) handle(y[u], i + u * stride);
-    }
-    for (; i < nvec; i += stride) handle(__builtin_nontemporal_load(vp + i), i);
-    // ragged tail (< V rows)
-    for (u64 r = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; r < rows; r += stride) {
-        T v = gld<T>(col + r);
-        if (((v >= lo) & (v <= hi)) ^ (negate != 0)) process((u64)(UT)v, r);
-    }
-    __syncthreads();
-    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
-}
-
-template <typename T>
-static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* batches, u32 bid, u64 rows, const TableDesc& t,
-                          u32 lslots, size_t table_bytes, bool pred, int op, i64 c, int count_only) {
-    constexpr u64 V = 16 / sizeof(T);
-    static const int xmode = getenv("DBG_FAST_XMODE") ? atoi(getenv("DBG_FAST_XMODE")) : 0;  // timing experiments only
-    // `v <op> c` as `(lo <= v <= hi) ^ negate`, exact over T's range (constants outside it fold)
-    typedef __int128 W;
-    const W tmin = (W)std::numeric_limits<T>::min(), tmax = (W)std::numeric_limits<T>::max();
-    const W C = std::is_signed<T>::value ? (W)c : (W)(u64)c;
-    W lo = 1, hi = 0;  // empty range
-    int neg = 0;
-    auto all = [&]() { lo = tmin; hi = tmax; };
-    switch (op) {
-        case DBG_CMP_EQ: if (C >= tmin && C <= tmax) lo = hi = C; break;
-        case DBG_CMP_NE: neg = 1; if (C >= tmin && C <= tmax) lo = hi = C; break;
-        case DBG_CMP_LT: if (C > tmax) all(); else if (C > tmin) { lo = tmin; hi = C - 1; } break;
-        case DBG_CMP_LE: if (C >= tmax) all(); else if (C >= tmin) { lo = tmin; hi = C; } break;
-        case DBG_CMP_GT: if (C < tmin) all(); else if (C < tmax) { lo = C + 1; hi = tmax; } break;
-        default: if (C <= tmin) all(); else if (C <= tmax) { lo = C; hi = tmax; } break;  // GE
-    }
-    if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
-    static const int sel_mode = getenv("DBG_SEL") ? atoi(getenv("DBG_SEL")) : 0;  // A/B knob: 1 = direct-insert kernel
-    if (pred && sel_mode && ((uintptr_t)batches != 0)) {
-        static const u64 sel_grid = getenv("DBG_SEL_GRID") ? strtoull(getenv("DBG_SEL_GRID"), nullptr, 10) : 512;
-        u64 nvec = rows / V;
-        u64 blocks = (nvec + 512 * SEL_UNROLL - 1) / (512 * SEL_UNROLL);
-        if (blocks > sel_grid) blocks = sel_grid;
-        if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
-        if (blocks < 1) blocks = 1;
-        hipLaunchKernelGGL((agg_insert_sel_kernel<T, 512>), dim3((u32)blocks), dim3(512), table_bytes, s, dspec, batches, bid, rows, t,
-                           lslots, (T)lo, (T)hi, neg, count_only);
-        return;
-    }
-    const int nt = 1024;
-    static const u64 max_blocks = getenv("DBG_FAST_MAXBLOCKS") ? strtoull(getenv("DBG_FAST_MAXBLOCKS"), nullptr, 10) : 256;
-    size_t shmem = table_bytes + (size_t)(nt / 64) * WQW * 8;
-    u64 quantum = V * (u64)nt * FAST_UNROLL;
-    u64 blocks = (rows + quantum - 1) / quantum;
-    if (blocks > max_blocks) blocks = max_blocks;
-    if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
-    if (blocks < 1) blocks = 1;
-#define FAST_LAUNCH(P, N, F)                                                                                                  \
-    hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, \
-                       lslots, (T)lo, (T)hi, neg, xmode)
-    // CO: COUNT(*) is the only aggregate (ClickBench Q8/Q16 shape) — the kernel then carries no
-    // apply_row code at all (smaller hot loop, fewer registers)
-    if (count_only) {
-        if (pred) FAST_LAUNCH(true, 1024, true); else FAST_LAUNCH(false, 1024, true);
-    } else {
-        if (pred) FAST_LAUNCH(true, 1024, false); else FAST_LAUNCH(false, 1024, false);
-    }
-#undef FAST_LAUNCH
-}
-
-// Host-side eligibility for the fast path (hb = host copy of the batch descriptor).
-static bool fast_eligible(const Spec& S, const BatchDesc& hb, bool records) {
-    if (records || !S.inline_keys || S.n_keys != 1 || S.key_types[0].nullable) return false;
-    const DCol& k = hb.keys[0];
-    int ty = k.type;
-    bool intlike = (ty >= DBG_INT8 && ty <= DBG_UINT64) || ty == DBG_DATE || ty == DBG_TIMESTAMP;
-    if (!intlike || k.layout != LAYOUT_ARROW || ((uintptr_t)k.data & 15)) return false;
-    if (hb.n_nodes == 0) return true;
-    if (hb.n_nodes != 1) return false;
-    const DNode& n = hb.nodes[0];
-    const DCol& f = hb.fcols[n.col];
-    return n.op == DBG_PRED_CMP_CONST && f.data == k.data && f.type == ty && !f.nullable;
-}
-
-void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, u32 bid, u64 rows, bool records,
-                   const TableDesc& t, bool use_lds, const BatchDesc* hb) {
-    if (rows == 0) return;
-    if (hb && use_lds && fast_eligible(S, *hb, records)) {
-        u32 lslots = lds_slots_for(S, 16 * 1024);
-        size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
-        bool pred = hb->n_nodes == 1;
-        int op = pred ? hb->nodes[0].cmp : 0;
-        i64 c = pred ? hb->nodes[0].i64v : 0;
-        int count_only = S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1;
-        switch (hb->keys[0].type) {
-            case DBG_INT8: launch_fast_t<int8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_UINT8: launch_fast_t<uint8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_INT16: launch_fast_t<int16_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_UINT16: launch_fast_t<uint16_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_INT32: case DBG_DATE: launch_fast_t<int32_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_UINT32: launch_fast_t<uint32_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_INT64: case DBG_TIMESTAMP: launch_fast_t<int64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-            case DBG_UINT64: launch_fast_t<uint64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only); return;
-        }
-    }
-    static const int gxmode = getenv("DBG_GEN_XMODE") ? atoi(getenv("DBG_GEN_XMODE")) : 0;  // timing experiments only
-    // LDS partial-table budget per workgroup (DBG_LDS_BYTES: A/B knob, default LDS_BUDGET_BYTES)
-    static const u32 lds_budget = getenv("DBG_LDS_BYTES") ? (u32)atoi(getenv("DBG_LDS_BYTES")) : (u32)LDS_BUDGET_BYTES;
-    u32 lslots = use_lds ? lds_slots_for(S, lds_budget) : 1;
-    // enough workgroups to fill 256 CUs several times over, each a contiguous row range
-    u64 min_rows_per_block = (u64)BLOCK * 16;
-    u64 blocks = (rows + min_rows_per_block - 1) / min_rows_per_block;
-    if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
-    if (blocks < 1) blocks = 1;
-    u64 rpb = (rows + blocks - 1) / blocks;
-    blocks = (rows + rpb - 1) / rpb;
-    size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
-    if (S.inline_keys) {
-        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
-        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
-    } else {
-        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
-        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, gxmode);
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1349,30 +808,32 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
 // ------------------------------------------------------------------------------------------
 #define FIN_NT 1024
 #define FIN_MAXPER (FIN_SMALL_SLOTS / FIN_NT)
-__global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                                TableDesc t, OutDesc out, u64* totals, u64* host_mirror,
-                                                                int recycle, u64 seq) {
-    const Spec& S = *spec;
+// The body, run by FIN_NT threads of one workgroup: the standalone kernel below, or the last
+// workgroup of a fused insert (agg_insert_fast with FusedFin::on).  `view` holds the slots to
+// read (t.slots, or a copy in LDS); the re-initialisation of a recycled table writes t.slots.
+template <int MAXPER>
+__device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDesc* batches, const TableDesc& t, const u64* view,
+                                                    const OutDesc& out, u64* totals, u64* host_mirror, int recycle, u64 seq) {
     __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
     __shared__ int do_recycle;
     const u64 n_slots = t.cap + 1;
-    const u32 per = (u32)((n_slots + FIN_NT - 1) / FIN_NT);  // <= FIN_MAXPER (host checks cap)
+    const u32 per = (u32)((n_slots + FIN_NT - 1) / FIN_NT);  // <= MAXPER (host checks cap)
     const u64 base = (u64)threadIdx.x * per;
     const bool ref_strings = S.has_strings && !S.inline_keys;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (threadIdx.x == 0)
         do_recycle = recycle && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
-    u64 ent[FIN_MAXPER];
+    u64 ent[MAXPER];
 #pragma unroll
-    for (u32 k = 0; k < FIN_MAXPER; ++k) {
+    for (u32 k = 0; k < MAXPER; ++k) {
         u64 s = base + k;
-        ent[k] = (k < per && s < n_slots) ? gld<u64>(t.slots + s * t.stride_words) : SLOT_EMPTY;
+        ent[k] = (k < per && s < n_slots) ? view[s * t.stride_words] : SLOT_EMPTY;
     }
     u64 cnt = 0, sb[DBG_MAX_KEYS];
     u32 occ = 0;  // occupied owned slots (bit k = slot base + k)
     for (int c = 0; c < DBG_MAX_KEYS; ++c) sb[c] = 0;
 #pragma unroll
-    for (u32 k = 0; k < FIN_MAXPER; ++k) {
+    for (u32 k = 0; k < MAXPER; ++k) {
         if (ent[k] == SLOT_EMPTY) continue;
         cnt++;
         occ |= 1u << k;
@@ -1419,8 +880,8 @@ __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __re
         const u32 k = __builtin_ctz(occ);
         occ &= occ - 1;
         const u64 s = base + k;
-        const u64* st = t.slots + s * t.stride_words;
-        write_group(S, batches, t, s, st, gld<u64>(st), p, sp, out);
+        const u64* st = view + s * t.stride_words;
+        write_group(S, batches, t, s, st, st[0], p, sp, out);
         p++;
     }
     __syncthreads();  // validity bytes of every row are written; every state word has been read
@@ -1487,10 +948,472 @@ __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __re
     }
 }
 
+__global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                TableDesc t, OutDesc out, u64* totals, u64* host_mirror,
+                                                                int recycle, u64 seq) {
+    finalize_small_body<FIN_MAXPER>(*spec, batches, t, t.slots, out, totals, host_mirror, recycle, seq);
+}
+
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
                            u64* totals, u64* host_mirror, int recycle, u64 seq) {
     hipLaunchKernelGGL(finalize_small_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, out, totals, host_mirror, recycle,
                        seq);
+}
+
+// The last workgroup of an insert launch finalizes the table (FusedFin).  Hand-off
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms: agent atomics / sc1 stores on
+// the producer side, the workgroup whose ticket add came last as the consumer, sc1 global loads
+// of every handed-off byte): every table word of this launch was written by agent-scope atomics
+// (g_find's CAS, apply_row / apply_state) and read back only by sc1 loads (g_find's volatile
+// entry loads, ld_sc1 here); every wave drains its memory operations and the barrier orders
+// them before lane 0's ticket add.  The last workgroup copies the table into LDS with sc1 loads
+// and runs the finalize_small body on the copy (recycle re-initialises t.slots directly).
+__device__ __forceinline__ void fused_finalize(const Spec& S, const BatchDesc* batches, const TableDesc& t, u64* lds,
+                                               const FusedFin& ff) {
+    __shared__ u32 is_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 tk = atomicAdd((unsigned long long*)(t.counters + CNT_FIN_TICKET), 1ULL);
+        is_last = tk == (u64)gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    const u64 n = (t.cap + 1) * t.stride_words;  // host: <= the launch's dynamic LDS
+    for (u64 i = threadIdx.x; i < n; i += FIN_NT) lds[i] = ld_sc1(t.slots + i);
+    if (threadIdx.x == 0) atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
+    __syncthreads();
+    finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq);
+}
+
+// ------------------------------------------------------------------------------------------
+// agg_insert_fast: one non-null integer key column, optional `key <cmp> constant` predicate on
+// that same column (GROUP BY x WHERE x <> c: ClickBench Q8; or no predicate: Q16).  Streams the
+// key column with 16-byte loads (4 in flight per lane), evaluates the predicate on every value,
+// and stages the selected rows in the LDS table exactly like agg_insert.
+// ------------------------------------------------------------------------------------------
+#define FAST_UNROLL 4
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+// Column data reached through a descriptor is a generic pointer to the compiler, which then
+// emits flat loads: those count against lgkmcnt too and retire out of order, so every LDS wait
+// (and every use of a loaded value) drains ALL loads in flight and the prefetch pipeline
+// collapses.  Streams read through this address-space-1 view compile to global_load.
+typedef const v4u __attribute__((address_space(1)))* gv4p;
+
+template <typename T>
+__device__ __forceinline__ bool fast_pred(T v, int op, i64 c) {
+    // the constant is in the column's domain (signed / unsigned by T)
+    T k = (T)c;
+    switch (op) {
+        case DBG_CMP_EQ: return v == k;
+        case DBG_CMP_NE: return v != k;
+        case DBG_CMP_LT: return v < k;
+        case DBG_CMP_LE: return v <= k;
+        case DBG_CMP_GT: return v > k;
+        default: return v >= k;
+    }
+}
+
+// Element j of a 16-byte vector viewed as T[16 / sizeof(T)], from registers (no address taken).
+template <typename T>
+__device__ __forceinline__ T vget(const v4u& y, int j) {
+    constexpr int W = sizeof(T);
+    if constexpr (W == 8) {
+        u32 lo = j ? y.z : y.x, hi = j ? y.w : y.y;
+        return (T)(((u64)hi << 32) | lo);
+    } else {
+        int wi = (j * W) >> 2;
+        u32 word = wi == 0 ? y.x : (wi == 1 ? y.y : (wi == 2 ? y.z : y.w));
+        return (T)(word >> (((j * W) & 3) * 8));
+    }
+}
+
+// Selected rows are appended to a per-wave LDS queue (ballot + mbcnt) and staged 64 at a time
+// with every lane active: at low selectivity (Q8: 0.63 %) a lane-divergent insert per row would
+// leave 63 of 64 lanes idle on every LDS round trip.
+#define WQ 128  // queue entries per wave
+#define WQW 384  // u64 words of per-wave queue space: rows (2 x WQ) or candidate vectors (WQ x (16 + 8) B)
+
+template <typename T, bool PRED, int NT, bool CO>
+__global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                               u32 bid, u64 rows, TableDesc t, u32 lds_slots,
+                                                               T lo, T hi, int negate, FusedFin ff) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    constexpr int V = 16 / sizeof(T);
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    const T* __restrict__ col = (const T*)B.keys[0].data;
+    const u32 sw = S.stride_words;
+    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // per-wave queue (keys and rows) after the table and its 16 bytes of counters
+    u64* qkey = lds + (u64)lds_slots * sw + 2 + (u64)wave * WQW;
+    u64* qrow = qkey + WQ;
+    // candidate-vector queue (the `<> c` path below) over the same per-wave space
+    v4u* vq = (v4u*)qkey;
+    u64* vqb = qkey + 2 * WQ;
+    lds_table_init(S, lds, lds_slots, sw, NT);
+    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
+    __syncthreads();
+    u32 my_claims = 0;
+
+    // predicate in range form: lo <= v <= hi, xor negate (host maps =, <>, <, <=, >, >=)
+    auto pass = [&](T v) -> bool { return ((v >= lo) & (v <= hi)) ^ (negate != 0); };
+
+    // stage one selected row (key bits, row index) — all callers have full or near-full lanes
+    auto process = [&](u64 key, u64 i) {
+        int ls = lds_find<true>(S, batches, nullptr, i, key, 0, lds, lmask, sw, lcount, llimit);
+        if (ls >= 0) {
+            wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
+            if (CO) at_add<AS_LDS>(st + 1, 1ULL);
+            else apply_row<AS_LDS>(S, st, B, i);
+            return;
+        }
+        bool claimed;
+        u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_row(t, bid, i);
+            return;
+        }
+        my_claims += claimed ? 1 : 0;
+        wptr<AS_GLB> gst = asp<AS_GLB>(t.slots + gs * t.stride_words);
+        if (CO) at_add<AS_GLB>(gst + 1, 1ULL);
+        else apply_row<AS_GLB>(S, gst, B, i);
+    };
+
+    u32 qn = 0;  // wave-uniform queue length
+    auto drain64 = [&]() {  // process entries [0, 64), shift [64, qn) down
+        vwptr<AS_LDS> qk = (vwptr<AS_LDS>)qkey, qr = (vwptr<AS_LDS>)qrow;
+        u64 k = qk[lane], r = qr[lane];
+        u64 k2 = 0, r2 = 0;
+        bool mv = lane + 64 < (int)qn;
+        if (mv) {
+            k2 = qk[lane + 64];
+            r2 = qr[lane + 64];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (mv) {
+            qk[lane] = k2;
+            qr[lane] = r2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        qn -= 64;
+        process(k, r);
+    };
+
+    // `key <> c` (ClickBench Q8: AdvEngineID <> 0) as a two-level compaction.  A row-level
+    // queue pays the per-row mask + ballot-prefix VALU work on every lane (SQ counters: ~350
+    // VALU per 32-row round, VALU ~60 % busy); instead each 16-byte vector is tested whole —
+    // "some element differs from c" is three ORs of XORs — and only candidate vectors (4.9 % at
+    // Q8's selectivity) are appended, whole, to a per-wave LDS queue; 64 at a time they are
+    // expanded with every lane busy.  ~10 VALU per 8-row vector instead of ~90.
+    const bool neq_fast = PRED && negate && lo == hi;
+    u32 cc_lo, cc_hi;
+    {
+        typedef typename std::make_unsigned<T>::type UT;
+        const u64 c = (u64)(UT)lo;
+        if (sizeof(T) == 8) { cc_lo = (u32)c; cc_hi = (u32)(c >> 32); }
+        else if (sizeof(T) == 4) { cc_lo = cc_hi = (u32)c; }
+        else if (sizeof(T) == 2) { cc_lo = cc_hi = (u32)(c | (c << 16)); }
+        else { cc_lo = cc_hi = (u32)(c * 0x01010101u); }
+    }
+    u32 vqn = 0;  // wave-uniform candidate count
+    // expand candidate vectors [0, n) (n <= 64, one per lane), shift [64, vqn) down
+    auto drain_vec = [&](u32 n) {
+        v4u v = {0, 0, 0, 0};
+        u64 bs = 0;
+        const bool have = lane < (int)n;
+        if (have) {
+            v = ((volatile v4u*)vq)[lane];
+            bs = ((volatile u64*)vqb)[lane];
+        }
+        const bool mv = lane + 64 < (int)vqn;
+        v4u v2 = {0, 0, 0, 0};
+        u64 b2 = 0;
+        if (mv) {
+            v2 = ((volatile v4u*)vq)[lane + 64];
+            b2 = ((volatile u64*)vqb)[lane + 64];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (mv) {
+            ((volatile v4u*)vq)[lane] = v2;
+            ((volatile u64*)vqb)[lane] = b2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        vqn -= n;
+        u32 mm = 0;
+        if (have)
+#pragma unroll
+            for (int j = 0; j < V; ++j) mm |= (pass(vget<T>(v, j)) ? 1u : 0u) << j;
+        while (mm) {
+            const int j = __builtin_ctz(mm);
+            mm &= mm - 1;
+            // element j of v from registers (j is lane-varying here): select over the dwords
+            const int W = (int)sizeof(T);
+            const int wi = (j * W) >> 2;
+            const u32 w0 = wi == 0 ? v.x : (wi == 1 ? v.y : (wi == 2 ? v.z : v.w));
+            u64 key;
+            if (W == 8) {
+                const u32 w1 = wi == 0 ? v.y : v.w;
+                key = ((u64)w1 << 32) | w0;
+            } else {
+                const u32 sh = (u32)((j * W) & 3) * 8;
+                key = (u64)((w0 >> sh) & (W == 4 ? 0xFFFFFFFFu : ((1u << (8 * W)) - 1u)));
+            }
+            process(key, bs + j);
+        }
+    };
+    const u64 ltmask = (1ULL << lane) - 1;
+    auto key_of = [&](const v4u& y, int j) -> u64 { return (u64)(typename std::make_unsigned<T>::type)vget<T>(y, j); };
+    // Stage the selected rows of a group of NV vectors (one per lane and slot u), all lanes
+    // together.  A lane's vector slots hold rows base[u] .. base[u] + V - 1.
+    auto handle_group = [&](const v4u* y, const u64* base, int nv, u32 actm) {
+        if (!PRED) {
+            for (int u = 0; u < nv; ++u)
+                if ((actm >> u) & 1)
+#pragma unroll
+                    for (int j = 0; j < V; ++j) process(key_of(y[u], j), base[u] + j);
+            return;
+        }
+        if (neq_fast) {
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                const v4u& v = y[u];
+                const bool any = (((v.x ^ cc_lo) | (v.y ^ cc_hi) | (v.z ^ cc_lo) | (v.w ^ cc_hi)) != 0) && ((actm >> u) & 1);
+                const u64 b = __ballot(any);
+                if (b == 0) continue;
+                if (any) {
+                    const u32 pos = vqn + (u32)__popcll(b & ltmask);
+                    vq[pos] = v;
+                    vqb[pos] = base[u];
+                }
+                vqn += (u32)__popcll(b);
+                if (vqn >= 64) {
+                    __builtin_amdgcn_wave_barrier();
+                    drain_vec(64);
+                }
+            }
+            return;
+        }
+        u32 m[FAST_UNROLL];
+        u32 cnt = 0;
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) {
+            m[u] = 0;
+            if (u < nv) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) m[u] |= (pass(vget<T>(y[u], j)) ? 1u : 0u) << j;
+            }
+            if (!((actm >> u) & 1)) m[u] = 0;
+            cnt += __popc(m[u]);
+        }
+        if (__ballot(cnt != 0) == 0) return;
+        // exclusive prefix and wave total of cnt (<= 32 = 6 bits) from one ballot per bit
+        u32 pre = 0, tot = 0;
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) {
+            u64 bal = __ballot((cnt >> bb) & 1);
+            pre += (u32)__popcll(bal & ltmask) << bb;
+            tot += (u32)__popcll(bal) << bb;
+        }
+        if (qn + tot <= WQ) {
+            u32 pos = qn + pre;
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u32 mm = m[u];
+                while (mm) {
+                    int j = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    qkey[pos] = key_of(y[u], j);
+                    qrow[pos] = base[u] + j;
+                    pos++;
+                }
+            }
+            qn += tot;
+            while (qn >= 64) {
+                __builtin_amdgcn_wave_barrier();
+                drain64();
+            }
+        } else {  // dense selection: lanes already busy, insert directly
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                u32 mm = m[u];
+                while (mm) {
+                    int j = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    process(key_of(y[u], j), base[u] + j);
+                }
+            }
+        }
+    };
+
+    // Grid-strided stream (all waves of the chip sweep one window of the column together: DRAM
+    // rows stay open, scripts/micro/stream.hip): FAST_UNROLL unconditional 16-byte loads per lane
+    // per round (an index past the end is clamped and its lane-slot masked off), so no branch
+    // sits around the loads; other waves of the CU keep HBM busy while one filters.  The loop
+    // condition is wave-uniform (ballot) because the queue needs all 64 lanes.
+    const u64 nvec = rows / V;
+    gv4p vp = (gv4p)col;
+    const u64 gstride = (u64)gridDim.x * NT;
+    u64 k = (u64)blockIdx.x * NT + threadIdx.x;
+    const u64 step = (u64)FAST_UNROLL * gstride;
+    const u64 lastv = nvec ? nvec - 1 : 0;
+    // Software pipeline: the next round's FAST_UNROLL loads are issued before this round is
+    // filtered and queued, so a wave busy with its ballots and LDS queue writes still has
+    // 64 B/lane in flight (without it the per-round processing sits on the load critical path).
+    v4u y[FAST_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FAST_UNROLL; ++u) {
+        u64 idx = k + u * gstride;
+        y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+    }
+    while (__ballot(k < nvec) != 0) {
+        const u64 kn = k + step;
+        v4u yn[FAST_UNROLL];
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) {
+            u64 idx = kn + u * gstride;
+            yn[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+        }
+        u64 bases[FAST_UNROLL];
+        u32 actm = 0;
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) {
+            u64 idx = k + u * gstride;
+            actm |= (idx < nvec ? 1u : 0u) << u;
+            bases[u] = idx * V;
+        }
+        handle_group(y, bases, FAST_UNROLL, actm);
+#pragma unroll
+        for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
+        k = kn;
+    }
+    if (PRED && vqn) {
+        __builtin_amdgcn_wave_barrier();
+        drain_vec(vqn);
+    }
+    // drain the queue's rest (< 64 entries): lanes below qn take one each
+    if (PRED && qn) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane < (int)qn) process(((vwptr<AS_LDS>)qkey)[lane], ((vwptr<AS_LDS>)qrow)[lane]);
+        qn = 0;
+    }
+    for (u64 i = nvec * V + (u64)blockIdx.x * NT + threadIdx.x; i < rows; i += gstride) {
+        T v = gld<T>(col + i);
+        if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
+    }
+    __syncthreads();
+    block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
+    if (ff.on) fused_finalize(S, batches, t, lds, ff);
+}
+
+
+static size_t fast_shmem(size_t table_bytes) { return table_bytes + (size_t)(1024 / 64) * WQW * 8; }
+static size_t fast_table_bytes(const Spec& S) { return (size_t)lds_slots_for(S, 16 * 1024) * S.stride_words * 8 + 16; }
+
+template <typename T>
+static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* batches, u32 bid, u64 rows, const TableDesc& t,
+                          u32 lslots, size_t table_bytes, bool pred, int op, i64 c, int count_only, const FusedFin* fused) {
+    constexpr u64 V = 16 / sizeof(T);
+    // `v <op> c` as `(lo <= v <= hi) ^ negate`, exact over T's range (constants outside it fold)
+    typedef __int128 W;
+    const W tmin = (W)std::numeric_limits<T>::min(), tmax = (W)std::numeric_limits<T>::max();
+    const W C = std::is_signed<T>::value ? (W)c : (W)(u64)c;
+    W lo = 1, hi = 0;  // empty range
+    int neg = 0;
+    auto all = [&]() { lo = tmin; hi = tmax; };
+    switch (op) {
+        case DBG_CMP_EQ: if (C >= tmin && C <= tmax) lo = hi = C; break;
+        case DBG_CMP_NE: neg = 1; if (C >= tmin && C <= tmax) lo = hi = C; break;
+        case DBG_CMP_LT: if (C > tmax) all(); else if (C > tmin) { lo = tmin; hi = C - 1; } break;
+        case DBG_CMP_LE: if (C >= tmax) all(); else if (C >= tmin) { lo = tmin; hi = C; } break;
+        case DBG_CMP_GT: if (C < tmin) all(); else if (C < tmax) { lo = C + 1; hi = tmax; } break;
+        default: if (C <= tmin) all(); else if (C <= tmax) { lo = C; hi = tmax; } break;  // GE
+    }
+    if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
+    const int nt = 1024;
+    static_assert(FIN_NT == 1024, "the fused finalize runs on the insert's workgroup");
+    const u64 max_blocks = 256;  // one 1024-lane workgroup per CU
+    size_t shmem = fast_shmem(table_bytes);
+    FusedFin ff;
+    if (fused) ff = *fused;
+    else memset(&ff, 0, sizeof(ff));
+    u64 quantum = V * (u64)nt * FAST_UNROLL;
+    u64 blocks = (rows + quantum - 1) / quantum;
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
+    if (blocks < 1) blocks = 1;
+#define FAST_LAUNCH(P, N, F)                                                                                                  \
+    hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, \
+                       lslots, (T)lo, (T)hi, neg, ff)
+    // CO: COUNT(*) is the only aggregate (ClickBench Q8/Q16 shape) — the kernel then carries no
+    // apply_row code at all (smaller hot loop, fewer registers)
+    if (count_only) {
+        if (pred) FAST_LAUNCH(true, 1024, true); else FAST_LAUNCH(false, 1024, true);
+    } else {
+        if (pred) FAST_LAUNCH(true, 1024, false); else FAST_LAUNCH(false, 1024, false);
+    }
+#undef FAST_LAUNCH
+}
+
+// Host-side eligibility for the fast path (hb = host copy of the batch descriptor).
+static bool fast_eligible(const Spec& S, const BatchDesc& hb, bool records) {
+    if (records || !S.inline_keys || S.n_keys != 1 || S.key_types[0].nullable) return false;
+    const DCol& k = hb.keys[0];
+    int ty = k.type;
+    bool intlike = (ty >= DBG_INT8 && ty <= DBG_UINT64) || ty == DBG_DATE || ty == DBG_TIMESTAMP;
+    if (!intlike || k.layout != LAYOUT_ARROW || ((uintptr_t)k.data & 15)) return false;
+    if (hb.n_nodes == 0) return true;
+    if (hb.n_nodes != 1) return false;
+    const DNode& n = hb.nodes[0];
+    const DCol& f = hb.fcols[n.col];
+    return n.op == DBG_PRED_CMP_CONST && f.data == k.data && f.type == ty && !f.nullable;
+}
+
+bool insert_can_fuse(const Spec& S, const BatchDesc& hb, u64 cap) {
+    return hb.rows > 0 && fast_eligible(S, hb, false) && cap + 1 <= FUSED_FIN_SLOTS &&
+           (cap + 1) * S.stride_words * 8 <= fast_shmem(fast_table_bytes(S));
+}
+
+void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, u32 bid, u64 rows, bool records,
+                   const TableDesc& t, bool use_lds, const BatchDesc* hb, const FusedFin* fused) {
+    if (rows == 0) return;
+    if (hb && use_lds && fast_eligible(S, *hb, records)) {
+        u32 lslots = lds_slots_for(S, 16 * 1024);
+        size_t shmem = fast_table_bytes(S);
+        bool pred = hb->n_nodes == 1;
+        int op = pred ? hb->nodes[0].cmp : 0;
+        i64 c = pred ? hb->nodes[0].i64v : 0;
+        int count_only = S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1;
+        switch (hb->keys[0].type) {
+            case DBG_INT8: launch_fast_t<int8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_UINT8: launch_fast_t<uint8_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_INT16: launch_fast_t<int16_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_UINT16: launch_fast_t<uint16_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_INT32: case DBG_DATE: launch_fast_t<int32_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_UINT32: launch_fast_t<uint32_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_INT64: case DBG_TIMESTAMP: launch_fast_t<int64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+            case DBG_UINT64: launch_fast_t<uint64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
+        }
+    }
+    u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
+    // enough workgroups to fill 256 CUs several times over, each a contiguous row range
+    u64 min_rows_per_block = (u64)BLOCK * 16;
+    u64 blocks = (rows + min_rows_per_block - 1) / min_rows_per_block;
+    if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
+    if (blocks < 1) blocks = 1;
+    u64 rpb = (rows + blocks - 1) / blocks;
+    blocks = (rows + rpb - 1) / rpb;
+    size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
+    if (S.inline_keys) {
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+    } else {
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+    }
 }
 
 // Fused finalize tail: bit-pack every nullable output's validity and close the string offsets,

@@ -86,7 +86,7 @@ struct TableDesc {
 #define SCR_GROUP 16
 #define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
-enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_WORDS = 8 };
+enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_FIN_TICKET = 6, CNT_WORDS = 8 };
 enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4 };
 
 // ---- device helpers shared by agg.hip and part.hip ----
@@ -151,6 +151,7 @@ __device__ __forceinline__ u64 ld_sc1(const u64* p) {
     return __hip_atomic_load((wptr<AS_GLB>)(u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+struct FusedFin;
 // ---- launch wrappers (agg.hip) ----
 // part.hip: radix-partitioned COUNT(*) insert for high-cardinality single integer keys
 u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap);  // 0 = not eligible
@@ -159,7 +160,8 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
                               size_t temp_bytes, u64* sorted, u64* bounds, const char** step);
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
-                   bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr);
+                   bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr,
+                   const FusedFin* fused = nullptr);
 void launch_retry(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                   u64 n_rows, u64 n_recs, const u64* rows_list, const u64* recs_list);
 void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const u64* old_slots,
@@ -185,6 +187,19 @@ void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* ba
                            u64* totals, u64* host_mirror /* mapped pinned: counters, totals, recycled, seq */,
                            int recycle, u64 seq);
 void launch_finish_outputs(hipStream_t s, const OutDesc& out, const u64* totals, int n_keys, int n_aggs);
+// finalize_small fused into the fast insert: the last workgroup to finish runs it (one launch per
+// batch).  Tables of at most FUSED_FIN_SLOTS slots whose copy fits the insert's LDS.
+#define FUSED_FIN_SLOTS 2048
+struct FusedFin {
+    OutDesc out;
+    u64* totals;
+    u64* host_mirror;
+    u64 seq;
+    int recycle;
+    int on;
+};
+// host side: would launch_insert of this batch take the fast kernel (and so could fuse)?
+bool insert_can_fuse(const Spec& S, const BatchDesc& hb, u64 cap);
 void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                           const u64* pos /* scanned hist */, const u64* str_pos, const OutDesc& out);
 void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);

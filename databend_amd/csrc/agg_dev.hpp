@@ -144,6 +144,48 @@ __device__ __forceinline__ U128 u128_div_u64(U128 a, u64 d) {
     q.lo = lo;
     return q;
 }
+// (hi:lo) / d for hi < d: the quotient fits 64 bits; *r = remainder
+__device__ __forceinline__ u64 div128_64(u64 hi, u64 lo, u64 d, u64* r) {
+    u64 q = 0, rr = hi;
+    for (int b = 63; b >= 0; --b) {
+        u64 top = rr >> 63;
+        rr = (rr << 1) | ((lo >> b) & 1);
+        if (top || rr >= d) {
+            rr -= d;
+            q |= 1ULL << b;
+        }
+    }
+    *r = rr;
+    return q;
+}
+// SQL avg's decimal divide: do_round_div(sum, count, k) (EXP/types/decimal.rs:480-489) — in
+// 256-bit arithmetic (sum * 10^k +- count / 2) / count, truncated toward zero, low 128 bits.
+// |sum| * 10^k (k <= 12) spans at most 192 bits; count > 0.
+__device__ __forceinline__ U128 dec_round_div(u64 lo, u64 hi, int k, u64 d) {
+    const bool neg = (i64)hi < 0;
+    U128 m{lo, hi};
+    if (neg) m = u128_neg(m);
+    u64 p = 1;
+    for (int i = 0; i < k; ++i) p *= 10;
+    // 192-bit product [l0, l1, l2]
+    u64 l0 = m.lo * p, c0 = __umul64hi(m.lo, p);
+    u64 t1 = m.hi * p, l2 = __umul64hi(m.hi, p);
+    u64 l1 = t1 + c0;
+    l2 += l1 < t1 ? 1 : 0;
+    // + d / 2 (same magnitude rounding for both signs: truncation is symmetric)
+    const u64 half = d >> 1;
+    u64 n0 = l0 + half;
+    if (n0 < l0) {
+        l1 += 1;
+        if (l1 == 0) l2 += 1;
+    }
+    u64 r;
+    div128_64(0, l2, d, &r);  // the quotient's top limb is dropped (low 128 bits)
+    u64 q1 = div128_64(r, l1, d, &r);
+    u64 q0 = div128_64(r, n0, d, &r);
+    U128 q{q0, q1};
+    return neg ? u128_neg(q) : q;
+}
 // 10^38 - 1 = 0x4B3B4CA85A86C47A_098A223FFFFFFFFF
 #define DEC38_MAX_HI 0x4B3B4CA85A86C47AULL
 #define DEC38_MAX_LO 0x098A223FFFFFFFFFULL
@@ -190,7 +232,12 @@ __device__ __forceinline__ bool agg_result(const Spec& S, const DAgg& A, const u
                 lo = hi = 0;
                 break;
             }
-            if (A.sumk == SUMK_I128) {
+            if (A.avg_round) {  // SQL avg on Decimal128: SUM's range check, then the rounding divide
+                if (A.dec_check && dec38_out_of_range(w[0], w[1])) atomicOr((unsigned long long*)err, (unsigned long long)ERR_DEC_OVERFLOW);
+                U128 q = dec_round_div(w[0], w[1], A.scale_add, cnt);
+                lo = q.lo;
+                hi = q.hi;
+            } else if (A.sumk == SUMK_I128) {
                 U128 m{w[0], w[1]};
                 bool neg = (i64)w[1] < 0;
                 if (neg) m = u128_neg(m);

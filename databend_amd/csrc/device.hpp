@@ -394,6 +394,7 @@ struct DAgg {
     uint8_t res_precision, res_scale, res_nullable, dec_check;  // dec_check: SUM p<=18 range check
     int32_t scale_add;  // AVG decimal
     int32_t res_width;
+    int32_t avg_round;  // AVG_SQL on Decimal128: round-half-away divide (kind is DBG_AGG_AVG)
 };
 
 // Monotone map of OrderedFloat<f64> onto u64 (NaN canonical & greatest).

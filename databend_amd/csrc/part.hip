@@ -241,12 +241,6 @@ template <typename U>
 hipError_t sort_t(void* temp, size_t& temp_bytes, const void* keys, u64* out, u64 rows, u32 b0, u32 b1, hipStream_t s) {
     auto it = rocprim::make_transform_iterator((const U*)keys, MixOf<U>());
     hipError_t e = rocprim::radix_sort_keys(temp, temp_bytes, it, out, (size_t)rows, b0, b1, s);
-    if (e != hipSuccess && temp && getenv("DBG_PART_DEBUG")) {
-        fprintf(stderr, "radix_sort_keys failed: %s (rows %llu bits [%u,%u) temp %zu); debug rerun:\n", hipGetErrorString(e),
-                (unsigned long long)rows, b0, b1, temp_bytes);
-        e = rocprim::radix_sort_keys(temp, temp_bytes, it, out, (size_t)rows, b0, b1, s, true);
-        fprintf(stderr, "debug rerun: %s\n", hipGetErrorString(e));
-    }
     return e;
 }
 
@@ -266,17 +260,15 @@ u32 log2u(u64 x) { return 63 - __builtin_clzll(x); }
 
 // Host-side shape of a partitioned insert: slice bits (0 = not eligible).
 u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap) {
-    const int mode = getenv("DBG_PART") ? atoi(getenv("DBG_PART")) : 1;  // 0 disables (A/B knob)
-    if (!mode || !S.inline_keys || S.n_keys != 1 || S.key_types[0].nullable || hb.n_nodes != 0) return 0;
+    if (!S.inline_keys || S.n_keys != 1 || S.key_types[0].nullable || hb.n_nodes != 0) return 0;
     if (!(S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1 && S.stride_words == 2))
         return 0;
     const DCol& k = hb.keys[0];
     int ty = k.type;
     bool intlike = (ty >= DBG_INT8 && ty <= DBG_UINT64) || ty == DBG_DATE || ty == DBG_TIMESTAMP;
     if (!intlike || k.layout != LAYOUT_ARROW || ((uintptr_t)k.data % k.width)) return 0;
-    const u64 min_rows = getenv("DBG_PART_MIN_ROWS") ? strtoull(getenv("DBG_PART_MIN_ROWS"), nullptr, 10) : (1ULL << 22);
-    const u64 min_cap = getenv("DBG_PART_MIN_CAP") ? strtoull(getenv("DBG_PART_MIN_CAP"), nullptr, 10) : (1ULL << 20);
-    if (rows < min_rows || cap < min_cap) return 0;
+    // below ~1M rows the sort's fixed cost outweighs the streaming insert's HBM atomics
+    if (rows < (1ULL << 20) || cap < (1ULL << 20)) return 0;
     // 4096 slots of 16 B per slice (the kernel is instantiated for this size only; at least two
     // slices)
     if (cap < (2ULL << PART_SB)) return 0;

@@ -226,28 +226,64 @@ __device__ __forceinline__ void pp_apply_raw(const Spec& S, wptr<AS> st, const u
 // ------------------------------------------------------------------------------------------
 // Cardinality probe: distinct group hashes among n_sample evenly spaced (selected) rows.
 // set: 2 * set_cap words [hash | count]; out: [0] selected, [1] distinct, [2] f1, [3] f2.
+// (Per-sample counts come out right even when the LDS set spills: one hash's count may then sit in
+// the global set from two adds, never in two slots.)
 // ------------------------------------------------------------------------------------------
+// Each workgroup counts its contiguous share of the samples in an LDS set first (a handful of
+// distinct keys — TPC-H Q1's four groups — would otherwise put every sample's atomics on the same
+// few HBM words) and adds each distinct hash to the global set once.
+#define PP_PROBE_SLOTS 2048
+__device__ __forceinline__ void pp_probe_global(u64* set, u64 set_cap, u64* out, u64 h, u64 c) {
+    u64 s = slot_mix(h) & (set_cap - 1);
+    for (u64 p = 0; p < set_cap; ++p) {
+        u64 old = atomicCAS((unsigned long long*)(set + 2 * s), 0ULL, (unsigned long long)h);
+        if (old == 0) atomicAdd((unsigned long long*)(out + 1), 1ULL);
+        if (old == 0 || old == h) {
+            atomicAdd((unsigned long long*)(set + 2 * s + 1), (unsigned long long)c);
+            return;
+        }
+        s = (s + 1) & (set_cap - 1);
+    }
+}
 __global__ void __launch_bounds__(256) pp_sample_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                        u32 bid, u64 rows, u64 n_sample, u64* set, u64 set_cap, u64* out) {
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
-    for (u64 k = blockIdx.x * 256ULL + threadIdx.x; k < n_sample; k += (u64)gridDim.x * 256) {
+    __shared__ u64 lkey[PP_PROBE_SLOTS];
+    __shared__ u32 lcnt[PP_PROBE_SLOTS];
+    __shared__ u32 nsel;
+    for (u32 t = threadIdx.x; t < PP_PROBE_SLOTS; t += 256) {
+        lkey[t] = 0;
+        lcnt[t] = 0;
+    }
+    if (threadIdx.x == 0) nsel = 0;
+    __syncthreads();
+    const u64 per = (n_sample + gridDim.x - 1) / gridDim.x;
+    const u64 k0 = (u64)blockIdx.x * per, k1 = min(n_sample, k0 + per);
+    u32 mysel = 0;
+    for (u64 k = k0 + threadIdx.x; k < k1; k += 256) {
         const u64 i = (k * rows) / n_sample;
         if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
-        atomicAdd((unsigned long long*)out, 1ULL);
+        mysel++;
         u64 h = pp_row_hash(S, B, i);
         h = h ? h : 1;
-        u64 s = slot_mix(h) & (set_cap - 1);
-        for (u64 p = 0; p < set_cap; ++p) {
-            u64 old = atomicCAS((unsigned long long*)(set + 2 * s), 0ULL, (unsigned long long)h);
-            if (old == 0) atomicAdd((unsigned long long*)(out + 1), 1ULL);
+        u32 s = (u32)slot_mix(h) & (PP_PROBE_SLOTS - 1);
+        bool done = false;
+        for (u32 p = 0; p < 64 && !done; ++p) {  // short probes: a full LDS set spills to the global one
+            u64 old = atomicCAS((unsigned long long*)&lkey[s], 0ULL, (unsigned long long)h);
             if (old == 0 || old == h) {
-                atomicAdd((unsigned long long*)(set + 2 * s + 1), 1ULL);
-                break;
+                atomicAdd(&lcnt[s], 1u);
+                done = true;
             }
-            s = (s + 1) & (set_cap - 1);
+            s = (s + 1) & (PP_PROBE_SLOTS - 1);
         }
+        if (!done) pp_probe_global(set, set_cap, out, h, 1);
     }
+    if (mysel) atomicAdd(&nsel, mysel);
+    __syncthreads();
+    for (u32 t = threadIdx.x; t < PP_PROBE_SLOTS; t += 256)
+        if (lcnt[t]) pp_probe_global(set, set_cap, out, lkey[t], lcnt[t]);
+    if (threadIdx.x == 0 && nsel) atomicAdd((unsigned long long*)out, (unsigned long long)nsel);
 }
 __global__ void __launch_bounds__(256) pp_sample_stats_kernel(const u64* set, u64 set_cap, u64* out) {
     u32 f1 = 0, f2 = 0;

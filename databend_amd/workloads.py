@@ -122,7 +122,7 @@ class QueryShape:
 SHAPES = {
     1: QueryShape("tpch_q1_sf1", ["l_returnflag", "l_linestatus"],
                   [("sum", "l_quantity"), ("sum", "l_extendedprice"), ("sum", "disc_price"), ("sum", "charge"),
-                   ("avg", "l_quantity"), ("avg", "l_extendedprice"), ("avg", "l_discount"), ("count", None)],
+                   ("sql_avg", "l_quantity"), ("sql_avg", "l_extendedprice"), ("sql_avg", "l_discount"), ("count", None)],
                   ("l_shipdate", "<=", 10471),
                   "TPC-H Q1: WHERE l_shipdate <= DATE '1998-09-02' GROUP BY l_returnflag, l_linestatus"),
     2: QueryShape("clickbench_q8_adv_engine_id", ["AdvEngineID"], [("count", None)], ("AdvEngineID", "<>", 0),
@@ -130,7 +130,7 @@ SHAPES = {
     3: QueryShape("clickbench_q17_user_id", ["UserID"], [("count", None)], None,
                   "SELECT UserID, COUNT(*) FROM hits GROUP BY UserID"),
     4: QueryShape("clickbench_q33_watchid_clientip", ["WatchID", "ClientIP"],
-                  [("count", None), ("sum", "IsRefresh"), ("avg", "ResolutionWidth")], None,
+                  [("count", None), ("sum", "IsRefresh"), ("sql_avg", "ResolutionWidth")], None,
                   "SELECT WatchID, ClientIP, COUNT(*), SUM(IsRefresh), AVG(ResolutionWidth) FROM hits GROUP BY WatchID, ClientIP"),
     5: QueryShape("clickbench_q13_search_phrase", ["SearchPhrase"], [("count", None)], ("SearchPhrase", "<>", ""),
                   "SELECT SearchPhrase, COUNT(*) FROM hits WHERE SearchPhrase <> '' GROUP BY SearchPhrase"),

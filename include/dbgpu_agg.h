@@ -101,7 +101,14 @@ typedef enum {
     DBG_AGG_SUM = 1,   /* NumberSumState / DecimalSumState<OVERFLOW> */
     DBG_AGG_MIN = 2,   /* MinMaxAnyState<T, CmpMin> */
     DBG_AGG_MAX = 3,   /* MinMaxAnyState<T, CmpMax> */
-    DBG_AGG_AVG = 4    /* NumberAvgState / DecimalAvgState<OVERFLOW> */
+    DBG_AGG_AVG = 4,   /* NumberAvgState / DecimalAvgState<OVERFLOW> */
+    /* SQL avg(x): the planner rewrites it to sum(x) / if(count(x) = 0, 1, count(x))
+     * (SQL/planner/semantic/aggregate_rewriter.rs:145-208); fused here into one aggregate with
+     * AVG's state.  Numbers: f64 / f64 (the value NumberAvgState gives).  Decimal128(p, s): SUM's
+     * state and range check, then the decimal divide by the count as Decimal(20, 0)
+     * (FUNCS/scalars/decimal/arithmetic.rs:87-112): result Decimal(38, max(s, min(s + 6, 12)))
+     * (EXP/types/decimal.rs:1015-1018), rounded half away from zero (do_round_div, :480-489). */
+    DBG_AGG_AVG_SQL = 5
 } dbg_agg_kind;
 
 typedef struct dbg_agg_spec {
@@ -220,7 +227,13 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
  * launch, leaving the handle as dbg_agg_reset would — the result columns are then the only copy
  * of the groups, and the next dbg_agg_reset costs no launch.  The partial table of
  * TransformPartialAggregate is dropped after on_finish (transform_aggregate_partial.rs:449-465),
- * so a processor that reuses one handle per batch stream loses nothing. */
+ * so a processor that reuses one handle per batch stream loses nothing.
+ * Also in recycle mode: the insert of an on-device dbg_agg_add_groups that takes the fast path
+ * (one non-null integer key, optional `key <op> constant` filter, small table) is enqueued by the
+ * NEXT call on the handle, and a dbg_agg_finalize_into(_async) then runs insert and finalize in
+ * one launch (the last workgroup of the insert finalizes).  The device columns of such a batch
+ * must therefore stay unchanged until that next call returns — true of DataBlocks, which are
+ * immutable once produced (EXP/block.rs).  Launch errors of the insert surface from that call. */
 int dbg_agg_set_recycle(dbg_agg_handle* h, int on);
 
 /* Aggregation strategy of a handle (set after create or reset, before any batch):

@@ -464,6 +464,69 @@ struct AvgDecFn : AggFn {
     size_t result_width() const override { return 16; }
 };
 
+// SQL avg(x) after the planner's rewrite sum(x) / if(count(x) = 0, 1, count(x))
+// (SQL/planner/semantic/aggregate_rewriter.rs:145-208), Decimal128 argument: the sum is
+// DecimalSumState<OVERFLOW = p <= 18> (as SumDecFn), the count UInt64 viewed as Decimal(20, 0),
+// and the decimal divide (FUNCS/scalars/decimal/arithmetic.rs:87-112) has result scale
+// max(s, min(s + 6, 12)) (EXP/types/decimal.rs:1015-1018) and value do_round_div(sum, count,
+// scale - s) (EXP/types/decimal.rs:480-489): (sum * 10^k + count/2) / count when sum >= 0,
+// (sum * 10^k - count/2) / count otherwise, in i256 (truncating), low 128 bits.
+// (Numbers: the rewrite's f64 / f64 equals NumberAvgState's result, so AvgNumFn serves.)
+struct SqlAvgDecFn : AggFn {
+    SumDecFn sum;
+    int k;
+    dbg_datatype rt;
+    SqlAvgDecFn(bool o, int kk, dbg_datatype r) : sum(o, r), k(kk), rt(r) {}
+    size_t size() const override { return 32; }
+    size_t align() const override { return 16; }
+    void init_state(u8* p) const override { memset(p, 0, 32); }
+    void accumulate_keys(u8* const* places, size_t off, const dbg_column* arg, u64 start, u64 n) const override {
+        for (u64 j = 0; j < n; ++j) accumulate_row(places[j] + off, arg, start + j);
+    }
+    void accumulate_row(u8* place, const dbg_column* arg, u64 row) const override {
+        sum.add(place, arg_as<i128>(*arg, row));
+        *(u64*)(place + 16) += 1;
+    }
+    void merge_states(u8* p, u8* r) const override {
+        i128 x;
+        memcpy(&x, r, 16);
+        sum.add(p, x);
+        *(u64*)(p + 16) += *(u64*)(r + 16);
+    }
+    void merge_result(u8* p, Builder& b) const override {
+        i128 s;
+        memcpy(&s, p, 16);
+        u64 c = *(u64*)(p + 16);
+        if (c == 0) c = 1;  // if(count = 0, 1, count)
+        const bool neg = s < 0;
+        u128 m = neg ? (u128)0 - (u128)s : (u128)s;
+        u64 mul = 1;
+        for (int i = 0; i < k; ++i) mul *= 10;
+        // |s| * 10^k as three 64-bit limbs, then + c / 2, then long division by c
+        u128 lo_p = (u128)(u64)m * mul, hi_p = (u128)(u64)(m >> 64) * mul;
+        u64 l0 = (u64)lo_p;
+        u128 mid = (lo_p >> 64) + (u128)(u64)hi_p;
+        u64 l1 = (u64)mid;
+        u64 l2 = (u64)(hi_p >> 64) + (u64)(mid >> 64);
+        u128 t = (u128)l0 + (c / 2);
+        l0 = (u64)t;
+        u128 t1 = (u128)l1 + (u64)(t >> 64);
+        l1 = (u64)t1;
+        l2 += (u64)(t1 >> 64);
+        u128 r = l2 % c;
+        u128 x1 = (r << 64) | l1;
+        u64 q1 = (u64)(x1 / c);
+        r = x1 % c;
+        u128 x0 = (r << 64) | l0;
+        u64 q0 = (u64)(x0 / c);
+        u128 q = ((u128)q1 << 64) | q0;
+        if (neg) q = (u128)0 - q;
+        b.push<i128>((i128)q);
+    }
+    dbg_datatype return_type() const override { return rt; }
+    size_t result_width() const override { return 16; }
+};
+
 // MinMaxAnyState<T, CmpMin/CmpMax> (FUN/aggregate_min_max_any.rs:46-115,
 // FUN/aggregate_scalar_state.rs:60-104): Option<T>; replace when l.partial_cmp(r) is Greater (MIN)
 // / Less (MAX).  Floats are OrderedFloat (NaN greatest, all NaNs equal, -0 == +0).
@@ -634,6 +697,14 @@ static AggFn* make_fn(const dbg_agg_spec& s) {
         else if (t == DBG_DECIMAL128) {
             int sc = std::max<int>(s.arg.scale, 4);
             base = new AvgDecFn(s.arg.precision > 18, sc - s.arg.scale, dbg_datatype{DBG_DECIMAL128, 38, (u8)sc, 0, 0});
+        }
+    } else if (s.kind == DBG_AGG_AVG_SQL) {
+        if (is_signed_int(t)) base = new AvgNumFn<i64>();
+        else if (is_unsigned_int(t)) base = new AvgNumFn<u64>();
+        else if (is_float(t)) base = new AvgNumFn<double>();
+        else if (t == DBG_DECIMAL128) {
+            int sc = std::max<int>(s.arg.scale, std::min<int>(s.arg.scale + 6, 12));
+            base = new SqlAvgDecFn(s.arg.precision <= 18, sc - s.arg.scale, dbg_datatype{DBG_DECIMAL128, 38, (u8)sc, 0, 0});
         }
     } else if (s.kind == DBG_AGG_MIN || s.kind == DBG_AGG_MAX) {
         bool mn = s.kind == DBG_AGG_MIN;

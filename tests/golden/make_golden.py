@@ -75,39 +75,60 @@ def parse_file(name, grouped):
 
 # 03_0043_new_agg_hashtable.test expected rows (hand transcription; file:line of each query).
 SLT = [
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:21-27",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:21-26",
          sql="SELECT number%3 as c1, sum(c1) FROM numbers_mt(10) where number > 2 group by number%3 order by c1",
          rows=[[0, 0], [1, 2], [2, 4]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:29-35",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:28-33",
          sql="SELECT a,b,sum(a),sum(b),count() from (SELECT cast((number%6) AS bigint) as a, cast((number%15) AS bigint) as b "
              "from numbers(1000)) group by a,b order by a,b limit 3",
          rows=[[0, 0, 0, 0, 34], [0, 3, 0, 99, 33], [0, 6, 0, 204, 34]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:46-51",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:44-49 (table: :39-42)",
          sql="SELECT a%3 as a1, count(1) as ct from t GROUP BY a1 ORDER BY a1 NULLS FIRST,ct "
              "(t.a = if(number % 3 = 2, null, number), numbers(10))",
          rows=[[None, 3], [0, 4], [1, 3]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:53-61",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:51-58",
          sql="SELECT a%2 as a1, a%3 as a2, count(0) as ct FROM t GROUP BY a1, a2",
          rows=[[None, None, 3], [0, 0, 2], [0, 1, 1], [1, 0, 2], [1, 1, 2]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:95-100",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:90-95 (table: :85-88)",
          sql="select created_at, sum(count) from t_datetime group by created_at "
              "(created_at = to_date('2024-04-01') + number % 3, count = 1, numbers(10))",
          rows=[[19814, 4], [19815, 3], [19816, 3]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:122-130",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:116-123",
          sql="SELECT number % 3 as a, number%4 as b, sum(a),avg(b) FROM numbers_mt(10000000) group by a,b order by a,b limit 5",
          rows=[[0, 0, 0, 0.0], [0, 1, 0, 1.0], [0, 2, 0, 2.0], [0, 3, 0, 3.0], [1, 0, 833333, 0.0]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:178-186",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:170-177",
          sql="select (number % 3)::Decimal(19, 2) a ,(number % 4)::Decimal(36, 4) b , count() from numbers(100) "
              "group by a,b order by a,b limit 5",
          rows=[["0.00", "0.0000", 9], ["0.00", "1.0000", 8], ["0.00", "2.0000", 8], ["0.00", "3.0000", 9],
                ["1.00", "0.0000", 8]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:188-193",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:179-184",
          sql="select (number % 3)::Decimal(19, 2) c, to_string(number % 3) d, count() from numbers(100) group by c,d",
          rows=[["0.00", "0", 34], ["1.00", "1", 33], ["2.00", "2", 33]]),
-    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:207-216",
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:200-208",
          sql="select number % 3 a, max(number) - 10, number % 2 b, sum(number) + 10 from numbers(1000000) group by all",
          rows=[[0, 999986, 0, 83333166676], [0, 999989, 1, 83333666677], [1, 999984, 0, 83332833344],
                [1, 999987, 1, 83333333343], [2, 999988, 0, 83333500010], [2, 999985, 1, 83333000010]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:60-67 (table: :39-42)",
+         sql="SELECT a%2 as a1, to_uint64(c % 3) as c1, count(0) as ct FROM t GROUP BY a1, c1 "
+             "ORDER BY a1 NULLS FIRST, c1, ct (t.a = if(number % 3 = 2, null, number), t.c = number + 6)",
+         rows=[[None, 2, 3], [0, 0, 2], [0, 1, 1], [1, 0, 2], [1, 1, 2]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:69-76 (table: :39-42)",
+         sql="SELECT to_uint64(c % 3) as c1, a%2 as a1, count(0) as ct FROM t GROUP BY a1, c1 "
+             "ORDER BY a1 NULLS FIRST, c1 NULLS FIRST, ct",
+         rows=[[2, None, 3], [0, 0, 2], [1, 0, 1], [0, 1, 2], [1, 1, 2]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:97-102 (table: :85-88)",
+         sql="select created_time, sum(count) from t_datetime group by created_time order by created_time "
+             "(created_time = to_datetime('2024-04-01 00:00:00') + number % 3 [microseconds], count = 1, numbers(10))",
+         rows=[["2024-04-01 00:00:00.000000", 4], ["2024-04-01 00:00:00.000001", 3], ["2024-04-01 00:00:00.000002", 3]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:107-114",
+         sql="SELECT number, count(*) FROM numbers_mt(10) group by number order by number limit 5",
+         rows=[[0, 1], [1, 1], [2, 1], [3, 1], [4, 1]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:158-161",
+         sql="select count() from numbers(10) group by 'ab'",
+         rows=[[10]]),
+    dict(source="tests/sqllogictests/suites/base/03_common/03_0043_new_agg_hashtable.test:163-166",
+         sql="select count() from numbers(10) group by to_nullable('ab')",
+         rows=[[10]]),
 ]
 
 

@@ -186,7 +186,7 @@ def test_random_keys_all_functions(kind, on_device):
     dec38 = Column.from_decimals(38, 6, [int(v) * 10**20 for v in rng.integers(-10**9, 10**9, n)])
     aggs = [("count", None), ("count", i64n), ("sum", i64), ("sum", i64n), ("sum", u32), ("sum", f64), ("sum", dec),
             ("sum", dec38), ("avg", i64), ("avg", f64), ("avg", dec), ("avg", i64n), ("min", i64), ("max", i64n),
-            ("min", f64), ("max", u32), ("max", dec)]
+            ("min", f64), ("max", u32), ("max", dec), ("sql_avg", dec), ("sql_avg", dec38), ("sql_avg", i64n), ("sql_avg", f64)]
     check_parity(keys, aggs, on_device=on_device)
 
 
@@ -235,19 +235,21 @@ def test_decimal_sum_overflow_error():
 
 
 def test_slt_cases_gpu():
-    from tests.test_oracle_golden import SLT, _slt_expected, _slt_inputs
+    from tests.test_oracle_golden import SLT, _row_order, _slt_expected, _slt_inputs
     from tests.parity import rows_of
+    kind_name = {abi.AGG_COUNT: "count", abi.AGG_SUM: "sum", abi.AGG_AVG: "avg", abi.AGG_MIN: "min",
+                 abi.AGG_MAX: "max", abi.AGG_AVG_SQL: "sql_avg"}
     for i, case in enumerate(SLT):
         keys, aggs, flt = _slt_inputs(i)
-        names = []
-        for spec, c in aggs:
-            names.append(({abi.AGG_COUNT: "count", abi.AGG_SUM: "sum", abi.AGG_AVG: "avg", abi.AGG_MIN: "min",
-                           abi.AGG_MAX: "max"}[spec.kind], c))
+        names = [(kind_name[spec.kind], c) for spec, c in aggs]
         filt = (flt[0], flt[1]) if flt else None
         gk, ga = gpu_aggregate(keys, names, filt)
-        got = sorted([list(r) for r in rows_of(gk, ga)], key=lambda r: [(-1 if v is None else v) for v in r[:len(keys)]])
+        got = sorted([list(r) for r in rows_of(gk, ga)], key=lambda r: _row_order(r, len(keys)))
         exp = _slt_expected(i, case)
-        got = got[:len(exp)] if "limit" in case["sql"] else got
+        if "limit" in case["sql"]:
+            got = got[:len(exp)]
+        else:
+            exp = sorted(exp, key=lambda r: _row_order(r, len(keys)))
         assert got == exp, case["source"]
 
 
@@ -515,20 +517,18 @@ PART_CASES = [
     # (key type, distinct keys, rows, capacity hint, batches)
     ("i64", 600_000, 3_000_000, 1 << 20, 2),      # slices hold every group (load ~0.3)
     ("i64", 1_500_000, 3_000_000, 1 << 19, 1),    # cap 2^20 too small: overflow records + growth
-    ("i32", 400_000, 2_000_000, 1 << 19, 3),
+    ("i32", 400_000, 3_300_000, 1 << 19, 3),
     ("i16", 65_536, 2_000_000, 1 << 19, 1),       # every i16 value, including -1 (all-ones key)
-    ("u8", 256, 1_000_000, 1 << 19, 1),
+    ("u8", 256, 1_200_000, 1 << 19, 1),
 ]
 
 
 @pytest.mark.parametrize("kind,distinct,n,hint,batches", PART_CASES, ids=lambda x: str(x))
-def test_partitioned_insert(kind, distinct, n, hint, batches, monkeypatch):
+def test_partitioned_insert(kind, distinct, n, hint, batches):
     """part.hip: radix-partitioned COUNT(*) insert (rocPRIM sort of mixed keys + one workgroup per
-    64 KB table slice in LDS).  Thresholds lowered so test-sized batches take the path; the
+    64 KB table slice in LDS).  Every batch holds >= 2^20 rows (the path's threshold); the
     sentinel key (all-ones), runs that leave a slice (overflow records -> agg_retry), growth,
     and several batches into one table are all covered."""
-    monkeypatch.setenv("DBG_PART_MIN_ROWS", "1000")
-    monkeypatch.setenv("DBG_PART_MIN_CAP", str(1 << 20))
     rng = np.random.default_rng(distinct)
     t = {"i64": col.Int64, "i32": col.Int32, "i16": col.Int16, "u8": col.UInt8}[kind]
     if kind == "i64":

@@ -57,6 +57,21 @@ def test_pp_random_keys_all_functions(kind, on_device):
     check_pp(keys, aggs, on_device=on_device, batches=3)
 
 
+@pytest.mark.parametrize("kind", ["i64", "string"])
+def test_pp_sql_avg(kind):
+    """SQL avg (DBG_AGG_AVG_SQL: sum / if(count = 0, 1, count), decimal round-half-away divide)
+    through the partitioned payload's fused finalize."""
+    rng = np.random.default_rng(41)
+    n = 300_000
+    keys = _rand_inputs(rng, n, kind)
+    dec = Column.from_decimals(15, 2, [int(v) for v in rng.integers(-10**12, 10**12, n)], validity=rng.random(n) > 0.1)
+    dec38 = Column.from_decimals(38, 6, [int(v) * 10**20 for v in rng.integers(-10**9, 10**9, n)])
+    i64n = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n), validity=rng.random(n) > 0.5)
+    f64 = Column.from_numbers(col.Float64, rng.random(n) * 1000)
+    check_pp(keys, [("count", None), ("sql_avg", dec), ("sql_avg", dec38), ("sql_avg", i64n), ("sql_avg", f64)],
+             on_device=True, batches=2)
+
+
 @pytest.mark.parametrize("kind", ["i64_hi", "string", "i64_i32"])
 def test_pp_multi_round_partitions(kind):
     """capacity_hint = 1 sizes the final partitions for one group each: 512 partitions of

@@ -27,6 +27,7 @@ GOLD = json.load(open(os.path.join(HERE, "golden", "agg_function_goldens.json"))
 SLT = json.load(open(os.path.join(HERE, "golden", "slt_group_by.json")))
 
 KIND = {"count": abi.AGG_COUNT, "sum": abi.AGG_SUM, "avg": abi.AGG_AVG, "min": abi.AGG_MIN, "max": abi.AGG_MAX}
+TS_2024_04_01 = 1711929600 * 1_000_000  # 2024-04-01 00:00:00 UTC in microseconds
 
 
 def spec(kind, arg_dt=None, or_null=True):
@@ -124,11 +125,11 @@ def _slt_inputs(i):
         d = Column.from_numbers(col.Date, 19814 + (num % 3).astype(np.int32))
         one = Column.from_numbers(col.Int32, np.ones(10, np.int32))
         return [d], [(spec(abi.AGG_SUM, col.Int32), one)], None
-    if i == 5:
+    if i == 5:  # SQL avg(b): the planner's sum / if(count = 0, 1, count) (DBG_AGG_AVG_SQL)
         num = _numbers(10_000_000)
         a = Column.from_numbers(col.UInt8, num % 3)
         b = Column.from_numbers(col.UInt8, num % 4)
-        return [a, b], [(spec(abi.AGG_SUM, col.UInt8), a), (spec(abi.AGG_AVG, col.UInt8), b)], None
+        return [a, b], [(spec(abi.AGG_SUM, col.UInt8), a), (spec(abi.AGG_AVG_SQL, col.UInt8), b)], None
     if i == 6:
         num = _numbers(100)
         a = Column.from_decimals(19, 2, [int(v % 3) * 100 for v in num])
@@ -145,6 +146,21 @@ def _slt_inputs(i):
         b = Column.from_numbers(col.UInt8, num % 2)
         n = Column.from_numbers(col.UInt64, num)
         return [a, b], [(spec(abi.AGG_MAX, col.UInt64), n), (spec(abi.AGG_SUM, col.UInt64), n)], None
+    if i in (9, 10):  # t(a UInt64 null = if(number % 3 = 2, null, number), c UInt32 = number + 6)
+        num = _numbers(10)
+        a1 = Column.from_numbers(col.UInt8, num % 2, validity=(num % 3) != 2)
+        c1 = Column.from_numbers(col.UInt64, (num + 6) % 3)
+        return ([a1, c1] if i == 9 else [c1, a1]), [(spec(abi.AGG_COUNT), None)], None
+    if i == 11:  # created_time = '2024-04-01 00:00:00' + number % 3 (microseconds)
+        num = _numbers(10)
+        t = Column.from_numbers(col.Timestamp, (TS_2024_04_01 + (num % 3)).astype(np.int64))
+        one = Column.from_numbers(col.Int32, np.ones(10, np.int32))
+        return [t], [(spec(abi.AGG_SUM, col.Int32), one)], None
+    if i == 12:
+        return [Column.from_numbers(col.UInt64, _numbers(10))], [(spec(abi.AGG_COUNT), None)], None
+    if i in (13, 14):  # GROUP BY a constant string ('ab', to_nullable('ab'))
+        k = Column.from_strings([b"ab"] * 10, validity=[True] * 10 if i == 14 else None)
+        return [k], [(spec(abi.AGG_COUNT), None)], None
     raise IndexError(i)
 
 
@@ -156,7 +172,15 @@ def _slt_expected(i, case):
         return [[int(Decimal(r[0]) * 100), r[1].encode(), r[2]] for r in rows]
     if i == 8:  # max(number) - 10, sum(number) + 10 are post-aggregate scalars
         return [[r[0], r[2], r[1] + 10, r[3] - 10] for r in rows]
+    if i == 11:
+        return [[TS_2024_04_01 + int(r[0][-6:]), r[1]] for r in rows]
+    if i in (13, 14):  # the constant key column is carried beside count()
+        return [[b"ab", r[0]] for r in rows]
     return rows
+
+
+def _row_order(r, nkeys):
+    return [(-1 if v is None else v) for v in r[:nkeys]]
 
 
 @pytest.mark.parametrize("i", range(len(SLT)))
@@ -165,9 +189,12 @@ def test_slt_group_by(i):
     keys, aggs, flt = _slt_inputs(i)
     prog = FilterProgram(flt[0], [c.to_abi() for c in flt[1]]) if flt else None
     k, a = oracle.aggregate(keys, aggs, filter_program=prog, threads=4)
-    got = sorted([list(r) for r in rows_of(k, a)], key=lambda r: [(-1 if v is None else v) for v in r[:len(keys)]])
+    got = sorted([list(r) for r in rows_of(k, a)], key=lambda r: _row_order(r, len(keys)))
     exp = _slt_expected(i, case)
-    got = got[:len(exp)] if "limit" in case["sql"] else got
+    if "limit" in case["sql"]:  # ORDER BY the group keys ... LIMIT n
+        got = got[:len(exp)]
+    else:  # compared as sets of rows
+        exp = sorted(exp, key=lambda r: _row_order(r, len(keys)))
     assert got == exp, f"{case['source']}\n got {got}\n exp {exp}"
 
 
@@ -244,3 +271,60 @@ def test_filter_three_valued_logic():
     assert list(oracle.filter_select(p, 6)) == [1, 2, 3, 4]
     p2 = FilterProgram(not_(cmp(0, ">", 3)), [v.to_abi()])
     assert list(oracle.filter_select(p2, 6)) == [0, 1]  # NOT(NULL) is NULL -> dropped
+
+
+def test_sql_avg_decimal_q1_shape():
+    """TPC-H Q1's avg(l_quantity) (Decimal(15, 2)) as Databend computes it: the planner's
+    sum / if(count = 0, 1, count) (SQL/planner/semantic/aggregate_rewriter.rs:145-208) with the
+    decimal divide (FUNCS/scalars/decimal/arithmetic.rs:87-112): Decimal(38, 8), rounded half away
+    from zero.  Expected values computed by hand; AggregateAvgFunction (DecimalAvgState, scale 4,
+    truncating) beside it for contrast."""
+    groups = {  # (l_returnflag, l_linestatus) -> quantities in cents
+        (b"A", b"F"): [100, 200, 200],          # 5.00 / 3   = 1.666666666.. -> 1.66666667
+        (b"N", b"O"): [1] + [0] * 127,          # 0.01 / 128 = 0.000078125   -> 0.00007813 (exact half: away)
+        (b"R", b"F"): [-1] + [0] * 127,         # -0.01 / 128                -> -0.00007813
+        (b"N", b"F"): [1700, 3600],             # 53.00 / 2  = 26.5          -> 26.50000000
+        (b"A", b"O"): [3] * 10 + [4],           # 0.34 / 11  = 0.030909..    -> 0.03090909
+    }
+    sql_expected = {(b"A", b"F"): 166666667, (b"N", b"O"): 7813, (b"R", b"F"): -7813,
+                    (b"N", b"F"): 2650000000, (b"A", b"O"): 3090909}
+    avg_expected = {(b"A", b"F"): 16666, (b"N", b"O"): 0, (b"R", b"F"): 0, (b"N", b"F"): 265000, (b"A", b"O"): 309}
+    rf, ls, q = [], [], []
+    for (a, b), vals in groups.items():
+        for v in vals:
+            rf.append(a)
+            ls.append(b)
+            q.append(v)
+    qty = Column.from_decimals(15, 2, q)
+    keys = [Column.from_strings(rf), Column.from_strings(ls)]
+    k, a = oracle.aggregate(keys, [(spec(abi.AGG_AVG_SQL, qty.dtype), qty), (spec(abi.AGG_AVG, qty.dtype), qty)])
+    assert (a[0].dtype.precision, a[0].dtype.scale) == (38, 8)
+    assert a[1].dtype.scale == 4
+    got = {(r[0], r[1]): (r[2], r[3]) for r in rows_of(k, a)}
+    assert got == {g: (sql_expected[g], avg_expected[g]) for g in groups}
+
+
+def test_sql_avg_scale_rule_and_nulls():
+    """Result scale max(s, min(s + 6, 12)) (EXP/types/decimal.rs:1015-1018) for s = 0, 4, 6, 10;
+    an all-NULL group gives NULL (sum is NULL; the if() only guards the division)."""
+    from decimal import ROUND_HALF_UP, localcontext
+    rng = np.random.default_rng(3)
+    for p, sc in ((10, 0), (18, 4), (20, 6), (38, 10)):
+        n = 500
+        g = rng.integers(0, 7, n)
+        v = [int(x) for x in rng.integers(-10**9, 10**9, n)]
+        valid = (g != 6) & (rng.random(n) > 0.2)  # group 6 is all NULL
+        arg = Column.from_decimals(p, sc, v, validity=valid)
+        k, a = oracle.aggregate([Column.from_numbers(col.Int32, g.astype(np.int32))], [(spec(abi.AGG_AVG_SQL, arg.dtype), arg)])
+        rs = max(sc, min(sc + 6, 12))
+        assert a[0].dtype.scale == rs and a[0].dtype.nullable
+        for key, res in rows_of(k, a):
+            sel = [v[i] for i in range(n) if g[i] == key and valid[i]]
+            if not sel:
+                assert res is None
+                continue
+            with localcontext() as ctx:
+                ctx.prec = 80
+                exact = Decimal(sum(sel)).scaleb(-sc) / Decimal(len(sel))
+                want = int(exact.scaleb(rs).quantize(Decimal(1), rounding=ROUND_HALF_UP))
+            assert res == want, (p, sc, key)
