@@ -15,7 +15,7 @@ Every call lands in libdbgpu_agg.so; the product path has no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import List, Optional, Sequence, Union
 
 import numpy as np
@@ -71,15 +71,76 @@ def _empty_column(t: DataType) -> Column:
     return Column(t, np.zeros(0, t.np_dtype), None, np.zeros(0, bool) if t.nullable else None)
 
 
+MAX_PAGE_SIZE = 256 * 1024  # EAGG/mod.rs:50
+
+
+class RadixBitsHint:
+    """`current_max_radix_bits: Arc<AtomicU64>` (EAGG/mod.rs:62): the one piece of state shared
+    by every partial table of a query, so their bucket counts converge (CAS loop of
+    maybe_repartition, EAGG/aggregate_hashtable.rs:467-484)."""
+
+    def __init__(self, bits: int):
+        import threading
+        self._v = bits
+        self._lock = threading.Lock()
+
+    def load(self) -> int:
+        return self._v
+
+    def fetch_max(self, bits: int) -> int:
+        with self._lock:
+            if bits > self._v:
+                self._v = bits
+            return self._v
+
+
 @dataclass
 class HashTableConfig:
-    """HashTableConfig (EAGG/mod.rs:59-83).  The radix/partial-capacity knobs of the CPU table have
-    no GPU meaning (the HBM table aggregates exactly); `capacity_hint` seeds the table size."""
+    """HashTableConfig (EAGG/mod.rs:59-132).  The HBM table aggregates exactly, so
+    max_partial_capacity has no GPU meaning; `capacity_hint` seeds the table size and the radix
+    knobs decide how many buckets a partial emits (partial_bucket_bits)."""
     partial_agg: bool = False
     capacity_hint: int = 0
+    current_max_radix_bits: RadixBitsHint = field(default_factory=lambda: RadixBitsHint(3))
+    initial_radix_bits: int = 3
+    max_radix_bits: int = 7
+    repartition_radix_bits_incr: int = 2
+    block_fill_factor: float = 1.8
 
     def with_partial(self, partial_agg: bool, active_threads: int = 1) -> "HashTableConfig":
-        return HashTableConfig(partial_agg, self.capacity_hint)
+        return replace(self, partial_agg=partial_agg)
+
+    def cluster_with_partial(self, partial_agg: bool, node_nums: int) -> "HashTableConfig":
+        return replace(self, partial_agg=partial_agg, repartition_radix_bits_incr=4)
+
+    def with_initial_radix_bits(self, bits: int) -> "HashTableConfig":
+        return replace(self, initial_radix_bits=bits, current_max_radix_bits=RadixBitsHint(bits))
+
+    def update_current_max_radix_bits(self) -> None:
+        self.current_max_radix_bits.fetch_max(self.max_radix_bits)
+
+
+def payload_tuple_size(group_types: Sequence[DataType], n_aggs: int) -> int:
+    """Payload::new (EAGG/payload.rs:88-130): validity byte per nullable key + rowformat_size of
+    each key (EAGG/payload_row.rs:43-64; strings 4 + 8) + hash 8 + state address 8."""
+    size = sum(1 for t in group_types if t.nullable)
+    for t in group_types:
+        size += 12 if t.type_id == abi.STRING else t.width
+    return size + 8 + (8 if n_aggs else 0)
+
+
+def partial_bucket_bits(config: HashTableConfig, n_groups: int, tuple_size: int) -> int:
+    """The radix bits a partial table ends with: maybe_repartition (EAGG/aggregate_hashtable.rs:
+    453-503) raises them by repartition_radix_bits_incr while the payload holds more than
+    MAX_PAGE_SIZE * (block_fill_factor as usize) bytes per partition, up to max_radix_bits, and
+    adopts the query-wide maximum.  The reference steps once per add_groups call; the GPU table
+    knows its exact group count at on_finish and applies the rule to convergence."""
+    bits = config.current_max_radix_bits.load()
+    limit = MAX_PAGE_SIZE * int(config.block_fill_factor)
+    mem = n_groups * tuple_size
+    while config.partial_agg and bits < config.max_radix_bits and mem // (1 << bits) > limit:
+        bits += config.repartition_radix_bits_incr
+    return config.current_max_radix_bits.fetch_max(bits)
 
 
 def _current_torch_stream():
@@ -144,6 +205,10 @@ class AggregateHashTable:
         # retained device inputs may go: later reuse of their memory is stream-ordered after
         # every launch that reads them (the handle runs on torch's current stream)
         self._retained.clear()
+
+    def set_host_staging(self, rows: int):
+        """Gather host blocks into launches of `rows` rows (dbg_agg_set_host_staging); 0 = off."""
+        check(lib().dbg_agg_set_host_staging(self.h, rows))
 
     def set_strategy(self, strategy: int):
         """abi.STRATEGY_AUTO / STRATEGY_TABLE / STRATEGY_PARTITIONED (include/dbgpu_agg.h)."""
@@ -265,25 +330,83 @@ class AggregateHashTable:
 
 
 @dataclass
+class Payload:
+    """One bucket of a partial table's groups as partial-state records resident in HBM
+    (the GPU form of `Payload`, EAGG/payload.rs:41-84): `n_records` records of
+    dbg_agg_record_width bytes ([hash][keys][state words], include/dbgpu_agg.h) and the bucket's
+    string blob.  `records` / `strings` are torch uint8 cuda tensors (views into one export)."""
+    records: "object"
+    strings: "object"
+    n_records: int
+    string_bytes: int
+
+    def __len__(self):
+        return self.n_records
+
+
+@dataclass
 class AggregateMeta:
-    """AggregateMeta::AggregatePayload (AGG/aggregate_meta.rs:124-134): one partial table's
-    exact partial aggregation, still resident in HBM, with its bucket count."""
-    table: AggregateHashTable
-    bucket: int = 0
+    """AggregateMeta (AGG/aggregate_meta.rs:124-134).  AggregatePayload: one bucket of one
+    partial (`bucket`, `payload`, `max_partition_count` = 2^radix bits of the partial that wrote
+    it).  Partitioned: every payload of one bucket after alignment (`data`)."""
+    bucket: int
+    payload: Optional[Payload] = None
     max_partition_count: int = 1
+    data: Optional[List["AggregateMeta"]] = None
+
+    @staticmethod
+    def create_agg_payload(bucket: int, payload: Payload, max_partition_count: int) -> "AggregateMeta":
+        return AggregateMeta(bucket, payload, max_partition_count)
+
+    @staticmethod
+    def create_partitioned(bucket: int, data: List["AggregateMeta"]) -> "AggregateMeta":
+        return AggregateMeta(bucket, None, 0, data)
+
+    def is_partitioned(self) -> bool:
+        return self.data is not None
+
+
+def _cuda_device():
+    import torch
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def export_buckets(table: AggregateHashTable, n_parts: int, scheme: int = 1) -> List[Payload]:
+    """All groups of `table` as n_parts bucket payloads (dbg_agg_partition + export_records), in
+    bucket order; scheme 1 = radix bits [48 - r, 48) (EAGG/partitioned_payload.rs:121, 267-275),
+    scheme 0 = hash % n_parts (EAGG/payload.rs:377-383)."""
+    import torch
+    counts, sbytes = table.partition(n_parts, scheme)
+    w = table.record_width()
+    dev = _cuda_device()
+    recs = torch.empty(max(1, sum(counts) * w), dtype=torch.uint8, device=dev)
+    strs = torch.empty(max(1, sum(sbytes)), dtype=torch.uint8, device=dev)
+    table.export_records(recs, strs)
+    out, r0, s0 = [], 0, 0
+    for c, b in zip(counts, sbytes):
+        out.append(Payload(recs[r0 * w:(r0 + c) * w], strs[s0:s0 + b], c, b))
+        r0, s0 = r0 + c, s0 + b
+    return out
 
 
 class TransformPartialAggregate:
-    """AGG/transform_aggregate_partial.rs:107-468 — AccumulatingTransform over DataBlocks."""
+    """AGG/transform_aggregate_partial.rs:107-468 — AccumulatingTransform over DataBlocks.
+    Host blocks (<= max_block_size rows, settings_default.rs:131) are gathered by the library's
+    host staging into launches of `staging_rows` rows (dbg_agg_set_host_staging)."""
 
-    def __init__(self, params: AggregatorParams, config: HashTableConfig = None, device: int = -1):
+    DEFAULT_STAGING_ROWS = 1 << 23
+
+    def __init__(self, params: AggregatorParams, config: HashTableConfig = None, device: int = -1,
+                 staging_rows: int = DEFAULT_STAGING_ROWS):
         self.params = params
         self.config = (config or HashTableConfig()).with_partial(True)
         self.hashtable = AggregateHashTable(params, self.config, device)
+        if staging_rows:
+            self.hashtable.set_host_staging(staging_rows)
 
     @classmethod
-    def try_create(cls, params: AggregatorParams, config: HashTableConfig = None, device: int = -1):
-        return cls(params, config, device)
+    def try_create(cls, params: AggregatorParams, config: HashTableConfig = None, device: int = -1, **kw):
+        return cls(params, config, device, **kw)
 
     def transform(self, block: DataBlock, group_indices: Sequence[int], arg_indices: Sequence[Optional[int]],
                   filter_program=None) -> List[DataBlock]:
@@ -295,13 +418,62 @@ class TransformPartialAggregate:
         return []
 
     def on_finish(self) -> List[AggregateMeta]:
-        """on_finish (:449-465): the partial payload(s)."""
-        return [AggregateMeta(self.hashtable)]
+        """on_finish (:449-465): one AggregatePayload per non-empty radix bucket, bucket = hash bits
+        [48 - r, 48), with r from the shared radix hint and this table's payload size."""
+        n_groups = sum(self.hashtable.partition(1, 1)[0])
+        tuple_size = payload_tuple_size(self.params.group_data_types, len(self.params.aggregate_functions))
+        bits = partial_bucket_bits(self.config, n_groups, tuple_size)
+        payloads = export_buckets(self.hashtable, 1 << bits)
+        return [AggregateMeta.create_agg_payload(b, p, 1 << bits) for b, p in enumerate(payloads) if len(p)]
+
+    def close(self):
+        self.hashtable.close()
+
+
+class TransformPartitionBucket:
+    """NewTransformPartitionBucket (AGG/new_transform_partition_bucket.rs:25-576): collects every
+    partial's AggregatePayloads, aligns those written with fewer buckets to the largest bucket
+    count by repartitioning their rows (partition_payload, :389-429 — here a scratch table merges
+    the payload and re-exports it at the larger radix), and emits one Partitioned meta per bucket
+    in ascending bucket order."""
+
+    def __init__(self, params: AggregatorParams, device: int = -1):
+        self.params = params
+        self.device = device
+        self.inputs: List[AggregateMeta] = []
+
+    def push(self, metas: Sequence[AggregateMeta]) -> None:
+        self.inputs.extend(metas)
+
+    def _partition_payload(self, meta: AggregateMeta, max_partition_count: int) -> List[AggregateMeta]:
+        scratch = AggregateHashTable(self.params, HashTableConfig(True), self.device)
+        try:
+            p = meta.payload
+            scratch.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
+            out = export_buckets(scratch, max_partition_count)
+            import torch
+            torch.cuda.current_stream().synchronize()  # exports complete before the scratch goes
+        finally:
+            scratch.close()
+        return [AggregateMeta.create_agg_payload(b, q, max_partition_count) for b, q in enumerate(out) if len(q)]
+
+    def finish(self) -> List[AggregateMeta]:
+        if not self.inputs:
+            return []
+        maxp = max(m.max_partition_count for m in self.inputs)
+        buckets = {}
+        for m in self.inputs:
+            aligned = [m] if m.max_partition_count == maxp else self._partition_payload(m, maxp)
+            for a in aligned:
+                buckets.setdefault(a.bucket, []).append(a)
+        self.inputs = []
+        return [AggregateMeta.create_partitioned(b, buckets[b]) for b in sorted(buckets)]
 
 
 class TransformFinalAggregate:
-    """AGG/transform_aggregate_final.rs:45-343 — merge_states of partial payloads, then the
-    output block [agg results..., group cols...]."""
+    """AGG/transform_aggregate_final.rs:45-343 — per bucket, a fresh final table merges the states
+    of every payload (transform_agg_hashtable, :71-156), then the output block
+    [agg results..., group cols...]."""
 
     def __init__(self, params: AggregatorParams, device: int = -1):
         self.params = params
@@ -311,22 +483,15 @@ class TransformFinalAggregate:
     def try_create(cls, params: AggregatorParams, device: int = -1):
         return cls(params, device)
 
-    def transform(self, metas: Sequence[AggregateMeta]) -> DataBlock:
-        import torch
-        metas = list(metas)
-        if not metas:
+    def transform(self, meta: AggregateMeta) -> DataBlock:
+        payloads = [m.payload for m in meta.data] if meta.is_partitioned() else [meta.payload]
+        payloads = [p for p in payloads if p is not None and len(p)]
+        if not payloads:
             return self.params.empty_result_block()
         final = AggregateHashTable(self.params, HashTableConfig(False), self.device)
         try:
-            for m in metas:
-                counts, sbytes = m.table.partition(1, 0)
-                w = m.table.record_width()
-                dev = torch.device("cuda", torch.cuda.current_device())
-                recs = torch.empty(max(1, counts[0] * w), dtype=torch.uint8, device=dev)
-                strs = torch.empty(max(1, sbytes[0]), dtype=torch.uint8, device=dev)
-                m.table.export_records(recs, strs)
-                torch.cuda.synchronize()
-                final.merge_records(recs, strs, [counts[0]], [sbytes[0]])
+            for p in payloads:
+                final.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
             return final.merge_result()
         finally:
             final.close()

@@ -16,6 +16,7 @@
 #include <chrono>
 
 #include "agg.hpp"
+#include "host_stage.hpp"
 #include "filter.hpp"
 #include "sort.hpp"
 
@@ -260,6 +261,9 @@ struct dbg_agg_handle {
     bool pp_grec_ready = false;
     u64 pp_nb = 0;            // blocks of the grec passes
     u64 pp_stat_rounds = 0;   // partitions that took more than one LDS round (last finalize)
+
+    // host-block staging (dbg_agg_set_host_staging, host_stage.hpp)
+    hstage::Stage stage;
 };
 
 static int dev_alloc(void** p, size_t bytes) {
@@ -856,6 +860,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
     h->def_on = false;  // the held-back insert is discarded with the groups
+    h->stage.clear();   // and so are staged host rows
     // inputs copied by earlier batches, and the pinned batch descriptors reused below, may still
     // be read by queued work: wait if any were queued since the last synchronisation
     if (!h->owned.empty() || h->uploads_pending) {
@@ -1302,9 +1307,8 @@ static int pp_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_b
     return DBG_OK;
 }
 
-int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols, const dbg_filter* filter,
-                       uint64_t rows, int on_device) {
-    if (!h || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
+static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols, const dbg_filter* filter,
+                          uint64_t rows, int on_device) {
     if (rows >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "a batch holds fewer than 2^32 rows");
     HIPCHECK(hipSetDevice(h->device));
     RETURN_IF(flush_deferred(h));
@@ -1363,6 +1367,68 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
     return DBG_OK;
 }
 
+// Staged host blocks -> one batch (host_stage.hpp).  The host path is synchronous (it resolves
+// overflow before returning), so the staging vectors are free again when this returns.
+static int stage_flush(dbg_agg_handle* h) {
+    if (h->stage.empty()) return DBG_OK;
+    std::vector<dbg_column> k, a, fc;
+    std::vector<dbg_pred_node> nd;
+    dbg_filter flt;
+    h->stage.views(k, a, fc, nd, flt);
+    int rc = add_groups_now(h, k.data(), a.data(), flt.n_nodes ? &flt : nullptr, h->stage.rows, 0);
+    if (rc == DBG_OK && hipStreamSynchronize(h->stream) != hipSuccess) rc = fail(DBG_ERR_DEVICE, "stream synchronize");
+    h->stage.clear();
+    return rc;
+}
+
+// Everything a caller queued (staged host rows, a held-back insert) reaches the table.
+static int flush_pending(dbg_agg_handle* h) {
+    RETURN_IF(stage_flush(h));
+    return flush_deferred(h);
+}
+
+int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const dbg_column* arg_cols, const dbg_filter* filter,
+                       uint64_t rows, int on_device) {
+    if (!h || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(h->device));
+    hstage::Stage& G = h->stage;
+    if (on_device || !G.cap || rows >= G.cap) {
+        RETURN_IF(stage_flush(h));
+        return add_groups_now(h, group_cols, arg_cols, filter, rows, on_device);
+    }
+    const Spec& S = h->spec;
+    // the checks add_groups_now would make, before the rows are accepted
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_column& g = group_cols[c];
+        if (g.len < rows) return fail(DBG_ERR_INVALID, "group column shorter than rows");
+        if (g.dt.type != S.key_types[c].type || (g.dt.type == DBG_DECIMAL128 && g.dt.scale != S.key_types[c].scale) ||
+            (g.dt.nullable && !S.key_types[c].nullable))
+            return fail(DBG_ERR_INVALID, "column type does not match the declared type");
+    }
+    for (int a = 0; a < S.n_aggs; ++a) {
+        if (S.aggs[a].arg_type < 0) continue;
+        if (!arg_cols) return fail(DBG_ERR_INVALID, "missing aggregate arguments");
+        if (arg_cols[a].len < rows) return fail(DBG_ERR_INVALID, "argument column shorter than rows");
+        if (arg_cols[a].dt.type != S.aggs[a].arg_type) return fail(DBG_ERR_INVALID, "column type does not match the declared type");
+    }
+    if (filter && filter->n_nodes)
+        for (int c = 0; c < filter->n_cols; ++c)
+            if (filter->cols[c].len < rows) return fail(DBG_ERR_INVALID, "filter column shorter than rows");
+    if (!G.empty() && (G.rows + rows > G.cap || !G.same_filter(filter))) RETURN_IF(stage_flush(h));
+    if (rows == 0) return DBG_OK;
+    G.append(S.n_keys, group_cols, S.n_aggs, arg_cols, filter, rows);
+    h->finalized = false;
+    return DBG_OK;
+}
+
+int dbg_agg_set_host_staging(dbg_agg_handle* h, uint64_t rows) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(stage_flush(h));
+    h->stage.cap = rows >= 0xFFFFFFFFULL ? 0xFFFFFFFEULL : rows;
+    return DBG_OK;
+}
+
 static int ensure_buf(u64** p, u64* cap, u64 n) {
     if (n <= *cap) return DBG_OK;
     if (*p) HIPCHECK(hipFree(*p));
@@ -1373,7 +1439,7 @@ static int ensure_buf(u64** p, u64* cap, u64 n) {
 int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     if (h->pp) return pp_finalize(h, n_groups, string_bytes);
     const Spec& S = h->spec;
     // Optimistic single round trip: count + scan are enqueued behind the inserts and read back
@@ -1431,7 +1497,7 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     if (!h->finalized) return fail(DBG_ERR_INVALID, "dbg_agg_finalize must precede dbg_agg_result");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     const Spec& S = h->spec;
     u64 n = h->n_groups;
     for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = h->result_types[a];
@@ -1620,6 +1686,7 @@ static int pp_fin_complete(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* stri
 static int fin_launch(dbg_agg_handle* h) {
     FinState& F = h->fin;
     const Spec& S = h->spec;
+    RETURN_IF(stage_flush(h));  // staged host rows first (this launches any held-back insert)
     u64 nb = finalize_blocks(h->cap);
     RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
     RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
@@ -1810,7 +1877,7 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
     if (!h || !n_groups) return fail(DBG_ERR_INVALID, "null argument");
     if (!h->fin.active) return fail(DBG_ERR_INVALID, "no finalize in flight");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     for (int round = 0; round < 3; ++round) {
         if (round) RETURN_IF(fin_launch(h));
         bool retry = false;
@@ -1853,7 +1920,7 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
     if (n_parts < 1 || n_parts > 256) return fail(DBG_ERR_UNSUPPORTED, "1..256 partitions");
     if (scheme == 1 && (n_parts & (n_parts - 1))) return fail(DBG_ERR_INVALID, "radix partitions must be a power of two");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     if (h->pp) RETURN_IF(pp_finalize(h, nullptr, nullptr));
     else RETURN_IF(resolve_overflow(h));
     const Spec& S = h->spec;
@@ -1902,7 +1969,7 @@ int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strin
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     if (!h->part_n) return fail(DBG_ERR_INVALID, "dbg_agg_partition must precede dbg_agg_export_records");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     prof::Scope ps("export_records", h->stream);
     if (h->pp)
         launch_pp_grec_export(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, h->part_n, h->part_scheme, h->d_part_pos,
@@ -1928,7 +1995,7 @@ int dbg_agg_export_fixed(dbg_agg_handle* h, void* dev_buf, uint64_t cap_records)
     if (h->cap + 1 > FIN_SMALL_SLOTS || h->pp) return fail(DBG_ERR_UNSUPPORTED, "fixed export is for small tables");
     if (S.rec_width < 16) return fail(DBG_ERR_INTERNAL, "record narrower than the fixed header");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     prof::Scope ps("export_fixed", h->stream);
     launch_export_fixed(h->stream, h->dspec, h->dbatches, table_desc(h), (u8*)dev_buf, cap_records, h->recycle);
     HIPCHECK(hipGetLastError());
@@ -1949,7 +2016,7 @@ int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs,
     const u64 n = (u64)n_bufs * (cap_records + 1);
     if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     h->finalized = false;
     h->clean = false;
     BatchDesc* st;
@@ -1988,7 +2055,7 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
                           const uint64_t* seg_records, const uint64_t* seg_string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_deferred(h));
+    RETURN_IF(flush_pending(h));
     h->finalized = false;
     h->clean = false;
     const Spec& S = h->spec;

@@ -21,7 +21,7 @@ EXPORTED = [
     "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_set_recycle", "dbg_agg_finalize_into_async", "dbg_agg_finalize_wait", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
     "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_sort_limit_indices", "dbg_prof_enable", "dbg_prof_reset",
     "dbg_prof_get", "dbg_datagen", "dbg_agg_set_strategy", "dbg_agg_get_strategy",
-    "dbg_agg_record_layout",
+    "dbg_agg_record_layout", "dbg_agg_set_host_staging",
 ]
 
 
@@ -71,6 +71,7 @@ def lib():
         L.dbg_agg_result.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), C.c_int]
         L.dbg_agg_finalize_into.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), U64, P(U64), P(U64), P(U64)]
         L.dbg_agg_set_recycle.argtypes = [VP, C.c_int]
+        L.dbg_agg_set_host_staging.argtypes = [VP, U64]
         L.dbg_agg_set_strategy.argtypes = [VP, C.c_int]
         L.dbg_agg_record_layout.argtypes = [P(abi.dbg_agg_params), P(abi.dbg_record_layout)]
         L.dbg_agg_get_strategy.argtypes = [VP, P(C.c_int), P(U64)]

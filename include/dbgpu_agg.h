@@ -236,6 +236,19 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
  * immutable once produced (EXP/block.rs).  Launch errors of the insert surface from that call. */
 int dbg_agg_set_recycle(dbg_agg_handle* h, int on);
 
+/* Host-block staging (default off).  The reference hands TransformPartialAggregate blocks of at
+ * most max_block_size = 65,536 rows (src/query/settings/src/settings_default.rs:131), one
+ * AggregateHashTable::add_groups per block (AGG/transform_aggregate_partial.rs:291-323).  With
+ * staging on, a host-resident (on_device = 0) dbg_agg_add_groups appends the block's rows to a
+ * host staging area of `rows` rows and returns; the staged rows go to the device as one batch
+ * when the area is full, when a block arrives with a different filter program, and before any
+ * call that reads the table (finalize, result, partition, export, merge) — so results are those
+ * of one add_groups per block.  Type and length errors are still reported by the appending call;
+ * device errors of a staged batch surface from the call that flushes it.  A block of >= `rows`
+ * rows, and every on_device call, is added directly (after a flush).  dbg_agg_reset discards
+ * staged rows.  rows = 0 turns staging off (after a flush). */
+int dbg_agg_set_host_staging(dbg_agg_handle* h, uint64_t rows);
+
 /* Aggregation strategy of a handle (set after create or reset, before any batch):
  *   DBG_STRATEGY_AUTO        — the first large batch (>= 4M rows) into an empty handle is probed
  *                              (distinct group hashes of 2^20 sampled rows); an estimated > 1M groups

@@ -30,8 +30,89 @@ def _sort_key(row):
     return out
 
 
+FAST_MIN_ROWS = 20_000
+
+
+def _canon(c, n):
+    """Numpy arrays that identify column c's values for sorting and exact comparison: NULL rows
+    zeroed behind a leading validity array; Decimal128 as (hi i64, lo u64); strings up to 64 B as
+    big-endian 8-byte words + length (lexicographic order).  None if the column needs the slow path."""
+    import numpy as np
+    t = c.dtype.type_id
+    if t == abi.STRING:
+        offs = np.asarray(c.offsets, dtype=np.int64)[: n + 1]
+        lens = offs[1:] - offs[:-1]
+        width = int(lens.max()) if n else 0
+        if width > 64:
+            return None
+        nw = max(1, (width + 7) // 8)
+        data = np.concatenate([np.asarray(c.data, np.uint8), np.zeros(8, np.uint8)])
+        starts = offs[:-1]
+        words = []
+        for w in range(nw):
+            acc = np.zeros(n, np.uint64)
+            for b in range(8):
+                j = w * 8 + b
+                byte = np.where(j < lens, data[np.minimum(starts + j, len(data) - 1)], 0).astype(np.uint64)
+                acc |= byte << np.uint64(8 * (7 - b))
+            words.append(acc)
+        cols = words + [lens.astype(np.uint64)]
+    elif t == abi.DECIMAL128:
+        b = np.asarray(c.data, np.uint8)[: n * 16].reshape(n, 16)
+        cols = [b[:, 8:].copy().view(np.int64).reshape(-1), b[:, :8].copy().view(np.uint64).reshape(-1)]
+    elif t == abi.BOOLEAN:
+        cols = [np.asarray(c.data, bool)[:n].astype(np.uint8)]
+    else:
+        cols = [np.asarray(c.data)[:n]]
+    if c.validity is not None and c.dtype.nullable:
+        v = np.asarray(c.validity, bool)[:n]
+        cols = [v.astype(np.uint8)] + [np.where(v, x, np.zeros_like(x)) for x in cols]
+    return cols
+
+
+def _fast_compare(got_keys, got_aggs, exp_keys, exp_aggs, float_rel):
+    """Vectorized assert_results_equal for large results; returns False when a column type needs
+    the row-by-row path (float keys, strings > 64 B)."""
+    import numpy as np
+    ng, ne = len(got_keys[0]), len(exp_keys[0])
+    assert ng == ne, f"group count differs: got {ng} expected {ne}"
+    if any(k.dtype.type_id in (abi.FLOAT32, abi.FLOAT64) for k in got_keys):
+        return False
+    gk = [_canon(c, ng) for c in got_keys]
+    ek = [_canon(c, ne) for c in exp_keys]
+    if any(x is None for x in gk + ek):
+        return False
+    gk = [a for cols in gk for a in cols]
+    ek = [a for cols in ek for a in cols]
+    if len(gk) != len(ek):  # e.g. string widths differ: the group sets differ
+        raise AssertionError("group key columns differ in shape")
+    go = np.lexsort(gk[::-1])
+    eo = np.lexsort(ek[::-1])
+    for j, (a, b) in enumerate(zip(gk, ek)):
+        a, b = a[go], b[eo]
+        bad = np.nonzero(a != b)[0]
+        assert bad.size == 0, f"group sets differ (key word {j}) at sorted row {bad[0]}: {a[bad[0]]!r} != {b[bad[0]]!r}"
+    for j, (g, e) in enumerate(zip(got_aggs, exp_aggs)):
+        assert g.dtype == e.dtype, f"agg {j}: type {g.dtype} != {e.dtype}"
+        gc, ec = _canon(g, ng), _canon(e, ne)
+        for a, b in zip(gc, ec):
+            a, b = a[go], b[eo]
+            if a.dtype.kind == "f":
+                ok = (a == b) | (np.isnan(a) & np.isnan(b)) | (np.abs(a - b) <= float_rel * np.maximum(np.abs(a), np.abs(b)))
+            else:
+                ok = a == b
+            bad = np.nonzero(~ok)[0]
+            assert bad.size == 0, f"agg {j} differs at sorted row {bad[0]}: {a[bad[0]]!r} != {b[bad[0]]!r} " \
+                                  f"({bad.size} rows differ)"
+    return True
+
+
 def assert_results_equal(got_keys, got_aggs, exp_keys, exp_aggs, float_rel=FLOAT_REL_TOL, n_key_cols=None):
     """Compare (keys, aggs) column lists as row multisets, sorted by the key columns."""
+    if n_key_cols is None and got_keys and exp_keys and len(got_keys) == len(exp_keys) \
+            and len(exp_keys[0]) >= FAST_MIN_ROWS:
+        if _fast_compare(got_keys, got_aggs, exp_keys, exp_aggs, float_rel):
+            return
     g = rows_of(got_keys, got_aggs)
     e = rows_of(exp_keys, exp_aggs)
     assert len(g) == len(e), f"group count differs: got {len(g)} expected {len(e)}"

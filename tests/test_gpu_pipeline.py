@@ -1,0 +1,205 @@
+"""The processor mirrors end to end on the GPU, fed like the reference feeds them.
+
+TransformPartialAggregate receives host DataBlocks of <= 65,536 rows (max_block_size,
+src/query/settings/src/settings_default.rs:131) which the library stages into large launches
+(dbg_agg_set_host_staging); on_finish emits one AggregatePayload per non-empty radix bucket
+(transform_aggregate_partial.rs:449-465, bucket = hash bits [48 - r, 48),
+EAGG/partitioned_payload.rs:121, 267-275); TransformPartitionBucket aligns partials written
+with fewer buckets to the largest count (new_transform_partition_bucket.rs:389-429) and emits the
+buckets in order; TransformFinalAggregate merges each bucket into its output block
+(transform_aggregate_final.rs:71-156).  Checked against the oracle: every output block holds
+only groups whose oracle group hash falls in its bucket, and the union of the blocks equals the
+oracle's aggregation of all rows.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from databend_amd import abi
+from databend_amd import column as col
+from databend_amd.aggregates import AggregateFunctionFactory
+from databend_amd.aggregator import (AggregateHashTable, AggregatorParams, HashTableConfig, TransformFinalAggregate,
+                                     TransformPartialAggregate, TransformPartitionBucket)
+from databend_amd.column import Column, DataBlock, pack_bits
+from databend_amd.filter import FilterProgram, cmp
+from oracle import oracle
+from tests.parity import assert_results_equal
+from tests.test_gpu_parity import oracle_aggregate, slice_col
+
+pytestmark = pytest.mark.gpu
+F = AggregateFunctionFactory.instance()
+BLOCK = 65536
+
+
+def concat(cols):
+    t = cols[0].dtype
+    val = None
+    if any(c.validity is not None for c in cols) and t.nullable:
+        val = np.concatenate([np.ones(len(c), bool) if c.validity is None else np.asarray(c.validity, bool) for c in cols])
+    if t.type_id == abi.STRING:
+        offs, data, base = [np.zeros(1, np.uint64)], [], 0
+        for c in cols:
+            o = np.asarray(c.offsets, np.uint64)
+            offs.append(o[1:] - o[0] + np.uint64(base))
+            data.append(np.asarray(c.data[int(o[0]):int(o[-1])], np.uint8))
+            base += int(o[-1] - o[0])
+        return Column(t, np.concatenate(data) if data else np.zeros(0, np.uint8), np.concatenate(offs), val)
+    return Column(t, np.concatenate([np.asarray(c.data) for c in cols]), None, val)
+
+
+def _data(case, n, rng):
+    if case == "i64":
+        keys = [Column.from_numbers(col.Int64, rng.integers(0, 600_000, n) * 7919 - 10**6)]
+        v = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n))
+        w = Column.from_numbers(col.Int32, rng.integers(-2**31, 2**31 - 1, n))
+        aggs = [("count", None), ("sum", v), ("min", w), ("max", v)]
+        pred_col = v
+    else:
+        words = [("k%05d" % i) * (1 + i % 3) for i in range(40_000)]
+        idx = rng.integers(0, len(words), n)
+        s = Column.from_strings([words[i] for i in idx])
+        k2 = Column.from_numbers(col.Int32, rng.integers(0, 3, n), validity=rng.random(n) < 0.8)
+        keys = [s, k2]
+        d = Column.from_decimals(15, 2, [int(x) for x in rng.integers(-10**9, 10**9, n)])
+        fv = Column.from_numbers(col.Float64, rng.integers(-50, 50, n).astype(np.float64), validity=rng.random(n) < 0.9)
+        aggs = [("count", None), ("sum", d), ("max", fv), ("sql_avg", d), ("count", fv)]
+        pred_col = k2
+    return keys, aggs, pred_col
+
+
+def _block(keys, aggs, pred_col, lo, hi):
+    cols = [slice_col(k, lo, hi) for k in keys] + [slice_col(c, lo, hi) for _, c in aggs if c is not None]
+    cols.append(slice_col(pred_col, lo, hi))
+    return DataBlock(cols)
+
+
+@pytest.mark.parametrize("case", ["i64", "str_dec"])
+def test_partial_bucket_final_pipeline(case):
+    rng = np.random.default_rng(7 if case == "i64" else 8)
+    n_a, n_b = 1_300_000, 40_000
+    keys, aggs, pred_col = _data(case, n_a + n_b, rng)
+    fns = [F.get(f, [], [c.dtype] if c is not None else []) for f, c in aggs]
+    params = AggregatorParams([k.dtype for k in keys], fns)
+    nk = len(keys)
+    arg_idx, j = [], nk
+    for _, c in aggs:
+        arg_idx.append(None if c is None else j)
+        j += c is not None
+    pred_idx = j
+    const = 7 if case == "i64" else 1
+    op = "<>"
+
+    config = HashTableConfig()  # one shared radix hint, as in one query
+    part_a = TransformPartialAggregate(params, config, staging_rows=1 << 20)
+    part_b = TransformPartialAggregate(params, config, staging_rows=1 << 20)
+    try:
+        for p, lo, hi in ((part_b, n_a, n_a + n_b), (part_a, 0, n_a)):
+            for s in range(lo, hi, BLOCK):
+                e = min(hi, s + BLOCK)
+                blk = _block(keys, aggs, pred_col, s, e)
+                fp = FilterProgram(cmp(0, op, const), [blk.columns[pred_idx].to_abi()])
+                p.transform(blk, list(range(nk)), arg_idx, filter_program=fp)
+        metas_b = part_b.on_finish()  # finishes first: the hint is still small
+        metas_a = part_a.on_finish()
+        pb = {m.max_partition_count for m in metas_b}
+        pa = {m.max_partition_count for m in metas_a}
+        assert len(pa) == 1 and len(pb) == 1
+        maxp = pa.pop()
+        assert pb.pop() < maxp, "the small partial finished with fewer buckets"
+        bits = maxp.bit_length() - 1
+        assert all(m.bucket < m.max_partition_count and len(m.payload) for m in metas_a + metas_b)
+
+        bucket = TransformPartitionBucket(params)
+        bucket.push(metas_b + metas_a)
+        parts = bucket.finish()
+        bs = [p.bucket for p in parts]
+        assert bs == sorted(set(bs)) and bs[-1] < maxp
+        final = TransformFinalAggregate.try_create(params)
+        na = len(aggs)
+        out_k, out_a = [[] for _ in range(nk)], [[] for _ in range(na)]
+        for p in parts:
+            blk = final.transform(p)
+            ks = blk.columns[na:]
+            h = oracle.group_hash(ks)
+            got = (h & np.uint64((1 << 48) - 1)) >> np.uint64(48 - bits)
+            assert (got == p.bucket).all(), f"bucket {p.bucket} holds groups of other buckets"
+            for i in range(nk):
+                out_k[i].append(ks[i])
+            for i in range(na):
+                out_a[i].append(blk.columns[i])
+        gk, ga = [concat(c) for c in out_k], [concat(c) for c in out_a]
+        ok, oa = oracle_aggregate(keys, aggs, (cmp(0, op, const), [pred_col]), threads=8)
+        assert_results_equal(gk, ga, ok, oa)
+    finally:
+        part_a.close()
+        part_b.close()
+
+
+def _abi_slice(parent: Column, packed_valid, lo, hi):
+    """An arrow-style slice [lo, hi) of a host column: pointers into the parent's buffers, the
+    validity bitmap shared with a bit offset (Bitmap::sliced), string offsets not rebased."""
+    c = abi.dbg_column()
+    c.dt = parent.dtype.to_abi()
+    t = parent.dtype.type_id
+    if t == abi.STRING:
+        c.data = parent.data.ctypes.data
+        c.offsets = parent.offsets.ctypes.data + lo * 8
+    else:
+        c.data = parent.data.ctypes.data + lo * parent.data.itemsize
+    if packed_valid is not None:
+        c.validity = packed_valid.ctypes.data
+        c.validity_offset = lo
+    c.len = hi - lo
+    return c
+
+
+def test_host_staging_ragged_blocks_and_filter_switch():
+    """dbg_agg_set_host_staging: ragged host blocks (1 .. 70,000 rows, some larger than the
+    staging area), validity bitmaps at odd bit offsets, string offsets not starting at 0, and a
+    filter program that changes mid-stream (forcing a flush) give the oracle's result over the
+    rows each block's own filter selected."""
+    from databend_amd.column import abi_array
+    from databend_amd.ffi import check, lib
+    rng = np.random.default_rng(11)
+    n = 700_000
+    words = ["w%d" % i * (1 + i % 4) for i in range(5000)]
+    s = Column.from_strings([words[i] for i in rng.integers(0, len(words), n)])
+    k = Column.from_numbers(col.Int32, rng.integers(0, 50, n), validity=rng.random(n) < 0.85)
+    v = Column.from_numbers(col.Int64, rng.integers(0, 100, n), validity=rng.random(n) < 0.9)
+    kv, vv = pack_bits(k.validity), pack_bits(v.validity)
+    aggs = [("count", None), ("sum", v), ("min", v), ("count", v)]
+    fns = [F.get(f, [], [c.dtype] if c is not None else []) for f, c in aggs]
+    params = AggregatorParams([s.dtype, k.dtype], fns)
+    ht = AggregateHashTable(params, HashTableConfig(True))
+    ht.set_host_staging(100_000)
+    bounds = [0]
+    while bounds[-1] < n:
+        step = int(rng.choice([1, 3, 999, 65536, 70_000, 150_000]))
+        bounds.append(min(n, bounds[-1] + step))
+    sel_parts = []
+    try:
+        for b in range(len(bounds) - 1):
+            lo, hi = bounds[b], bounds[b + 1]
+            first = lo < n // 2
+            op, c0 = ("<", 60) if first else (">=", 25)
+            keys = abi_array([_abi_slice(s, None, lo, hi), _abi_slice(k, kv, lo, hi)])
+            va = _abi_slice(v, vv, lo, hi)
+            none = abi.dbg_column()
+            none.dt = abi.dbg_datatype(-1, 0, 0, 0, 0)
+            args = abi_array([none, va, va, va])
+            fp = FilterProgram(cmp(0, op, c0), [va])
+            check(lib().dbg_agg_add_groups(ht.h, keys, args, fp.ptr(), hi - lo, 0))
+            vals = np.asarray(v.data[lo:hi])
+            ok = np.asarray(v.validity[lo:hi]) & ((vals < c0) if first else (vals >= c0))
+            sel_parts.append(np.nonzero(ok)[0] + lo)
+        blk = ht.merge_result()
+    finally:
+        ht.close()
+    sel = np.concatenate(sel_parts)
+    svals = s.values()
+    ks = Column.from_strings([svals[i] for i in sel])
+    kk = Column.from_numbers(col.Int32, k.data[sel], validity=k.validity[sel])
+    vs = Column.from_numbers(col.Int64, v.data[sel], validity=v.validity[sel])
+    ok_, oa = oracle_aggregate([ks, kk], [(f, vs if c is not None else None) for f, c in aggs], threads=8)
+    assert_results_equal(blk.columns[4:], blk.columns[:4], ok_, oa)
