@@ -74,7 +74,14 @@ class dbg_record_layout(C.Structure):
                 ("flags_word", C.c_int32), ("n_words", C.c_int32)]
 
 
+class dbg_exchange_stats(C.Structure):
+    _fields_ = [("sent_bytes", C.c_uint64), ("remote_bytes", C.c_uint64), ("received_records", C.c_uint64),
+                ("received_string_bytes", C.c_uint64)]
+
+
+DBG_COMM_ID_BYTES = 128
+
 EXPECTED_SIZES = {
     "dbg_datatype": 8, "dbg_column": 56, "dbg_out_column": 32, "dbg_agg_spec": 16,
-    "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 48, "dbg_record_layout": 328,
+    "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 48, "dbg_record_layout": 328, "dbg_exchange_stats": 32,
 }

@@ -17,6 +17,9 @@
 
 #include "agg.hpp"
 #include "host_stage.hpp"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: the entry points are resolved with dlsym (exchange section)
 #include "filter.hpp"
 #include "sort.hpp"
 
@@ -2213,6 +2216,223 @@ int dbg_datagen(int cfg, uint64_t seed, uint64_t row_start, uint64_t rows, void*
     hipStream_t s = (hipStream_t)stream;
     if (launch_datagen(s, cfg, seed, row_start, rows, outs, n_outs, aux) != 0) return fail(DBG_ERR_INVALID, "bad datagen config");
     HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// multi-GPU exchange over RCCL (replaces the Flight shuffle of
+// AGG/aggregate_exchange_injector.rs:154-354 for the final-merge stage)
+// ------------------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+// RCCL is loaded on first use, so the library (and a host without RCCL) works for single-GPU
+// aggregation.  DBG_RCCL_LIB overrides the library path.
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*ErrorString)(ncclResult_t) = nullptr;
+};
+
+RcclApi& rccl_api() {
+    static RcclApi A;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* env = getenv("DBG_RCCL_LIB");
+        const char* names[] = {env, "librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
+        void* so = nullptr;
+        for (const char* n : names)
+            if (n && (so = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!so) {
+            A.err = std::string("cannot load RCCL: ") + dlerror();
+            return;
+        }
+        auto sym = [&](const char* n) { return dlsym(so, n); };
+        A.GetUniqueId = (decltype(A.GetUniqueId))sym("ncclGetUniqueId");
+        A.CommInitRank = (decltype(A.CommInitRank))sym("ncclCommInitRank");
+        A.CommDestroy = (decltype(A.CommDestroy))sym("ncclCommDestroy");
+        A.AllGather = (decltype(A.AllGather))sym("ncclAllGather");
+        A.Send = (decltype(A.Send))sym("ncclSend");
+        A.Recv = (decltype(A.Recv))sym("ncclRecv");
+        A.GroupStart = (decltype(A.GroupStart))sym("ncclGroupStart");
+        A.GroupEnd = (decltype(A.GroupEnd))sym("ncclGroupEnd");
+        A.ErrorString = (decltype(A.ErrorString))sym("ncclGetErrorString");
+        A.ok = A.GetUniqueId && A.CommInitRank && A.CommDestroy && A.AllGather && A.Send && A.Recv && A.GroupStart &&
+               A.GroupEnd && A.ErrorString;
+        if (!A.ok) A.err = "RCCL library lacks an entry point";
+    });
+    return A;
+}
+}  // namespace
+
+#define RCCLCHECK(x)                                                                              \
+    do {                                                                                          \
+        ncclResult_t r_ = (x);                                                                    \
+        if (r_ != ncclSuccess) return fail(DBG_ERR_DEVICE, std::string("RCCL: ") + R.ErrorString(r_)); \
+    } while (0)
+
+struct dbg_comm {
+    ncclComm_t comm = nullptr;
+    int n = 0, rank = 0, device = 0;
+    u64* dsizes = nullptr;  // device: [2n] own sizes, then [n][2n] gathered
+    u64* hsizes = nullptr;  // pinned mirror of the gathered sizes
+    u8* send_recs = nullptr;
+    u8* send_strs = nullptr;
+    u64 send_recs_cap = 0, send_strs_cap = 0;
+    hipEvent_t sent = nullptr;  // the last exchange's sends: the next export into the buffers waits
+    bool sent_valid = false;
+};
+
+extern "C" {
+
+int dbg_comm_get_unique_id(uint8_t* id) {
+    if (!id) return fail(DBG_ERR_INVALID, "null argument");
+    RcclApi& R = rccl_api();
+    if (!R.ok) return fail(DBG_ERR_UNSUPPORTED, R.err);
+    ncclUniqueId u;
+    RCCLCHECK(R.GetUniqueId(&u));
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return DBG_OK;
+}
+
+int dbg_comm_create(const uint8_t* id, int n_ranks, int rank, int device, dbg_comm** out) {
+    if (!id || !out || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(DBG_ERR_INVALID, "bad communicator arguments");
+    RcclApi& R = rccl_api();
+    if (!R.ok) return fail(DBG_ERR_UNSUPPORTED, R.err);
+    if (device < 0) HIPCHECK(hipGetDevice(&device));
+    HIPCHECK(hipSetDevice(device));
+    auto* c = new dbg_comm();
+    c->n = n_ranks;
+    c->rank = rank;
+    c->device = device;
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t r = R.CommInitRank(&c->comm, n_ranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(DBG_ERR_DEVICE, std::string("ncclCommInitRank: ") + R.ErrorString(r));
+    }
+    const u64 words = 2ull * n_ranks * (n_ranks + 1);
+    if (dev_alloc((void**)&c->dsizes, words * 8) != DBG_OK || hipHostMalloc((void**)&c->hsizes, words * 8, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sent, hipEventDisableTiming) != hipSuccess) {
+        dbg_comm_destroy(c);
+        return fail(DBG_ERR_OOM, "communicator scratch");
+    }
+    *out = c;
+    return DBG_OK;
+}
+
+void dbg_comm_destroy(dbg_comm* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->sent_valid) hipEventSynchronize(c->sent);
+    RcclApi& R = rccl_api();
+    if (c->comm && R.ok) R.CommDestroy(c->comm);
+    if (c->dsizes) hipFree(c->dsizes);
+    if (c->send_recs) hipFree(c->send_recs);
+    if (c->send_strs) hipFree(c->send_strs);
+    if (c->hsizes) hipHostFree(c->hsizes);
+    if (c->sent) hipEventDestroy(c->sent);
+    delete c;
+}
+
+int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final_h, dbg_exchange_stats* stats) {
+    if (!c || !partial || !final_h) return fail(DBG_ERR_INVALID, "null argument");
+    if (partial->device != c->device || final_h->device != c->device)
+        return fail(DBG_ERR_INVALID, "communicator and tables are on different devices");
+    if (partial->spec.n_keys != final_h->spec.n_keys || partial->spec.n_aggs != final_h->spec.n_aggs ||
+        partial->spec.stride_words != final_h->spec.stride_words)
+        return fail(DBG_ERR_INVALID, "partial and final tables have different parameters");
+    RcclApi& R = rccl_api();
+    if (!R.ok) return fail(DBG_ERR_UNSUPPORTED, R.err);
+    HIPCHECK(hipSetDevice(c->device));
+    const int n = c->n, me = c->rank;
+    std::vector<u64> counts(n), sbytes(n);
+    // Payload::scatter's routing (EAGG/payload.rs:377-383): group -> rank hash % n
+    RETURN_IF(dbg_agg_partition(partial, (uint32_t)n, 0, counts.data(), sbytes.data()));
+    uint32_t w = 0;
+    RETURN_IF(dbg_agg_record_width(partial, &w));
+    hipStream_t s = partial->stream;
+    // 1. sizes: every rank's [records, string bytes] per destination, one all-gather
+    u64* own = c->hsizes;
+    for (int d = 0; d < n; ++d) {
+        own[2 * d] = counts[d];
+        own[2 * d + 1] = sbytes[d];
+    }
+    HIPCHECK(hipMemcpyAsync(c->dsizes, own, 16ull * n, hipMemcpyHostToDevice, s));
+    RCCLCHECK(R.AllGather(c->dsizes, c->dsizes + 2 * n, 2 * n, ncclUint64, c->comm, s));
+    HIPCHECK(hipMemcpyAsync(c->hsizes + 2 * n, c->dsizes + 2 * n, 16ull * n * n, hipMemcpyDeviceToHost, s));
+    // 2. records + blobs, partition-major, into the communicator's send buffers
+    u64 tot_r = 0, tot_s = 0;
+    for (int d = 0; d < n; ++d) {
+        tot_r += counts[d];
+        tot_s += sbytes[d];
+    }
+    if (c->sent_valid) HIPCHECK(hipEventSynchronize(c->sent));
+    c->sent_valid = false;
+    if (tot_r * w > c->send_recs_cap) {
+        if (c->send_recs) HIPCHECK(hipFree(c->send_recs));
+        c->send_recs_cap = std::max<u64>(tot_r * w, 1 << 20);
+        RETURN_IF(dev_alloc((void**)&c->send_recs, c->send_recs_cap));
+    }
+    if (tot_s > c->send_strs_cap) {
+        if (c->send_strs) HIPCHECK(hipFree(c->send_strs));
+        c->send_strs_cap = std::max<u64>(tot_s, 1 << 16);
+        RETURN_IF(dev_alloc((void**)&c->send_strs, c->send_strs_cap));
+    }
+    if (!c->send_recs) RETURN_IF(dev_alloc((void**)&c->send_recs, c->send_recs_cap = 1 << 20));
+    if (!c->send_strs) RETURN_IF(dev_alloc((void**)&c->send_strs, c->send_strs_cap = 1 << 16));
+    RETURN_IF(dbg_agg_export_records(partial, c->send_recs, c->send_strs));
+    HIPCHECK(hipStreamSynchronize(s));  // gathered sizes on the host (the one host round trip)
+    const u64* g = c->hsizes + 2 * n;   // g[src * 2n + 2 * dst + {0, 1}]
+    std::vector<u64> seg_r(n), seg_s(n);
+    u64 rr = 0, rs = 0;
+    for (int src = 0; src < n; ++src) {
+        seg_r[src] = g[(u64)src * 2 * n + 2 * me];
+        seg_s[src] = g[(u64)src * 2 * n + 2 * me + 1];
+        rr += seg_r[src];
+        rs += seg_s[src];
+    }
+    if (seg_r[me] != counts[me] || seg_s[me] != sbytes[me]) return fail(DBG_ERR_INTERNAL, "exchange sizes disagree");
+    // receive buffers belong to the final table: merge_records retains them until its reset
+    void *rrec = nullptr, *rstr = nullptr;
+    RETURN_IF(dev_alloc(&rrec, rr * w));
+    final_h->owned.push_back({rrec, (size_t)std::max<u64>(rr * w, 16)});
+    RETURN_IF(dev_alloc(&rstr, rs));
+    final_h->owned.push_back({rstr, (size_t)std::max<u64>(rs, 16)});
+    // 3. grouped point-to-point over xGMI (records and blobs; self included)
+    RCCLCHECK(R.GroupStart());
+    u64 so_r = 0, so_s = 0, ro_r = 0, ro_s = 0;
+    for (int p = 0; p < n; ++p) {
+        if (counts[p]) RCCLCHECK(R.Send(c->send_recs + so_r * w, counts[p] * w, ncclUint8, p, c->comm, s));
+        if (sbytes[p]) RCCLCHECK(R.Send(c->send_strs + so_s, sbytes[p], ncclUint8, p, c->comm, s));
+        if (seg_r[p]) RCCLCHECK(R.Recv((u8*)rrec + ro_r * w, seg_r[p] * w, ncclUint8, p, c->comm, s));
+        if (seg_s[p]) RCCLCHECK(R.Recv((u8*)rstr + ro_s, seg_s[p], ncclUint8, p, c->comm, s));
+        so_r += counts[p];
+        so_s += sbytes[p];
+        ro_r += seg_r[p];
+        ro_s += seg_s[p];
+    }
+    RCCLCHECK(R.GroupEnd());
+    HIPCHECK(hipEventRecord(c->sent, s));
+    c->sent_valid = true;
+    if (final_h->stream != s) HIPCHECK(hipStreamWaitEvent(final_h->stream, c->sent, 0));
+    // 4. merge_states of what arrived into this rank's final table
+    RETURN_IF(dbg_agg_merge_records(final_h, rrec, rstr, n, seg_r.data(), seg_s.data()));
+    if (stats) {
+        stats->sent_bytes = tot_r * w + tot_s;
+        stats->remote_bytes = stats->sent_bytes - counts[me] * w - sbytes[me];
+        stats->received_records = rr;
+        stats->received_string_bytes = rs;
+    }
     return DBG_OK;
 }
 

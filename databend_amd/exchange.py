@@ -104,6 +104,58 @@ def exchange_partial(partial, final, device) -> dict:
     return dict(sent_bytes=sent, remote_bytes=sent - counts[me] * w - sbytes[me], received_records=sum(seg_records))
 
 
+class AbiComm:
+    """A communicator of the C ABI (dbg_comm_*): the exchange a Rust host drives without torch.
+    `unique_id` is created by one rank and handed to every rank by the host's own channel (here
+    torch.distributed's object broadcast when a process group exists)."""
+
+    def __init__(self, uid: bytes, n_ranks: int, rank: int, device: int = -1):
+        import ctypes as C
+        from .ffi import check, lib
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib().dbg_comm_create(buf, n_ranks, rank, device, C.byref(h)))
+        self.h = h
+        self.n_ranks, self.rank = n_ranks, rank
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+        from .ffi import check, lib
+        buf = (C.c_uint8 * 128)()
+        check(lib().dbg_comm_get_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def from_process_group(cls, device: int = -1) -> "AbiComm":
+        dist = _dist()
+        obj = [cls.unique_id() if dist.get_rank() == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return cls(obj[0], dist.get_world_size(), dist.get_rank(), device)
+
+    def exchange(self, partial, final) -> dict:
+        """dbg_agg_exchange: route partial's groups to rank hash % n, merge arrivals into final."""
+        import ctypes as C
+        from . import abi
+        from .ffi import check, lib
+        st = abi.dbg_exchange_stats()
+        check(lib().dbg_agg_exchange(self.h, partial.h, final.h, C.byref(st)))
+        return dict(sent_bytes=st.sent_bytes, remote_bytes=st.remote_bytes, received_records=st.received_records,
+                    received_string_bytes=st.received_string_bytes)
+
+    def close(self):
+        if getattr(self, "h", None):
+            from .ffi import lib
+            lib().dbg_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 _FIXED_BUFS = {}
 
 

@@ -22,6 +22,7 @@ EXPORTED = [
     "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_sort_limit_indices", "dbg_prof_enable", "dbg_prof_reset",
     "dbg_prof_get", "dbg_datagen", "dbg_agg_set_strategy", "dbg_agg_get_strategy",
     "dbg_agg_record_layout", "dbg_agg_set_host_staging",
+    "dbg_comm_get_unique_id", "dbg_comm_create", "dbg_comm_destroy", "dbg_agg_exchange",
 ]
 
 
@@ -72,6 +73,11 @@ def lib():
         L.dbg_agg_finalize_into.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), U64, P(U64), P(U64), P(U64)]
         L.dbg_agg_set_recycle.argtypes = [VP, C.c_int]
         L.dbg_agg_set_host_staging.argtypes = [VP, U64]
+        L.dbg_comm_get_unique_id.argtypes = [VP]
+        L.dbg_comm_create.argtypes = [VP, C.c_int, C.c_int, C.c_int, P(VP)]
+        L.dbg_comm_destroy.argtypes = [VP]
+        L.dbg_comm_destroy.restype = None
+        L.dbg_agg_exchange.argtypes = [VP, VP, VP, P(abi.dbg_exchange_stats)]
         L.dbg_agg_set_strategy.argtypes = [VP, C.c_int]
         L.dbg_agg_record_layout.argtypes = [P(abi.dbg_agg_params), P(abi.dbg_record_layout)]
         L.dbg_agg_get_strategy.argtypes = [VP, P(C.c_int), P(U64)]

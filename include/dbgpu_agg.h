@@ -307,6 +307,32 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
                           int32_t n_segments, const uint64_t* seg_records,
                           const uint64_t* seg_string_bytes);
 
+/* ---- multi-GPU exchange over RCCL ----
+ * Replaces, for the final-merge stage, the cluster shuffle of AggregateMeta between nodes
+ * (AGG/aggregate_exchange_injector.rs:154-354: Payload::scatter by hash % n, EAGG/payload.rs:
+ * 356-391, then Flight).  One process (or thread) per GPU; the host distributes a unique id the
+ * way the reference's cluster layer distributes its endpoints, every rank creates its
+ * communicator with it, then calls dbg_agg_exchange collectively: the partial table's groups are
+ * routed to rank hash % n_ranks, sizes move with one RCCL all-gather (the only host round trip),
+ * records and string blobs with grouped send/recv over xGMI, and what arrives is merged into the
+ * rank's final table (merge_states).  Group sets of the ranks' finals are disjoint afterwards.
+ * RCCL is loaded on first use (DBG_ERR_UNSUPPORTED without it; DBG_RCCL_LIB overrides its path). */
+#define DBG_COMM_ID_BYTES 128
+typedef struct dbg_comm dbg_comm;
+typedef struct dbg_exchange_stats {
+    uint64_t sent_bytes;             /* records + blobs this rank exported */
+    uint64_t remote_bytes;           /* of which left the GPU (xGMI) */
+    uint64_t received_records;
+    uint64_t received_string_bytes;
+} dbg_exchange_stats;
+int dbg_comm_get_unique_id(uint8_t* id /* DBG_COMM_ID_BYTES */);
+int dbg_comm_create(const uint8_t* id, int n_ranks, int rank, int device /* -1 = current */, dbg_comm** out);
+void dbg_comm_destroy(dbg_comm* c);
+/* Collective over the communicator's ranks.  partial and final live on the communicator's device
+ * and have the same dbg_agg_params (partial = 1 / 0).  Asynchronous except for the size
+ * all-gather; stats may be NULL. */
+int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final_table, dbg_exchange_stats* stats);
+
 /* ---- fixed-capacity exchange: replicas + gather for low-cardinality tables ----
  * Replaces, for small inline-key partial tables, the Serialized/Flight hand-off of
  * TransformPartialAggregate::on_finish (AGG/transform_aggregate_partial.rs:449-465) to the final

@@ -93,3 +93,11 @@ def test_library_refuses_bad_arguments_without_gpu():
     out = abi.dbg_datatype()
     assert L.dbg_agg_result_type(C.byref(spec), C.byref(out)) == abi.DBG_ERR_UNSUPPORTED
     assert b"sum" in L.dbg_last_error()
+
+
+def test_rccl_unique_id_without_device():
+    """The exchange's RCCL entry points load on first use (dlopen), and a unique id can be made
+    on a host without a GPU (the id carries the bootstrap endpoint, not device state)."""
+    from databend_amd.exchange import AbiComm
+    uid = AbiComm.unique_id()
+    assert len(uid) == abi.DBG_COMM_ID_BYTES and any(uid)

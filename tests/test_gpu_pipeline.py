@@ -203,3 +203,36 @@ def test_host_staging_ragged_blocks_and_filter_switch():
     vs = Column.from_numbers(col.Int64, v.data[sel], validity=v.validity[sel])
     ok_, oa = oracle_aggregate([ks, kk], [(f, vs if c is not None else None) for f, c in aggs], threads=8)
     assert_results_equal(blk.columns[4:], blk.columns[:4], ok_, oa)
+
+
+def test_abi_exchange_single_rank():
+    """dbg_comm_* + dbg_agg_exchange at N = 1 (the degenerate all-to-all: every group routed to
+    rank 0, sent to itself over RCCL) equals the oracle; a second exchange on the same
+    communicator reuses its send buffers."""
+    from databend_amd.exchange import AbiComm
+    rng = np.random.default_rng(21)
+    comm = AbiComm(AbiComm.unique_id(), 1, 0)
+    try:
+        for rnd in range(2):
+            n = 400_000
+            words = ["p%d" % i * (1 + i % 5) for i in range(30_000 + rnd)]
+            s = Column.from_strings([words[i] for i in rng.integers(0, len(words), n)])
+            k = Column.from_numbers(col.Int16, rng.integers(-5, 5, n))
+            d = Column.from_decimals(20, 3, [int(x) for x in rng.integers(-10**12, 10**12, n)])
+            aggs = [("count", None), ("sum", d), ("min", k)]
+            fns = [F.get(f, [], [c.dtype] if c is not None else []) for f, c in aggs]
+            params = AggregatorParams([s.dtype, k.dtype], fns)
+            partial = AggregateHashTable(params, HashTableConfig(True))
+            final = AggregateHashTable(params, HashTableConfig(False))
+            try:
+                partial.add_groups([s, k], [None, d, k])
+                st = comm.exchange(partial, final)
+                blk = final.merge_result()
+            finally:
+                partial.close()
+                final.close()
+            ok, oa = oracle_aggregate([s, k], aggs, threads=8)
+            assert_results_equal(blk.columns[3:], blk.columns[:3], ok, oa)
+            assert st["remote_bytes"] == 0 and st["received_records"] == len(ok[0])
+    finally:
+        comm.close()
