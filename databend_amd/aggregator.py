@@ -256,6 +256,35 @@ class AggregateHashTable:
         cols = [self._to_column(b, n) for b in aggs] + [self._to_column(b, n) for b in keys]
         return DataBlock(cols)
 
+    def serialized_strides(self) -> List[int]:
+        n = len(self.params.aggregate_functions)
+        st = (C.c_uint32 * max(1, n))()
+        check(lib().dbg_agg_serialized_stride(self.h, st))
+        return list(st)[:n]
+
+    def result_serialized(self) -> DataBlock:
+        """AggregateMeta::Serialized's block (EAGG/payload_flush.rs:129-164): one Binary column of
+        borsh states per aggregate (as byte strings), then the group columns."""
+        n, sbytes = self.finalize()
+        strides = self.serialized_strides()
+        bin_t = DataType(abi.STRING)
+        states = []
+        for s in strides:
+            data = np.zeros(max(1, n * s), np.uint8)
+            offs = np.zeros(n + 1, np.uint64)
+            states.append(dict(t=bin_t, data=data, offs=offs, val=None,
+                               ptrs=(data.ctypes.data, offs.ctypes.data, None)))
+        _, keys = self._out_buffers(n, sbytes)
+        out_a = (abi.dbg_out_column * max(1, len(states)))()
+        out_k = (abi.dbg_out_column * max(1, len(keys)))()
+        for i, b in enumerate(states):
+            out_a[i].data, out_a[i].offsets, out_a[i].validity = b["ptrs"]
+        for i, b in enumerate(keys):
+            out_k[i].data, out_k[i].offsets, out_k[i].validity = b["ptrs"]
+        check(lib().dbg_agg_result_serialized(self.h, out_a, out_k, 0))
+        cols = [self._to_column(b, n) for b in states] + [self._to_column(b, n) for b in keys]
+        return DataBlock(cols)
+
     def _out_buffers(self, n, sbytes):
         def buf(t: DataType, strbytes=0):
             if t.type_id == abi.STRING:

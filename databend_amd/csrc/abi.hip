@@ -139,6 +139,7 @@ struct dbg_agg_handle {
     Spec spec{};
     Spec* dspec = nullptr;
     std::vector<dbg_datatype> result_types;
+    std::vector<int> src_kinds;  // dbg_agg_kind as created (AVG_SQL is stored as AVG)
     bool partial = true;
 
     // table
@@ -323,8 +324,6 @@ static int result_type_of(const dbg_agg_spec& s, dbg_datatype* out) {
             break;
         case DBG_AGG_MIN: case DBG_AGG_MAX:
             if (t == DBG_STRING || t == DBG_BOOLEAN) return fail(DBG_ERR_UNSUPPORTED, "min/max: String/Boolean arguments stay on the CPU path");
-            if (t == DBG_DECIMAL128 && s.arg.precision > 18)
-                return fail(DBG_ERR_UNSUPPORTED, "min/max: Decimal128 with precision > 18 stays on the CPU path");
             r = dbg_datatype{t, s.arg.precision, s.arg.scale, 0, 0};
             break;
         default: return fail(DBG_ERR_INVALID, "unknown aggregate kind");
@@ -383,12 +382,13 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
         int t = A.arg_type;
         A.sumk = t == DBG_DECIMAL128 ? SUMK_I128 : (is_float(t) ? SUMK_F64 : SUMK_I64);
         A.mmk = is_unsigned_i(t) ? MMK_U64 : (is_float(t) ? MMK_F64 : MMK_I64);
+        if (t == DBG_DECIMAL128 && s.arg.precision > 18) A.mmk = MMK_I128;
         A.w0 = word;
         switch (A.kind) {
             case DBG_AGG_COUNT: A.nwords = 1; break;
             case DBG_AGG_SUM: A.nwords = A.sumk == SUMK_I128 ? 2 : 1; break;
             case DBG_AGG_AVG: A.nwords = A.sumk == SUMK_I128 ? 3 : 2; break;
-            default: A.nwords = 1;
+            default: A.nwords = A.mmk == MMK_I128 ? 3 : 1;
         }
         word += A.nwords;
         A.flag_bit = -1;
@@ -402,6 +402,11 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
         A.scale_add = (A.kind == DBG_AGG_AVG && t == DBG_DECIMAL128) ? (int)rt.scale - (int)s.arg.scale : 0;
         A.avg_round = sql_avg && t == DBG_DECIMAL128;
         A.res_width = (int)type_width(rt.type);
+        A.ser_flags = 0;
+        if (s.kind != DBG_AGG_COUNT) {
+            if (s.or_null) A.ser_flags |= SER_OR_NULL;
+            if (A.arg_nullable) A.ser_flags |= SER_NULL_ADPT;
+        }
     }
     if (flag_bits > 64) return fail(DBG_ERR_UNSUPPORTED, "too many nullable aggregates");
     S.flags_word = flag_bits ? word++ : -1;
@@ -413,7 +418,8 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     S.stride_words = sw;
     for (int w = 0; w < DBG_MAX_WORDS; ++w) S.slot_init[w] = w == 0 ? SLOT_EMPTY : 0;
     for (int a = 0; a < S.n_aggs; ++a)
-        if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) S.slot_init[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+        if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX)
+            for (int k = 0; k < S.aggs[a].nwords; ++k) S.slot_init[S.aggs[a].w0 + k] = state_init_word(S.aggs[a], k);
     S.rec_state_off = off;
     S.rec_width = off + 8 * (u32)S.n_words;
     // partitioned payload record formats (pp.hip): key part, then each argument value aligned to
@@ -769,6 +775,7 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
         delete h;
         return rc;
     }
+    for (int a = 0; a < params->n_aggs; ++a) h->src_kinds.push_back(params->aggs[a].kind);
     h->partial = params->partial != 0;
     if (params->device >= 0) h->device = params->device;
     else {
@@ -1496,14 +1503,52 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
     return fail(DBG_ERR_INTERNAL, "finalize did not converge");
 }
 
+// Upper bound of one group's serialized state of aggregate a (agg_serialize).
+static u32 ser_stride_of(const DAgg& A) {
+    u32 n;
+    switch (A.kind) {
+        case DBG_AGG_COUNT: return 8;
+        case DBG_AGG_SUM: n = A.sumk == SUMK_I128 ? 16 : 8; break;
+        case DBG_AGG_AVG: n = A.sumk == SUMK_I128 ? 24 : 16; break;
+        default: n = 1 + type_width(A.arg_type);
+    }
+    if (A.ser_flags & SER_NULL_ADPT) n++;
+    if (A.ser_flags & SER_OR_NULL) n++;
+    return n;
+}
+
+static int result_impl(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device, bool ser);
+
 int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device) {
+    return result_impl(h, out_aggs, out_keys, on_device, false);
+}
+
+int dbg_agg_serialized_stride(dbg_agg_handle* h, uint32_t* stride) {
+    if (!h || !stride) return fail(DBG_ERR_INVALID, "null argument");
+    for (int a = 0; a < h->spec.n_aggs; ++a) {
+        if (h->src_kinds[a] == DBG_AGG_AVG_SQL)
+            return fail(DBG_ERR_UNSUPPORTED, "serialized states: SQL avg is sum and count in the reference plan");
+        stride[a] = ser_stride_of(h->spec.aggs[a]);
+    }
+    return DBG_OK;
+}
+
+int dbg_agg_result_serialized(dbg_agg_handle* h, dbg_out_column* out_states, dbg_out_column* out_keys, int on_device) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    for (int a = 0; a < h->spec.n_aggs; ++a)
+        if (h->src_kinds[a] == DBG_AGG_AVG_SQL)
+            return fail(DBG_ERR_UNSUPPORTED, "serialized states: SQL avg is sum and count in the reference plan");
+    return result_impl(h, out_states, out_keys, on_device, true);
+}
+
+static int result_impl(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device, bool ser) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     if (!h->finalized) return fail(DBG_ERR_INVALID, "dbg_agg_finalize must precede dbg_agg_result");
     HIPCHECK(hipSetDevice(h->device));
     RETURN_IF(flush_pending(h));
     const Spec& S = h->spec;
     u64 n = h->n_groups;
-    for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = h->result_types[a];
+    for (int a = 0; a < S.n_aggs; ++a) out_aggs[a].dt = ser ? dbg_datatype{DBG_STRING, 0, 0, 0, 0} : h->result_types[a];
     for (int c = 0; c < S.n_keys; ++c) out_keys[c].dt = S.key_types[c];
     if (n == 0) {
         for (int c = 0; c < S.n_keys; ++c)
@@ -1511,6 +1556,12 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
                 u64 z = 0;
                 if (on_device) HIPCHECK(hipMemcpy(out_keys[c].offsets, &z, 8, hipMemcpyHostToDevice));
                 else out_keys[c].offsets[0] = 0;
+            }
+        for (int a = 0; a < S.n_aggs && ser; ++a)
+            if (out_aggs[a].offsets) {
+                u64 z = 0;
+                if (on_device) HIPCHECK(hipMemcpy(out_aggs[a].offsets, &z, 8, hipMemcpyHostToDevice));
+                else out_aggs[a].offsets[0] = 0;
             }
         return DBG_OK;
     }
@@ -1542,6 +1593,13 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
     }
     for (int a = 0; a < S.n_aggs && rc == DBG_OK; ++a) {
         const dbg_datatype& t = h->result_types[a];
+        if (ser) {  // fixed-stride rows + lengths, compacted into Binary columns below
+            od.ser = 1;
+            od.ser_stride[a] = ser_stride_of(S.aggs[a]);
+            rc = tmp(n * od.ser_stride[a], &od.agg_data[a]);
+            if (rc == DBG_OK) rc = tmp(n, (void**)&od.agg_valid[a]);
+            continue;
+        }
         if (on_device) od.agg_data[a] = out_aggs[a].data;
         else rc = tmp(n * type_width(t.type), &od.agg_data[a]);
         if (rc == DBG_OK && t.nullable) rc = tmp(n, (void**)&od.agg_valid[a]);
@@ -1578,7 +1636,38 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
                 hipMemcpyAsync(out_keys[c].validity, bits, (n + 7) / 8, hipMemcpyDeviceToHost, h->stream);
         }
     }
-    for (int a = 0; a < S.n_aggs; ++a) {
+    std::vector<u64> ser_tot(S.n_aggs, 0);
+    u64* dser_tot = nullptr;
+    if (ser) {
+        if (tmp(8ull * S.n_aggs, (void**)&dser_tot) != DBG_OK) {
+            free_temps();
+            return DBG_ERR_OOM;
+        }
+        for (int a = 0; a < S.n_aggs; ++a) {
+            u64* offs = nullptr;
+            u8* data = nullptr;
+            if (on_device) {
+                offs = out_aggs[a].offsets;
+                data = (u8*)out_aggs[a].data;
+            } else if (tmp((n + 1) * 8, (void**)&offs) != DBG_OK || tmp(n * od.ser_stride[a], (void**)&data) != DBG_OK) {
+                free_temps();
+                return DBG_ERR_OOM;
+            }
+            launch_ser_compact(h->stream, od.agg_valid[a], (const u8*)od.agg_data[a], od.ser_stride[a], n, offs, data, dser_tot + a);
+            if (!on_device) {
+                od.agg_data[a] = data;  // copied out below with the totals known
+                if (out_aggs[a].offsets)
+                    hipMemcpyAsync(out_aggs[a].offsets, offs, (n + 1) * 8, hipMemcpyDeviceToHost, h->stream);
+            }
+        }
+        HIPCHECK(hipMemcpyAsync(ser_tot.data(), dser_tot, 8ull * S.n_aggs, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        if (!on_device)
+            for (int a = 0; a < S.n_aggs; ++a)
+                if (out_aggs[a].data && ser_tot[a])
+                    hipMemcpyAsync(out_aggs[a].data, od.agg_data[a], ser_tot[a], hipMemcpyDeviceToHost, h->stream);
+    }
+    for (int a = 0; a < S.n_aggs && !ser; ++a) {
         const dbg_datatype& t = h->result_types[a];
         if (t.nullable) {
             u8* bits = nullptr;
@@ -1600,7 +1689,7 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
             if (t.type == DBG_STRING && out_keys[c].offsets)
                 hipMemcpyAsync(out_keys[c].offsets, od.key_offsets[c], (n + 1) * 8, hipMemcpyDeviceToHost, h->stream);
         }
-        for (int a = 0; a < S.n_aggs; ++a)
+        for (int a = 0; a < S.n_aggs && !ser; ++a)
             if (out_aggs[a].data)
                 hipMemcpyAsync(out_aggs[a].data, od.agg_data[a], n * type_width(h->result_types[a].type), hipMemcpyDeviceToHost, h->stream);
     }
@@ -2161,6 +2250,44 @@ int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, v
     u8* vbytes = nullptr;
     if (out_validity && col->dt.nullable) RETURN_IF(dev_alloc((void**)&vbytes, n_sel + 1));
     launch_take_fixed(s, d, sel, n_sel, (u8*)out_data, vbytes);
+    if (vbytes) launch_pack_bits(s, vbytes, n_sel, out_validity);
+    HIPCHECK(hipStreamSynchronize(s));
+    if (vbytes) hipFree(vbytes);
+    return DBG_OK;
+}
+
+int dbg_take_string(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, uint64_t* out_offsets, void* out_data,
+                    uint64_t data_cap, uint8_t* out_validity, uint64_t* total_bytes, void* stream) {
+    if (!col || !out_offsets || !total_bytes || (n_sel && !sel)) return fail(DBG_ERR_INVALID, "null argument");
+    if (col->dt.type != DBG_STRING || !col->offsets) return fail(DBG_ERR_INVALID, "dbg_take_string: String columns only");
+    hipStream_t s = (hipStream_t)stream;
+    launch_take_string_offsets(s, col->offsets, sel, n_sel, out_offsets);
+    // n_sel lengths + one zero -> exclusive scan -> n_sel + 1 offsets; the total lands in a pinned word
+    HIPCHECK(hipMemsetAsync(out_offsets + n_sel, 0, 8, s));
+    u64* dtot = nullptr;
+    RETURN_IF(dev_alloc((void**)&dtot, 8));
+    u64 total = 0;
+    hipError_t e = hipMemsetAsync(dtot, 0, 8, s);
+    if (e == hipSuccess && n_sel) launch_exclusive_scan(s, out_offsets, n_sel + 1, dtot);
+    if (e == hipSuccess) e = hipMemcpyAsync(&total, dtot, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(dtot);
+    if (e != hipSuccess) return fail(DBG_ERR_DEVICE, hipGetErrorString(e));
+    *total_bytes = total;
+    if (total > data_cap) return fail(DBG_ERR_INVALID, "dbg_take_string: data buffer too small (*total_bytes needed)");
+    if (!n_sel) return DBG_OK;
+    if (!out_data) return fail(DBG_ERR_INVALID, "null argument");
+    DCol d;
+    memset(&d, 0, sizeof(d));
+    d.type = DBG_STRING;
+    d.nullable = col->dt.nullable;
+    d.data = (const u8*)col->data;
+    d.offsets = col->offsets;
+    d.validity = col->validity;
+    d.validity_offset = col->validity_offset;
+    u8* vbytes = nullptr;
+    if (out_validity && col->dt.nullable) RETURN_IF(dev_alloc((void**)&vbytes, n_sel + 1));
+    launch_take_string_bytes(s, d, sel, n_sel, out_offsets, (u8*)out_data, vbytes);
     if (vbytes) launch_pack_bits(s, vbytes, n_sel, out_validity);
     HIPCHECK(hipStreamSynchronize(s));
     if (vbytes) hipFree(vbytes);

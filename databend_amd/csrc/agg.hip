@@ -221,7 +221,8 @@ __device__ __forceinline__ void lds_table_init(const Spec& S, u64* lds, u32 lds_
         p[0] = SLOT_EMPTY;
         for (u32 w = 1; w < sw; ++w) p[w] = 0;
         for (int a = 0; a < S.n_aggs; ++a)
-            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX) p[S.aggs[a].w0] = state_init_word(S.aggs[a], 0);
+            if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX)
+                for (int k = 0; k < S.aggs[a].nwords; ++k) p[S.aggs[a].w0 + k] = state_init_word(S.aggs[a], k);
     }
 }
 
@@ -721,13 +722,7 @@ __device__ __forceinline__ void write_group(const Spec& S, const BatchDesc* batc
             }
         }
     }
-    for (int a = 0; a < S.n_aggs; ++a) {
-        const DAgg& A = S.aggs[a];
-        u64 lo, hi;
-        bool v = agg_result(S, A, st, lo, hi, t.counters + CNT_ERR);
-        write_bytes(out.agg_data[a], p, A.res_width, lo, hi);
-        if (out.agg_valid[a]) out.agg_valid[a][p] = v ? 1 : 0;
-    }
+    for (int a = 0; a < S.n_aggs; ++a) write_agg(S, a, st, p, out, t.counters + CNT_ERR);
 }
 
 // Slot order within the block: iteration k covers slots base + k*BLOCK + tid (coalesced entry
@@ -1629,4 +1624,27 @@ __global__ void __launch_bounds__(FIN_NT) export_fixed_kernel(const Spec* __rest
 void launch_export_fixed(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, u8* buf, u64 cap_records,
                          int recycle) {
     hipLaunchKernelGGL(export_fixed_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, buf, cap_records, recycle);
+}
+
+// ------------------------------------------------------------------------------------------
+// Serialized states (dbg_agg_result_serialized): rows written at a fixed stride with their
+// lengths -> a Binary column (offsets from an exclusive scan of the lengths, then the bytes).
+// ------------------------------------------------------------------------------------------
+__global__ void ser_lengths_kernel(const u8* __restrict__ lens, u64 n, u64* __restrict__ offs) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i <= n; i += (u64)gridDim.x * blockDim.x)
+        offs[i] = i < n ? lens[i] : 0;
+}
+__global__ void ser_copy_kernel(const u8* __restrict__ src, u32 stride, u64 n, const u64* __restrict__ offs,
+                                u8* __restrict__ dst) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const u64 o = offs[i], len = offs[i + 1] - o;
+        for (u64 b = 0; b < len; ++b) dst[o + b] = src[i * stride + b];
+    }
+}
+void launch_ser_compact(hipStream_t s, const u8* lens, const u8* src, u32 stride, u64 n, u64* offs, u8* dst, u64* total) {
+    u64 blocks = (n + 256) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(ser_lengths_kernel, dim3((u32)blocks), dim3(256), 0, s, lens, n, offs);
+    launch_exclusive_scan(s, offs, n + 1, total);
+    if (n) hipLaunchKernelGGL(ser_copy_kernel, dim3((u32)blocks), dim3(256), 0, s, src, stride, n, offs, dst);
 }

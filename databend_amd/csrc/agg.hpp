@@ -140,6 +140,34 @@ template <int AS> __device__ __forceinline__ void at_minmax(wptr<AS> p, u64 v, b
         else __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, AT_SCOPE(AS));
     }
 }
+// i128 MIN/MAX (Decimal128, precision > 18).  CDNA4 has no 128-bit atomics, so the state is
+// [seq, lo, hi] under a seqlock: a candidate that does not beat a consistent snapshot is dropped
+// (the value only moves one way, so it never will); otherwise the lane that wins the CAS of seq to
+// odd writes both words and publishes seq + 2 in the same loop iteration — a lane never waits on
+// a lock held by a lane of its own wave.  Readers of a finished table (merge, result) see seq even.
+__device__ __forceinline__ bool i128_less(u64 alo, u64 ahi, u64 blo, u64 bhi) {
+    return (long long)ahi < (long long)bhi || (ahi == bhi && alo < blo);
+}
+template <int AS> __device__ __forceinline__ void at_minmax128(wptr<AS> w, u64 lo, u64 hi, bool mn) {
+    for (;;) {
+        const u64 s1 = __hip_atomic_load(w, __ATOMIC_ACQUIRE, AT_SCOPE(AS));
+        if (s1 & 1) continue;
+        const u64 clo = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        const u64 chi = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        if (AS == AS_LDS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const u64 s2 = __hip_atomic_load(w, __ATOMIC_RELAXED, AT_SCOPE(AS));
+        if (s1 != s2) continue;
+        if (!(mn ? i128_less(lo, hi, clo, chi) : i128_less(clo, chi, lo, hi))) return;
+        u64 e = s1;
+        if (__hip_atomic_compare_exchange_strong(w, &e, s1 + 1, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED, AT_SCOPE(AS))) {
+            __hip_atomic_store(w + 1, lo, __ATOMIC_RELAXED, AT_SCOPE(AS));
+            __hip_atomic_store(w + 2, hi, __ATOMIC_RELAXED, AT_SCOPE(AS));
+            __hip_atomic_store(w, s1 + 2, __ATOMIC_RELEASE, AT_SCOPE(AS));
+            return;
+        }
+    }
+}
 template <int AS> __device__ __forceinline__ u64 at_cas(wptr<AS> p, u64 expected, u64 desired) {
     __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AT_SCOPE(AS));
     return expected;  // the old value (== the expected one iff the exchange happened)
@@ -181,12 +209,17 @@ struct OutDesc {
     u64 cap_str[DBG_MAX_KEYS];    // payload bytes the string key buffers hold
     u8* key_bits[DBG_MAX_KEYS];   // bit-packed destinations of key_valid (fused path)
     u8* agg_bits[DBG_MAX_AGGS];
+    // serialize mode (dbg_agg_result_serialized): agg_data[a] receives each group's borsh state
+    // at row * ser_stride[a], agg_valid[a] its length in bytes
+    int32_t ser;
+    u32 ser_stride[DBG_MAX_AGGS];
 };
 #define FIN_SMALL_SLOTS 16384  // tables up to this many slots finalize in one workgroup
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
                            u64* totals, u64* host_mirror /* mapped pinned: counters, totals, recycled, seq */,
                            int recycle, u64 seq);
 void launch_finish_outputs(hipStream_t s, const OutDesc& out, const u64* totals, int n_keys, int n_aggs);
+void launch_ser_compact(hipStream_t s, const u8* lens, const u8* src, u32 stride, u64 n, u64* offs, u8* dst, u64* total);
 // finalize_small fused into the fast insert: the last workgroup to finish runs it (one launch per
 // batch).  Tables of at most FUSED_FIN_SLOTS slots whose copy fits the insert's LDS.
 #define FUSED_FIN_SLOTS 2048

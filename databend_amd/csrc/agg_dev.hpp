@@ -61,7 +61,8 @@ __device__ __forceinline__ void apply_row(const Spec& S, wptr<AS> st, const Batc
             }
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 bool mn = A.kind == DBG_AGG_MIN;
-                if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)dcol_i64(c, i), mn, true);
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, dcol_bits(c, i), dcol_hi(c, i), mn);
+                else if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)dcol_i64(c, i), mn, true);
                 else at_minmax<AS>(w, A.mmk == MMK_U64 ? dcol_bits(c, i) : f64_order_key(dcol_f64(c, i)), mn, false);
                 break;
             }
@@ -96,8 +97,10 @@ __device__ __forceinline__ void apply_state(const Spec& S, wptr<AS> st, const u6
                 }
                 break;
             }
-            case DBG_AGG_MIN: at_minmax<AS>(w, x0, true, A.mmk == MMK_I64); break;
-            case DBG_AGG_MAX: at_minmax<AS>(w, x0, false, A.mmk == MMK_I64); break;
+            case DBG_AGG_MIN: case DBG_AGG_MAX:
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, rdw<SC1, RAS>(x + 1), rdw<SC1, RAS>(x + 2), A.kind == DBG_AGG_MIN);
+                else at_minmax<AS>(w, x0, A.kind == DBG_AGG_MIN, A.mmk == MMK_I64);
+                break;
         }
     }
     if (S.flags_word >= 0) {
@@ -196,6 +199,58 @@ __device__ __forceinline__ bool dec38_out_of_range(u64 lo, u64 hi) {
     return m.lo > DEC38_MAX_LO;
 }
 
+// AggregateFunction::serialize of one state (AggregateMeta::Serialized, EAGG/payload_flush.rs:
+// 129-164): the borsh encoding of the reference's state struct — NumberSumState {value} (8 B of
+// the sum type), DecimalSumState {value: i128}, Number/DecimalAvgState {value, count: u64},
+// AggregateCountState's u64, MinMaxAnyState {value: Option<T>} (tag byte, then T's own width) —
+// then the flag byte of AggregateNullUnaryAdaptor<true> (nullable argument: "had a non-NULL
+// input", aggregate_null_unary_adaptor.rs:200-207) and of AggregateFunctionOrNullAdaptor (1: the
+// group received rows, aggregate_ornull_adaptor.rs:135-163, 175-179).  Returns the byte count.
+__device__ __forceinline__ u32 agg_serialize(const Spec& S, const DAgg& A, const u64* st, u8* d) {
+    const u64* w = st + A.w0;
+    u32 n = 0;
+    auto put = [&](u64 v, u32 bytes) {
+        for (u32 b = 0; b < bytes; ++b) d[n++] = (u8)(v >> (8 * b));
+    };
+    bool has = true;  // the null adaptor's flag: a non-NULL input reached the state
+    switch (A.kind) {
+        case DBG_AGG_COUNT: put(w[0], 8); return n;
+        case DBG_AGG_SUM:
+            put(w[0], 8);
+            if (A.sumk == SUMK_I128) put(w[1], 8);
+            if (A.flag_bit >= 0) has = (st[S.flags_word] >> A.flag_bit) & 1;
+            break;
+        case DBG_AGG_AVG: {
+            const int k = A.sumk == SUMK_I128 ? 2 : 1;
+            put(w[0], 8);
+            if (k == 2) put(w[1], 8);
+            put(w[k], 8);
+            has = w[k] != 0;
+            break;
+        }
+        default: {  // MIN / MAX
+            if (A.flag_bit >= 0) has = (st[S.flags_word] >> A.flag_bit) & 1;
+            put(has ? 1 : 0, 1);
+            if (has) {
+                const u32 aw = type_width(A.arg_type);
+                if (A.mmk == MMK_I128) {
+                    put(w[1], 8);
+                    put(w[2], 8);
+                } else if (A.mmk == MMK_F64) {
+                    const double x = f64_from_order_key(w[0]);
+                    if (A.arg_type == DBG_FLOAT32) put((u64)__float_as_uint((float)x), 4);
+                    else put((u64)__double_as_longlong(x), 8);
+                } else {
+                    put(w[0], aw);  // low bytes of the (sign-extended) value: T's own width
+                }
+            }
+        }
+    }
+    if (A.ser_flags & SER_NULL_ADPT) put(has ? 1 : 0, 1);
+    if (A.ser_flags & SER_OR_NULL) put(1, 1);
+    return n;
+}
+
 __device__ __forceinline__ void write_bytes(void* dst, u64 pos, u32 w, u64 lo, u64 hi) {
     u8* p = (u8*)dst + pos * w;
     switch (w) {
@@ -267,7 +322,10 @@ __device__ __forceinline__ bool agg_result(const Spec& S, const DAgg& A, const u
                 break;
             }
             u64 v = w[0];
-            if (A.mmk == MMK_F64) {
+            if (A.mmk == MMK_I128) {
+                lo = w[1];
+                hi = w[2];
+            } else if (A.mmk == MMK_F64) {
                 double d = f64_from_order_key(v);
                 if (A.res_type == DBG_FLOAT32) lo = (u64)__float_as_uint((float)d);
                 else lo = (u64)__double_as_longlong(d);
@@ -279,4 +337,19 @@ __device__ __forceinline__ bool agg_result(const Spec& S, const DAgg& A, const u
         }
     }
     return valid;
+}
+
+// One aggregate's output for group row `row`: its result (merge_result) or, in serialize mode,
+// its serialized state.
+__device__ __forceinline__ void write_agg(const Spec& S, int a, const u64* st, u64 row, const OutDesc& out, u64* err) {
+    const DAgg& A = S.aggs[a];
+    if (out.ser) {
+        const u32 len = agg_serialize(S, A, st, (u8*)out.agg_data[a] + row * out.ser_stride[a]);
+        out.agg_valid[a][row] = (u8)len;
+        return;
+    }
+    u64 lo, hi;
+    const bool v = agg_result(S, A, st, lo, hi, err);
+    write_bytes(out.agg_data[a], row, A.res_width, lo, hi);
+    if (out.agg_valid[a]) out.agg_valid[a][row] = v ? 1 : 0;
 }

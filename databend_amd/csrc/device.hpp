@@ -377,7 +377,8 @@ enum {
 enum {
     MMK_I64 = 0,  // signed (ints, date, timestamp, Decimal128 with precision <= 18)
     MMK_U64 = 1,  // unsigned
-    MMK_F64 = 2   // OrderedFloat order via the monotone u64 transform
+    MMK_F64 = 2,  // OrderedFloat order via the monotone u64 transform
+    MMK_I128 = 3  // Decimal128 with precision > 18: [seq, lo, hi] under a seqlock (agg.hpp at_minmax128)
 };
 
 struct DAgg {
@@ -395,6 +396,11 @@ struct DAgg {
     int32_t scale_add;  // AVG decimal
     int32_t res_width;
     int32_t avg_round;  // AVG_SQL on Decimal128: round-half-away divide (kind is DBG_AGG_AVG)
+    int32_t ser_flags;  // serialized state (AggregateMeta::Serialized): SER_* bits
+};
+enum {
+    SER_OR_NULL = 1,   // AggregateFunctionOrNullAdaptor appends its flag byte
+    SER_NULL_ADPT = 2  // AggregateNullUnaryAdaptor<true> (nullable argument) appends its flag byte
 };
 
 // Monotone map of OrderedFloat<f64> onto u64 (NaN canonical & greatest).
@@ -409,6 +415,13 @@ __device__ __forceinline__ double f64_from_order_key(u64 k) {
 }
 
 __host__ __device__ inline u64 state_init_word(const DAgg& a, int w) {
+    if ((a.kind == DBG_AGG_MIN || a.kind == DBG_AGG_MAX) && a.mmk == MMK_I128) {
+        // identity: i128::MAX for MIN, i128::MIN for MAX; word 0 is the sequence counter
+        if (w == 0) return 0ULL;
+        const bool mn = a.kind == DBG_AGG_MIN;
+        if (w == 1) return mn ? ~0ULL : 0ULL;
+        return mn ? 0x7fffffffffffffffULL : 0x8000000000000000ULL;
+    }
     if (a.kind == DBG_AGG_MIN) {
         if (a.mmk == MMK_I64) return 0x7fffffffffffffffULL;
         return ~0ULL;  // U64 / F64-order

@@ -81,6 +81,45 @@ __global__ void take_fixed_kernel(DCol c, const u32* sel, u64 n, u8* out, u8* vb
     }
 }
 
+// StringColumn take (EXP/kernels/take.rs:56-91): lengths of the selected rows, then (after an
+// exclusive scan turns them into the output offsets) their bytes.  Rows are copied 8 bytes at a
+// time where source and destination allow it.
+__global__ void take_str_len_kernel(const u64* __restrict__ offs, const u32* __restrict__ sel, u64 n, u64* __restrict__ out_offs) {
+    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < n; k += (u64)gridDim.x * blockDim.x) {
+        const u64 i = sel[k];
+        out_offs[k] = offs[i + 1] - offs[i];
+    }
+}
+
+__global__ void take_str_bytes_kernel(DCol c, const u32* __restrict__ sel, u64 n, const u64* __restrict__ out_offs,
+                                      u8* __restrict__ out, u8* __restrict__ vbytes) {
+    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < n; k += (u64)gridDim.x * blockDim.x) {
+        const u64 i = sel[k];
+        const u64 so = c.offsets[i], len = c.offsets[i + 1] - so;
+        const u8* src = c.data + so;
+        u8* dst = out + out_offs[k];
+        u64 b = 0;
+        if ((((uintptr_t)src | (uintptr_t)dst) & 7) == 0)
+            for (; b + 8 <= len; b += 8) *(u64*)(dst + b) = *(const u64*)(src + b);
+        for (; b < len; ++b) dst[b] = src[b];
+        if (vbytes) vbytes[k] = dcol_valid(c, i) ? 1 : 0;
+    }
+}
+
+void launch_take_string_offsets(hipStream_t s, const u64* offs, const u32* sel, u64 n, u64* out_offs) {
+    if (!n) return;
+    u64 blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(take_str_len_kernel, dim3((u32)blocks), dim3(256), 0, s, offs, sel, n, out_offs);
+}
+
+void launch_take_string_bytes(hipStream_t s, const DCol& c, const u32* sel, u64 n, const u64* out_offs, u8* out, u8* vbytes) {
+    if (!n) return;
+    u64 blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(take_str_bytes_kernel, dim3((u32)blocks), dim3(256), 0, s, c, sel, n, out_offs, out, vbytes);
+}
+
 void launch_take_fixed(hipStream_t s, const DCol& c, const u32* sel, u64 n, u8* out, u8* vbytes) {
     if (!n) return;
     u64 blocks = (n + 255) / 256;

@@ -210,7 +210,8 @@ __device__ __forceinline__ void pp_apply_raw(const Spec& S, wptr<AS> st, const u
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 const bool mn = A.kind == DBG_AGG_MIN;
                 const u64 b = ld_le(p, aw < 8 ? aw : 8);  // Decimal128 (p <= 18): the low word
-                if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, b, ld_le(p + 8, 8), mn);
+                else if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
                 else if (A.mmk == MMK_U64) at_minmax<AS>(w, b, mn, false);
                 else
                     at_minmax<AS>(w, f64_order_key(A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)b)
@@ -1002,7 +1003,8 @@ __device__ __forceinline__ void pp_apply_rec(const Spec& S, wptr<AS_LDS> st, con
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 const bool mn = A.kind == DBG_AGG_MIN;
                 const u64 b = rk.le(off, aw < 8 ? aw : 8);  // Decimal128 (p <= 18): the low word
-                if (A.mmk == MMK_I64) at_minmax<AS_LDS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
+                if (A.mmk == MMK_I128) at_minmax128<AS_LDS>(w, b, rk.le(off + 8, 8), mn);
+                else if (A.mmk == MMK_I64) at_minmax<AS_LDS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
                 else if (A.mmk == MMK_U64) at_minmax<AS_LDS>(w, b, mn, false);
                 else
                     at_minmax<AS_LDS>(w, f64_order_key(A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)b)
@@ -1034,13 +1036,7 @@ __device__ __forceinline__ void pp_write_fixed_row(const Spec& S, const l64* e, 
         if (out.key_valid[c]) out.key_valid[c][row] = v ? 1 : 0;
     }
     const u64* st = (const u64*)(e + kw8);
-    for (int a = 0; a < S.n_aggs; ++a) {
-        const DAgg& A = S.aggs[a];
-        u64 lo, hi;
-        const bool v = agg_result(S, A, st, lo, hi, err);
-        write_bytes(out.agg_data[a], row, A.res_width, lo, hi);
-        if (out.agg_valid[a]) out.agg_valid[a][row] = v ? 1 : 0;
-    }
+    for (int a = 0; a < S.n_aggs; ++a) write_agg(S, a, st, row, out, err);
 }
 
 template <typename R>
@@ -1347,13 +1343,7 @@ __global__ void __launch_bounds__(PP_GNT) pp_grec_write_kernel(const Spec* __res
         }
         if (in && r < out.cap_groups) {
             const u64* st = (const u64*)(k + S.pp_kw) - 1;
-            for (int a = 0; a < S.n_aggs; ++a) {
-                const DAgg& A = S.aggs[a];
-                u64 lo, hi;
-                const bool v = agg_result(S, A, st, lo, hi, err);
-                write_bytes(out.agg_data[a], r, A.res_width, lo, hi);
-                if (out.agg_valid[a]) out.agg_valid[a][r] = v ? 1 : 0;
-            }
+            for (int a = 0; a < S.n_aggs; ++a) write_agg(S, a, st, r, out, err);
         }
     }
 }

@@ -144,3 +144,34 @@ class FilterProgram:
 
     def ptr(self):
         return C.byref(self.struct)
+
+
+class FilterExecutor:
+    """FilterExecutor (EXP/filter/filter_executor.rs:73-128) over device-resident blocks:
+    `select` fills the ascending u32 selection of rows where the predicate is TRUE
+    (dbg_filter_select), `take` gathers every column of the block at it (DataBlock::take,
+    EXP/kernels/take.rs:56-91: dbg_take_fixed / dbg_take_string), `filter` does both.  The
+    GROUP BY path never materialises the filtered block: its insert evaluates the predicate itself."""
+
+    def __init__(self, pred: Pred, predicate_columns: Sequence[int]):
+        self.pred = pred
+        self.predicate_columns = list(predicate_columns)
+
+    def select(self, columns, rows: int):
+        import torch
+        from .ffi import check, lib
+        prog = FilterProgram(self.pred, [columns[i].to_abi() for i in self.predicate_columns])
+        sel = torch.empty(max(1, rows), dtype=torch.int32, device=columns[0].data.device)
+        n = C.c_uint64()
+        check(lib().dbg_filter_select(prog.ptr(), rows, sel.data_ptr(), C.byref(n), None))
+        return sel[: n.value]
+
+    def take(self, columns, sel):
+        from .sort import take
+        return [take(c, sel) for c in columns]
+
+    def filter(self, columns, rows: int):
+        sel = self.select(columns, rows)
+        if sel.numel() == rows:  # everything selected: the block passes through (filter_executor.rs:95-100)
+            return list(columns)
+        return self.take(columns, sel)

@@ -47,8 +47,18 @@ def sort_limit_indices(col: DeviceColumn, asc: bool, nulls_first: bool, limit: O
 
 
 def take(col: DeviceColumn, idx) -> DeviceColumn:
-    """DataBlock::take of one fixed-width column by device indices."""
+    """DataBlock::take of one column by device u32 indices (EXP/kernels/take.rs:56-91):
+    dbg_take_fixed for fixed-width columns, dbg_take_string for strings."""
     n = int(idx.numel())
+    if col.dtype.type_id == abi.STRING:
+        cap = max(1, int(col.data.numel()))
+        out = empty(col.dtype, n, device=col.data.device, string_bytes=cap)
+        total = C.c_uint64()
+        check(lib().dbg_take_string(C.byref(col.to_abi()), idx.data_ptr() if n else None, n, out.offsets.data_ptr(),
+                                    out.data.data_ptr(), cap,
+                                    out.validity.data_ptr() if out.validity is not None else None, C.byref(total), None))
+        out.data = out.data[: max(1, total.value)]
+        return out
     out = empty(col.dtype, n, device=col.data.device)
     check(lib().dbg_take_fixed(C.byref(col.to_abi()), idx.data_ptr(), n, out.data.data_ptr(),
                                out.validity.data_ptr() if out.validity is not None else None, None))

@@ -204,6 +204,20 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
 /* TransformFinalAggregate output DataBlock [agg results..., group cols...]
  * (AGG/transform_aggregate_final.rs:128-133): fills caller buffers (host when on_device == 0). */
 int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* out_keys, int on_device);
+/* AggregateMeta::Serialized (AGG/aggregate_meta.rs:44-109; EAGG/payload_flush.rs:129-164): the
+ * partial states as Binary columns, one per aggregate, + the group columns — what the reference
+ * ships over Flight or spills, so a CPU final stage (or a GPU one) merges them.  Each row is the
+ * reference's own bytes: the borsh state (NumberSumState / DecimalSumState {value},
+ * Number/DecimalAvgState {value, count: u64}, AggregateCountState u64, MinMaxAnyState
+ * {value: Option<T>} in T's own width), then AggregateNullUnaryAdaptor's flag byte (nullable
+ * argument), then AggregateFunctionOrNullAdaptor's flag byte (FUN/aggregator_common.rs:159-170,
+ * adaptors/aggregate_null_unary_adaptor.rs:200-207, adaptors/aggregate_ornull_adaptor.rs:175-179).
+ * After dbg_agg_finalize; out_states[a] is a Binary column: data sized n_groups * stride[a]
+ * (dbg_agg_serialized_stride, an upper bound: MIN/MAX of a group without input is shorter),
+ * offsets n_groups + 1.  Group order equals dbg_agg_result's.  SQL avg (DBG_AGG_AVG_SQL) has no
+ * single reference state: DBG_ERR_UNSUPPORTED. */
+int dbg_agg_serialized_stride(dbg_agg_handle* h, uint32_t* stride /* n_aggs */);
+int dbg_agg_result_serialized(dbg_agg_handle* h, dbg_out_column* out_states, dbg_out_column* out_keys, int on_device);
 
 /* Fused finalize + result into device buffers (on_device outputs) in one host round trip:
  * count, scan and write are enqueued together and the group count is read back once.  Buffers
@@ -279,7 +293,9 @@ int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width);
  * mixed CPU/GPU exchange or a test packs and unpacks records with it.  Offsets are in bytes from
  * the record start; the group hash (u64) is at 0; a string key's (offset u64, len u64) pair is at
  * key_off; state word j (1-based, as agg_w0 / flags_word count them) is the u64 at
- * state_off + 8 * (j - 1).  SUM/AVG of Decimal128 hold (lo, hi) words, AVG appends its count. */
+ * state_off + 8 * (j - 1).  SUM/AVG of Decimal128 hold (lo, hi) words, AVG appends its count;
+ * MIN/MAX of Decimal128 with precision > 18 hold (sequence, lo, hi): the sequence word is even in
+ * every exported record and is ignored by a merge. */
 typedef struct dbg_record_layout {
     uint32_t width;
     uint32_t state_off;
@@ -362,6 +378,13 @@ int dbg_filter_select(const dbg_filter* filter, uint64_t rows, uint32_t* sel_out
  * out[i] = in[sel[i]] (value bytes; validity gathered into out_validity bit-packed when non-NULL). */
 int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, void* out_data,
                    uint8_t* out_validity, void* hip_stream);
+/* DataBlock::take of one String column on device (StringColumn, EXP/kernels/take.rs:56-91):
+ * out_offsets (n_sel + 1 u64, device) receives the offsets from 0, *total_bytes the payload size;
+ * if it exceeds data_cap the call returns DBG_ERR_INVALID with *total_bytes set and no bytes
+ * copied (size the buffer and call again), otherwise out_data receives the selected rows' bytes.
+ * Validity as dbg_take_fixed.  Synchronous. */
+int dbg_take_string(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, uint64_t* out_offsets, void* out_data,
+                    uint64_t data_cap, uint8_t* out_validity, uint64_t* total_bytes, void* hip_stream);
 
 /* ---- ORDER BY one column LIMIT k (DataBlock::sort, EXP/kernels/sort.rs:79-107 -> arrow
  * sort_to_indices / indices_sorted_unstable_by, src/common/arrow/src/arrow/compute/sort/common.rs:95-174)

@@ -545,3 +545,104 @@ def test_partitioned_insert(kind, distinct, n, hint, batches):
     key = Column.from_numbers(t, vals.astype(t.np_dtype))
     g = check_parity([key], [("count", None)], on_device=True, capacity_hint=hint, batches=batches)
     assert g == len(np.unique(vals))
+
+
+def _i128_column(rng, n, p, s, nullable):
+    """Decimal128(p, s) values spanning the full 128-bit range of precision p (|v| < 10^p)."""
+    lim = 10**p - 1
+    small = rng.integers(-10**6, 10**6, n)
+    vals = []
+    for i in range(n):
+        r = i % 7
+        if r == 0:
+            vals.append(lim - int(small[i] % 1000))
+        elif r == 1:
+            vals.append(-lim + int(small[i] % 1000))
+        elif r == 2:
+            vals.append(int(small[i]) * (1 << 64) + int(small[i] % 97))  # hi words differ, lo small
+        else:
+            vals.append(int(small[i]))
+    valid = rng.random(n) > 0.2 if nullable else None
+    if valid is not None:
+        vals = [v if ok else None for v, ok in zip(vals, valid)]
+    return Column.from_decimals(p, s, vals, validity=valid)
+
+
+@pytest.mark.parametrize("groups,strategy", [(3, abi.STRATEGY_AUTO), (5000, abi.STRATEGY_AUTO),
+                                             (200_000, abi.STRATEGY_PARTITIONED)],
+                         ids=["hot-lds", "table", "partitioned"])
+@pytest.mark.parametrize("nullable", [False, True])
+def test_decimal128_wide_min_max(groups, strategy, nullable):
+    """MIN/MAX of Decimal128 with precision > 18 (FUN/aggregate_min_max_any.rs:46-115): full
+    128-bit order (hi signed, lo unsigned) through the seqlocked [seq, lo, hi] state — three
+    groups put every row of a workgroup on the same LDS state (maximum contention), and the
+    partitioned engine and the merge of exported records see the same states."""
+    rng = np.random.default_rng(groups)
+    n = 600_000 if groups < 100_000 else 2_400_000
+    d = _i128_column(rng, n, 38, 4, nullable)
+    k = Column.from_numbers(col.Int64, rng.integers(0, groups, n))
+    aggs = [("min", d), ("max", d), ("count", d), ("sum", d)]
+    check_parity([k], aggs, on_device=True, strategy=strategy)
+    check_parity([k], [("max", d), ("min", d)], batches=3)
+
+
+def test_decimal128_wide_min_max_exchange_merge():
+    """The 3-word MIN/MAX state crosses dbg_agg_export_records -> dbg_agg_merge_records intact."""
+    torch = _torch()
+    rng = np.random.default_rng(3)
+    n = 300_000
+    d = _i128_column(rng, n, 30, 2, True)
+    k = Column.from_numbers(col.Int32, rng.integers(0, 20_000, n))
+    fns = [F.get("min", [], [d.dtype]), F.get("max", [], [d.dtype])]
+    params = AggregatorParams([k.dtype], fns)
+    final = AggregateHashTable(params, HashTableConfig(False))
+    parts = []
+    try:
+        for lo, hi in ((0, n // 2), (n // 2, n)):
+            p = AggregateHashTable(params, HashTableConfig(True))
+            p.add_groups([slice_col(k, lo, hi)], [slice_col(d, lo, hi)] * 2)
+            counts, sb = p.partition(4, 0)
+            w = p.record_width()
+            recs = torch.empty(max(1, sum(counts) * w), dtype=torch.uint8, device="cuda")
+            strs = torch.empty(max(1, sum(sb)), dtype=torch.uint8, device="cuda")
+            p.export_records(recs, strs)
+            final.merge_records(recs, strs, counts, sb)
+            parts.append(p)
+        blk = final.merge_result()
+    finally:
+        final.close()
+        for p in parts:
+            p.close()
+    ok, oa = oracle_aggregate([k], [("min", d), ("max", d)])
+    assert_results_equal(blk.columns[2:], blk.columns[:2], ok, oa)
+
+
+def test_filter_executor_take_strings_and_decimals():
+    """FilterExecutor.filter on a device block with String (nullable), Decimal128 and Int16
+    columns: dbg_filter_select + dbg_take_string / dbg_take_fixed equal numpy's take."""
+    torch = _torch()
+    from databend_amd.device import DeviceColumn
+    from databend_amd.filter import FilterExecutor
+    rng = np.random.default_rng(17)
+    n = 500_001
+    words = ["", "a", "bb", "search phrase %d" % 7, "x" * 40]
+    sv = [words[i] for i in rng.integers(0, len(words), n)]
+    svalid = rng.random(n) > 0.1
+    s = Column.from_strings(sv, validity=svalid)
+    d = Column.from_decimals(38, 3, [int(x) * (1 << 70) + 5 for x in rng.integers(-1000, 1000, n)])
+    k = Column.from_numbers(col.Int16, rng.integers(-5, 5, n))
+    dev = [DeviceColumn.from_host(c) for c in (s, d, k)]
+    ex = FilterExecutor(and_(cmp(0, "<>", ""), cmp(1, ">", 0)), [0, 1])
+    out = ex.filter(dev, n)
+    torch.cuda.synchronize()
+    dv = np.array(i128_vals := d.values(), dtype=object)
+    keep = np.array([svalid[i] and sv[i] != "" and i128_vals[i] > 0 for i in range(n)])
+    idx = np.nonzero(keep)[0]
+    hs = out[0].to_host()
+    got_s = [bytes(hs.data[int(hs.offsets[j]):int(hs.offsets[j + 1])]) for j in range(len(idx))]
+    assert got_s == [sv[i].encode() for i in idx]
+    assert np.array_equal(out[1].data.cpu().numpy(), d.data.reshape(-1, 16)[idx].reshape(-1))
+    assert np.array_equal(out[2].data.cpu().numpy().view(np.int16), k.data[idx])
+    vb = np.unpackbits(out[0].validity.cpu().numpy(), bitorder="little")[:len(idx)]
+    assert vb.all()
+    del dv
