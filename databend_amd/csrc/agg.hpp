@@ -143,31 +143,42 @@ template <int AS> __device__ __forceinline__ void at_minmax(wptr<AS> p, u64 v, b
 // i128 MIN/MAX (Decimal128, precision > 18).  CDNA4 has no 128-bit atomics, so the state is
 // [seq, lo, hi] under a seqlock: a candidate that does not beat a consistent snapshot is dropped
 // (the value only moves one way, so it never will); otherwise the lane that wins the CAS of seq to
-// odd writes both words and publishes seq + 2 in the same loop iteration — a lane never waits on
-// a lock held by a lane of its own wave.  Readers of a finished table (merge, result) see seq even.
+// odd writes both words and publishes seq + 2.  The writes and the publish stay INSIDE the loop
+// body (no early exit after the CAS): a block that leaves the loop is a loop exit, which the
+// structurizer runs only once every lane of the wave has left — a winner whose publish sat there
+// would keep the other lanes of its wave spinning on the odd seq forever.
 __device__ __forceinline__ bool i128_less(u64 alo, u64 ahi, u64 blo, u64 bhi) {
     return (long long)ahi < (long long)bhi || (ahi == bhi && alo < blo);
 }
 template <int AS> __device__ __forceinline__ void at_minmax128(wptr<AS> w, u64 lo, u64 hi, bool mn) {
-    for (;;) {
+    u32 done = 0;
+    u32 spins = 0;  // every iteration settles at least one contender; the cap only guards a hang
+    do {
         const u64 s1 = __hip_atomic_load(w, __ATOMIC_ACQUIRE, AT_SCOPE(AS));
-        if (s1 & 1) continue;
         const u64 clo = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, AT_SCOPE(AS));
         const u64 chi = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, AT_SCOPE(AS));
         if (AS == AS_LDS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const u64 s2 = __hip_atomic_load(w, __ATOMIC_RELAXED, AT_SCOPE(AS));
-        if (s1 != s2) continue;
-        if (!(mn ? i128_less(lo, hi, clo, chi) : i128_less(clo, chi, lo, hi))) return;
-        u64 e = s1;
-        if (__hip_atomic_compare_exchange_strong(w, &e, s1 + 1, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED, AT_SCOPE(AS))) {
-            __hip_atomic_store(w + 1, lo, __ATOMIC_RELAXED, AT_SCOPE(AS));
-            __hip_atomic_store(w + 2, hi, __ATOMIC_RELAXED, AT_SCOPE(AS));
-            __hip_atomic_store(w, s1 + 2, __ATOMIC_RELEASE, AT_SCOPE(AS));
-            return;
+        if (!(s1 & 1) && s1 == s2) {
+            if (!(mn ? i128_less(lo, hi, clo, chi) : i128_less(clo, chi, lo, hi))) {
+                done = 1;
+            } else {
+                u64 e = s1;
+                if (__hip_atomic_compare_exchange_strong(w, &e, s1 + 1, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED, AT_SCOPE(AS))) {
+                    __hip_atomic_store(w + 1, lo, __ATOMIC_RELAXED, AT_SCOPE(AS));
+                    __hip_atomic_store(w + 2, hi, __ATOMIC_RELAXED, AT_SCOPE(AS));
+                    __hip_atomic_store(w, s1 + 2, __ATOMIC_RELEASE, AT_SCOPE(AS));
+                    done = 1;
+                }
+            }
         }
-    }
+        // `done` made opaque at the end of the body: every path, the publish included, has to
+        // reach the latch, so no branch can jump-thread the winner's writes into the loop exit
+        asm volatile("" : "+v"(done));
+    } while (!done && ++spins < (1u << 20));
 }
+
 template <int AS> __device__ __forceinline__ u64 at_cas(wptr<AS> p, u64 expected, u64 desired) {
     __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED, AT_SCOPE(AS));
     return expected;  // the old value (== the expected one iff the exchange happened)

@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-for c in ${CONFIGS:-2 1 3 4 5}; do
+for c in ${CONFIGS-2 1 3 4 5}; do
   timeout -k 10 300 python -u bench.py --config $c --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline > gpurun_out/bench_c$c.json 2> gpurun_out/bench_c$c.err || { echo "bench $c failed"; tail -20 gpurun_out/bench_c$c.err; exit 1; }
   python3 -c "
 import json;d=json.loads(open('gpurun_out/bench_c$c.json').read().strip().splitlines()[-1])
