@@ -469,6 +469,7 @@ static TableDesc table_desc(dbg_agg_handle* h) {
     t.ovf_recs_cap = h->ovf_recs_cap;
     t.scratch = h->scratch;
     t.scr_blocks = h->scr_blocks;
+
     return t;
 }
 
@@ -812,6 +813,7 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if ((rc = dev_alloc((void**)&h->scratch, (size_t)h->scr_blocks * 8 * (2 + SCR_ENTRIES * (size_t)h->spec.stride_words))) != DBG_OK)
         return cleanup(rc);
     if (hipMemset(h->scratch, 0, (size_t)h->scr_blocks * 16) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
+
     // the (empty) batch table
     BatchDesc* st;
     u32 bid;
@@ -1361,7 +1363,8 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
         return DBG_OK;
     }
     RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
-    if (on_device && h->recycle && h->hcounters_dev && insert_can_fuse(S, *st, h->cap)) {  // held back: see def_on
+    static const bool x_nofuse = getenv("DBG_X_NOFUSE") != nullptr;  // EXPERIMENT
+    if (!x_nofuse && on_device && h->recycle && h->hcounters_dev && insert_can_fuse(S, *st, h->cap)) {  // held back: see def_on
         h->def_on = true;
         h->def_bid = bid;
         h->def_rows = rows;
@@ -1835,6 +1838,38 @@ static int fin_launch(dbg_agg_handle* h) {
         ff.seq = F.seq;
         ff.recycle = h->recycle;
         ff.on = 1;
+        ff.trace = nullptr;
+        static u64* x_trace = nullptr;  // EXPERIMENT (DBG_X_TRACE): 8 words per launch, 4096 launches
+        static std::vector<u64> x_init;
+        if (getenv("DBG_X_TRACE")) {
+            if (!x_trace) {
+                RETURN_IF(dev_alloc((void**)&x_trace, 4096 * 128));
+                x_init.assign(16, 0);
+                x_init[0] = x_init[1] = ~0ULL;
+                atexit([] {
+                    std::vector<u64> hb(4096 * 16);
+                    hipDeviceSynchronize();
+                    hipMemcpy(hb.data(), x_trace, hb.size() * 8, hipMemcpyDeviceToHost);
+                    std::vector<std::vector<double>> d(14);
+                    for (int k = 0; k < 4096; ++k) {
+                        const u64* r = &hb[k * 16];
+                        if (r[0] == 0 || r[0] == ~0ULL || r[6] == 0) continue;
+                        for (int p = 1; p <= 14; ++p) d[p - 1].push_back((double)(r[p] - r[0]) * 0.01);
+                    }
+                    const char* nm[] = {"first WG stream end", "last WG stream end", "last block_flush end",
+                                        "ticket (last WG)", "table copied", "finalize end", "fin: scanned",
+                                        "fin: groups written", "fin: bits packed", "fin: counters read",
+                                        "tail: view+counts", "tail: prefix", "tail: t0 loads", "tail: t0 merged"};
+                    for (int p = 0; p < 14; ++p) {
+                        if (d[p].empty()) continue;
+                        std::sort(d[p].begin(), d[p].end());
+                        fprintf(stderr, "trace %-22s median %7.2f us  (n=%zu)\n", nm[p], d[p][d[p].size() / 2], d[p].size());
+                    }
+                });
+            }
+            ff.trace = x_trace + (F.seq & 4095) * 16;
+            HIPCHECK(hipMemcpyAsync(ff.trace, x_init.data(), 128, hipMemcpyHostToDevice, h->stream));
+        }
         h->def_on = false;
         prof::Scope ps("agg_insert", h->stream);
         launch_insert(h->stream, h->dspec, S, h->dbatches, h->def_bid, h->def_rows, false, t, true, &h->def_hb, &ff);

@@ -807,17 +807,30 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
 // workgroup of a fused insert (agg_insert_fast with FusedFin::on).  `view` holds the slots to
 // read (t.slots, or a copy in LDS); the re-initialisation of a recycled table writes t.slots.
 template <int MAXPER>
-__device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDesc* batches, const TableDesc& t, const u64* view,
-                                                    const OutDesc& out, u64* totals, u64* host_mirror, int recycle, u64 seq) {
+__device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDesc* batches, const TableDesc& t, const u64* view,
+                                                    const OutDesc& out, u64* totals, u64* host_mirror, int recycle, u64 seq,
+                                                    u64* trace = nullptr) {
     __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
-    __shared__ int do_recycle;
+    __shared__ u64 cnts[CNT_WORDS];
+    auto mark = [&](int k) { if (trace && threadIdx.x == 0) trace[k] = __builtin_amdgcn_s_memrealtime(); };
+    // Barriers here are LDS-only (no wait for this workgroup's global stores) unless a later
+    // phase reads what other threads stored to global memory: every __syncthreads costs a
+    // store round trip (vmcnt 0, ~1 us).
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     const u64 n_slots = t.cap + 1;
     const u32 per = (u32)((n_slots + FIN_NT - 1) / FIN_NT);  // <= MAXPER (host checks cap)
     const u64 base = (u64)threadIdx.x * per;
     const bool ref_strings = S.has_strings && !S.inline_keys;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0)
-        do_recycle = recycle && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+    bool has_bits = false, dec_err = false;  // uniform
+    for (int c = 0; c < S.n_keys; ++c) has_bits |= out.key_valid[c] && out.key_bits[c];
+    for (int a = 0; a < S.n_aggs; ++a) {
+        has_bits |= out.agg_valid[a] && out.agg_bits[a];
+        dec_err |= S.aggs[a].dec_check || (S.aggs[a].kind == DBG_AGG_AVG && S.aggs[a].sumk == SUMK_I128);
+    }
+    // the table counters, in flight while the table is scanned (final: every inserting workgroup
+    // has finished; write_group may still set decimal-overflow bits, reloaded below)
+    u64 myc = threadIdx.x < CNT_WORDS ? ld_sc1(t.counters + threadIdx.x) : 0;
     u64 ent[MAXPER];
 #pragma unroll
     for (u32 k = 0; k < MAXPER; ++k) {
@@ -853,7 +866,7 @@ __device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDe
         if (ref_strings)
             for (int c = 0; c < S.n_keys; ++c) wsum[wave][1 + c] = isb[c];
     }
-    __syncthreads();
+    lds_barrier();
     u64 p = ic - cnt, sp[DBG_MAX_KEYS];
     for (int w = 0; w < wave; ++w) p += wsum[w][0];
     if (ref_strings)
@@ -868,6 +881,7 @@ __device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDe
         if (ref_strings)
             for (int w = 0; w < FIN_NT / 64; ++w) stot[c] += wsum[w][1 + c];
     }
+    mark(7);
     // write pass over the occupied slots only (one write_group instance in the code; the entry
     // is re-read from the cache rather than indexed out of the register array)
     const u32 occ_all = occ;
@@ -879,20 +893,23 @@ __device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDe
         write_group(S, batches, t, s, st, st[0], p, sp, out);
         p++;
     }
-    __syncthreads();  // validity bytes of every row are written; every state word has been read
+    mark(8);
     u64 n = total < out.cap_groups ? total : out.cap_groups;
-    for (u64 k = threadIdx.x; k < (n + 7) / 8; k += FIN_NT)
-        for (int c = 0; c < S.n_keys + S.n_aggs; ++c) {
-            const u8* bytes = c < S.n_keys ? out.key_valid[c] : out.agg_valid[c - S.n_keys];
-            u8* bits = c < S.n_keys ? out.key_bits[c] : out.agg_bits[c - S.n_keys];
-            if (!bytes || !bits) continue;
-            u8 b = 0;
-            for (int j = 0; j < 8; ++j) {
-                u64 i = k * 8 + j;
-                if (i < n && bytes[i]) b |= (u8)(1u << j);
+    if (has_bits) {
+        __syncthreads();  // validity bytes of every row are in global memory
+        for (u64 k = threadIdx.x; k < (n + 7) / 8; k += FIN_NT)
+            for (int c = 0; c < S.n_keys + S.n_aggs; ++c) {
+                const u8* bytes = c < S.n_keys ? out.key_valid[c] : out.agg_valid[c - S.n_keys];
+                u8* bits = c < S.n_keys ? out.key_bits[c] : out.agg_bits[c - S.n_keys];
+                if (!bytes || !bits) continue;
+                u8 b = 0;
+                for (int j = 0; j < 8; ++j) {
+                    u64 i = k * 8 + j;
+                    if (i < n && bytes[i]) b |= (u8)(1u << j);
+                }
+                bits[k] = b;
             }
-            bits[k] = b;
-        }
+    }
     if (threadIdx.x == 0) {
         totals[0] = total;
         for (int c = 0; c < S.n_keys; ++c) {
@@ -900,22 +917,23 @@ __device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDe
             if (out.key_offsets[c] && total <= out.cap_groups) out.key_offsets[c][total] = stot[c];
         }
     }
-    __syncthreads();  // decimal-overflow bits of write_group are in the counters
+    if (dec_err) {
+        __syncthreads();  // decimal-overflow bits of write_group are in the counters
+        if (threadIdx.x == CNT_ERR) myc = ld_sc1(t.counters + CNT_ERR);
+    }
+    if (threadIdx.x < CNT_WORDS) cnts[threadIdx.x] = myc;
+    lds_barrier();
+    mark(9);
     // recycle only when the caller got every group (short buffers: the table must stay intact
-    // for the retry with larger ones)
-    bool rc = do_recycle != 0 && total <= out.cap_groups;
+    // for the retry with larger ones) and no insert overflowed (the host grows and finalizes again)
+    bool rc = recycle && cnts[CNT_OVF_ROWS] == 0 && cnts[CNT_OVF_RECS] == 0 && total <= out.cap_groups;
     for (int c = 0; c < S.n_keys; ++c)
         if (ref_strings && S.key_types[c].type == DBG_STRING && stot[c] > out.cap_str[c]) rc = false;
+    if (rc && threadIdx.x < CNT_WORDS) t.counters[threadIdx.x] = 0;  // dbg_agg_reset
     // zero-copy read-back: the table counters and the totals go straight to mapped pinned host
     // memory ([0, CNT_WORDS) counters, then totals), so finalize needs no copy launches
     // (system-scope stores: written through to host memory, never parked in the L2)
     auto put = [&](int w, u64 v) { __hip_atomic_store(host_mirror + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-    __shared__ u64 cnts[CNT_WORDS];
-    if (threadIdx.x < CNT_WORDS) {  // one load per thread, all in flight together
-        cnts[threadIdx.x] = ld_sc1(t.counters + threadIdx.x);
-        if (rc) t.counters[threadIdx.x] = 0;  // dbg_agg_reset
-    }
-    __syncthreads();
     if (threadIdx.x == 0) {
         if (host_mirror) {
             for (int w = 0; w < CNT_WORDS; ++w) put(w, cnts[w]);
@@ -924,6 +942,7 @@ __device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDe
             put(CNT_WORDS + 1 + DBG_MAX_KEYS, rc ? 1 : 0);  // recycled
         }
     }
+    mark(10);
     if (rc) {  // table_init of the owned slots that were claimed (an EMPTY slot is still in its
                // initial state: state words are only written after the entry is claimed)
         const u32 sw = (u32)t.stride_words;
@@ -941,6 +960,7 @@ __device__ __forceinline__ void finalize_small_body(const Spec& S, const BatchDe
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(host_mirror + CNT_WORDS + 2 + DBG_MAX_KEYS, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    return rc;
 }
 
 __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
@@ -974,11 +994,15 @@ __device__ __forceinline__ void fused_finalize(const Spec& S, const BatchDesc* b
     }
     __syncthreads();
     if (!is_last) return;
+    if (ff.trace && threadIdx.x == 0) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
     const u64 n = (t.cap + 1) * t.stride_words;  // host: <= the launch's dynamic LDS
     for (u64 i = threadIdx.x; i < n; i += FIN_NT) lds[i] = ld_sc1(t.slots + i);
     if (threadIdx.x == 0) atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
     __syncthreads();
-    finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq);
+    if (ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
+    finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq,
+                                                  ff.trace);
+    if (ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1049,6 +1073,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     // candidate-vector queue (the `<> c` path below) over the same per-wave space
     v4u* vq = (v4u*)qkey;
     u64* vqb = qkey + 2 * WQ;
+    if (ff.trace && threadIdx.x == 0) atomicMin((unsigned long long*)ff.trace, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     lds_table_init(S, lds, lds_slots, sw, NT);
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
@@ -1300,7 +1325,13 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
     }
     __syncthreads();
+    if (ff.trace && threadIdx.x == 0) {
+        const u64 tm = __builtin_amdgcn_s_memrealtime();
+        atomicMin((unsigned long long*)ff.trace + 1, (unsigned long long)tm);
+        atomicMax((unsigned long long*)ff.trace + 2, (unsigned long long)tm);
+    }
     block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
+    if (ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     if (ff.on) fused_finalize(S, batches, t, lds, ff);
 }
 
@@ -1330,7 +1361,8 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
     const int nt = 1024;
     static_assert(FIN_NT == 1024, "the fused finalize runs on the insert's workgroup");
-    const u64 max_blocks = 256;  // one 1024-lane workgroup per CU
+    static const u64 xb = getenv("DBG_X_BLOCKS") ? strtoull(getenv("DBG_X_BLOCKS"), nullptr, 10) : 256;  // EXPERIMENT
+    const u64 max_blocks = xb;  // one 1024-lane workgroup per CU
     size_t shmem = fast_shmem(table_bytes);
     FusedFin ff;
     if (fused) ff = *fused;

@@ -241,6 +241,7 @@ struct FusedFin {
     u64 seq;
     int recycle;
     int on;
+    u64* trace;  // EXPERIMENT (DBG_X_TRACE): phase timestamps of this launch, s_memrealtime ticks
 };
 // host side: would launch_insert of this batch take the fast kernel (and so could fuse)?
 bool insert_can_fuse(const Spec& S, const BatchDesc& hb, u64 cap);

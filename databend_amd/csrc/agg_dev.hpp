@@ -77,36 +77,42 @@ __device__ __forceinline__ void apply_row(const Spec& S, wptr<AS> st, const Batc
 template <bool SC1, int RAS>
 __device__ __forceinline__ u64 rdw(const u64* p) { return SC1 ? ld_sc1(p) : *asp<RAS>(p); }
 
-template <int AS, bool SC1 = false, int RAS = AS_GLB>
-__device__ __forceinline__ void apply_state(const Spec& S, wptr<AS> st, const u64* r) {
+// merge_states with the partial state's word w given by get(w) (memory or registers)
+template <int AS, typename G>
+__device__ __forceinline__ void apply_state_get(const Spec& S, wptr<AS> st, G get) {
     for (int a = 0; a < S.n_aggs; ++a) {
         const DAgg& A = S.aggs[a];
         wptr<AS> w = st + A.w0;
-        const u64* x = r + A.w0;
-        const u64 x0 = rdw<SC1, RAS>(x);
+        const int x = A.w0;
+        const u64 x0 = get(x);
         switch (A.kind) {
             case DBG_AGG_COUNT: if (x0) at_add<AS>(w, x0); break;
             case DBG_AGG_SUM: case DBG_AGG_AVG: {
                 if (A.sumk == SUMK_I64) { if (x0) at_add<AS>(w, x0); }
                 else if (A.sumk == SUMK_F64) at_addf<AS>(w, __longlong_as_double((long long)x0));
-                else add128<AS>(w, x0, rdw<SC1, RAS>(x + 1));
+                else add128<AS>(w, x0, get(x + 1));
                 if (A.kind == DBG_AGG_AVG) {
                     int k = A.sumk == SUMK_I128 ? 2 : 1;
-                    u64 xk = rdw<SC1, RAS>(x + k);
+                    u64 xk = get(x + k);
                     if (xk) at_add<AS>(w + k, xk);
                 }
                 break;
             }
             case DBG_AGG_MIN: case DBG_AGG_MAX:
-                if (A.mmk == MMK_I128) at_minmax128<AS>(w, rdw<SC1, RAS>(x + 1), rdw<SC1, RAS>(x + 2), A.kind == DBG_AGG_MIN);
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, get(x + 1), get(x + 2), A.kind == DBG_AGG_MIN);
                 else at_minmax<AS>(w, x0, A.kind == DBG_AGG_MIN, A.mmk == MMK_I64);
                 break;
         }
     }
     if (S.flags_word >= 0) {
-        u64 f = rdw<SC1, RAS>(r + S.flags_word);
+        u64 f = get(S.flags_word);
         if (f) at_or<AS>(st + S.flags_word, f);
     }
+}
+
+template <int AS, bool SC1 = false, int RAS = AS_GLB>
+__device__ __forceinline__ void apply_state(const Spec& S, wptr<AS> st, const u64* r) {
+    apply_state_get<AS>(S, st, [&](int w) { return rdw<SC1, RAS>(r + w); });
 }
 
 struct U128 {

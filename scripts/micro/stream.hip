@@ -1,75 +1,64 @@
-// Streaming-read ceiling on MI355X: how fast can one launch read N bytes (16-B loads)?
-// Used to calibrate what the C2 insert kernel can reach.
+// Read-bandwidth ceiling for the C2 insert's access pattern: a 200 MB int16 column streamed with
+// 16-byte nontemporal loads, grid-strided, U loads in flight per lane, a trivial reduction so the
+// loads are live.  Prints GB/s per configuration (hipEvent timing, median of 20 launches).
+// Build: hipcc --offload-arch=gfx950 -O3 -o stream stream.hip
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdio>
-#include <cstdlib>
+#include <vector>
+
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef const v4u __attribute__((address_space(1)))* gv4p;
 
-template <int UNROLL>
-__global__ void __launch_bounds__(1024) rd(const v4u* __restrict__ p, size_t nvec, unsigned* out) {
+template <int U>
+__global__ void rd(const v4u* __restrict__ p, unsigned long long n, unsigned* out) {
+    gv4p vp = (gv4p)p;
+    const unsigned long long g = (unsigned long long)gridDim.x * blockDim.x;
+    unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     unsigned acc = 0;
-    size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    for (; i + (UNROLL - 1) * stride < nvec; i += UNROLL * stride) {
-        v4u y[UNROLL];
+    for (; k + (U - 1) * g < n; k += U * g) {
+        v4u y[U];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) y[u] = __builtin_nontemporal_load(p + i + u * stride);
+        for (int u = 0; u < U; ++u) y[u] = __builtin_nontemporal_load(vp + k + u * g);
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) acc ^= y[u].x ^ y[u].y ^ y[u].z ^ y[u].w;
+        for (int u = 0; u < U; ++u) acc |= (y[u].x | y[u].y | y[u].z | y[u].w) == 0x12345 ? 1u : 0u;
     }
-    for (; i < nvec; i += stride) { v4u y = p[i]; acc ^= y.x ^ y.y ^ y.z ^ y.w; }
-    if (acc == 0x12345678) out[0] = acc;
+    for (; k < n; k += g) acc |= vp[k].x == 0x12345;
+    if (acc) out[0] = acc;
 }
 
-// contiguous chunk per block
-template <int UNROLL>
-__global__ void __launch_bounds__(1024) rdc(const v4u* __restrict__ p, size_t nvec, size_t per_block, unsigned* out) {
-    unsigned acc = 0;
-    size_t b0 = blockIdx.x * per_block, b1 = b0 + per_block < nvec ? b0 + per_block : nvec;
-    size_t i = b0 + threadIdx.x;
-    for (; i + (UNROLL - 1) * blockDim.x < b1; i += UNROLL * blockDim.x) {
-        v4u y[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) y[u] = __builtin_nontemporal_load(p + i + u * blockDim.x);
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) acc ^= y[u].x ^ y[u].y ^ y[u].z ^ y[u].w;
+template <int U>
+float run(const v4u* p, unsigned long long n, unsigned* out, int blocks, int nt) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    std::vector<float> ts;
+    for (int r = 0; r < 23; ++r) {
+        hipEventRecord(a);
+        hipLaunchKernelGGL(rd<U>, dim3(blocks), dim3(nt), 0, 0, p + (r & 3) * n, n, out);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        if (r >= 3) ts.push_back(ms);
     }
-    for (; i < b1; i += blockDim.x) { v4u y = p[i]; acc ^= y.x ^ y.y ^ y.z ^ y.w; }
-    if (acc == 0x12345678) out[0] = acc;
+    std::sort(ts.begin(), ts.end());
+    return ts[ts.size() / 2];
 }
 
-int main(int argc, char** argv) {
-    size_t bytes = argc > 1 ? strtoull(argv[1], 0, 10) : 200000000ull;
-    int copies = 4;
-    size_t nvec = bytes / 16;
-    v4u* bufs[4];
-    for (int c = 0; c < copies; ++c) { hipMalloc(&bufs[c], bytes); hipMemset(bufs[c], c + 1, bytes); }
-    unsigned* out; hipMalloc(&out, 4);
-    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-    int grids[] = {256, 512, 1024, 2048, 4096};
-    int blocks[] = {256, 512, 1024};
-    for (int mode = 0; mode < 2; ++mode)
-    for (int bs : blocks) for (int g : grids) for (int un = 4; un <= 8; un += 4) {
-        auto launch = [&](int c) {
-            if (mode == 0) {
-                if (un == 4) hipLaunchKernelGGL(rd<4>, dim3(g), dim3(bs), 0, 0, bufs[c], nvec, out);
-                else hipLaunchKernelGGL(rd<8>, dim3(g), dim3(bs), 0, 0, bufs[c], nvec, out);
-            } else {
-                size_t per = (nvec + g - 1) / g;
-                if (un == 4) hipLaunchKernelGGL(rdc<4>, dim3(g), dim3(bs), 0, 0, bufs[c], nvec, per, out);
-                else hipLaunchKernelGGL(rdc<8>, dim3(g), dim3(bs), 0, 0, bufs[c], nvec, per, out);
-            }
-        };
-        for (int w = 0; w < 8; ++w) launch(w % copies);
-        hipDeviceSynchronize();
-        int iters = 40;
-        float tot = 0;
-        for (int it = 0; it < iters; ++it) {
-            hipEventRecord(e0); launch(it % copies); hipEventRecord(e1); hipEventSynchronize(e1);
-            float ms; hipEventElapsedTime(&ms, e0, e1); tot += ms;
-        }
-        float us = tot / iters * 1000;
-        printf("%s bs=%4d grid=%4d unroll=%d  %7.2f us  %6.0f GB/s\n", mode ? "chunk " : "stride", bs, g, un, us, bytes / (us * 1e3));
+int main() {
+    const unsigned long long bytes = 200000000ull, n = bytes / 16;
+    v4u* p;
+    unsigned* out;
+    hipMalloc(&p, 4 * bytes);  // 4 rotating copies: not served from the 256 MiB MALL
+    hipMalloc(&out, 4);
+    hipMemset(p, 1, 4 * bytes);
+    hipDeviceSynchronize();
+    struct C { int blocks, nt, u; } cs[] = {{256, 1024, 4}, {256, 1024, 8}, {512, 512, 4}, {512, 512, 8}, {1024, 256, 8},
+                                          {2048, 256, 4}, {4096, 256, 4}, {512, 1024, 4}, {1024, 1024, 2}};
+    for (auto c : cs) {
+        float ms = c.u == 8 ? run<8>(p, n, out, c.blocks, c.nt) : (c.u == 4 ? run<4>(p, n, out, c.blocks, c.nt) : run<2>(p, n, out, c.blocks, c.nt));
+        printf("blocks %5d nt %4d unroll %d: %.2f us  %.0f GB/s\n", c.blocks, c.nt, c.u, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
     }
     return 0;
 }
