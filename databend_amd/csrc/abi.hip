@@ -1256,6 +1256,23 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     PPAggOut o;
     memset(&o, 0, sizeof(o));
     o.tot = h->pp_tot;
+    static u64* x_pptrace = nullptr;  // EXPERIMENT (DBG_X_PPTRACE)
+    if (getenv("DBG_X_PPTRACE")) {
+        if (!x_pptrace) {
+            RETURN_IF(dev_alloc((void**)&x_pptrace, 64));
+            HIPCHECK(hipMemset(x_pptrace, 0, 64));
+            atexit([] {
+                u64 v[8];
+                hipDeviceSynchronize();
+                hipMemcpy(v, x_pptrace, 64, hipMemcpyDeviceToHost);
+                const double n = v[5] ? (double)v[5] : 1.0;
+                fprintf(stderr, "pptrace partitions %llu groups/partition %.0f  per partition us: insert %.2f sync %.2f "
+                                "atomic %.2f write %.2f tail %.2f\n", (unsigned long long)v[5], v[6] / n, v[0] * 0.01 / n,
+                        v[1] * 0.01 / n, v[2] * 0.01 / n, v[3] * 0.01 / n, v[4] * 0.01 / n);
+            });
+        }
+        o.trace = x_pptrace;
+    }
     if (mode == 0) {
         o.cols = *od;
     } else {

@@ -311,6 +311,7 @@ struct PPAggOut {
     u8* grec;       // mode 1
     u64 grec_cap;
     u64* tot;       // PPT_* words (device)
+    u64* trace;     // EXPERIMENT (DBG_X_PPTRACE): summed phase durations of sampled workgroups
 };
 // device totals of one partitioned finalize: groups, string bytes per key column, extra rounds, errors
 enum { PPT_GROUPS = 0, PPT_STR = 1, PPT_ROUNDS = 1 + DBG_MAX_KEYS, PPT_ERR = 2 + DBG_MAX_KEYS, PPT_WORDS = 4 + DBG_MAX_KEYS };

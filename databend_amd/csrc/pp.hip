@@ -1091,6 +1091,8 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     load_tile(pre, raw, nx_r0, nx_nr, 0);
     part_range(blockIdx.x + gridDim.x, nn_r0, nn_nr);
     __syncthreads();
+    const bool tr = out.trace && (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+    u64 tm0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
     for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
         const u64 r0 = nx_r0, s0 = st_off ? st_off[p] : 0;
         u64 nr = nx_nr, ns = st_off ? st_off[p + 1] - s0 : 0;
@@ -1125,7 +1127,9 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
                 else
                     pp_store_rec(sout + (s0 + atomicAdd(&novf[1], 1u)) * rws, rk, rws);
             }
+            if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 0, tm - tm0); tm0 = tm; }
             __syncthreads();
+            if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 1, tm - tm0); tm0 = tm; }
             if (round == 0) {  // prefetch: next partition's first tile, the one after's offsets
                 nx_r0 = nn_r0;
                 nx_nr = nn_nr;
@@ -1134,6 +1138,7 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
             }
             if (threadIdx.x == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
             __syncthreads();
+            if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 2, tm - tm0); tm0 = tm; }
             // emit the claimed slots in claim order, clearing their tags for the next table
             const u32 ng = nlist;
             for (u32 k = threadIdx.x; k < ng; k += PP_AGG_NT) {
@@ -1149,9 +1154,17 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
                 e[0] = 0;
             }
             const u32 o0 = novf[0], o1 = novf[1];
+            if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 3, tm - tm0); tm0 = tm; }
             __syncthreads();
             if (threadIdx.x == 0) nlist = novf[0] = novf[1] = 0;
             __syncthreads();
+            if (tr) {
+                const u64 tm = __builtin_amdgcn_s_memrealtime();
+                atomicAdd((unsigned long long*)out.trace + 4, tm - tm0);
+                atomicAdd((unsigned long long*)out.trace + 5, 1ULL);
+                atomicAdd((unsigned long long*)out.trace + 6, (unsigned long long)ng);
+                tm0 = tm;
+            }
             if (o0 == 0 && o1 == 0) break;
             if (threadIdx.x == 0) atomicAdd((unsigned long long*)(out.tot + PPT_ROUNDS), 1ULL);
             // the overflow, written to this partition's region of the alternate buffers, is the
