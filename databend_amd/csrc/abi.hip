@@ -17,6 +17,7 @@
 
 #include "agg.hpp"
 #include "host_stage.hpp"
+#include "legacy.hpp"
 
 #include <dlfcn.h>
 #include <rccl/rccl.h>  // types only: the entry points are resolved with dlsym (exchange section)
@@ -2343,6 +2344,94 @@ int dbg_take_string(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, 
     if (vbytes) launch_pack_bits(s, vbytes, n_sel, out_validity);
     HIPCHECK(hipStreamSynchronize(s));
     if (vbytes) hipFree(vbytes);
+    return DBG_OK;
+}
+
+// HashMethodKind::choose_hash_method_with_types (EXP/kernels/group_by.rs:48-97)
+static int legacy_method(const dbg_datatype* types, int n, int* kind, uint32_t* key_bytes) {
+    if (n < 1 || n > DBG_MAX_KEYS) return fail(DBG_ERR_UNSUPPORTED, "1..8 group columns");
+    if (n == 1 && types[0].type == DBG_STRING && !types[0].nullable) {
+        *kind = DBG_LEGACY_SINGLE_BINARY;
+        *key_bytes = 0;
+        return DBG_OK;
+    }
+    u32 len = 0;
+    for (int j = 0; j < n; ++j) {
+        const int t = types[j].type;
+        if (t == DBG_STRING || t == DBG_BOOLEAN || !valid_type(t)) {
+            *kind = DBG_LEGACY_SERIALIZER;
+            *key_bytes = 0;
+            return DBG_OK;
+        }
+        len += type_width(t) + (types[j].nullable ? 1 : 0);
+    }
+    *key_bytes = len;
+    *kind = len == 1 ? DBG_LEGACY_KEYS_U8 : len == 2 ? DBG_LEGACY_KEYS_U16 : len <= 4 ? DBG_LEGACY_KEYS_U32
+          : len <= 8 ? DBG_LEGACY_KEYS_U64 : len <= 16 ? DBG_LEGACY_KEYS_U128 : len <= 32 ? DBG_LEGACY_KEYS_U256
+          : DBG_LEGACY_SERIALIZER;
+    return DBG_OK;
+}
+
+int dbg_legacy_hash_method(const dbg_datatype* types, int n, int* kind, uint32_t* key_bytes) {
+    if (!types || !kind || !key_bytes) return fail(DBG_ERR_INVALID, "null argument");
+    return legacy_method(types, n, kind, key_bytes);
+}
+
+int dbg_legacy_group_hash(const dbg_column* cols, int n, uint64_t rows, uint64_t* out_hash, uint32_t* out_bucket,
+                          int bucket_bits, void* stream) {
+    if (!cols || !out_hash) return fail(DBG_ERR_INVALID, "null argument");
+    if (out_bucket && (bucket_bits < 1 || bucket_bits > 31)) return fail(DBG_ERR_INVALID, "bucket bits 1..31");
+    std::vector<dbg_datatype> types(n > 0 ? n : 1);
+    for (int j = 0; j < n; ++j) types[j] = cols[j].dt;
+    int kind = 0;
+    uint32_t kb = 0;
+    RETURN_IF(legacy_method(types.data(), n, &kind, &kb));
+    for (int j = 0; j < n; ++j)
+        if (cols[j].len < rows) return fail(DBG_ERR_INVALID, "column shorter than rows");
+    hipStream_t s = (hipStream_t)stream;
+    auto dcol = [&](const dbg_column& c) {
+        DCol d;
+        memset(&d, 0, sizeof(d));
+        d.type = c.dt.type;
+        d.nullable = c.dt.nullable;
+        d.layout = LAYOUT_ARROW;
+        d.width = type_width(c.dt.type);
+        d.stride = d.width;
+        d.data = (const u8*)c.data;
+        d.offsets = c.offsets;
+        d.validity = c.dt.nullable ? c.validity : nullptr;
+        d.validity_offset = c.validity_offset;
+        d.data_offset = c.data_offset;
+        return d;
+    };
+    if (kind == DBG_LEGACY_SINGLE_BINARY) {
+        launch_legacy_binary_hash(s, dcol(cols[0]), rows, out_hash, out_bucket, (u32)bucket_bits);
+    } else if (kind == DBG_LEGACY_SERIALIZER) {
+        return fail(DBG_ERR_UNSUPPORTED, "legacy HashMethodSerializer keys stay on the CPU path");
+    } else {
+        LegacyKeyDesc d;
+        memset(&d, 0, sizeof(d));
+        d.n = n;
+        const u32 width = kind == DBG_LEGACY_KEYS_U8 ? 1 : kind == DBG_LEGACY_KEYS_U16 ? 2 : kind == DBG_LEGACY_KEYS_U32 ? 4
+                        : kind == DBG_LEGACY_KEYS_U64 ? 8 : kind == DBG_LEGACY_KEYS_U128 ? 16 : 32;
+        d.words = width <= 8 ? 1 : width / 8;
+        // build_keys_vec: stable sort by value width, widest first; null bytes after all values
+        std::vector<int> order(n);
+        for (int j = 0; j < n; ++j) order[j] = j;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return type_width(cols[a].dt.type) > type_width(cols[b].dt.type); });
+        u32 off = 0, noff = 0;
+        for (int j = 0; j < n; ++j) noff += type_width(cols[j].dt.type);
+        for (int j = 0; j < n; ++j) {
+            const dbg_column& c = cols[order[j]];
+            d.cols[j] = dcol(c);
+            d.off[j] = off;
+            off += type_width(c.dt.type);
+            if (c.dt.nullable) d.null_off[j] = noff++;
+        }
+        launch_legacy_fixed_hash(s, d, rows, out_hash, out_bucket, (u32)bucket_bits);
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s));
     return DBG_OK;
 }
 

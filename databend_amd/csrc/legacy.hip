@@ -1,0 +1,104 @@
+// legacy.hip — group keys and FastHash of the legacy HashMethod path
+// (enable_experimental_aggregate_hashtable = 0).
+//
+// HashMethodKind::choose_hash_method_with_types (EXP/kernels/group_by.rs:48-97) picks
+//   SingleBinary for one String/Binary key, FixedKeys<T> when every key is a number, date,
+//   timestamp or decimal (T = u8 / u16 / u32 / u64 / u128 / U256 by the packed width: value bytes
+//   plus one null byte per nullable key), Serializer otherwise (not on this path: UNSUPPORTED).
+// FixedKeys packs a row (build_keys_vec / fixed_hash, EXP/kernels/group_by_hash/
+// method_fixed_keys.rs:74-100, 366-470): columns stably sorted by byte width, widest first, values
+// little-endian from offset 0, each nullable column's null byte after all the values (1 = NULL, the
+// value bytes then stay 0).  FastHash (HT/traits.rs:172-330, the sse4.2 build): CRC32C of the key's
+// little-endian u64 words, `_mm_crc32_u64(u64::MAX, w)` chained (no final inversion; the result is
+// the 32-bit CRC zero-extended); [u8] hashes 8-byte words, the last one (1..8 bytes) read
+// little-endian and zero-padded, and an empty slice hashes to u64::MAX.  The partitioned table's
+// bucket is hash2bucket<BITS, true> = (hash >> (32 - BITS)) & (2^BITS - 1)
+// (HT/partitioned_hashtable.rs:77-83).
+#include "device.hpp"
+#include "legacy.hpp"
+
+// CRC32C (Castagnoli, reflected 0x82F63B78) of 8 little-endian bytes, table-driven from LDS
+__device__ __forceinline__ u32 crc32c_u64(const u32* tab, u32 crc, u64 v) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) crc = tab[(crc ^ (u32)(v >> (8 * b))) & 0xffu] ^ (crc >> 8);
+    return crc;
+}
+
+__device__ __forceinline__ void crc_table_init(u32* tab) {
+    for (u32 i = threadIdx.x; i < 256; i += blockDim.x) {
+        u32 c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+        tab[i] = c;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) legacy_fixed_hash_kernel(LegacyKeyDesc d, u64 rows, u64* __restrict__ hash,
+                                                               u32* __restrict__ bucket, u32 bits) {
+    __shared__ u32 tab[256];
+    crc_table_init(tab);
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < rows; i += (u64)gridDim.x * blockDim.x) {
+        u64 k[4] = {0, 0, 0, 0};
+        for (int j = 0; j < d.n; ++j) {
+            const DCol& c = d.cols[j];
+            if (c.nullable && !dcol_valid(c, i)) {
+                const u32 o = d.null_off[j];
+                k[o >> 3] |= 1ULL << (8 * (o & 7));
+                continue;
+            }
+            const u32 w = c.width, o = d.off[j];
+            const u64 lo = dcol_bits(c, i), hi = w == 16 ? dcol_hi(c, i) : 0;
+            // value bytes at offset o (little-endian; may straddle words)
+            const u32 wi = o >> 3, sh = 8 * (o & 7);
+            k[wi] |= lo << sh;
+            if (sh && wi + 1 < 4) k[wi + 1] |= lo >> (64 - sh);
+            if (w == 16) {
+                k[wi + 1] |= hi << sh;
+                if (sh && wi + 2 < 4) k[wi + 2] |= hi >> (64 - sh);
+            }
+        }
+        u32 crc = 0xFFFFFFFFu;
+        for (u32 w = 0; w < d.words; ++w) crc = crc32c_u64(tab, crc, k[w]);
+        hash[i] = crc;
+        if (bucket) bucket[i] = (crc >> (32 - bits)) & ((1u << bits) - 1);
+    }
+}
+
+__global__ void __launch_bounds__(256) legacy_binary_hash_kernel(DCol c, u64 rows, u64* __restrict__ hash,
+                                                                u32* __restrict__ bucket, u32 bits) {
+    __shared__ u32 tab[256];
+    crc_table_init(tab);
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < rows; i += (u64)gridDim.x * blockDim.x) {
+        // a NULL of a nullable String key hashes as its (empty) value bytes — NullableColumn keeps
+        // the inner column's bytes; the reference hashes what the column holds at the row
+        const StrRef s = dcol_str(c, i);
+        u64 v = ~0ULL;
+        if (s.len) {
+            u32 crc = 0xFFFFFFFFu;
+            for (u64 o = 0; o < s.len; o += 8) {
+                const u64 n = s.len - o < 8 ? s.len - o : 8;
+                u64 w = 0;
+                for (u64 b = 0; b < n; ++b) w |= (u64)s.p[o + b] << (8 * b);
+                crc = crc32c_u64(tab, crc, w);
+            }
+            v = crc;
+        }
+        hash[i] = v;
+        if (bucket) bucket[i] = (u32)((v >> (32 - bits)) & ((1ULL << bits) - 1));
+    }
+}
+
+static u32 grid_of(u64 rows) {
+    u64 b = (rows + 255) / 256;
+    return (u32)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
+void launch_legacy_fixed_hash(hipStream_t s, const LegacyKeyDesc& d, u64 rows, u64* hash, u32* bucket, u32 bits) {
+    if (!rows) return;
+    hipLaunchKernelGGL(legacy_fixed_hash_kernel, dim3(grid_of(rows)), dim3(256), 0, s, d, rows, hash, bucket, bits);
+}
+
+void launch_legacy_binary_hash(hipStream_t s, const DCol& c, u64 rows, u64* hash, u32* bucket, u32 bits) {
+    if (!rows) return;
+    hipLaunchKernelGGL(legacy_binary_hash_kernel, dim3(grid_of(rows)), dim3(256), 0, s, c, rows, hash, bucket, bits);
+}

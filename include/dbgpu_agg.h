@@ -386,6 +386,24 @@ int dbg_take_fixed(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, v
 int dbg_take_string(const dbg_column* col, const uint32_t* sel, uint64_t n_sel, uint64_t* out_offsets, void* out_data,
                     uint64_t data_cap, uint8_t* out_validity, uint64_t* total_bytes, void* hip_stream);
 
+/* ---- legacy HashMethod path (enable_experimental_aggregate_hashtable = 0) ----
+ * dbg_legacy_hash_method mirrors HashMethodKind::choose_hash_method_with_types
+ * (EXP/kernels/group_by.rs:48-97); dbg_legacy_group_hash computes, on device columns, the FastHash
+ * of each row's legacy group key (HT/traits.rs:172-330, the x86_64 sse4.2 build: CRC32C of the
+ * key's little-endian u64 words from u64::MAX, no final inversion): FixedKeys<T> packs the keys as
+ * build_keys_vec does (EXP/kernels/group_by_hash/method_fixed_keys.rs:74-100, 366-470: columns
+ * widest first, null bytes after the values), SingleBinary hashes the string bytes (an empty
+ * string: u64::MAX).  out_bucket (optional) receives hash2bucket<bucket_bits, true>
+ * (HT/partitioned_hashtable.rs:77-83).  Serializer keys (Boolean, mixed strings) return
+ * DBG_ERR_UNSUPPORTED.  Synchronous. */
+enum {
+    DBG_LEGACY_KEYS_U8 = 1, DBG_LEGACY_KEYS_U16, DBG_LEGACY_KEYS_U32, DBG_LEGACY_KEYS_U64, DBG_LEGACY_KEYS_U128,
+    DBG_LEGACY_KEYS_U256, DBG_LEGACY_SINGLE_BINARY, DBG_LEGACY_SERIALIZER
+};
+int dbg_legacy_hash_method(const dbg_datatype* types, int n, int* kind, uint32_t* key_bytes);
+int dbg_legacy_group_hash(const dbg_column* cols, int n, uint64_t rows, uint64_t* out_hash, uint32_t* out_bucket,
+                          int bucket_bits, void* hip_stream);
+
 /* ---- ORDER BY one column LIMIT k (DataBlock::sort, EXP/kernels/sort.rs:79-107 -> arrow
  * sort_to_indices / indices_sorted_unstable_by, src/common/arrow/src/arrow/compute/sort/common.rs:95-174)
  * over a device-resident fixed-width number column (ints, date, timestamp, float32/64, boolean) —

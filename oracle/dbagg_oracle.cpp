@@ -1528,9 +1528,96 @@ struct orc_result {
     Result r;
 };
 
+// ------------------------------------------------------------------------------------------
+// Legacy HashMethod keys + FastHash (enable_experimental_aggregate_hashtable = 0)
+// choose_hash_method_with_types (EXP/kernels/group_by.rs:48-97); FixedKeys packing build_keys_vec /
+// build / fixed_hash (EXP/kernels/group_by_hash/method_fixed_keys.rs:74-100, 366-470); FastHash
+// (HT/traits.rs:172-330, sse4.2 build: _mm_crc32_u64 chained from u64::MAX); [u8] hash with the
+// 1..8-byte little-endian tail (read_le, HT/utils.rs:94-102), an empty slice -> u64::MAX.
+// ------------------------------------------------------------------------------------------
+// CRC32C bytewise (reflected Castagnoli 0x82F63B78), bit by bit: the SSE4.2 crc32 instruction
+// consumes its 8 bytes in little-endian order, the same as eight single-byte steps.
+static u32 crc32c_byte(u32 crc, u8 b) {
+    crc ^= b;
+    for (int k = 0; k < 8; ++k) crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+    return crc;
+}
+static u32 crc32c_u64_ref(u32 crc, u64 v) {  // _mm_crc32_u64(crc, v) (low 32 bits)
+    for (int b = 0; b < 8; ++b) crc = crc32c_byte(crc, (u8)(v >> (8 * b)));
+    return crc;
+}
+
+static void legacy_group_hash(const dbg_column* cols, int n, u64 rows, u64* out) {
+    if (n == 1 && cols[0].dt.type == DBG_STRING && !cols[0].dt.nullable) {  // HashMethodSingleBinary
+        for (u64 i = 0; i < rows; ++i) {
+            const u8* p = str_ptr(cols[0], i);
+            const u64 len = str_len(cols[0], i);
+            u64 value = ~0ULL;  // u64::MAX; each crc step leaves a 32-bit value
+            for (u64 o = 0; o < len; o += 8) {
+                u64 w = 0;
+                const u64 k = std::min<u64>(8, len - o);
+                for (u64 b = 0; b < k; ++b) w |= (u64)p[o + b] << (8 * b);
+                value = crc32c_u64_ref((u32)value, w);
+            }
+            out[i] = value;
+        }
+        return;
+    }
+    u64 len = 0;
+    for (int j = 0; j < n; ++j) {
+        const int t = cols[j].dt.type;
+        if (t == DBG_STRING || t == DBG_BOOLEAN) throw UnsupportedError("legacy Serializer keys");
+        len += fixed_width(t) + (cols[j].dt.nullable ? 1 : 0);
+    }
+    if (len > 32) throw UnsupportedError("legacy Serializer keys");
+    const u64 step = len == 1 ? 1 : len == 2 ? 2 : len <= 4 ? 4 : len <= 8 ? 8 : len <= 16 ? 16 : 32;
+    // build_keys_vec: sort_by (stable) widest first; null bytes start after every value byte
+    std::vector<int> order(n);
+    for (int j = 0; j < n; ++j) order[j] = j;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return fixed_width(cols[a].dt.type) > fixed_width(cols[b].dt.type); });
+    u64 values = 0;
+    for (int j = 0; j < n; ++j) values += fixed_width(cols[j].dt.type);
+    std::vector<u8> key(32);
+    for (u64 i = 0; i < rows; ++i) {
+        std::fill(key.begin(), key.end(), 0);
+        u64 off = 0, noff = values;
+        for (int j = 0; j < n; ++j) {
+            const dbg_column& c = cols[order[j]];
+            const u64 w = fixed_width(c.dt.type);
+            const bool nul = c.dt.nullable;
+            if (nul && !is_valid(c, i)) key[noff] = 1;
+            else memcpy(&key[off], (const u8*)c.data + i * w, w);
+            off += w;
+            if (nul) noff++;
+        }
+        u32 crc = 0xFFFFFFFFu;
+        for (u64 wd = 0; wd < (step <= 8 ? 1 : step / 8); ++wd) {
+            u64 v;
+            memcpy(&v, &key[wd * 8], 8);
+            crc = crc32c_u64_ref(crc, v);
+        }
+        out[i] = crc;
+    }
+}
+
 extern "C" {
 
 const char* orc_last_error(void) { return g_err.c_str(); }
+
+int orc_legacy_group_hash(const dbg_column* cols, int n, uint64_t rows, uint64_t* out) {
+    try {
+        legacy_group_hash(cols, n, rows, out);
+        return DBG_OK;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return DBG_ERR_UNSUPPORTED;
+    }
+}
+
+uint32_t orc_crc32c_bytes(uint32_t crc, const uint8_t* p, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) crc = crc32c_byte(crc, p[i]);
+    return crc;
+}
 
 int orc_group_hash(const dbg_column* cols, int ncols, uint64_t rows, uint64_t* out) {
     try {

@@ -42,6 +42,9 @@ def lib():
         L.orc_aggregate.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                     C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]
         L.orc_group_hash.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_void_p]
+        L.orc_legacy_group_hash.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_void_p]
+        L.orc_crc32c_bytes.argtypes = [C.c_uint32, C.c_void_p, C.c_uint64]
+        L.orc_crc32c_bytes.restype = C.c_uint32
         L.orc_filter_select.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64)]
         L.orc_datagen.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_datagen_c5_bytes.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
@@ -70,6 +73,21 @@ def group_hash(cols: Sequence[Column]) -> np.ndarray:
     arr = abi_array([c.to_abi() for c in cols])
     _check(lib().orc_group_hash(arr, len(cols), n, out.ctypes.data))
     return out
+
+
+def legacy_group_hash(cols: Sequence[Column]) -> np.ndarray:
+    """FastHash of the legacy HashMethod key (FixedKeys / SingleBinary), HT/traits.rs:172-330."""
+    n = len(cols[0])
+    out = np.zeros(max(1, n), dtype=np.uint64)
+    arr = abi_array([c.to_abi() for c in cols])
+    _check(lib().orc_legacy_group_hash(arr, len(cols), n, out.ctypes.data))
+    return out[:n]
+
+
+def crc32c(data: bytes, crc: int = 0xFFFFFFFF) -> int:
+    """Raw CRC32C update (no final inversion) of `data` from `crc`."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    return int(lib().orc_crc32c_bytes(crc, buf.ctypes.data, len(data)))
 
 
 def result_type(spec: abi.dbg_agg_spec) -> DataType:
