@@ -1092,12 +1092,14 @@ static PPFast pp_fast_desc(const Spec& S, const BatchDesc& B, u32 bid, int kind)
 }
 
 static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const u8* recs, const std::vector<PPChunk>& ch,
-                         const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out, const PPFast* F = nullptr) {
+                         const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out, const PPFast* F = nullptr,
+                         bool counted = false) {
     const u64 K = 1ULL << kbits;
     RETURN_IF(pp_upload_chunks(h, ch, c0));
+    if (counted && h->pp_cnt_cap < ch.size() * K) return fail(DBG_ERR_INTERNAL, "fused counts: buffer too small");
     RETURN_IF(ensure_dev(&h->pp_cnt, &h->pp_cnt_cap, ch.size() * K));
     RETURN_IF(ensure_dev(&h->pp_off, &h->pp_off_cap, ch.size() * K));
-    {
+    if (!counted) {
         prof::Scope ps(PP_COUNT_NAME[level], h->stream);
         if (F && F->kind)
             launch_pp_l1_fast(h->stream, *F, 1, h->pp_dchunks, (u32)ch.size(), h->pp_cnt, nullptr, nullptr, nullptr);
@@ -1116,7 +1118,7 @@ static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const 
 }
 
 static int pp_scatter(dbg_agg_handle* h, int level, int src, int kind, const u8* recs, u32 n_chunks, u32 shift, u32 kbits,
-                      u8* dst, const PPFast* F = nullptr) {
+                      u8* dst, const PPFast* F = nullptr, u32* cnt_next = nullptr, u32 sh_next = 0, u32 kb_next = 0) {
     prof::Scope ps(PP_SCATTER_NAME[level], h->stream);
     if (F && F->kind) {
         launch_pp_l1_fast(h->stream, *F, 0, h->pp_dchunks, n_chunks, nullptr, h->pp_off, h->pp_last_part, dst);
@@ -1124,7 +1126,7 @@ static int pp_scatter(dbg_agg_handle* h, int level, int src, int kind, const u8*
         return DBG_OK;
     }
     launch_pp_scatter(h->stream, h->dspec, h->spec, h->dbatches, src, kind, recs, h->pp_dchunks, n_chunks, shift, kbits, h->pp_off,
-                      h->pp_last_part, dst);
+                      h->pp_last_part, dst, cnt_next, sh_next, kb_next);
     HIPCHECK(hipGetLastError());
     return DBG_OK;
 }
@@ -1216,15 +1218,28 @@ static int pp_prepare(dbg_agg_handle* h) {
             p2 = h->pp_mid;
         }
         RETURN_IF(pp_count_scan(h, 2, 1, kind, K.l1, ch, c0, sh2, k2, p2));
-        RETURN_IF(pp_scatter(h, 2, 1, kind, K.l1, (u32)ch.size(), sh2, k2, K.a));
+        const u64 G2 = 256ULL << k2;
+        const u32 sh3 = sh2 - k3;
+        // Level 3's counts ride on the level-2 scatter when every level-2 partition is one level-3
+        // unit (<= PP_CHUNK records): one fewer pass over the records.
+        bool fused3 = false;
+        if (k3) {
+            RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, G2 + 1));
+            HIPCHECK(hipMemcpyAsync(h->pp_hpart, p2, (G2 + 1) * 8, hipMemcpyDeviceToHost, h->stream));
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            u64 mx = 0;
+            for (u64 g2 = 0; g2 < G2; ++g2) mx = std::max<u64>(mx, h->pp_hpart[g2 + 1] - h->pp_hpart[g2]);
+            fused3 = mx <= PP_CHUNK && ((1u << k2) << k3) <= PP_NEXT_HIST_MAX && !getenv("DBG_X_NOFUSE3");
+            if (fused3) {
+                RETURN_IF(ensure_dev(&h->pp_cnt, &h->pp_cnt_cap, G2 << k3));
+                HIPCHECK(hipMemsetAsync(h->pp_cnt, 0, (G2 << k3) * 4, h->stream));
+            }
+        }
+        RETURN_IF(pp_scatter(h, 2, 1, kind, K.l1, (u32)ch.size(), sh2, k2, K.a, nullptr, fused3 ? h->pp_cnt : nullptr, sh3, k3));
         K.fin = K.a;
         K.alt = K.b;
         if (!k3) continue;
         // level 3: units inside level-2 partitions
-        const u64 G2 = 256ULL << k2;
-        RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, G2 + 1));
-        HIPCHECK(hipMemcpyAsync(h->pp_hpart, p2, (G2 + 1) * 8, hipMemcpyDeviceToHost, h->stream));
-        HIPCHECK(hipStreamSynchronize(h->stream));
         ch.clear();
         c0.clear();
         for (u64 g2 = 0; g2 < G2; ++g2) {
@@ -1234,8 +1249,8 @@ static int pp_prepare(dbg_agg_handle* h) {
             if (c0.back() == ch.size()) ch.push_back(PPChunk{0, 0, 0, (u32)g2});
         }
         c0.push_back((u32)ch.size());
-        const u32 sh3 = sh2 - k3;
-        RETURN_IF(pp_count_scan(h, 3, 1, kind, K.a, ch, c0, sh3, k3, K.part));
+        if (fused3 && ch.size() != G2) return fail(DBG_ERR_INTERNAL, "fused level-3 counts: unit layout");
+        RETURN_IF(pp_count_scan(h, 3, 1, kind, K.a, ch, c0, sh3, k3, K.part, nullptr, fused3));
         RETURN_IF(pp_scatter(h, 3, 1, kind, K.a, (u32)ch.size(), sh3, k3, K.b));
         K.fin = K.b;
         K.alt = K.a;

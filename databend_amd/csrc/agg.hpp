@@ -279,7 +279,10 @@ void launch_pp_scan(hipStream_t s, const u32* cnt, u32 n_chunks, u32 kbits, cons
                     u64* part_off, u64* scratch);
 void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
                        const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
-                       const u64* part_off, u8* dst);
+                       const u64* part_off, u8* dst, u32* cnt_next = nullptr, u32 sh_next = 0, u32 kb_next = 0);
+// the next level's counts fused into a records scatter (cnt_next, zeroed: one unit per destination
+// partition, cnt_next[(group * K + b) << kb_next | digit]) when this LDS bound holds
+#define PP_NEXT_HIST_MAX 8192
 // Level 1 from raw columns, specialised (pp.hip): kind 1 = fixed-width non-null keys and
 // arguments (<= 8 columns, records <= 64 bytes) with an optional `column <cmp> constant` on a
 // fixed-width non-null integer column; kind 2 = one non-null String key, no arguments, optional

@@ -560,7 +560,8 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
                                                                  int kind, const u8* __restrict__ recs,
                                                                  const PPChunk* __restrict__ chunks, u32 shift, u32 kbits,
                                                                  const u64* __restrict__ off, const u64* __restrict__ part_off,
-                                                                 u8* __restrict__ dst) {
+                                                                 u8* __restrict__ dst, u32* __restrict__ cnt_next, u32 sh_next,
+                                                                 u32 kb_next) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     const Spec& S = *spec;
     const u32 K = 1u << kbits;
@@ -577,10 +578,30 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
         hist[b] = 0;
         run[b] = part_off[(u64)ch.group * K + b] + off[(u64)blockIdx.x * K + b];
     }
+    // next level's histogram per destination partition (records only): [b][digit] after the scratch
+    const u32 KN = cnt_next ? K << kb_next : 0;
+    l32* hn = (l32*)(scratch + (W == 0 ? (size_t)T * U * rw : 0));
+    for (u32 i = threadIdx.x; i < KN; i += PP_NT) hn[i] = 0;
     __syncthreads();
     const u64 end = ch.start + ch.n;
     const BatchDesc& B = batches[ch.bid];
     const u64 step = (u64)T * U;
+    // records in registers (W > 0): the next tile's loads are issued before this tile is ranked and
+    // stored, so the tile's three barriers do not each wait out a memory latency
+    RegRec<(W > 0 ? W : 1)> nx[UMAX];
+    auto load_tile = [&](u64 base) {
+        if constexpr (SRC == 1 && W > 0) {
+#pragma unroll
+            for (u32 u = 0; u < UMAX; ++u) {
+                const u64 i = base + (u64)u * T + threadIdx.x;
+                if (u >= U || i >= end) continue;
+                const u8* r = recs + i * rw;
+#pragma unroll
+                for (int w = 0; w < W; ++w) nx[u].r[w] = gld<u64>(r + 8 * w);
+            }
+        }
+    };
+    load_tile(ch.start);
     for (u64 base = ch.start; base < end; base += step) {
         u32 bk[UMAX], rk[UMAX];
         RegRec<(W > 0 ? W : 1)> rr[UMAX];
@@ -589,13 +610,10 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
         for (u32 u = 0; u < UMAX; ++u) {
             const u64 i = base + (u64)u * T + threadIdx.x;
             if (u >= U || threadIdx.x >= T || i >= end) continue;
-            if constexpr (SRC == 1 && W > 0) {
-                const u8* r = recs + i * rw;
-#pragma unroll
-                for (int w = 0; w < (W > 0 ? W : 1); ++w) rr[u].r[w] = gld<u64>(r + 8 * w);
-            }
+            if constexpr (SRC == 1 && W > 0) rr[u] = nx[u];
             m |= 1u << u;
         }
+        if (base + step < end) load_tile(base + step);
 #pragma unroll
         for (u32 u = 0; u < UMAX; ++u) {
             if (!((m >> u) & 1)) continue;
@@ -622,6 +640,10 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
             }
             bk[u] = (u32)(pp_mix(h) >> shift) & (K - 1);
             rk[u] = __hip_atomic_fetch_add(&hist[bk[u]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (KN) {
+                const u32 dn = (u32)(pp_mix(h) >> sh_next) & ((1u << kb_next) - 1);
+                __hip_atomic_fetch_add(&hn[(bk[u] << kb_next) | dn], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -645,21 +667,28 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
         }
         __syncthreads();
     }
+    // every unit of the next level is a whole destination partition: add this chunk's share
+    for (u32 i = threadIdx.x; i < KN; i += PP_NT) {
+        const u32 v = hn[i];
+        if (v) atomicAdd(cnt_next + (u64)ch.group * KN + i, v);
+    }
 }
 
 void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int src, int kind,
                        const u8* src_recs, const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, const u64* off,
-                       const u64* part_off, u8* dst) {
+                       const u64* part_off, u8* dst, u32* cnt_next, u32 sh_next, u32 kb_next) {
     if (!n_chunks) return;
     const u32 rw = kind ? hspec.pp_rw_state : hspec.pp_rw_raw;
     const u32 K = 1u << kbits;
     const u32 wpr = rw / 8;
     const int W = src == 0 ? 0 : (wpr == 1 ? 1 : wpr == 2 ? 2 : wpr == 4 ? 4 : wpr == 6 ? 6 : wpr == 8 ? 8 : 0);
+    if (src == 0 || (K << kb_next) > PP_NEXT_HIST_MAX) cnt_next = nullptr;  // host checks: never taken
     const size_t lds = 4 * (size_t)(K + (K & 1)) + 8 * (size_t)K +
-                       (W == 0 ? (size_t)pp_direct_t(rw) * pp_direct_u(0, rw) * rw : 0);
+                       (W == 0 ? (size_t)pp_direct_t(rw) * pp_direct_u(0, rw) * rw : 0) +
+                       (cnt_next ? 4 * ((size_t)K << kb_next) : 0);
 #define PP_SC(SR, WW)                                                                                                     \
     hipLaunchKernelGGL((pp_scatter_direct_kernel<SR, WW>), dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, \
-                       chunks, shift, kbits, off, part_off, dst)
+                       chunks, shift, kbits, off, part_off, dst, cnt_next, sh_next, kb_next)
     if (src == 0) {
         PP_SC(0, 0);
     } else {
