@@ -730,7 +730,7 @@ __device__ __forceinline__ bool pp_fast_pred(const PPFast& F, u64 v) {
     return apply_cmp(F.pcmp, o);
 }
 
-template <int COUNT, int W>
+template <int COUNT, int W, int NC>
 __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, const PPChunk* __restrict__ chunks, u32 shift,
                                                            u32* __restrict__ cnt, const u64* __restrict__ off,
                                                            const u64* __restrict__ part_off, u8* __restrict__ dst) {
@@ -745,19 +745,25 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
     }
     __syncthreads();
     const u64 end = ch.start + ch.n;
-    for (u64 base = ch.start; base < end; base += (u64)PP_NT * U) {
-        u64 v[U][8], pv[U];
+    const u64 step = (u64)PP_NT * U;
+    const u32 nload = COUNT ? F.nk : F.ncol;  // the count needs the key columns only
+    u64 v[U][NC], pv[U];
+    auto load = [&](u64 base) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const u64 i = base + (u64)u * PP_NT + threadIdx.x;
             const u64 ii = i < end ? i : ch.start;
 #pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if ((u32)c < F.ncol) v[u][c] = pp_ld_width(F.ptr[c], F.width[c], ii);
+            for (int c = 0; c < NC; ++c)
+                if ((u32)c < nload) v[u][c] = pp_ld_width(F.ptr[c], F.width[c], ii);
             pv[u] = F.has_pred ? pp_ld_width(F.pptr, F.pwidth, ii) : 0;
         }
-        u32 bk[U], rk[U], m = 0;
-        RegRec<W> rec[U];
+    };
+    u32 bk[U], rk[U], m = 0;
+    RegRec<W> rec[U];
+    // selection mask, bucket and (scatter) record of the tile at base from v / pv
+    auto assemble = [&](u64 base) {
+        m = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const u64 i = base + (u64)u * PP_NT + threadIdx.x;
@@ -767,8 +773,8 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
 #pragma unroll
             for (int k = 0; k < W; ++k) rec[u].r[k] = 0;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                if ((u32)c >= F.ncol) continue;
+            for (int c = 0; c < NC; ++c) {
+                if ((u32)c >= nload) continue;
                 u64 x = v[u][c];
                 if (F.type[c] == DBG_FLOAT32 || F.type[c] == DBG_FLOAT64) x = canon_float_bits(F.type[c], x);
                 if ((u32)c < F.nk) {
@@ -786,30 +792,47 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
             }
             bk[u] = (u32)(pp_mix(h) >> shift) & (K - 1);
         }
-        if (COUNT) {
+    };
+    if (COUNT) {
+        for (u64 base = ch.start; base < end; base += step) {
+            load(base);
+            assemble(base);
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if ((m >> u) & 1) atomicAdd(&hist[bk[u]], 1u);
-            continue;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if ((m >> u) & 1) rk[u] = atomicAdd(&hist[bk[u]], 1u);
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!((m >> u) & 1)) continue;
-            u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[bk[u]] + rk[u]) * (8 * F.wpr));
-#pragma unroll
-            for (int k = 0; k < W; ++k)
-                if ((u32)k < F.wpr) o[k] = rec[u].r[k];
+    } else {
+        // software pipeline: tile k + 1's column loads are in flight while tile k is ranked and
+        // stored (three barriers per tile would otherwise each sit behind a memory latency)
+        u64 base = ch.start;
+        if (base < end) {
+            load(base);
+            assemble(base);
         }
-        __syncthreads();
-        for (u32 b = threadIdx.x; b < K; b += PP_NT) {
-            run[b] += hist[b];
-            hist[b] = 0;
+        while (base < end) {
+            const u64 nb = base + step;
+            if (nb < end) load(nb);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if ((m >> u) & 1) rk[u] = atomicAdd(&hist[bk[u]], 1u);
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!((m >> u) & 1)) continue;
+                u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[bk[u]] + rk[u]) * (8 * F.wpr));
+#pragma unroll
+                for (int k = 0; k < W; ++k)
+                    if ((u32)k < F.wpr) o[k] = rec[u].r[k];
+            }
+            __syncthreads();
+            for (u32 b = threadIdx.x; b < K; b += PP_NT) {
+                run[b] += hist[b];
+                hist[b] = 0;
+            }
+            __syncthreads();
+            if (nb < end) assemble(nb);
+            base = nb;
         }
-        __syncthreads();
     }
     if (COUNT) {
         __syncthreads();
@@ -917,7 +940,16 @@ int launch_pp_l1_fast(hipStream_t s, const PPFast& F, int count, const PPChunk* 
         return 0;
     }
     const int W = F.wpr <= 1 ? 1 : F.wpr <= 2 ? 2 : F.wpr <= 4 ? 4 : F.wpr <= 6 ? 6 : 8;
-#define PP_L1F(C, WW) hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW>), dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, part_off, dst)
+    // columns held per row: 4 (the benchmark shapes) or all 8 — fewer VGPRs, more waves
+#define PP_L1F(C, WW)                                                                                                      \
+    do {                                                                                                                    \
+        if (F.ncol <= 4)                                                                                                    \
+            hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW, 4>), dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, \
+                               part_off, dst);                                                                              \
+        else                                                                                                                \
+            hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW, 8>), dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, \
+                               part_off, dst);                                                                              \
+    } while (0)
 #define PP_L1F_W(C)                      \
     switch (W) {                         \
         case 1: PP_L1F(C, 1); break;     \
@@ -1092,12 +1124,14 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     __shared__ u64 gbase;
     for (u32 s = threadIdx.x; s < cap; s += PP_AGG_NT) slots[(size_t)s * sw] = 0;
     if (threadIdx.x == 0) nlist = novf[0] = novf[1] = 0;
-    // Software pipeline over this workgroup's partitions p, p + G, p + 2G, ...: while partition p's
-    // group count is reserved and its groups are written, the first record tile of p + G is
-    // already being loaded into registers (its offsets were read one partition earlier, the
-    // offsets of p + 2G are read now), so a partition's inserts start on data in registers.
-    constexpr int AU = W > 0 ? (W <= 2 ? PP_AU : (W <= 4 ? 2 : 1)) : 1;  // records in flight within 128 VGPRs
-    RegRec<(W > 0 ? W : 1)> pre[AU];
+    // Software pipeline over this workgroup's partitions p, p + G, p + 2G, ...: the first record tile
+    // of a partition is loaded into registers two partitions ahead — buffer A serves p, p + 2G, ...,
+    // buffer B p + G, p + 3G, ... — and reloaded as soon as it is consumed, so a partition's inserts
+    // start on data that has had two partitions' worth of time to arrive (with one partition of
+    // lead time the insert phase still waited on its own records).  Tiles of AU x NT records: the
+    // final partitions hold ~0.45 x cap groups, fewer than 2 x NT for the usual record widths.
+    constexpr int AU = W > 0 ? (W <= 2 ? 2 : 1) : 1;
+    typedef RegRec<(W > 0 ? W : 1)> Tile[AU];
     auto part_range = [&](u32 q, u64& o0, u64& n) {
         o0 = (raw_off && q < n_parts) ? raw_off[q] : 0;
         n = (raw_off && q < n_parts) ? raw_off[q + 1] - o0 : 0;
@@ -1115,20 +1149,24 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
             }
         }
     };
-    u64 nx_r0, nx_nr, nn_r0, nn_nr;
-    part_range(blockIdx.x, nx_r0, nx_nr);
-    load_tile(pre, raw, nx_r0, nx_nr, 0);
-    part_range(blockIdx.x + gridDim.x, nn_r0, nn_nr);
+    Tile bufA, bufB;
+    u64 a_r0, a_nr, b_r0, b_nr;
+    part_range(blockIdx.x, a_r0, a_nr);
+    load_tile(bufA, raw, a_r0, a_nr, 0);
+    part_range(blockIdx.x + gridDim.x, b_r0, b_nr);
+    load_tile(bufB, raw, b_r0, b_nr, 0);
     __syncthreads();
     const bool tr = out.trace && (blockIdx.x & 63) == 0 && threadIdx.x == 0;
     u64 tm0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
-    for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
-        const u64 r0 = nx_r0, s0 = st_off ? st_off[p] : 0;
-        u64 nr = nx_nr, ns = st_off ? st_off[p + 1] - s0 : 0;
+    auto run_part = [&](u32 p, Tile& buf, u64& br0, u64& bnr) {
+        const u64 r0 = br0, s0 = st_off ? st_off[p] : 0;
+        u64 nr = bnr, ns = st_off ? st_off[p + 1] - s0 : 0;
         u8 *rin = raw, *rout = raw_alt, *sin = st, *sout = st_alt;
-        RegRec<(W > 0 ? W : 1)> cur[AU];
+        Tile cur;
 #pragma unroll
-        for (int u = 0; u < AU; ++u) cur[u] = pre[u];
+        for (int u = 0; u < AU; ++u) cur[u] = buf[u];
+        part_range(p + 2 * gridDim.x, br0, bnr);  // the buffer's next partition, loaded now
+        load_tile(buf, raw, br0, bnr, 0);
         for (int round = 0;; ++round) {
             auto raw_one = [&](const auto& rk) {
                 const u64 pm = pp_mix(pp_hash_of(S, rk));
@@ -1159,12 +1197,6 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
             if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 0, tm - tm0); tm0 = tm; }
             __syncthreads();
             if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 1, tm - tm0); tm0 = tm; }
-            if (round == 0) {  // prefetch: next partition's first tile, the one after's offsets
-                nx_r0 = nn_r0;
-                nx_nr = nn_nr;
-                load_tile(pre, raw, nx_r0, nx_nr, 0);
-                part_range(p + 2 * gridDim.x, nn_r0, nn_nr);
-            }
             if (threadIdx.x == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
             __syncthreads();
             if (tr) { const u64 tm = __builtin_amdgcn_s_memrealtime(); atomicAdd((unsigned long long*)out.trace + 2, tm - tm0); tm0 = tm; }
@@ -1203,6 +1235,10 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
             nr = o0;
             ns = o1;
         }
+    };
+    for (u32 p = blockIdx.x; p < n_parts; p += 2 * gridDim.x) {
+        run_part(p, bufA, a_r0, a_nr);
+        if (p + gridDim.x < n_parts) run_part(p + gridDim.x, bufB, b_r0, b_nr);  // uniform
     }
 }
 
