@@ -1104,7 +1104,8 @@ static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const 
         if (F && F->kind)
             launch_pp_l1_fast(h->stream, *F, 1, h->pp_dchunks, (u32)ch.size(), h->pp_cnt, nullptr, nullptr, nullptr);
         else
-            launch_pp_count(h->stream, h->dspec, h->dbatches, src, kind, recs, h->pp_dchunks, (u32)ch.size(), shift, kbits, h->pp_cnt);
+            launch_pp_count(h->stream, h->dspec, h->dbatches, src, kind, recs, h->pp_dchunks, (u32)ch.size(), shift, kbits, h->pp_cnt,
+                            (kind ? h->spec.pp_rw_state : h->spec.pp_rw_raw) / 8);
     }
     RETURN_IF(ensure_dev(&h->pp_scan_tmp, &h->pp_scan_tmp_cap, pp_scan_scratch_words((u32)(c0.size() - 1), kbits)));
     {

@@ -271,7 +271,7 @@ void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches
                       u64* set, u64 set_cap, u64* out);
 // level scatter: src = 0 raw batch rows (records built from the batch), 1 records of `src_recs`
 void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches, int src, int kind, const u8* src_recs,
-                     const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt);
+                     const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt, u32 wpr = 0);
 // off[unit][bucket]: relative start of the unit's run inside partition (group, bucket);
 // part_off[g * K + b]: partition starts (G * K + 1 words); scratch: pp_scan_scratch_words
 u64 pp_scan_scratch_words(u32 n_groups, u32 kbits);

@@ -305,11 +305,53 @@ void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches
     hipLaunchKernelGGL(pp_sample_stats_kernel, dim3(1024), dim3(256), 0, s, set, set_cap, out);
 }
 
+// A record as the aggregation reads it: W words held in registers (raw records of up to 64 bytes,
+// loaded PP_AU per thread before any LDS work so the loads overlap), or read from global memory
+// (wide raw records, state records).  word(w) / le(off, bytes) give little-endian fields.
+template <int W>
+struct RegRec {
+    u64 r[W];
+    __device__ __forceinline__ u64 word(u32 w) const {
+        u64 v = r[0];
+#pragma unroll
+        for (int k = 1; k < W; ++k)
+            if (w == (u32)k) v = r[k];
+        return v;
+    }
+    __device__ __forceinline__ u64 le(u32 off, u32 nb) const {
+        const u32 wi = off >> 3, sh = (off & 7) * 8;
+        u64 v = word(wi) >> sh;
+        if (sh && (off & 7) + nb > 8) v |= word(wi + 1) << (64 - sh);
+        return v & width_mask(nb);
+    }
+};
+struct GlbRec {
+    const u8* p;
+    __device__ __forceinline__ u64 word(u32 w) const { return gld<u64>(p + 8 * w); }
+    __device__ __forceinline__ u64 le(u32 off, u32 nb) const { return ld_le(p + off, nb); }
+};
+
+template <typename R>
+__device__ __forceinline__ u64 pp_hash_of(const Spec& S, const R& rk) {
+    if (S.pp_str) return rk.word(0);
+    u64 h = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const dbg_datatype& t = S.key_types[c];
+        u64 x;
+        const bool v = !t.nullable || rk.le(S.voff[c], 1) != 0;
+        if (!v) x = NULL_HASH_VAL;
+        else if (t.type == DBG_DECIMAL128) x = hash_i128(rk.le(S.koff[c], 8), rk.le(S.koff[c] + 8, 8));
+        else x = hash_bits(t.type, rk.le(S.koff[c], type_width(t.type)));
+        h = c == 0 ? x : (h * NULL_HASH_VAL) ^ x;
+    }
+    return h;
+}
+
 // ------------------------------------------------------------------------------------------
 // count: per work unit, a histogram of the level's local bucket over its (selected) rows/records
 // ------------------------------------------------------------------------------------------
 #define PP_CU 8  // rows / records per thread in flight (count)
-template <int SRC>
+template <int SRC, int W = 0>
 __global__ void __launch_bounds__(PP_NT) pp_count_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                         int kind, const u8* __restrict__ recs, const PPChunk* __restrict__ chunks,
                                                         u32 shift, u32 kbits, u32* __restrict__ cnt) {
@@ -332,6 +374,11 @@ __global__ void __launch_bounds__(PP_NT) pp_count_kernel(const Spec* __restrict_
             if (SRC == 0) {
                 if (!B.is_records && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
                 bk[u] = (u32)(pp_mix(pp_row_hash(S, B, i)) >> shift) & (K - 1);
+            } else if constexpr (W > 0) {  // records of W words: whole-word loads, key fields from registers
+                RegRec<(W > 0 ? W : 1)> rr;
+#pragma unroll
+                for (int w = 0; w < W; ++w) rr.r[w] = gld<u64>(recs + i * rw + 8 * w);
+                bk[u] = (u32)(pp_mix(pp_hash_of(S, rr)) >> shift) & (K - 1);
             } else {
                 bk[u] = (u32)(pp_mix(pp_rec_hash(S, recs + i * rw)) >> shift) & (K - 1);
             }
@@ -345,12 +392,19 @@ __global__ void __launch_bounds__(PP_NT) pp_count_kernel(const Spec* __restrict_
 }
 
 void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches, int src, int kind, const u8* src_recs,
-                     const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt) {
+                     const PPChunk* chunks, u32 n_chunks, u32 shift, u32 kbits, u32* cnt, u32 wpr) {
     if (!n_chunks) return;
-    if (src == 0)
+    if (src == 0) {
         hipLaunchKernelGGL(pp_count_kernel<0>, dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
+        return;
+    }
+    // raw records of 1 or 2 words (the fixed-key shapes): key fields from whole-word loads
+    if (wpr == 1)
+        hipLaunchKernelGGL((pp_count_kernel<1, 1>), dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
+    else if (wpr == 2)
+        hipLaunchKernelGGL((pp_count_kernel<1, 2>), dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
     else
-        hipLaunchKernelGGL(pp_count_kernel<1>, dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
+        hipLaunchKernelGGL((pp_count_kernel<1>), dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -496,48 +550,6 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* wtot, u32& total) {
     return pre + x - v;
 }
 
-// A record as the aggregation reads it: W words held in registers (raw records of up to 64 bytes,
-// loaded PP_AU per thread before any LDS work so the loads overlap), or read from global memory
-// (wide raw records, state records).  word(w) / le(off, bytes) give little-endian fields.
-template <int W>
-struct RegRec {
-    u64 r[W];
-    __device__ __forceinline__ u64 word(u32 w) const {
-        u64 v = r[0];
-#pragma unroll
-        for (int k = 1; k < W; ++k)
-            if (w == (u32)k) v = r[k];
-        return v;
-    }
-    __device__ __forceinline__ u64 le(u32 off, u32 nb) const {
-        const u32 wi = off >> 3, sh = (off & 7) * 8;
-        u64 v = word(wi) >> sh;
-        if (sh && (off & 7) + nb > 8) v |= word(wi + 1) << (64 - sh);
-        return v & width_mask(nb);
-    }
-};
-struct GlbRec {
-    const u8* p;
-    __device__ __forceinline__ u64 word(u32 w) const { return gld<u64>(p + 8 * w); }
-    __device__ __forceinline__ u64 le(u32 off, u32 nb) const { return ld_le(p + off, nb); }
-};
-
-template <typename R>
-__device__ __forceinline__ u64 pp_hash_of(const Spec& S, const R& rk) {
-    if (S.pp_str) return rk.word(0);
-    u64 h = 0;
-    for (int c = 0; c < S.n_keys; ++c) {
-        const dbg_datatype& t = S.key_types[c];
-        u64 x;
-        const bool v = !t.nullable || rk.le(S.voff[c], 1) != 0;
-        if (!v) x = NULL_HASH_VAL;
-        else if (t.type == DBG_DECIMAL128) x = hash_i128(rk.le(S.koff[c], 8), rk.le(S.koff[c] + 8, 8));
-        else x = hash_bits(t.type, rk.le(S.koff[c], type_width(t.type)));
-        h = c == 0 ? x : (h * NULL_HASH_VAL) ^ x;
-    }
-    return h;
-}
-
 // Direct scatter (the form every level runs): per tile of T x U rows, each selected row's bucket
 // and its rank in the bucket (one LDS atomic) give its destination run[bucket] + rank, and the
 // record is stored straight there — from registers (records of W words, W > 0) or from a
@@ -555,14 +567,38 @@ __host__ __device__ __forceinline__ u32 pp_direct_u(int W, u32 rw) {  // rows pe
     return u >= 4 ? 4 : (u >= 1 ? u : 1);
 }
 
+// Exclusive scan of a tile histogram (K <= 1024 buckets) by wave 0 into toff; *total = sum.
+__device__ __forceinline__ void pp_tile_scan(const l32* hist, u32 K, l32* toff, l32* total) {
+    if (threadIdx.x >= 64) return;
+    const u32 per = (K + 63) / 64, b0 = threadIdx.x * per;
+    u32 t = 0;
+    for (u32 j = 0; j < per; ++j)
+        if (b0 + j < K) t += hist[b0 + j];
+    u32 incl = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(incl, d);
+        if ((int)threadIdx.x >= d) incl += y;
+    }
+    u32 e = incl - t;
+    for (u32 j = 0; j < per; ++j)
+        if (b0 + j < K) {
+            const u32 c = hist[b0 + j];
+            toff[b0 + j] = e;
+            e += c;
+        }
+    if (threadIdx.x == 63) *total = incl;
+}
+
 template <int SRC, int W>
 __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                  int kind, const u8* __restrict__ recs,
                                                                  const PPChunk* __restrict__ chunks, u32 shift, u32 kbits,
                                                                  const u64* __restrict__ off, const u64* __restrict__ part_off,
                                                                  u8* __restrict__ dst, u32* __restrict__ cnt_next, u32 sh_next,
-                                                                 u32 kb_next) {
+                                                                 u32 kb_next, int sorted) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    __shared__ u32 tile_total;
     const Spec& S = *spec;
     const u32 K = 1u << kbits;
     const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
@@ -582,6 +618,11 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
     const u32 KN = cnt_next ? K << kb_next : 0;
     l32* hn = (l32*)(scratch + (W == 0 ? (size_t)T * U * rw : 0));
     for (u32 i = threadIdx.x; i < KN; i += PP_NT) hn[i] = 0;
+    // tile-sorted stores (records in registers, `sorted`): as pp_l1_fixed_kernel — staged words
+    // [T * U * W] u64 | bucket per staged record [T * U] u16 | tile offsets [K] u32
+    l64* stage = (l64*)(hn + KN + (KN & 1));
+    l16* sbk = (l16*)(stage + (size_t)T * U * (W > 0 ? W : 1));
+    l32* toff = (l32*)(sbk + (size_t)T * U + ((T * U) & 1));
     __syncthreads();
     const u64 end = ch.start + ch.n;
     const BatchDesc& B = batches[ch.bid];
@@ -646,18 +687,40 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
             }
         }
         __syncthreads();
+        if (SRC == 1 && W > 0 && sorted) {  // wpr == W here
+            pp_tile_scan(hist, K, toff, (l32*)&tile_total);
+            __syncthreads();
 #pragma unroll
-        for (u32 u = 0; u < UMAX; ++u) {
-            if (!((m >> u) & 1)) continue;
-            const u64 di = run[bk[u]] + rk[u];
-            u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + di * rw);
-            if constexpr (SRC == 1 && W > 0) {
+            for (u32 u = 0; u < UMAX; ++u) {
+                if (!((m >> u) & 1)) continue;
+                const u32 pos = toff[bk[u]] + rk[u];
 #pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if ((u32)w < wpr) o[w] = rr[u].r[w];
-            } else {
-                const l64* s = (const l64*)(scratch + ((size_t)threadIdx.x * U + u) * rw);
-                for (u32 w = 0; w < wpr; ++w) o[w] = s[w];
+                for (int w = 0; w < (W > 0 ? W : 1); ++w) stage[(size_t)pos * (W > 0 ? W : 1) + w] = rr[u].r[w];
+                sbk[pos] = (u16)bk[u];
+            }
+            __syncthreads();
+            constexpr u32 WW = W > 0 ? W : 1;
+            const u32 nw = tile_total * WW;
+            for (u32 q = threadIdx.x; q < nw; q += PP_NT) {
+                const u32 j = q / WW, w = q - j * WW;
+                const u32 b = sbk[j];
+                u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[b] + (j - toff[b])) * rw);
+                o[w] = stage[q];
+            }
+        } else {
+#pragma unroll
+            for (u32 u = 0; u < UMAX; ++u) {
+                if (!((m >> u) & 1)) continue;
+                const u64 di = run[bk[u]] + rk[u];
+                u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + di * rw);
+                if constexpr (SRC == 1 && W > 0) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        if ((u32)w < wpr) o[w] = rr[u].r[w];
+                } else {
+                    const l64* s = (const l64*)(scratch + ((size_t)threadIdx.x * U + u) * rw);
+                    for (u32 w = 0; w < wpr; ++w) o[w] = s[w];
+                }
             }
         }
         __syncthreads();
@@ -683,12 +746,18 @@ void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, cons
     const u32 wpr = rw / 8;
     const int W = src == 0 ? 0 : (wpr == 1 ? 1 : wpr == 2 ? 2 : wpr == 4 ? 4 : wpr == 6 ? 6 : wpr == 8 ? 8 : 0);
     if (src == 0 || (K << kb_next) > PP_NEXT_HIST_MAX) cnt_next = nullptr;  // host checks: never taken
+    static const bool unsorted = getenv("DBG_X_UNSORTED") != nullptr;  // EXPERIMENT (A/B of the tile-sorted stores)
+    // only wide fanouts: with few buckets a tile's runs are long already and the staging LDS costs
+    // occupancy (level 3 at 32 buckets: 9.3 -> 10.3 ms sorted, C4)
+    const int sorted = (src == 1 && W > 0 && K >= 128 && !unsorted) ? 1 : 0;
+    const size_t KN = cnt_next ? ((size_t)K << kb_next) : 0;
+    const size_t TU = (size_t)PP_NT * pp_direct_u(W, rw);
     const size_t lds = 4 * (size_t)(K + (K & 1)) + 8 * (size_t)K +
-                       (W == 0 ? (size_t)pp_direct_t(rw) * pp_direct_u(0, rw) * rw : 0) +
-                       (cnt_next ? 4 * ((size_t)K << kb_next) : 0);
+                       (W == 0 ? (size_t)pp_direct_t(rw) * pp_direct_u(0, rw) * rw : 0) + 4 * (KN + (KN & 1)) +
+                       (sorted ? TU * W * 8 + 2 * (TU + (TU & 1)) + 4 * (size_t)K : 0);
 #define PP_SC(SR, WW)                                                                                                     \
     hipLaunchKernelGGL((pp_scatter_direct_kernel<SR, WW>), dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, \
-                       chunks, shift, kbits, off, part_off, dst, cnt_next, sh_next, kb_next)
+                       chunks, shift, kbits, off, part_off, dst, cnt_next, sh_next, kb_next, sorted)
     if (src == 0) {
         PP_SC(0, 0);
     } else {
@@ -730,14 +799,29 @@ __device__ __forceinline__ bool pp_fast_pred(const PPFast& F, u64 v) {
     return apply_cmp(F.pcmp, o);
 }
 
+// Tile-sorted stores (scatter, `sorted`): the tile's records are placed in LDS in bucket order
+// (exclusive scan of the tile histogram + each record's rank) and written back by consecutive
+// threads, so consecutive lanes store consecutive 8-byte words of one bucket's run — whole lines
+// per wave instead of 64 scattered records per store instruction.  LDS (dynamic): staged words
+// [NT * U * W] u64 | bucket of each staged record [NT * U] u16 | tile offsets [K] u32.
+__host__ __device__ constexpr int pp_l1_u(int W) { return W <= 2 ? 4 : (W <= 4 ? 2 : 1); }
+__host__ __device__ constexpr size_t pp_l1_sorted_lds(int W) {
+    return (size_t)PP_NT * pp_l1_u(W) * W * 8 + (size_t)PP_NT * pp_l1_u(W) * 2 + 4 * (1u << PP_L1_BITS);
+}
+
 template <int COUNT, int W, int NC>
 __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, const PPChunk* __restrict__ chunks, u32 shift,
                                                            u32* __restrict__ cnt, const u64* __restrict__ off,
-                                                           const u64* __restrict__ part_off, u8* __restrict__ dst) {
+                                                           const u64* __restrict__ part_off, u8* __restrict__ dst, int sorted) {
     constexpr u32 K = 1u << PP_L1_BITS;
-    constexpr int U = W <= 2 ? 4 : (W <= 4 ? 2 : 1);
+    constexpr int U = pp_l1_u(W);
     __shared__ u32 hist[K];
     __shared__ u64 run[K];
+    __shared__ u32 hist_total_;
+    extern __shared__ __attribute__((aligned(16))) u64 l1_dyn[];
+    l64* stage = (l64*)l1_dyn;
+    l16* sbk = (l16*)(stage + (size_t)PP_NT * U * W);
+    l32* toff = (l32*)(sbk + (size_t)PP_NT * U);
     const PPChunk ch = chunks[blockIdx.x];
     for (u32 b = threadIdx.x; b < K; b += PP_NT) {
         hist[b] = 0;
@@ -816,13 +900,57 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
             for (int u = 0; u < U; ++u)
                 if ((m >> u) & 1) rk[u] = atomicAdd(&hist[bk[u]], 1u);
             __syncthreads();
+            if (sorted) {
+                if (threadIdx.x < 64) {  // wave 0: exclusive scan of the K-bucket tile histogram
+                    constexpr u32 PER = K / 64;
+                    u32 c[PER], t = 0;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!((m >> u) & 1)) continue;
-                u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[bk[u]] + rk[u]) * (8 * F.wpr));
+                    for (u32 j = 0; j < PER; ++j) {
+                        c[j] = hist[threadIdx.x * PER + j];
+                        t += c[j];
+                    }
+                    u32 incl = t;
 #pragma unroll
-                for (int k = 0; k < W; ++k)
-                    if ((u32)k < F.wpr) o[k] = rec[u].r[k];
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const u32 y = __shfl_up(incl, d);
+                        if ((int)threadIdx.x >= d) incl += y;
+                    }
+                    u32 e = incl - t;
+#pragma unroll
+                    for (u32 j = 0; j < PER; ++j) {
+                        toff[threadIdx.x * PER + j] = e;
+                        e += c[j];
+                    }
+                    if (threadIdx.x == 63) hist_total_ = incl;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!((m >> u) & 1)) continue;
+                    const u32 pos = toff[bk[u]] + rk[u];
+#pragma unroll
+                    for (int k = 0; k < W; ++k) stage[(size_t)pos * W + k] = rec[u].r[k];
+                    sbk[pos] = (u16)bk[u];
+                }
+                __syncthreads();
+                // word q of the tile's staged records -> consecutive threads, consecutive words
+                const u32 nw = hist_total_ * F.wpr;
+                for (u32 q = threadIdx.x; q < nw; q += PP_NT) {
+                    const u32 j = q / F.wpr, k = q - j * F.wpr;
+                    const u32 b = sbk[j];
+                    u64 __attribute__((address_space(1)))* o =
+                        (u64 __attribute__((address_space(1)))*)(dst + (run[b] + (j - toff[b])) * (8 * F.wpr));
+                    o[k] = stage[(size_t)j * W + k];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!((m >> u) & 1)) continue;
+                    u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + (run[bk[u]] + rk[u]) * (8 * F.wpr));
+#pragma unroll
+                    for (int k = 0; k < W; ++k)
+                        if ((u32)k < F.wpr) o[k] = rec[u].r[k];
+                }
             }
             __syncthreads();
             for (u32 b = threadIdx.x; b < K; b += PP_NT) {
@@ -941,14 +1069,16 @@ int launch_pp_l1_fast(hipStream_t s, const PPFast& F, int count, const PPChunk* 
     }
     const int W = F.wpr <= 1 ? 1 : F.wpr <= 2 ? 2 : F.wpr <= 4 ? 4 : F.wpr <= 6 ? 6 : 8;
     // columns held per row: 4 (the benchmark shapes) or all 8 — fewer VGPRs, more waves
-#define PP_L1F(C, WW)                                                                                                      \
-    do {                                                                                                                    \
-        if (F.ncol <= 4)                                                                                                    \
-            hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW, 4>), dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, \
-                               part_off, dst);                                                                              \
-        else                                                                                                                \
-            hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW, 8>), dim3(n_chunks), dim3(PP_NT), 0, s, F, chunks, shift, cnt, off, \
-                               part_off, dst);                                                                              \
+    static const int sorted = getenv("DBG_X_UNSORTED") ? 0 : 1;  // EXPERIMENT (A/B of the tile-sorted stores)
+    const size_t dyn = (count || !sorted) ? 0 : pp_l1_sorted_lds(W);
+#define PP_L1F(C, WW)                                                                                                        \
+    do {                                                                                                                      \
+        if (F.ncol <= 4)                                                                                                      \
+            hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW, 4>), dim3(n_chunks), dim3(PP_NT), dyn, s, F, chunks, shift, cnt, off, \
+                               part_off, dst, sorted);                                                                        \
+        else                                                                                                                  \
+            hipLaunchKernelGGL((pp_l1_fixed_kernel<C, WW, 8>), dim3(n_chunks), dim3(PP_NT), dyn, s, F, chunks, shift, cnt, off, \
+                               part_off, dst, sorted);                                                                        \
     } while (0)
 #define PP_L1F_W(C)                      \
     switch (W) {                         \
