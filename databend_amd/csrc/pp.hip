@@ -590,13 +590,13 @@ __device__ __forceinline__ void pp_tile_scan(const l32* hist, u32 K, l32* toff, 
     if (threadIdx.x == 63) *total = incl;
 }
 
-template <int SRC, int W>
+template <int SRC, int W, int SORTED>
 __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                  int kind, const u8* __restrict__ recs,
                                                                  const PPChunk* __restrict__ chunks, u32 shift, u32 kbits,
                                                                  const u64* __restrict__ off, const u64* __restrict__ part_off,
                                                                  u8* __restrict__ dst, u32* __restrict__ cnt_next, u32 sh_next,
-                                                                 u32 kb_next, int sorted) {
+                                                                 u32 kb_next) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     __shared__ u32 tile_total;
     const Spec& S = *spec;
@@ -687,7 +687,7 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
             }
         }
         __syncthreads();
-        if (SRC == 1 && W > 0 && sorted) {  // wpr == W here
+        if constexpr (SRC == 1 && W > 0 && SORTED) {  // wpr == W here
             pp_tile_scan(hist, K, toff, (l32*)&tile_total);
             __syncthreads();
 #pragma unroll
@@ -755,21 +755,27 @@ void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, cons
     const size_t lds = 4 * (size_t)(K + (K & 1)) + 8 * (size_t)K +
                        (W == 0 ? (size_t)pp_direct_t(rw) * pp_direct_u(0, rw) * rw : 0) + 4 * (KN + (KN & 1)) +
                        (sorted ? TU * W * 8 + 2 * (TU + (TU & 1)) + 4 * (size_t)K : 0);
-#define PP_SC(SR, WW)                                                                                                     \
-    hipLaunchKernelGGL((pp_scatter_direct_kernel<SR, WW>), dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, \
-                       chunks, shift, kbits, off, part_off, dst, cnt_next, sh_next, kb_next, sorted)
+#define PP_SC(SR, WW, SO)                                                                                                     \
+    hipLaunchKernelGGL((pp_scatter_direct_kernel<SR, WW, SO>), dim3(n_chunks), dim3(PP_NT), lds, s, dspec, batches, kind, src_recs, \
+                       chunks, shift, kbits, off, part_off, dst, cnt_next, sh_next, kb_next)
+#define PP_SC2(WW)                   \
+    do {                             \
+        if (sorted) PP_SC(1, WW, 1); \
+        else PP_SC(1, WW, 0);        \
+    } while (0)
     if (src == 0) {
-        PP_SC(0, 0);
+        PP_SC(0, 0, 0);
     } else {
         switch (W) {
-            case 1: PP_SC(1, 1); break;
-            case 2: PP_SC(1, 2); break;
-            case 4: PP_SC(1, 4); break;
-            case 6: PP_SC(1, 6); break;
-            case 8: PP_SC(1, 8); break;
-            default: PP_SC(1, 0); break;
+            case 1: PP_SC2(1); break;
+            case 2: PP_SC2(2); break;
+            case 4: PP_SC2(4); break;
+            case 6: PP_SC2(6); break;
+            case 8: PP_SC2(8); break;
+            default: PP_SC(1, 0, 0); break;
         }
     }
+#undef PP_SC2
 #undef PP_SC
 }
 
