@@ -1230,7 +1230,7 @@ static int pp_prepare(dbg_agg_handle* h) {
             HIPCHECK(hipStreamSynchronize(h->stream));
             u64 mx = 0;
             for (u64 g2 = 0; g2 < G2; ++g2) mx = std::max<u64>(mx, h->pp_hpart[g2 + 1] - h->pp_hpart[g2]);
-            fused3 = mx <= PP_CHUNK && ((1u << k2) << k3) <= PP_NEXT_HIST_MAX && !getenv("DBG_X_NOFUSE3");
+            fused3 = mx <= PP_CHUNK && ((1u << k2) << k3) <= PP_NEXT_HIST_MAX;
             if (fused3) {
                 RETURN_IF(ensure_dev(&h->pp_cnt, &h->pp_cnt_cap, G2 << k3));
                 HIPCHECK(hipMemsetAsync(h->pp_cnt, 0, (G2 << k3) * 4, h->stream));
@@ -1397,8 +1397,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
         return DBG_OK;
     }
     RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
-    static const bool x_nofuse = getenv("DBG_X_NOFUSE") != nullptr;  // EXPERIMENT
-    if (!x_nofuse && on_device && h->recycle && h->hcounters_dev && insert_can_fuse(S, *st, h->cap)) {  // held back: see def_on
+    if (on_device && h->recycle && h->hcounters_dev && insert_can_fuse(S, *st, h->cap)) {  // held back: see def_on
         h->def_on = true;
         h->def_bid = bid;
         h->def_rows = rows;

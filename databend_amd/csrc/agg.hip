@@ -1361,8 +1361,7 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
     const int nt = 1024;
     static_assert(FIN_NT == 1024, "the fused finalize runs on the insert's workgroup");
-    static const u64 xb = getenv("DBG_X_BLOCKS") ? strtoull(getenv("DBG_X_BLOCKS"), nullptr, 10) : 256;  // EXPERIMENT
-    const u64 max_blocks = xb;  // one 1024-lane workgroup per CU
+    const u64 max_blocks = 256;  // one 1024-lane workgroup per CU
     size_t shmem = fast_shmem(table_bytes);
     FusedFin ff;
     if (fused) ff = *fused;

@@ -746,10 +746,9 @@ void launch_pp_scatter(hipStream_t s, const Spec* dspec, const Spec& hspec, cons
     const u32 wpr = rw / 8;
     const int W = src == 0 ? 0 : (wpr == 1 ? 1 : wpr == 2 ? 2 : wpr == 4 ? 4 : wpr == 6 ? 6 : wpr == 8 ? 8 : 0);
     if (src == 0 || (K << kb_next) > PP_NEXT_HIST_MAX) cnt_next = nullptr;  // host checks: never taken
-    static const bool unsorted = getenv("DBG_X_UNSORTED") != nullptr;  // EXPERIMENT (A/B of the tile-sorted stores)
     // only wide fanouts: with few buckets a tile's runs are long already and the staging LDS costs
     // occupancy (level 3 at 32 buckets: 9.3 -> 10.3 ms sorted, C4)
-    const int sorted = (src == 1 && W > 0 && K >= 128 && !unsorted) ? 1 : 0;
+    const int sorted = (src == 1 && W > 0 && K >= 128) ? 1 : 0;
     const size_t KN = cnt_next ? ((size_t)K << kb_next) : 0;
     const size_t TU = (size_t)PP_NT * pp_direct_u(W, rw);
     const size_t lds = 4 * (size_t)(K + (K & 1)) + 8 * (size_t)K +
@@ -1075,8 +1074,8 @@ int launch_pp_l1_fast(hipStream_t s, const PPFast& F, int count, const PPChunk* 
     }
     const int W = F.wpr <= 1 ? 1 : F.wpr <= 2 ? 2 : F.wpr <= 4 ? 4 : F.wpr <= 6 ? 6 : 8;
     // columns held per row: 4 (the benchmark shapes) or all 8 — fewer VGPRs, more waves
-    static const int sorted = getenv("DBG_X_UNSORTED") ? 0 : 1;  // EXPERIMENT (A/B of the tile-sorted stores)
-    const size_t dyn = (count || !sorted) ? 0 : pp_l1_sorted_lds(W);
+    const int sorted = 1;  // tile-sorted stores (C4 level 1: 26.5 -> 16.0 ms)
+    const size_t dyn = count ? 0 : pp_l1_sorted_lds(W);
 #define PP_L1F(C, WW)                                                                                                        \
     do {                                                                                                                      \
         if (F.ncol <= 4)                                                                                                      \
