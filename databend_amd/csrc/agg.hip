@@ -733,7 +733,9 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
                                                              TableDesc t, const u64* pos, const u64* str_pos, u64 nblocks,
                                                              OutDesc out) {
     const Spec& S = *spec;
-    __shared__ u64 wsum[BLOCK / 64][1 + DBG_MAX_KEYS];
+    // double-buffered per-wave sums: iteration k writes buffer k & 1, so one barrier per iteration
+    // orders both its reads and the next iteration's writes
+    __shared__ u64 wsum2[2][BLOCK / 64][1 + DBG_MAX_KEYS];
     const bool ref_strings = S.has_strings && !S.inline_keys;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 base = (u64)blockIdx.x * SLOTS_PER_BLOCK;
@@ -749,15 +751,24 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
         }
         return v;
     };
+    // the next iteration's entry is loaded before this iteration's barrier
+    auto entry_at = [&](u32 k) -> u64 {
+        const u64 s = base + (u64)k * BLOCK + threadIdx.x;
+        return s <= t.cap ? t.slots[s * t.stride_words] : SLOT_EMPTY;
+    };
+    u64 e_next = entry_at(0);
     for (u32 k = 0; k < SLOTS_PER_THREAD; ++k) {
         if (base + (u64)k * BLOCK > t.cap) break;  // uniform
+        u64 (*wsum)[1 + DBG_MAX_KEYS] = wsum2[k & 1];
         const u64 s = base + (u64)k * BLOCK + threadIdx.x;
         const bool in = s <= t.cap;
         const u64* st = t.slots + (in ? s : 0) * t.stride_words;
-        const u64 e = in ? st[0] : SLOT_EMPTY;
+        const u64 e = e_next;
+        if (k + 1 < SLOTS_PER_THREAD) e_next = entry_at(k + 1);
         const u64 cnt = e != SLOT_EMPTY ? 1 : 0;
         u64 sb[DBG_MAX_KEYS];
-        const u64 ic = wave_incl(cnt);
+        // inclusive count within the wave from one ballot (cnt is 0 / 1)
+        const u64 ic = (u64)__popcll(__ballot(cnt != 0) & (lane == 63 ? ~0ULL : ((2ULL << lane) - 1)));
         if (lane == 63) wsum[wave][0] = ic;
         if (ref_strings)
             for (int c = 0; c < S.n_keys; ++c) {
@@ -783,7 +794,6 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
                 }
                 srun[c] += stot;
             }
-        __syncthreads();
         run += tot;
         if (cnt && p < out.cap_groups) write_group(S, batches, t, s, st, e, p, sp, out);
     }
