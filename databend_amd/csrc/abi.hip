@@ -957,7 +957,7 @@ extern "C" {
 
 #define PP_MIN_ROWS (1ULL << 22)
 #define PP_MIN_GROUPS (1ULL << 20)
-#define PP_SET_CAP (1ULL << 22)
+#define PP_SET_CAP (1ULL << 21)  // 2^20 samples at most: <= 50 % load
 
 // Cardinality probe of the first batch into an empty handle (AggregateHashTable decides its
 // partial strategy by observed cardinality too: clear_ht / maybe_repartition,
