@@ -45,6 +45,10 @@ def parse():
                    help="aggregation strategy of the tables (dbg_agg_set_strategy); auto = the cardinality probe")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher plumbing only: every rank joins a gloo group, rank 0 prints n_gpus (no GPU work)")
+    p.add_argument("--extra-configs", default=None,
+                   help="comma list of further configs timed in the same run (single GPU), reported under 'configs' "
+                        "(default: 1,3,4,5 with the headline config 2 at N=1; none otherwise; 'none' disables)")
+    p.add_argument("--extra-steps", type=int, default=3)
     p.add_argument("--scaling", choices=["weak", "strong"], default=None,
                    help="weak: every GPU aggregates the config's rows; strong: the config's rows are split over "
                         "the GPUs (default: strong for the 1B-row configs 3-5, weak for 1-2)")
@@ -101,6 +105,79 @@ def spawn_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.run(cmd, env=env).returncode
+
+
+def load_traffic(cfg):
+    """PMC-measured HBM bytes per step / launch (scripts/pmc_step_traffic.py, profiles/)."""
+    tf = os.path.join(ROOT, "profiles", f"pmc_traffic_c{cfg}.json")
+    if not os.path.exists(tf):
+        return None, None
+    try:
+        t = json.load(open(tf))
+        return t.get("hbm_bytes_per_launch"), os.path.relpath(tf, ROOT)
+    except Exception:
+        return None, None
+
+
+def measure_extra(cfg, steps, warmup, with_cpu):
+    """One more configuration at its full size on this GPU (single rank): the same step as the
+    headline (reset -> fused filter + GROUP BY -> finalize into HBM result columns), timed over
+    `steps` steps after `warmup`, its roofline over the whole step's kernels (from
+    the first launch to result columns in HBM), and the CPU baseline on a bounded sample."""
+    import torch
+    from databend_amd import ffi
+    from databend_amd.workloads import DEFAULT_ROWS, SHAPES, ConfigRunner, algorithmic_bytes
+    rows = DEFAULT_ROWS[cfg]
+    shape = SHAPES[cfg]
+    copies = 2 if cfg == 1 else 1  # C1's 600 MB would sit in the 256 MiB L3 less than twice over
+    runner = ConfigRunner(cfg, rows, copies=copies)
+    try:
+        for k in range(warmup):
+            runner.step(k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            runner.step(warmup + k)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ffi.prof_reset()
+        ffi.prof_enable(True)
+        for k in range(steps):
+            runner.step(warmup + steps + k)
+        torch.cuda.synchronize()
+        ffi.prof_enable(False)
+        prof = ffi.prof_read()
+        step_kernel_ms = sum(v[0] for v in prof.values()) / steps
+        n_groups = runner.n_groups
+        ci = next((i for i, (f, c) in enumerate(shape.aggs) if f == "count" and c is None), None)
+        sel = int(runner.out_aggs[ci].data[: 8 * n_groups].view(torch.int64).sum().item()) if ci is not None else rows
+        alg = algorithmic_bytes(cfg, runner.inputs[0], rows, sel, n_groups, runner.result_types, runner.key_string_bytes)
+        achieved = alg / (step_kernel_ms * 1e-3) / 1e9 if step_kernel_ms > 0 else 0.0
+        traffic, tsrc = load_traffic(cfg)
+        partitioned = runner.table.strategy()[0]
+        dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
+        rec = {
+            "workload": shape.name, "query": shape.sql, "rows": rows, "groups": n_groups, "selected_rows": sel,
+            "strategy": "partitioned" if partitioned else "hbm_table",
+            "steps": steps, "warmup": warmup, "ms_per_step": elapsed / steps * 1e3, "rows_per_s": rows * steps / elapsed,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": "step (every kernel of one step)", "kernel_avg_ms": step_kernel_ms,
+                         "algorithmic_bytes_per_launch": alg,
+                         "traffic_over_algorithmic": traffic / alg if traffic else None},
+            "dominant_kernel": dom,
+            "kernels_ms_per_step": {k: v[0] / steps for k, v in prof.items()},
+        }
+    finally:
+        runner.close()
+        del runner
+        torch.cuda.empty_cache()
+    if with_cpu:
+        sample = {1: 6_001_215, 3: 20_000_000, 4: 10_000_000, 5: 20_000_000}[cfg]
+        cb, _, _ = cpu_baseline(cfg, sample)
+        rec["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        rec["gpu_vs_cpu"] = rec["rows_per_s"] / cb["value"]
+    return rec
 
 
 def main():
@@ -296,14 +373,10 @@ def main():
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
     }
     # measured PMC traffic (rocprofv3 --pmc, committed under profiles/) if present for this config
-    tf = os.path.join(ROOT, "profiles", f"pmc_traffic_c{cfg}.json")
-    if os.path.exists(tf):
-        try:
-            t = json.load(open(tf))
-            out["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
-            out["roofline"]["traffic_source"] = os.path.relpath(tf, ROOT)
-        except Exception:
-            pass
+    traffic, tsrc = load_traffic(cfg)
+    if traffic:
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic_source"] = tsrc
     # The ORDER BY <count> DESC LIMIT 10 that ends the ClickBench query, on the device result
     # (untimed leg, reported beside the step; dbg_sort_limit_indices).
     if world == 1 and n_groups > 0:
@@ -339,6 +412,23 @@ def main():
                 out["parity_vs_cpu"] = "bit-exact"
             except AssertionError as e:
                 out["parity_vs_cpu"] = f"MISMATCH: {e}"
+    # the other configurations of BASELINE.json, each at full size on this GPU, in the same run
+    extra = args.extra_configs
+    if extra is None:
+        extra = "1,3,4,5" if (world == 1 and cfg == 2 and not args.rows) else "none"
+    if world == 1 and extra != "none":
+        runner.close()
+        del runner
+        torch.cuda.empty_cache()
+        out["configs"] = {}
+        for c in [int(x) for x in extra.split(",") if x.strip()]:
+            if c == cfg:
+                continue
+            try:
+                out["configs"][f"C{c}"] = measure_extra(c, args.extra_steps, 1, not args.no_cpu_baseline)
+            except Exception as e:  # reported, never hidden: the headline line still prints
+                out["configs"][f"C{c}"] = {"error": f"{type(e).__name__}: {e}"}
+            print(f"bench.py: C{c} done", file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -30,12 +30,19 @@ class AggregateFunction:
     kind: int
     arg: Optional[DataType]  # None => count(*)
     or_null: bool = True
+    # AggregateDistinctCombinator over the nested kind (suffix "_distinct",
+    # FUN/aggregate_combinator_distinct.rs): run by databend_amd.distinct.DistinctAggregator
+    distinct: bool = False
 
     def name(self) -> str:
         # AggregateCountFunction reports its struct name (FUN/aggregate_count.rs:69-71)
         return "AggregateCountFunction" if self.kind == abi.AGG_COUNT else self.display_name
 
     def to_abi(self) -> abi.dbg_agg_spec:
+        if self.distinct:
+            from .ffi import Unsupported
+            raise Unsupported(abi.DBG_ERR_UNSUPPORTED, f"{self.display_name}: a DISTINCT aggregate is not one table "
+                              "state; run it with databend_amd.distinct.DistinctAggregator")
         s = abi.dbg_agg_spec()
         s.kind = self.kind
         if self.arg is None:
@@ -47,6 +54,9 @@ class AggregateFunction:
 
     def return_type(self) -> DataType:
         from .ffi import lib, check
+        if self.distinct:  # the combinator returns the nested function's type (:60-62)
+            from dataclasses import replace
+            return replace(self, distinct=False, arg=self.arg.wrap_nullable() if self.arg else None).return_type()
         out = abi.dbg_datatype()
         spec = self.to_abi()
         check(lib().dbg_agg_result_type(abi.C.byref(spec), abi.C.byref(out)))
@@ -69,6 +79,11 @@ class AggregateFunctionFactory:
 
     def get_or_null(self, name: str, params: Sequence, arguments: Sequence[DataType], or_null: bool) -> AggregateFunction:
         lname = name.lower()
+        distinct = lname.endswith("_distinct") and lname != "sql_avg_distinct"
+        if distinct:  # the combinator suffix (FUN/aggregate_function_factory.rs: combinator_desc)
+            lname = lname[: -len("_distinct")]
+            if not arguments:
+                raise ValueError(f"{name} requires an argument")
         if lname not in _KINDS:
             raise NotImplementedError(f"Unsupported AggregateFunction on the GPU path: {name}")
         if len(arguments) > 1:
@@ -76,4 +91,4 @@ class AggregateFunctionFactory:
         arg = arguments[0] if arguments else None
         if lname != "count" and arg is None:
             raise ValueError(f"{name} requires one argument")
-        return AggregateFunction(name, _KINDS[lname], arg, or_null)
+        return AggregateFunction(name, _KINDS[lname], arg, or_null, distinct)

@@ -36,6 +36,7 @@ class AggregatorParams:
     max_block_size: int = 65536
 
     def to_abi(self, partial: bool, capacity_hint: int, device: int):
+        # a DISTINCT aggregate raises here (AggregateFunction.to_abi): DistinctAggregator runs it
         gt = (abi.dbg_datatype * max(1, len(self.group_data_types)))(*[t.to_abi() for t in self.group_data_types])
         ag = (abi.dbg_agg_spec * max(1, len(self.aggregate_functions)))(*[f.to_abi() for f in self.aggregate_functions])
         p = abi.dbg_agg_params(gt, len(self.group_data_types), ag, len(self.aggregate_functions), device,
@@ -234,6 +235,16 @@ class AggregateHashTable:
         if on_device:
             self._retained.append((group_columns, params, filter_program))
 
+    def add_groups_abi(self, keys: Sequence["abi.dbg_column"], args: Sequence["abi.dbg_column"], rows: int,
+                       filter_program=None, on_device: bool = False) -> None:
+        """add_groups over ready-made dbg_column structs (the caller keeps their memory alive, and
+        device memory until reset/close)."""
+        fp = filter_program.ptr() if filter_program is not None else None
+        check(lib().dbg_agg_add_groups(self.h, abi_array(list(keys)), abi_array(list(args)), fp, rows,
+                                       1 if on_device else 0))
+        if on_device:
+            self._retained.append(filter_program)
+
     # ---- merge_result
     def finalize(self):
         n = C.c_uint64()
@@ -255,6 +266,24 @@ class AggregateHashTable:
         check(lib().dbg_agg_result(self.h, out_a, out_k, 0))
         cols = [self._to_column(b, n) for b in aggs] + [self._to_column(b, n) for b in keys]
         return DataBlock(cols)
+
+    def merge_result_device(self) -> list:
+        """All groups as device columns [agg results..., group cols...] (DeviceColumn, HBM): only the
+        group count and string sizes reach the host."""
+        from .device import DeviceColumn, empty
+        n, sbytes = self.finalize()
+        gt = self.params.group_data_types
+        aggs = [empty(f.return_type(), n) for f in self.params.aggregate_functions]
+        keys = [empty(t, n, string_bytes=sbytes[i]) for i, t in enumerate(gt)]
+        out_a = (abi.dbg_out_column * max(1, len(aggs)))()
+        out_k = (abi.dbg_out_column * max(1, len(keys)))()
+        for arr, cols in ((out_a, aggs), (out_k, keys)):
+            for i, c in enumerate(cols):
+                arr[i].data = c.data.data_ptr()
+                arr[i].offsets = c.offsets.data_ptr() if c.offsets is not None else None
+                arr[i].validity = c.validity.data_ptr() if c.validity is not None else None
+        check(lib().dbg_agg_result(self.h, out_a, out_k, 1))
+        return aggs + keys
 
     def serialized_strides(self) -> List[int]:
         n = len(self.params.aggregate_functions)
@@ -315,6 +344,21 @@ class AggregateHashTable:
             data, offs = b["data"][:n * t.width].view(t.np_dtype), None
         val = unpack_bits(b["val"], n) if b["val"] is not None else None
         return Column(t, data, offs, val)
+
+    def merge_serialized(self, state_columns: Sequence[ColumnLike], group_columns: Sequence[ColumnLike],
+                         rows: Optional[int] = None, on_device: Optional[bool] = None) -> None:
+        """add_groups with agg_states: AggregateMeta::Serialized's block re-inserted with batch_merge
+        (SerializedPayload::convert_to_aggregate_table, AGG/aggregate_meta.rs:57-101).
+        state_columns: one Binary column of borsh states per aggregate."""
+        if rows is None:
+            rows = len(group_columns[0])
+        if on_device is None:
+            on_device = not isinstance(group_columns[0], Column)
+        keys = abi_array([c.to_abi() for c in group_columns])
+        states = abi_array([c.to_abi() for c in state_columns]) if state_columns else None
+        check(lib().dbg_agg_merge_serialized(self.h, states, keys, rows, 1 if on_device else 0))
+        if on_device:
+            self._retained.append((state_columns, group_columns))
 
     # ---- partial-state records (exchange / partition bucket)
     def record_width(self) -> int:
@@ -377,15 +421,23 @@ class Payload:
 class AggregateMeta:
     """AggregateMeta (AGG/aggregate_meta.rs:124-134).  AggregatePayload: one bucket of one
     partial (`bucket`, `payload`, `max_partition_count` = 2^radix bits of the partial that wrote
-    it).  Partitioned: every payload of one bucket after alignment (`data`)."""
+    it).  Serialized: the same bucket as a DataBlock [Binary state per aggregate..., group
+    columns...] (SerializedPayload, :44-109) — what crosses the Flight exchange or comes back from
+    spill, from a CPU node or a GPU one.  Partitioned: every payload of one bucket after alignment
+    (`data`)."""
     bucket: int
     payload: Optional[Payload] = None
     max_partition_count: int = 1
     data: Optional[List["AggregateMeta"]] = None
+    serialized: Optional[DataBlock] = None
 
     @staticmethod
     def create_agg_payload(bucket: int, payload: Payload, max_partition_count: int) -> "AggregateMeta":
         return AggregateMeta(bucket, payload, max_partition_count)
+
+    @staticmethod
+    def create_serialized(bucket: int, block: DataBlock, max_partition_count: int) -> "AggregateMeta":
+        return AggregateMeta(bucket, None, max_partition_count, serialized=block)
 
     @staticmethod
     def create_partitioned(bucket: int, data: List["AggregateMeta"]) -> "AggregateMeta":
@@ -393,6 +445,9 @@ class AggregateMeta:
 
     def is_partitioned(self) -> bool:
         return self.data is not None
+
+    def is_serialized(self) -> bool:
+        return self.serialized is not None
 
 
 def _cuda_device():
@@ -475,10 +530,16 @@ class TransformPartitionBucket:
         self.inputs.extend(metas)
 
     def _partition_payload(self, meta: AggregateMeta, max_partition_count: int) -> List[AggregateMeta]:
+        """partition_payload (:389-429) for AggregatePayload, partition_block (:341-387) for
+        Serialized: the rows re-inserted into a scratch table (merge_states / batch_merge), then
+        exported as records at the larger radix."""
         scratch = AggregateHashTable(self.params, HashTableConfig(True), self.device)
         try:
-            p = meta.payload
-            scratch.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
+            if meta.is_serialized():
+                _merge_serialized_block(scratch, self.params, meta.serialized)
+            else:
+                p = meta.payload
+                scratch.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
             out = export_buckets(scratch, max_partition_count)
             import torch
             torch.cuda.current_stream().synchronize()  # exports complete before the scratch goes
@@ -513,14 +574,44 @@ class TransformFinalAggregate:
         return cls(params, device)
 
     def transform(self, meta: AggregateMeta) -> DataBlock:
-        payloads = [m.payload for m in meta.data] if meta.is_partitioned() else [meta.payload]
-        payloads = [p for p in payloads if p is not None and len(p)]
-        if not payloads:
+        """AggregatePayload -> combine_payload (merge_states); Serialized -> add_groups with the
+        Binary states (batch_merge), as transform_agg_hashtable does for each variant."""
+        items = list(meta.data) if meta.is_partitioned() else [meta]
+        items = [m for m in items if (m.is_serialized() and m.serialized.num_rows()) or
+                 (m.payload is not None and len(m.payload))]
+        if not items:
             return self.params.empty_result_block()
         final = AggregateHashTable(self.params, HashTableConfig(False), self.device)
         try:
-            for p in payloads:
-                final.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
+            for m in items:
+                if m.is_serialized():
+                    _merge_serialized_block(final, self.params, m.serialized)
+                else:
+                    p = m.payload
+                    final.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
             return final.merge_result()
         finally:
             final.close()
+
+
+def _merge_serialized_block(table: AggregateHashTable, params: AggregatorParams, block: DataBlock) -> None:
+    """The Serialized DataBlock's column order is [states..., group columns...]
+    (AGG/aggregate_meta.rs:80-84)."""
+    na = len(params.aggregate_functions)
+    cols = block.columns
+    table.merge_serialized(cols[:na], cols[na:], rows=block.num_rows())
+
+
+def serialize_payload(params: AggregatorParams, meta: AggregateMeta, device: int = -1) -> AggregateMeta:
+    """TransformExchangeAggregateSerializer's AggregatePayload arm
+    (AGG/serde/transform_exchange_aggregate_serializer.rs:121-240 -> Payload::aggregate_flush,
+    EAGG/payload_flush.rs:129-164): one bucket's groups as AggregateMeta::Serialized, the block a
+    remote (CPU or GPU) final stage merges."""
+    scratch = AggregateHashTable(params, HashTableConfig(True), device)
+    try:
+        p = meta.payload
+        scratch.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
+        block = scratch.result_serialized()
+    finally:
+        scratch.close()
+    return AggregateMeta.create_serialized(meta.bucket, block, meta.max_partition_count)

@@ -18,6 +18,7 @@
 #include "agg.hpp"
 #include "host_stage.hpp"
 #include "legacy.hpp"
+#include "serde.hpp"
 
 #include <dlfcn.h>
 #include <rccl/rccl.h>  // types only: the entry points are resolved with dlsym (exchange section)
@@ -28,6 +29,8 @@
 // errors
 // ------------------------------------------------------------------------------------------
 static thread_local std::string g_last_error;
+static const char* const MINMAX_SPIN_MSG =
+    "Decimal128 MIN/MAX: a state update gave up after 2^20 contended attempts (the result would be wrong)";
 
 static int fail(int code, const std::string& msg) {
     g_last_error = msg;
@@ -220,6 +223,7 @@ struct dbg_agg_handle {
     // ---- partitioned payload (pp.hip): high-cardinality mode ----
     bool pp = false;          // batches go to the radix-partitioned payload, not the HBM table
     double pp_ratio = 1.0;    // estimated groups per selected row (cardinality probe)
+    bool pp_probed = false;   // pp_ratio comes from a probe (not the default upper bound)
     struct Seg {
         u64 base, n;
         std::vector<u64> off;  // level-1 partition offsets (257), relative to base
@@ -266,6 +270,7 @@ struct dbg_agg_handle {
     bool pp_grec_ready = false;
     u64 pp_nb = 0;            // blocks of the grec passes
     u64 pp_stat_rounds = 0;   // partitions that took more than one LDS round (last finalize)
+    u64* ser_err = nullptr;   // serialized-state ingest error bits (serde.hip)
 
     // host-block staging (dbg_agg_set_host_staging, host_stage.hpp)
     hstage::Stage stage;
@@ -794,10 +799,11 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if (hipSetDevice(h->device) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "hipStreamCreate failed"));
     h->stream = h->own_stream;
-    if ((rc = dev_alloc((void**)&h->dspec, sizeof(Spec))) != DBG_OK) return cleanup(rc);
-    if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
     if ((rc = dev_alloc((void**)&h->counters, CNT_WORDS * 8)) != DBG_OK) return cleanup(rc);
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
+    h->spec.err = h->counters + CNT_ERR;  // error bits raised from inside state updates
+    if ((rc = dev_alloc((void**)&h->dspec, sizeof(Spec))) != DBG_OK) return cleanup(rc);
+    if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
     if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));
     if (hipHostGetDevicePointer((void**)&h->hcounters_dev, h->hcounters, 0) != hipSuccess) h->hcounters_dev = nullptr;
     // initial capacity: 2x the hint, or 1024 slots (the CPU table starts at 32768 =
@@ -833,7 +839,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
                     h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->vbytes, h->part_sorted, h->part_bounds,
-                    h->part_temp};
+                    h->part_temp, h->ser_err};
     for (void* p : bufs)
         if (p) hipFree(p);
     for (auto& K : h->ppk) {
@@ -996,6 +1002,7 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     const double gee = std::sqrt(nsel / sel) * f1 + (D - f1);
     const double g = std::min(nsel, std::max(1.25 * gu, gee));
     h->pp_ratio = std::min(1.0, std::max(g / nsel, 1e-9));
+    h->pp_probed = true;
     // the partitioned payload beats the HBM table when keys are mostly unique (ClickBench Q33:
     // 1e9 groups in 1e9 rows); moderate cardinality stays on the table
     if (mode == 2 || (g > (double)PP_MIN_GROUPS && h->pp_ratio > 0.5)) h->pp = true;
@@ -1175,8 +1182,12 @@ static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 row
 static int pp_prepare(dbg_agg_handle* h) {
     const Spec& S = h->spec;
     const u64 nr = h->ppk[0].l1_n, nsr = h->ppk[1].l1_n;
-    // estimated groups: the capacity hint when the caller gave one, else the probe's ratio
-    const double est = h->hint_groups ? (double)h->hint_groups : h->pp_ratio * (double)nr + (double)nsr;
+    // estimated groups: the probe's, raised to the capacity hint (a hint below what the probe saw
+    // would leave too few partition bits: many LDS overflow rounds); without a probe the hint, else
+    // every record its own group
+    const double probed = h->pp_ratio * (double)nr + (double)nsr;
+    const double est = h->pp_probed ? std::max((double)h->hint_groups, probed)
+                                    : (h->hint_groups ? (double)h->hint_groups : probed);
     const double g = std::min((double)(nr + nsr), est);
     // 45 % load: a wave's probe runs as long as its longest lane's (64 lanes in lockstep)
     const double target = std::max(64.0, 0.45 * (double)pp_agg_slots(S));
@@ -1334,8 +1345,23 @@ static int pp_read_tot(dbg_agg_handle* h) {
 }
 
 // dbg_agg_finalize in partitioned mode: group records built, sizes known.
+// Decimal128 MIN/MAX (precision > 18) states are the only updates that can give up
+// (at_minmax128); handles without them skip the read-back.
+static int check_minmax_spin(dbg_agg_handle* h) {
+    bool any = false;
+    for (int a = 0; a < h->spec.n_aggs; ++a) any |= h->spec.aggs[a].mmk == MMK_I128 &&
+                                                    (h->spec.aggs[a].kind == DBG_AGG_MIN || h->spec.aggs[a].kind == DBG_AGG_MAX);
+    if (!any) return DBG_OK;
+    u64 e = 0;
+    HIPCHECK(hipMemcpyAsync(&e, h->counters + CNT_ERR, 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    if (e & ERR_MINMAX_SPIN) return fail(DBG_ERR_INTERNAL, MINMAX_SPIN_MSG);
+    return DBG_OK;
+}
+
 static int pp_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_bytes) {
     const Spec& S = h->spec;
+    RETURN_IF(check_minmax_spin(h));
     if (!h->pp_grec_ready) {
         RETURN_IF(pp_grec_build(h));
         RETURN_IF(pp_read_tot(h));
@@ -1462,7 +1488,9 @@ int dbg_agg_add_groups(dbg_agg_handle* h, const dbg_column* group_cols, const db
             if (filter->cols[c].len < rows) return fail(DBG_ERR_INVALID, "filter column shorter than rows");
     if (!G.empty() && (G.rows + rows > G.cap || !G.same_filter(filter))) RETURN_IF(stage_flush(h));
     if (rows == 0) return DBG_OK;
-    G.append(S.n_keys, group_cols, S.n_aggs, arg_cols, filter, rows);
+    int32_t arg_types[DBG_MAX_AGGS];
+    for (int a = 0; a < S.n_aggs; ++a) arg_types[a] = S.aggs[a].arg_type;
+    G.append(S.n_keys, group_cols, S.n_aggs, arg_cols, arg_types, filter, rows);
     h->finalized = false;
     return DBG_OK;
 }
@@ -1509,6 +1537,7 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
         HIPCHECK(hipMemcpyAsync(h->hcounters + CNT_WORDS, totals, 8 * (S.n_keys + 1), hipMemcpyDeviceToHost, h->stream));
         HIPCHECK(hipStreamSynchronize(h->stream));
         if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+        if (h->hcounters[CNT_ERR] & ERR_MINMAX_SPIN) return fail(DBG_ERR_INTERNAL, MINMAX_SPIN_MSG);
         if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
             return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
                                          "buffer, or unresolved overflow): use dbg_agg_partition + export_records");
@@ -1746,6 +1775,9 @@ int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy) {
     if (strategy < DBG_STRATEGY_AUTO || strategy > DBG_STRATEGY_PARTITIONED) return fail(DBG_ERR_INVALID, "unknown strategy");
     if (h->table_rows || h->ppk[0].l1_n || h->ppk[1].l1_n)
         return fail(DBG_ERR_INVALID, "dbg_agg_set_strategy: the handle holds groups (call it after create or reset)");
+    // the partitioned payload's kernels are sized for records of <= 256 bytes (build_spec: pp_ok)
+    if (strategy == DBG_STRATEGY_PARTITIONED && !h->spec.pp_ok)
+        return fail(DBG_ERR_UNSUPPORTED, "dbg_agg_set_strategy: records too wide for the partitioned payload");
     h->strategy = strategy;
     h->pp = strategy == DBG_STRATEGY_PARTITIONED;
     return DBG_OK;
@@ -1805,6 +1837,7 @@ static int pp_fin_complete(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* stri
     h->pp_grec_ready = S.has_strings != 0;
     h->finalized = h->pp_grec_ready;
     if (t[PPT_ERR] & ERR_DEC_OVERFLOW) return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
+    RETURN_IF(check_minmax_spin(h));
     if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
     return DBG_OK;
 }
@@ -1954,6 +1987,7 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
     }
     h->uploads_pending = false;
     if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
+    if (h->hcounters[CNT_ERR] & ERR_MINMAX_SPIN) return fail(DBG_ERR_INTERNAL, MINMAX_SPIN_MSG);
     if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
         return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
                                      "buffer, or unresolved overflow): use dbg_agg_partition + export_records");
@@ -2211,6 +2245,45 @@ int dbg_agg_merge_fixed(dbg_agg_handle* h, const void* dev_bufs, int32_t n_bufs,
     return DBG_OK;
 }
 
+// One segment of state records -> the table (combine_payload's merge_states).  strs[c]: the
+// string bytes key column c's (offset, len) pairs point into.
+static int merge_record_batch(dbg_agg_handle* h, const u8* base, u64 n, const u8* const* strs) {
+    const Spec& S = h->spec;
+    if (n == 0) return DBG_OK;
+    if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
+    BatchDesc* st;
+    u32 bid;
+    RETURN_IF(new_batch(h, &st, &bid));
+    st->rows = n;
+    st->is_records = 1;
+    st->rec_width = S.rec_width;
+    st->rec_base = base;
+    for (int c = 0; c < S.n_keys; ++c) {
+        DCol& d = st->keys[c];
+        const dbg_datatype& t = S.key_types[c];
+        d.type = t.type;
+        d.precision = t.precision;
+        d.scale = t.scale;
+        d.nullable = t.nullable;
+        d.layout = LAYOUT_RECORD;
+        d.width = type_width(t.type);
+        d.stride = S.rec_width;
+        d.data = base + S.rec_key_off[c];
+        d.validity = t.nullable ? base + S.rec_val_off[c] : nullptr;
+        d.strings = strs[c];
+    }
+    RETURN_IF(upload_batch(h, st, bid));
+    if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, n));
+    if (h->pp) return pp_add_batch(h, st, bid, n, 1);
+    h->table_rows += n;
+    u64 blocks = std::min<u64>(2048, (n + 4095) / 4096) + 1;
+    RETURN_IF(ensure_ovf(h, n, blocks * 4096));
+    prof::Scope ps("agg_merge", h->stream);
+    launch_insert(h->stream, h->dspec, S, h->dbatches, bid, n, true, table_desc(h), true);
+    HIPCHECK(hipGetLastError());
+    return DBG_OK;
+}
+
 int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void* dev_strings, int32_t n_segments,
                           const uint64_t* seg_records, const uint64_t* seg_string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
@@ -2226,43 +2299,65 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
         const u8* strs = (const u8*)dev_strings + str_off;
         rec_off += n;
         str_off += seg_string_bytes ? seg_string_bytes[g] : 0;
-        if (n == 0) continue;
-        if (n >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "segment too large");
-        BatchDesc* st;
-        u32 bid;
-        RETURN_IF(new_batch(h, &st, &bid));
-        st->rows = n;
-        st->is_records = 1;
-        st->rec_width = S.rec_width;
-        st->rec_base = base;
-        for (int c = 0; c < S.n_keys; ++c) {
-            DCol& d = st->keys[c];
-            const dbg_datatype& t = S.key_types[c];
-            d.type = t.type;
-            d.precision = t.precision;
-            d.scale = t.scale;
-            d.nullable = t.nullable;
-            d.layout = LAYOUT_RECORD;
-            d.width = type_width(t.type);
-            d.stride = S.rec_width;
-            d.data = base + S.rec_key_off[c];
-            d.validity = t.nullable ? base + S.rec_val_off[c] : nullptr;
-            d.strings = strs;
-        }
-        RETURN_IF(upload_batch(h, st, bid));
-        if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, n));
-        if (h->pp) {
-            RETURN_IF(pp_add_batch(h, st, bid, n, 1));
-            continue;
-        }
-        h->table_rows += n;
-        u64 blocks = std::min<u64>(2048, (n + 4095) / 4096) + 1;
-        RETURN_IF(ensure_ovf(h, n, blocks * 4096));
-        prof::Scope ps("agg_merge", h->stream);
-        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, n, true, table_desc(h), true);
-        HIPCHECK(hipGetLastError());
+        const u8* per_col[DBG_MAX_KEYS];
+        for (int c = 0; c < DBG_MAX_KEYS; ++c) per_col[c] = strs;
+        RETURN_IF(merge_record_batch(h, base, n, per_col));
     }
     return DBG_OK;
+}
+
+// AggregateMeta::Serialized -> this table (SerializedPayload::convert_to_aggregate_table,
+// AGG/aggregate_meta.rs:57-101; AggregateFunction::batch_merge, EAGG/aggregate_function.rs:96-103).
+int dbg_agg_merge_serialized(dbg_agg_handle* h, const dbg_column* state_cols, const dbg_column* group_cols, uint64_t rows,
+                             int on_device) {
+    if (!h || (!state_cols && h->spec.n_aggs) || !group_cols) return fail(DBG_ERR_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    h->finalized = false;
+    h->clean = false;
+    const Spec& S = h->spec;
+    for (int a = 0; a < S.n_aggs; ++a)
+        if (h->src_kinds[a] == DBG_AGG_AVG_SQL)
+            return fail(DBG_ERR_UNSUPPORTED, "serialized states: SQL avg is sum and count in the reference plan");
+    if (rows == 0) return DBG_OK;
+    if (rows >= 0xFFFFFFFFULL) return fail(DBG_ERR_UNSUPPORTED, "a block holds fewer than 2^32 rows");
+    SerIngest in;
+    memset(&in, 0, sizeof(in));
+    for (int c = 0; c < S.n_keys; ++c) {
+        if (group_cols[c].len < rows) return fail(DBG_ERR_INVALID, "group column shorter than rows");
+        RETURN_IF(to_dcol(h, group_cols[c], S.key_types[c], true, on_device, in.keys[c]));
+    }
+    const dbg_datatype bin{DBG_STRING, 0, 0, 0, 0};
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const dbg_column& sc = state_cols[a];
+        if (sc.dt.type != DBG_STRING || sc.dt.nullable || !sc.offsets) return fail(DBG_ERR_INVALID, "a state column is a non-null Binary column");
+        if (sc.len < rows) return fail(DBG_ERR_INVALID, "state column shorter than rows");
+        DCol d;
+        RETURN_IF(to_dcol(h, sc, bin, true, on_device, d));
+        in.st_data[a] = d.data;
+        in.st_offs[a] = d.offsets;
+    }
+    // records are retained (the table's ref-key entries point at them) until reset
+    DevBuf rb;
+    RETURN_IF(dev_alloc(&rb.p, rows * S.rec_width));
+    h->owned.push_back(rb);
+    if (!h->ser_err) RETURN_IF(dev_alloc((void**)&h->ser_err, 8));
+    HIPCHECK(hipMemsetAsync(h->ser_err, 0, 8, h->stream));
+    {
+        prof::Scope ps("ser_ingest", h->stream);
+        launch_ser_ingest(h->stream, h->dspec, in, rows, (u8*)rb.p, h->ser_err);
+    }
+    HIPCHECK(hipGetLastError());
+    u64 e = 0;
+    HIPCHECK(hipMemcpyAsync(&e, h->ser_err, 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    if (e & ERR_SER_MALFORMED) return fail(DBG_ERR_INVALID, "serialized state bytes do not match the aggregate's state layout");
+    if (e & ERR_SER_UNREP)
+        return fail(DBG_ERR_UNSUPPORTED, "serialized state with a NULL result that the GPU state cannot carry "
+                                         "(OrNull flag 0 or None without a nullable argument)");
+    const u8* per_col[DBG_MAX_KEYS];
+    for (int c = 0; c < DBG_MAX_KEYS; ++c) per_col[c] = c < S.n_keys ? in.keys[c].data : nullptr;
+    return merge_record_batch(h, (const u8*)rb.p, rows, per_col);
 }
 
 // ---- standalone filter ----
@@ -2490,6 +2585,17 @@ int dbg_prof_get(int i, const char** name, double* total_ms, uint64_t* launches)
     *name = prof::totals[i].first.c_str();
     *total_ms = prof::totals[i].second.first;
     *launches = prof::totals[i].second.second;
+    return DBG_OK;
+}
+
+}  // extern "C"
+
+__global__ void dbg_marker_kernel() {}
+
+extern "C" {
+int dbg_prof_marker(void* stream) {
+    hipLaunchKernelGGL(dbg_marker_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream);
+    HIPCHECK(hipGetLastError());
     return DBG_OK;
 }
 

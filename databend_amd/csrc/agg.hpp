@@ -47,6 +47,7 @@ struct Spec {
     u64 pp_klast_mask;      // key bytes of the key part's last word (raw records put args after them)
     uint16_t pp_aoff[DBG_MAX_AGGS];  // raw arg value offset (0: the aggregate takes no argument)
     int16_t pp_avbit[DBG_MAX_AGGS];  // raw arg validity bit (-1: always valid)
+    u64* err;               // the handle's CNT_ERR word (device): errors raised inside state updates
 };
 #define PP_BLOB 39        // inline blob bytes of a string key part
 #define PP_KLEN_LONG 0xFF  // key too long for the blob: reference into the retained input
@@ -87,7 +88,7 @@ struct TableDesc {
 #define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
 enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_FIN_TICKET = 6, CNT_WORDS = 8 };
-enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4 };
+enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4, ERR_MINMAX_SPIN = 8 };
 
 // ---- device helpers shared by agg.hip and part.hip ----
 // Slot placement for inline keys: any good mixer works (placement is not observable); the
@@ -150,7 +151,9 @@ template <int AS> __device__ __forceinline__ void at_minmax(wptr<AS> p, u64 v, b
 __device__ __forceinline__ bool i128_less(u64 alo, u64 ahi, u64 blo, u64 bhi) {
     return (long long)ahi < (long long)bhi || (ahi == bhi && alo < blo);
 }
-template <int AS> __device__ __forceinline__ void at_minmax128(wptr<AS> w, u64 lo, u64 hi, bool mn) {
+// A lane still unsettled after 2^20 rounds gives up and raises ERR_MINMAX_SPIN in *err (finalize
+// then fails with DBG_ERR_INTERNAL instead of returning a MIN/MAX that missed the candidate).
+template <int AS> __device__ __forceinline__ void at_minmax128(wptr<AS> w, u64 lo, u64 hi, bool mn, u64* err) {
     u32 done = 0;
     u32 spins = 0;  // every iteration settles at least one contender; the cap only guards a hang
     do {
@@ -177,6 +180,7 @@ template <int AS> __device__ __forceinline__ void at_minmax128(wptr<AS> w, u64 l
         // reach the latch, so no branch can jump-thread the winner's writes into the loop exit
         asm volatile("" : "+v"(done));
     } while (!done && ++spins < (1u << 20));
+    if (!done) __hip_atomic_fetch_or(err, (u64)ERR_MINMAX_SPIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int AS> __device__ __forceinline__ u64 at_cas(wptr<AS> p, u64 expected, u64 desired) {

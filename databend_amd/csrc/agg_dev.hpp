@@ -61,7 +61,7 @@ __device__ __forceinline__ void apply_row(const Spec& S, wptr<AS> st, const Batc
             }
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 bool mn = A.kind == DBG_AGG_MIN;
-                if (A.mmk == MMK_I128) at_minmax128<AS>(w, dcol_bits(c, i), dcol_hi(c, i), mn);
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, dcol_bits(c, i), dcol_hi(c, i), mn, S.err);
                 else if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)dcol_i64(c, i), mn, true);
                 else at_minmax<AS>(w, A.mmk == MMK_U64 ? dcol_bits(c, i) : f64_order_key(dcol_f64(c, i)), mn, false);
                 break;
@@ -99,7 +99,7 @@ __device__ __forceinline__ void apply_state_get(const Spec& S, wptr<AS> st, G ge
                 break;
             }
             case DBG_AGG_MIN: case DBG_AGG_MAX:
-                if (A.mmk == MMK_I128) at_minmax128<AS>(w, get(x + 1), get(x + 2), A.kind == DBG_AGG_MIN);
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, get(x + 1), get(x + 2), A.kind == DBG_AGG_MIN, S.err);
                 else at_minmax<AS>(w, x0, A.kind == DBG_AGG_MIN, A.mmk == MMK_I64);
                 break;
         }
@@ -246,6 +246,9 @@ __device__ __forceinline__ u32 agg_serialize(const Spec& S, const DAgg& A, const
                     const double x = f64_from_order_key(w[0]);
                     if (A.arg_type == DBG_FLOAT32) put((u64)__float_as_uint((float)x), 4);
                     else put((u64)__double_as_longlong(x), 8);
+                } else if (aw == 16) {  // Decimal128 with precision <= 18: i64 state, i128 bytes
+                    put(w[0], 8);
+                    put((i64)w[0] < 0 ? ~0ULL : 0ULL, 8);
                 } else {
                     put(w[0], aw);  // low bytes of the (sign-extended) value: T's own width
                 }

@@ -151,12 +151,15 @@ struct Stage {
         return true;
     }
 
-    void append(int n_keys, const dbg_column* k, int n_aggs, const dbg_column* a, const dbg_filter* f, uint64_t n) {
+    // arg_types[c] < 0: aggregate c takes no argument (count(*)); its column is never read, as in
+    // the unstaged add_groups (a zero-initialised dbg_column there has type 0 and no data)
+    void append(int n_keys, const dbg_column* k, int n_aggs, const dbg_column* a, const int32_t* arg_types,
+                const dbg_filter* f, uint64_t n) {
         keys.resize(n_keys);
         args.resize(n_aggs);
         for (int c = 0; c < n_keys; ++c) keys[c].append(k[c], n);
         for (int c = 0; c < n_aggs; ++c)
-            if (a && a[c].dt.type >= 0) args[c].append(a[c], n);
+            if (a && arg_types[c] >= 0) args[c].append(a[c], n);
         if (f && f->n_nodes) {
             if (!has_filter) {
                 has_filter = true;

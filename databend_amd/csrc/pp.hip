@@ -210,7 +210,7 @@ __device__ __forceinline__ void pp_apply_raw(const Spec& S, wptr<AS> st, const u
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 const bool mn = A.kind == DBG_AGG_MIN;
                 const u64 b = ld_le(p, aw < 8 ? aw : 8);  // Decimal128 (p <= 18): the low word
-                if (A.mmk == MMK_I128) at_minmax128<AS>(w, b, ld_le(p + 8, 8), mn);
+                if (A.mmk == MMK_I128) at_minmax128<AS>(w, b, ld_le(p + 8, 8), mn, S.err);
                 else if (A.mmk == MMK_I64) at_minmax<AS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
                 else if (A.mmk == MMK_U64) at_minmax<AS>(w, b, mn, false);
                 else
@@ -1199,7 +1199,7 @@ __device__ __forceinline__ void pp_apply_rec(const Spec& S, wptr<AS_LDS> st, con
             case DBG_AGG_MIN: case DBG_AGG_MAX: {
                 const bool mn = A.kind == DBG_AGG_MIN;
                 const u64 b = rk.le(off, aw < 8 ? aw : 8);  // Decimal128 (p <= 18): the low word
-                if (A.mmk == MMK_I128) at_minmax128<AS_LDS>(w, b, rk.le(off + 8, 8), mn);
+                if (A.mmk == MMK_I128) at_minmax128<AS_LDS>(w, b, rk.le(off + 8, 8), mn, S.err);
                 else if (A.mmk == MMK_I64) at_minmax<AS_LDS>(w, (u64)pp_sext(A.arg_type, b), mn, true);
                 else if (A.mmk == MMK_U64) at_minmax<AS_LDS>(w, b, mn, false);
                 else

@@ -1,56 +1,192 @@
-"""COUNT(DISTINCT x) GROUP BY keys on the GPU table.
+"""Aggregates with the DISTINCT combinator on the GPU table.
 
-The reference builds `count(DISTINCT x)` as AggregateDistinctCombinator over count
-(FUN/aggregate_combinator_distinct.rs:60-140, 186-240): a per-group set of the argument values,
-merge_result = the set's size as UInt64; a nullable argument is first stripped by the Null
-combinator, so NULLs are not counted (FUN/aggregate_function_factory.rs:188-211).  ClickBench
-Q9/Q14 (`SELECT RegionID, COUNT(DISTINCT UserID) … GROUP BY RegionID`) are this shape.
+The reference builds `f(DISTINCT x)` (`count_distinct`, `sum_distinct`, ...) as
+AggregateDistinctCombinator over the nested f (FUN/aggregate_combinator_distinct.rs:60-140,
+186-260): a per-group set of the argument values; merge_result feeds the set to f (count: the
+set's size).  A nullable argument is stripped by the Null combinator first, so NULL is never in
+the set, and the group still appears (count 0 / NULL for sum) when all its values are NULL
+(FUN/aggregate_function_factory.rs:170-211).  ClickBench Q10 mixes it with plain aggregates:
+`SELECT RegionID, SUM(AdvEngineID), COUNT(*), AVG(ResolutionWidth), COUNT(DISTINCT UserID)
+ FROM hits GROUP BY RegionID` (benchmark/clickbench/hits/queries/09.sql).
 
-On the GPU the per-group set is itself a GROUP BY: phase 1 aggregates (keys…, x) WHERE
-x IS NOT NULL [AND the query's predicate] into distinct pairs, phase 2 counts the pairs per key —
-two passes of the same HBM table, no per-group set objects.
+On the GPU the per-group set is itself a GROUP BY, and every aggregate of the query lands in ONE
+final table T whose aggregates take nullable arguments:
+
+* raw rows (the query's filter fused) go into T with their plain aggregates' arguments and an
+  all-NULL column for each distinct aggregate (the rows create their groups, count nothing);
+* per distinct aggregate j, the rows go into a pair table P_j keyed (keys..., x_j) — NULL x_j is
+  a pair of its own — whose result columns stay in HBM; its pairs then go into T with x_j as the
+  argument of aggregate j and all-NULL columns for every other aggregate.  f over distinct pairs
+  is f over the group's value set; NULL x_j is skipped by the nullable-argument state.
+
+Declaring the plain aggregates' arguments nullable does not change them: every raw row is valid,
+and every result that can be NULL is already Nullable through the OrNull adaptor (count stays
+UInt64, count(*) becomes count of a never-NULL dummy).  Between the phases only group counts reach
+the host; the pairs never leave the device.
 """
 from __future__ import annotations
 
-from typing import Optional, Sequence
+from dataclasses import replace
+from typing import List, Optional, Sequence
+
+import numpy as np
 
 from . import abi
-from .aggregates import AggregateFunctionFactory
+from .aggregates import AggregateFunction, AggregateFunctionFactory
 from .aggregator import AggregateHashTable, AggregatorParams, HashTableConfig
-from .column import Column, DataBlock
-from .filter import FilterProgram, Pred, and_, is_not_null
+from .column import Column, DataBlock, DataType
+from .ffi import Unsupported
+
+_DUMMY = DataType(abi.UINT8, 0, 0, True)  # count(*)'s never-NULL stand-in argument
 
 
-def count_distinct(group_columns: Sequence[Column], arg: Column, filter_pred: Optional[Pred] = None,
+def _torch():
+    import torch
+    return torch
+
+
+class _NullSource:
+    """All-NULL argument columns of any type and length: one zeroed buffer serves as data,
+    offsets (strings) and the validity bitmap."""
+
+    def __init__(self, rows: int, on_device: bool):
+        nbytes = max(64, rows * 16 + 16)
+        if on_device:
+            self.buf = _torch().zeros(nbytes, dtype=_torch().uint8, device="cuda")
+            self.ptr = self.buf.data_ptr()
+        else:
+            self.buf = np.zeros(nbytes, np.uint8)
+            self.ptr = self.buf.ctypes.data
+        self.rows = rows
+
+    def column(self, dtype: DataType, rows: int) -> abi.dbg_column:
+        assert rows <= self.rows
+        c = abi.dbg_column()
+        c.dt = dtype.wrap_nullable().to_abi()
+        c.data = self.ptr
+        c.offsets = self.ptr if dtype.type_id == abi.STRING else None
+        c.validity = self.ptr
+        c.len = rows
+        return c
+
+
+class _Ones:
+    """A never-NULL UInt8 column of `rows` rows (count(*)'s dummy argument)."""
+
+    def __init__(self, rows: int, on_device: bool):
+        if on_device:
+            self.buf = _torch().ones(max(1, rows), dtype=_torch().uint8, device="cuda")
+            self.ptr = self.buf.data_ptr()
+        else:
+            self.buf = np.ones(max(1, rows), np.uint8)
+            self.ptr = self.buf.ctypes.data
+
+    def column(self, rows: int) -> abi.dbg_column:
+        c = abi.dbg_column()
+        c.dt = _DUMMY.to_abi()
+        c.data = self.ptr
+        c.len = rows
+        return c
+
+
+def _check_supported(keys: Sequence[DataType], functions: Sequence[AggregateFunction]) -> None:
+    if not keys:
+        raise Unsupported(abi.DBG_ERR_UNSUPPORTED, "DISTINCT aggregates without GROUP BY keys run in the "
+                          "reference's single-key processor (AGG/transform_single_key.rs), not on this path")
+    for f in functions:
+        if f.distinct and f.arg is None:
+            raise Unsupported(abi.DBG_ERR_UNSUPPORTED, f"{f.display_name}: DISTINCT needs an argument")
+        if f.distinct and f.arg.type_id == abi.BOOLEAN:
+            raise Unsupported(abi.DBG_ERR_UNSUPPORTED, "DISTINCT over Boolean stays on the CPU path")
+    if any(t.type_id == abi.BOOLEAN for t in keys):
+        raise Unsupported(abi.DBG_ERR_UNSUPPORTED, "Boolean group keys with DISTINCT stay on the CPU path")
+
+
+class DistinctAggregator:
+    """One GROUP BY whose aggregate list may hold DISTINCT aggregates (AggregatorParams with
+    `AggregateFunction.distinct`), run as described in the module docstring.  `run` returns the
+    TransformFinalAggregate block [agg results..., group columns...]."""
+
+    def __init__(self, params: AggregatorParams, device: int = -1):
+        self.params = params
+        self.device = device
+        _check_supported(params.group_data_types, params.aggregate_functions)
+        fns = []
+        for f in params.aggregate_functions:
+            if f.arg is None:
+                fns.append(replace(f, arg=_DUMMY, distinct=False))
+            else:
+                fns.append(replace(f, arg=f.arg.wrap_nullable(), distinct=False))
+        self.t_params = AggregatorParams(list(params.group_data_types), fns)
+        self.distinct_idx = [j for j, f in enumerate(params.aggregate_functions) if f.distinct]
+
+    def run(self, group_columns: Sequence, args: Sequence, filter_program=None,
+            rows: Optional[int] = None, on_device: Optional[bool] = None) -> DataBlock:
+        """group_columns / args (one per aggregate, None for count(*)): host Columns or
+        DeviceColumns, like AggregateHashTable.add_groups."""
+        if rows is None:
+            rows = len(group_columns[0])
+        if on_device is None:
+            on_device = not isinstance(group_columns[0], Column)
+        fns = self.params.aggregate_functions
+        keys = [c.to_abi() for c in group_columns]
+        nulls = _NullSource(rows, on_device)
+        ones = _Ones(rows, on_device)
+        keep = [nulls, ones]
+        final = AggregateHashTable(self.t_params, HashTableConfig(False), self.device)
+        try:
+            # raw rows: plain aggregates' arguments, all-NULL for the distinct ones
+            a = []
+            for j, f in enumerate(fns):
+                if f.distinct:
+                    a.append(nulls.column(f.arg, rows))
+                elif args[j] is None:
+                    a.append(ones.column(rows))
+                else:
+                    a.append(args[j].to_abi())
+            final.add_groups_abi(keys, a, rows, filter_program, on_device)
+            # each distinct aggregate: pairs (keys..., x) in HBM, then into the final table
+            for j in self.distinct_idx:
+                pairs = self._pairs(group_columns, args[j], filter_program, rows, on_device)
+                keep.append(pairs)
+                n = len(pairs[0])
+                if n == 0:
+                    continue
+                big = nulls if (on_device and n <= rows) else _NullSource(n, True)  # pairs live in HBM
+                keep.append(big)
+                a = []
+                for i, f in enumerate(fns):
+                    if i == j:
+                        a.append(pairs[-1].to_abi())
+                    else:
+                        a.append(big.column(_DUMMY if f.arg is None else f.arg, n))
+                final.add_groups_abi([c.to_abi() for c in pairs[:-1]], a, n, None, True)
+            return final.merge_result()
+        finally:
+            final.close()
+
+    def _pairs(self, group_columns, x, filter_program, rows, on_device):
+        """P_j: the distinct (keys..., x) of the selected rows, as device columns."""
+        F = AggregateFunctionFactory.instance()
+        xt = x.dtype
+        p = AggregatorParams(list(self.params.group_data_types) + [xt], [F.get("count")])
+        t = AggregateHashTable(p, HashTableConfig(True), self.device)
+        try:
+            t.add_groups(list(group_columns) + [x], [None], rows=rows, filter_program=filter_program,
+                         on_device=on_device)
+            out = t.merge_result_device()
+        finally:
+            t.close()
+        return out[1:]  # drop the pair count: [keys..., x]
+
+
+def count_distinct(group_columns: Sequence[Column], arg: Column, filter_pred=None,
                    filter_columns: Sequence[Column] = ()) -> DataBlock:
-    """[count_distinct UInt64, group columns…] (TransformFinalAggregate's column order)."""
+    """[count_distinct(arg) UInt64, group columns...] — the lone COUNT(DISTINCT x) GROUP BY keys
+    shape of ClickBench Q9/Q14."""
+    from .filter import FilterProgram
     F = AggregateFunctionFactory.instance()
     keys = list(group_columns)
-    rows = len(keys[0]) if keys else len(arg)
-    fcols = [c.to_abi() for c in filter_columns]
-    pred = filter_pred
-    if arg.dtype.nullable:
-        cond = is_not_null(len(fcols))
-        fcols.append(arg.to_abi())
-        pred = cond if pred is None else and_(pred, cond)
-    prog = FilterProgram(pred, fcols) if pred is not None else None
-    # phase 1: the distinct (keys…, x) pairs
-    p1 = AggregatorParams([k.dtype for k in keys] + [arg.dtype], [F.get("count")])
-    t1 = AggregateHashTable(p1, HashTableConfig(True))
-    try:
-        t1.add_groups(keys + [arg], [None], rows=rows, filter_program=prog)
-        pairs = t1.merge_result()
-    finally:
-        t1.close()
-    pair_keys = pairs.columns[1:1 + len(keys)]
-    # phase 2: pairs per key
-    p2 = AggregatorParams([k.dtype for k in keys], [F.get("count")])
-    t2 = AggregateHashTable(p2, HashTableConfig(False))
-    try:
-        n = pairs.num_rows()
-        if n:
-            t2.add_groups(pair_keys, [None], rows=n)
-        out = t2.merge_result()
-    finally:
-        t2.close()
-    return out
+    params = AggregatorParams([k.dtype for k in keys], [F.get("count_distinct", [], [arg.dtype])])
+    prog = FilterProgram(filter_pred, [c.to_abi() for c in filter_columns]) if filter_pred is not None else None
+    return DistinctAggregator(params).run(keys, [arg], filter_program=prog)

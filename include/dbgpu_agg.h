@@ -219,6 +219,23 @@ int dbg_agg_result(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_column* 
 int dbg_agg_serialized_stride(dbg_agg_handle* h, uint32_t* stride /* n_aggs */);
 int dbg_agg_result_serialized(dbg_agg_handle* h, dbg_out_column* out_states, dbg_out_column* out_keys, int on_device);
 
+/* AggregateMeta::Serialized -> this table: the final stage's ingest of a partial that crossed the
+ * wire or went to spill as [Binary state per aggregate..., group columns...]
+ * (SerializedPayload::convert_to_aggregate_table, AGG/aggregate_meta.rs:57-101, reached from
+ * TransformFinalAggregate::transform_agg_hashtable, AGG/transform_aggregate_final.rs:71-156, and
+ * NewTransformPartitionBucket::partition_block, AGG/new_transform_partition_bucket.rs:341-387).
+ * Each row's group is probed and every state is merged with AggregateFunction::merge's meaning
+ * (batch_merge, EAGG/aggregate_function.rs:96-103): the bytes are the layout
+ * dbg_agg_result_serialized writes (borsh state, NullUnary flag, OrNull flag).  state_cols[a] is a
+ * non-null Binary column (dt.type = DBG_STRING, offsets rows + 1) for aggregate a; group_cols as
+ * in dbg_agg_add_groups.  Errors: DBG_ERR_INVALID when a state's length does not match its
+ * aggregate; DBG_ERR_UNSUPPORTED for SQL avg, or for a state whose NULL result the GPU state
+ * cannot carry (OrNull flag 0 / None on a non-nullable argument: states the reference's partial
+ * never writes).  Device inputs are retained like dbg_agg_add_groups'; parse errors are reported
+ * by this call (it synchronises the stream once). */
+int dbg_agg_merge_serialized(dbg_agg_handle* h, const dbg_column* state_cols, const dbg_column* group_cols, uint64_t rows,
+                             int on_device);
+
 /* Fused finalize + result into device buffers (on_device outputs) in one host round trip:
  * count, scan and write are enqueued together and the group count is read back once.  Buffers
  * hold max_groups rows (and max_string_bytes[c] payload bytes per string key column, may be NULL
@@ -422,6 +439,9 @@ int dbg_prof_enable(int on);
 int dbg_prof_reset(void);
 /* i-th kernel seen so far: name, summed milliseconds, launches.  Returns DBG_ERR_INVALID past end. */
 int dbg_prof_get(int i, const char** name, double* total_ms, uint64_t* launches);
+/* An empty kernel (dbg_marker_kernel) on hip_stream: delimits a region in a rocprofv3 trace or
+ * counter collection (scripts/pmc_step_traffic.py attributes the dispatches between two markers). */
+int dbg_prof_marker(void* hip_stream);
 
 /* ---- synthetic workload generator (the numbers_mt analog) ----
  * Fills caller-allocated device buffers for rows [row_start, row_start+rows) of config cfg,

@@ -290,7 +290,23 @@ struct AggFn {
     virtual void merge_result(u8* place, Builder& b) const = 0;
     virtual dbg_datatype return_type() const = 0;
     virtual size_t result_width() const = 0;
+    // AggregateFunction::serialize / merge (EAGG/aggregate_function.rs:88-105): the borsh bytes of
+    // the state struct (FUN/aggregator_common.rs:159-170) — little-endian fixed-width integers and
+    // floats, Option<T> = tag byte + T — and the inverse, merging a serialized state into place.
+    virtual void serialize(const u8* place, std::vector<u8>& w) const = 0;
+    virtual void merge(u8* place, const u8* r, size_t len) const = 0;
 };
+
+template <class T>
+static inline void put_le(std::vector<u8>& w, T v, size_t bytes = sizeof(T)) {
+    u8 b[16];
+    memcpy(b, &v, sizeof(T));
+    w.insert(w.end(), b, b + bytes);
+}
+// borsh_deserialize_state: a reader that must hold exactly the state's bytes
+static inline void need(size_t len, size_t want) {
+    if (len != want) throw UnsupportedError("serialized state: " + std::to_string(len) + " bytes, expected " + std::to_string(want));
+}
 
 // AggregateCountFunction (FUN/aggregate_count.rs:37-214): u64 state, counts rows / valid args.
 struct CountFn : AggFn {
@@ -310,6 +326,14 @@ struct CountFn : AggFn {
     void merge_result(u8* p, Builder& b) const override { b.push<u64>(*(u64*)p); }
     dbg_datatype return_type() const override { return dbg_datatype{DBG_UINT64, 0, 0, 0, 0}; }
     size_t result_width() const override { return 8; }
+    // aggregate_count.rs:152-162: borsh u64
+    void serialize(const u8* p, std::vector<u8>& w) const override { put_le<u64>(w, *(const u64*)p); }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        need(len, 8);
+        u64 x;
+        memcpy(&x, r, 8);
+        *(u64*)p += x;
+    }
 };
 
 // Read an argument as a signed/unsigned/f64/i128 value.
@@ -357,6 +381,14 @@ struct SumNumFn : AggFn {
     void merge_result(u8* p, Builder& b) const override { b.push<S>(*(S*)p); }
     dbg_datatype return_type() const override { return rt; }
     size_t result_width() const override { return 8; }
+    // NumberSumState {value: TSum} (aggregate_sum.rs:64-113, derive(BorshSerialize))
+    void serialize(const u8* p, std::vector<u8>& w) const override { put_le<S>(w, *(const S*)p); }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        need(len, 8);
+        S x;
+        memcpy(&x, r, 8);
+        add(*(S*)p, x);
+    }
 };
 
 // DecimalSumState<OVERFLOW, Decimal128> (FUN/aggregate_sum.rs:115-170): i128 `+=` (wrapping in
@@ -391,6 +423,14 @@ struct SumDecFn : AggFn {
     }
     dbg_datatype return_type() const override { return rt; }
     size_t result_width() const override { return 16; }
+    // DecimalSumState {value: i128}; merge = add (aggregate_sum.rs:158-160, range-checked)
+    void serialize(const u8* p, std::vector<u8>& w) const override { w.insert(w.end(), p, p + 16); }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        need(len, 16);
+        i128 x;
+        memcpy(&x, r, 16);
+        add(p, x);
+    }
 };
 
 // NumberAvgState<T, TSum> (FUN/aggregate_avg.rs:38-99): {value: TSum, count: u64};
@@ -418,6 +458,16 @@ struct AvgNumFn : AggFn {
     }
     dbg_datatype return_type() const override { return dbg_datatype{DBG_FLOAT64, 0, 0, 0, 0}; }
     size_t result_width() const override { return 8; }
+    // NumberAvgState {value: TSum, count: u64} (aggregate_avg.rs:38-88)
+    void serialize(const u8* p, std::vector<u8>& w) const override { w.insert(w.end(), p, p + 16); }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        need(len, 16);
+        S x;
+        u64 c;
+        memcpy(&x, r, 8);
+        memcpy(&c, r + 8, 8);
+        add(p, x, c);
+    }
 };
 
 // DecimalAvgState<OVERFLOW, Decimal128> (FUN/aggregate_avg.rs:113-201): {value: i128, count};
@@ -462,6 +512,16 @@ struct AvgDecFn : AggFn {
     }
     dbg_datatype return_type() const override { return rt; }
     size_t result_width() const override { return 16; }
+    // DecimalAvgState {value: i128, count: u64} (aggregate_avg.rs:113-171)
+    void serialize(const u8* p, std::vector<u8>& w) const override { w.insert(w.end(), p, p + 24); }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        need(len, 24);
+        i128 x;
+        u64 c;
+        memcpy(&x, r, 16);
+        memcpy(&c, r + 16, 8);
+        add(p, x, c);
+    }
 };
 
 // SQL avg(x) after the planner's rewrite sum(x) / if(count(x) = 0, 1, count(x))
@@ -525,6 +585,9 @@ struct SqlAvgDecFn : AggFn {
     }
     dbg_datatype return_type() const override { return rt; }
     size_t result_width() const override { return 16; }
+    // the SQL rewrite has two reference states (sum, count), not one
+    void serialize(const u8*, std::vector<u8>&) const override { throw UnsupportedError("serialized SQL avg"); }
+    void merge(u8*, const u8*, size_t) const override { throw UnsupportedError("serialized SQL avg"); }
 };
 
 // MinMaxAnyState<T, CmpMin/CmpMax> (FUN/aggregate_min_max_any.rs:46-115,
@@ -592,6 +655,41 @@ struct MinMaxFn : AggFn {
     }
     dbg_datatype return_type() const override { return rt; }
     size_t result_width() const override { return fixed_width(rt.type); }
+    // MinMaxAnyState {value: Option<T>} in T's own width (aggregate_min_max_any.rs:46-56):
+    // merge = add(rhs value) when Some (:95-100)
+    void serialize(const u8* p, std::vector<u8>& w) const override {
+        w.push_back(p[0] ? 1 : 0);
+        if (!p[0]) return;
+        T v;
+        memcpy(&v, p + 16, sizeof(T));
+        if (rt.type == DBG_FLOAT32) put_le<float>(w, (float)(double)v);
+        else put_le<T>(w, v, fixed_width(rt.type));
+    }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        if (len < 1) need(len, 1);
+        if (r[0] == 0) {
+            need(len, 1);
+            return;
+        }
+        const size_t wd = fixed_width(rt.type);
+        need(len, 1 + wd);
+        T x;
+        if (rt.type == DBG_FLOAT32) {
+            float f;
+            memcpy(&f, r + 1, 4);
+            x = (T)(double)f;
+        } else if constexpr (std::is_same<T, double>::value) {
+            memcpy(&x, r + 1, 8);
+        } else if constexpr (std::is_same<T, i128>::value) {
+            memcpy(&x, r + 1, 16);
+        } else {
+            u64 raw = 0;
+            memcpy(&raw, r + 1, wd);
+            if (std::is_signed<T>::value && wd < 8 && ((raw >> (8 * wd - 1)) & 1)) raw |= ~0ULL << (8 * wd);
+            x = (T)raw;
+        }
+        add(p, x);
+    }
 };
 
 // AggregateNullUnaryAdaptor<NULLABLE_RESULT=true> (FUN/adaptors/aggregate_null_unary_adaptor.rs):
@@ -630,6 +728,19 @@ struct NullUnaryAdaptor : AggFn {
         if (p[inner->size()] == 1) inner->merge_result(p, b);
         else b.push_null(inner->result_width());
     }
+    // aggregate_null_unary_adaptor.rs:200-224: nested state, then the flag byte
+    void serialize(const u8* p, std::vector<u8>& w) const override {
+        inner->serialize(p, w);
+        w.push_back(p[inner->size()]);
+    }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        if (len < 1) need(len, 1);
+        if (p[inner->size()] == 0) inner->init_state(p);
+        if (r[len - 1] == 1) {
+            p[inner->size()] = 1;
+            inner->merge(p, r, len - 1);
+        }
+    }
     dbg_datatype return_type() const override {
         dbg_datatype t = inner->return_type();
         t.nullable = 1;
@@ -664,6 +775,17 @@ struct OrNullAdaptor : AggFn {
     void merge_result(u8* p, Builder& b) const override {
         if (p[inner->size()] == 0) b.push_null(inner->result_width());
         else inner->merge_result(p, b);
+    }
+    // aggregate_ornull_adaptor.rs:175-187: inner state, then the flag byte
+    void serialize(const u8* p, std::vector<u8>& w) const override {
+        inner->serialize(p, w);
+        w.push_back(p[inner->size()]);
+    }
+    void merge(u8* p, const u8* r, size_t len) const override {
+        if (len < 1) need(len, 1);
+        const bool flag = p[inner->size()] > 0 || r[len - 1] > 0;
+        inner->merge(p, r, len - 1);
+        p[inner->size()] = flag ? 1 : 0;
     }
     dbg_datatype return_type() const override {
         dbg_datatype t = inner->return_type();
@@ -1049,13 +1171,27 @@ struct AggregateHashTable {
     void add_groups(const dbg_column* groups, const dbg_column* const* args, u64 rows) {
         for (u64 s = 0; s < rows; s += BATCH_SIZE) add_groups_inner(groups, args, s, std::min<u64>(BATCH_SIZE, rows - s));
     }
-    void add_groups_inner(const dbg_column* groups, const dbg_column* const* args, u64 start, u64 n) {
+    // add_groups with agg_states (AggregateMeta::Serialized: SerializedPayload::convert_to_aggregate_table,
+    // AGG/aggregate_meta.rs:57-101): the same probe, then AggregateFunction::batch_merge of each
+    // Binary state column (EAGG/aggregate_function.rs:96-103) instead of accumulate_keys.
+    void add_groups_merge(const dbg_column* groups, const dbg_column* states, u64 rows) {
+        for (u64 s = 0; s < rows; s += BATCH_SIZE) add_groups_inner(groups, nullptr, s, std::min<u64>(BATCH_SIZE, rows - s), states);
+    }
+    void add_groups_inner(const dbg_column* groups, const dbg_column* const* args, u64 start, u64 n,
+                          const dbg_column* states = nullptr) {
         group_hash_columns(groups, (int)L->group_types.size(), start, n, group_hashes.data());
         probe_and_create(groups, start, n);
         if (!L->aggs.empty()) {
             for (u64 k = 0; k < n; ++k) state_places[k] = (u8*)(uintptr_t)rd<u64>(addresses[k] + L->state_offset);
-            for (size_t a = 0; a < L->aggs.size(); ++a)
-                L->aggs[a]->accumulate_keys(state_places.data(), L->state_addr_offsets[a], args[a], start, n);
+            for (size_t a = 0; a < L->aggs.size(); ++a) {
+                if (states) {
+                    for (u64 k = 0; k < n; ++k)
+                        L->aggs[a]->merge(state_places[k] + L->state_addr_offsets[a], str_ptr(states[a], start + k),
+                                          str_len(states[a], start + k));
+                } else {
+                    L->aggs[a]->accumulate_keys(state_places.data(), L->state_addr_offsets[a], args[a], start, n);
+                }
+            }
         }
         if (config.partial_agg) {  // :225-239
             if (count + BATCH_SIZE > resize_threshold() && capacity >= config.max_partial_capacity) {
@@ -1218,7 +1354,8 @@ struct AggregateHashTable {
         }
     }
     // merge_result (:427-451) + flush of group columns: append every group to the outputs.
-    void merge_result(std::vector<OwnedColumn>& keys, std::vector<OwnedColumn>& results) {
+    // ser: the states as Binary columns (payload_flush.rs:129-164 aggregate_flush) instead of results
+    void merge_result(std::vector<OwnedColumn>& keys, std::vector<OwnedColumn>& results, bool ser = false) {
         for (auto& p : payload->payloads)
             for (auto& pg : p->pages)
                 for (size_t r = 0; r < pg->rows; ++r) {
@@ -1241,6 +1378,14 @@ struct AggregateHashTable {
                     if (!L->aggs.empty()) {
                         u8* place = (u8*)(uintptr_t)rd<u64>(row + L->state_offset);
                         for (size_t a = 0; a < L->aggs.size(); ++a) {
+                            if (ser) {
+                                OwnedColumn& o = results[a];
+                                L->aggs[a]->serialize(place + L->state_addr_offsets[a], o.data);
+                                o.offsets.push_back(o.data.size());
+                                o.valid.push_back(1);
+                                o.rows++;
+                                continue;
+                            }
                             Builder b{&results[a]};
                             L->aggs[a]->merge_result(place + L->state_addr_offsets[a], b);
                         }
@@ -1350,6 +1495,7 @@ struct PipelineSpec {
     u64 rows = 0;
     int threads = 1;
     size_t block_size = 65536;  // max_block_size (settings_default.rs:131)
+    bool serialize = false;     // emit the final states as Binary columns (AggregateMeta::Serialized)
 };
 
 static void run_pipeline(const PipelineSpec& ps, Result& out) {
@@ -1474,8 +1620,11 @@ static void run_pipeline(const PipelineSpec& ps, Result& out) {
                 r.keys.resize(ps.keys.size());
                 r.aggs.resize(fns.size());
                 for (size_t c = 0; c < ps.keys.size(); ++c) { r.keys[c].clear(); r.keys[c].dt = ps.keys[c].dt; }
-                for (size_t a = 0; a < fns.size(); ++a) { r.aggs[a].clear(); r.aggs[a].dt = fns[a]->return_type(); }
-                ht->merge_result(r.keys, r.aggs);
+                for (size_t a = 0; a < fns.size(); ++a) {
+                    r.aggs[a].clear();
+                    r.aggs[a].dt = ps.serialize ? dbg_datatype{DBG_STRING, 0, 0, 0, 0} : fns[a]->return_type();
+                }
+                ht->merge_result(r.keys, r.aggs, ps.serialize);
             }
         } catch (OverflowError& e) {
             ferrs[t] = e.what();
@@ -1500,7 +1649,10 @@ static void run_pipeline(const PipelineSpec& ps, Result& out) {
     out.keys.assign(ps.keys.size(), OwnedColumn());
     out.aggs.assign(fns.size(), OwnedColumn());
     for (size_t c = 0; c < ps.keys.size(); ++c) { out.keys[c].clear(); out.keys[c].dt = ps.keys[c].dt; }
-    for (size_t a = 0; a < fns.size(); ++a) { out.aggs[a].clear(); out.aggs[a].dt = fns[a]->return_type(); }
+    for (size_t a = 0; a < fns.size(); ++a) {
+        out.aggs[a].clear();
+        out.aggs[a].dt = ps.serialize ? dbg_datatype{DBG_STRING, 0, 0, 0, 0} : fns[a]->return_type();
+    }
     auto cat = [](OwnedColumn& d, OwnedColumn& s) {
         if (d.dt.type == DBG_STRING) {
             u64 base = d.data.size();
@@ -1515,6 +1667,35 @@ static void run_pipeline(const PipelineSpec& ps, Result& out) {
         for (size_t a = 0; a < r.aggs.size(); ++a) cat(out.aggs[a], r.aggs[a]);
     }
     out.rows = out.keys.empty() ? (out.aggs.empty() ? 0 : out.aggs[0].rows) : out.keys[0].rows;
+}
+
+// TransformFinalAggregate over AggregateMeta::Serialized blocks [states..., groups...]
+// (AGG/transform_aggregate_final.rs:71-156 -> SerializedPayload::convert_to_aggregate_table,
+// AGG/aggregate_meta.rs:57-101): one final table re-inserts every block's groups, merging the
+// Binary states (batch_merge), then merge_result (or serialize again).
+static void run_merge_serialized(const std::vector<dbg_column>& keys, const std::vector<dbg_column>& states,
+                                 const std::vector<dbg_agg_spec>& specs, u64 rows, bool ser, Result& out) {
+    std::vector<std::unique_ptr<AggFn>> owned;
+    std::vector<AggFn*> fns;
+    for (auto& s : specs) {
+        owned.emplace_back(make_fn(s));
+        fns.push_back(owned.back().get());
+    }
+    std::vector<dbg_datatype> gtypes;
+    for (auto& k : keys) gtypes.push_back(k.dt);
+    Layout L;
+    L.init(gtypes, fns);
+    AggregateHashTable ht(&L, Config().with_initial_radix_bits(0), AggregateHashTable::get_capacity_for_count(rows));
+    ht.add_groups_merge(keys.data(), states.data(), rows);
+    out.keys.assign(keys.size(), OwnedColumn());
+    out.aggs.assign(fns.size(), OwnedColumn());
+    for (size_t c = 0; c < keys.size(); ++c) { out.keys[c].clear(); out.keys[c].dt = keys[c].dt; }
+    for (size_t a = 0; a < fns.size(); ++a) {
+        out.aggs[a].clear();
+        out.aggs[a].dt = ser ? dbg_datatype{DBG_STRING, 0, 0, 0, 0} : fns[a]->return_type();
+    }
+    ht.merge_result(out.keys, out.aggs, ser);
+    out.rows = out.keys.empty() ? 0 : out.keys[0].rows;
 }
 
 }  // namespace orc
@@ -1667,6 +1848,54 @@ int orc_aggregate(const dbg_column* keys, int n_keys, const dbg_column* args, co
         ps.threads = threads;
         auto* r = new orc_result();
         run_pipeline(ps, r->r);
+        *out = r;
+        return DBG_OK;
+    } catch (OverflowError& e) {
+        g_err = e.what();
+        return DBG_ERR_OVERFLOW;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return DBG_ERR_UNSUPPORTED;
+    }
+}
+
+// The same pipeline, the final states serialized (AggregateMeta::Serialized's Binary columns).
+int orc_aggregate_serialized(const dbg_column* keys, int n_keys, const dbg_column* args, const dbg_agg_spec* specs,
+                             int n_aggs, const dbg_filter* filter, uint64_t rows, int threads, orc_result** out) {
+    try {
+        PipelineSpec ps;
+        ps.keys.assign(keys, keys + n_keys);
+        ps.args.assign(args, args + n_aggs);
+        ps.specs.assign(specs, specs + n_aggs);
+        ps.filter = filter;
+        ps.rows = rows;
+        ps.threads = threads;
+        ps.serialize = true;
+        auto* r = new orc_result();
+        run_pipeline(ps, r->r);
+        *out = r;
+        return DBG_OK;
+    } catch (OverflowError& e) {
+        g_err = e.what();
+        return DBG_ERR_OVERFLOW;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return DBG_ERR_UNSUPPORTED;
+    }
+}
+
+// Final aggregate of one Serialized block (states: n_aggs Binary columns); ser = 1 re-serializes.
+int orc_merge_serialized(const dbg_column* keys, int n_keys, const dbg_column* states, const dbg_agg_spec* specs,
+                         int n_aggs, uint64_t rows, int ser, orc_result** out) {
+    try {
+        auto* r = new orc_result();
+        try {
+            run_merge_serialized(std::vector<dbg_column>(keys, keys + n_keys), std::vector<dbg_column>(states, states + n_aggs),
+                                 std::vector<dbg_agg_spec>(specs, specs + n_aggs), rows, ser != 0, r->r);
+        } catch (...) {
+            delete r;
+            throw;
+        }
         *out = r;
         return DBG_OK;
     } catch (OverflowError& e) {

@@ -41,6 +41,9 @@ def lib():
                                         C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.orc_aggregate.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                     C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]
+        L.orc_aggregate_serialized.argtypes = L.orc_aggregate.argtypes
+        L.orc_merge_serialized.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64, C.c_int,
+                                           C.POINTER(C.c_void_p)]
         L.orc_group_hash.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_void_p]
         L.orc_legacy_group_hash.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_void_p]
         L.orc_crc32c_bytes.argtypes = [C.c_uint32, C.c_void_p, C.c_uint64]
@@ -126,9 +129,21 @@ def _to_column(r, which: int, idx: int, rows: int) -> Column:
     return Column(d, data_arr, offsets, v if d.nullable else None)
 
 
+def _collect(out, n_keys: int, n_aggs: int):
+    try:
+        rows = lib().orc_result_rows(out)
+        kc = [_to_column(out, 0, i, rows) for i in range(n_keys)]
+        ac = [_to_column(out, 1, i, rows) for i in range(n_aggs)]
+    finally:
+        lib().orc_result_free(out)
+    return kc, ac
+
+
 def aggregate(keys: Sequence[Column], aggs: Sequence[Tuple[abi.dbg_agg_spec, Optional[Column]]],
-              filter_program=None, threads: int = 1) -> Tuple[List[Column], List[Column]]:
-    """Run the restated pipeline (partial x threads -> bucket -> final).  Returns (keys, aggs)."""
+              filter_program=None, threads: int = 1, serialize: bool = False) -> Tuple[List[Column], List[Column]]:
+    """Run the restated pipeline (partial x threads -> bucket -> final).  Returns (keys, aggs);
+    serialize=True returns each aggregate's final state as a Binary column of borsh bytes
+    (AggregateMeta::Serialized's state columns) instead of its result."""
     n = len(keys[0])
     karr = abi_array([k.to_abi() for k in keys])
     arg_structs = []
@@ -142,16 +157,23 @@ def aggregate(keys: Sequence[Column], aggs: Sequence[Tuple[abi.dbg_agg_spec, Opt
     aarr = abi_array(arg_structs)
     sarr = abi_array([s for s, _ in aggs], abi.dbg_agg_spec)
     out = C.c_void_p()
-    _check(lib().orc_aggregate(karr, len(keys), aarr, sarr, len(aggs),
-                               filter_program.ptr() if filter_program is not None else None,
-                               n, threads, C.byref(out)))
-    try:
-        rows = lib().orc_result_rows(out)
-        kc = [_to_column(out, 0, i, rows) for i in range(len(keys))]
-        ac = [_to_column(out, 1, i, rows) for i in range(len(aggs))]
-    finally:
-        lib().orc_result_free(out)
-    return kc, ac
+    fn = lib().orc_aggregate_serialized if serialize else lib().orc_aggregate
+    _check(fn(karr, len(keys), aarr, sarr, len(aggs), filter_program.ptr() if filter_program is not None else None,
+              n, threads, C.byref(out)))
+    return _collect(out, len(keys), len(aggs))
+
+
+def merge_serialized(keys: Sequence[Column], states: Sequence[Column], specs: Sequence[abi.dbg_agg_spec],
+                     serialize: bool = False) -> Tuple[List[Column], List[Column]]:
+    """TransformFinalAggregate over one AggregateMeta::Serialized block (group columns + Binary
+    state columns): re-insert with batch_merge, then merge_result (or serialize again)."""
+    n = len(keys[0])
+    karr = abi_array([k.to_abi() for k in keys])
+    st = abi_array([c.to_abi() for c in states]) if states else None
+    sarr = abi_array(list(specs), abi.dbg_agg_spec) if specs else None
+    out = C.c_void_p()
+    _check(lib().orc_merge_serialized(karr, len(keys), st, sarr, len(specs), n, 1 if serialize else 0, C.byref(out)))
+    return _collect(out, len(keys), len(specs))
 
 
 # ---- CPU workload generator (include/dbgpu_datagen.h) ----

@@ -29,6 +29,7 @@ EXAMPLE = {
 }
 
 AST = re.compile(r"^ast: (count|sum|avg|min|max)\((\w*)\)$")
+AST_DISTINCT = re.compile(r"^ast: (sum_distinct)\((\w*)\)$")  # AggregateDistinctCombinator cases
 OUT_PLAIN = re.compile(r"\| Output\s*\| (\w+)\(\[([^\]]*)\]\)")
 OUT_NULL = re.compile(r"\| Output\s*\| NullableColumn \{ column: (\w+)\(\[([^\]]*)\]\), validity: \[0b_*([01]+)\] \}")
 
@@ -42,13 +43,13 @@ def parse_values(typ, s):
     return [int(v) for v in vals]
 
 
-def parse_file(name, grouped):
+def parse_file(name, grouped, ast=AST):
     path = os.path.join(REF, TESTDATA, name)
     lines = open(path).read().splitlines()
     out = []
     i = 0
     while i < len(lines):
-        m = AST.match(lines[i])
+        m = ast.match(lines[i])
         if m:
             fn, arg = m.group(1), m.group(2)
             if arg == "" or arg in EXAMPLE:
@@ -140,7 +141,10 @@ def main():
         json.dump(dict(inputs=EXAMPLE, cases=goldens), f, indent=1)
     with open(os.path.join(HERE, "slt_group_by.json"), "w") as f:
         json.dump(SLT, f, indent=1)
-    print(f"{len(goldens)} function goldens, {len(SLT)} sqllogictest cases")
+    distinct = parse_file("agg_group_by.txt", True, AST_DISTINCT) + parse_file("agg.txt", False, AST_DISTINCT)
+    with open(os.path.join(HERE, "distinct_goldens.json"), "w") as f:
+        json.dump(dict(inputs=EXAMPLE, cases=distinct), f, indent=1)
+    print(f"{len(goldens)} function goldens, {len(distinct)} distinct goldens, {len(SLT)} sqllogictest cases")
 
 
 if __name__ == "__main__":
