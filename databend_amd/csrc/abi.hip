@@ -36,6 +36,8 @@ static int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
 }
+// the other translation units (scan.hip) report through the same last-error slot
+int abi_fail(int code, const std::string& msg) { return fail(code, msg); }
 
 #define HIPCHECK(expr)                                                                         \
     do {                                                                                       \
@@ -154,6 +156,7 @@ struct dbg_agg_handle {
     // finalize_into_async of a small table then runs in the same launch (FusedFin); any other
     // call launches it first (flush_deferred).
     bool def_on = false;
+    bool def_clean = false;  // the table was empty (recycled / reset) when the insert was held back
     u32 def_bid = 0;
     u64 def_rows = 0;
     BatchDesc def_hb;
@@ -817,8 +820,7 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if ((rc = alloc_table(h, h->cap, &h->slots)) != DBG_OK) return cleanup(rc);
     // parking rows for every workgroup of an insert launch (launch_insert caps its grid here)
     h->scr_blocks = DBG_INSERT_MAX_BLOCKS;
-    if ((rc = dev_alloc((void**)&h->scratch, (size_t)h->scr_blocks * 8 * (2 + SCR_ENTRIES * (size_t)h->spec.stride_words))) != DBG_OK)
-        return cleanup(rc);
+    if ((rc = dev_alloc((void**)&h->scratch, scr_words(h->scr_blocks, (u32)h->spec.stride_words) * 8)) != DBG_OK) return cleanup(rc);
     if (hipMemset(h->scratch, 0, (size_t)h->scr_blocks * 16) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
 
     // the (empty) batch table
@@ -1409,6 +1411,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
     if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, rows));
     if (h->pp) return pp_add_batch(h, st, bid, rows, 0);
     h->table_rows += rows;
+    const bool was_clean = h->clean;
     h->clean = false;
     // worst-case pushes of this launch: every row, and every LDS slot of every workgroup
     u64 blocks = std::min<u64>(2048, (rows + 4095) / 4096) + 1;
@@ -1425,6 +1428,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
     RETURN_IF(ensure_ovf(h, rows, 2 * blocks * 4096));
     if (on_device && h->recycle && h->hcounters_dev && insert_can_fuse(S, *st, h->cap)) {  // held back: see def_on
         h->def_on = true;
+        h->def_clean = was_clean;
         h->def_bid = bid;
         h->def_rows = rows;
         h->def_hb = *st;
@@ -1775,8 +1779,12 @@ int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy) {
     if (strategy < DBG_STRATEGY_AUTO || strategy > DBG_STRATEGY_PARTITIONED) return fail(DBG_ERR_INVALID, "unknown strategy");
     if (h->table_rows || h->ppk[0].l1_n || h->ppk[1].l1_n)
         return fail(DBG_ERR_INVALID, "dbg_agg_set_strategy: the handle holds groups (call it after create or reset)");
-    // the partitioned payload's kernels are sized for records of <= 256 bytes (build_spec: pp_ok)
-    if (strategy == DBG_STRATEGY_PARTITIONED && !h->spec.pp_ok)
+    // AUTO switches only for records of <= 256 bytes (build_spec: pp_ok); a forced partitioned
+    // payload runs up to the scatter's limit: a tile needs one wave of 64 rows in its 32 KiB
+    // scratch (pp_direct_t > 0, i.e. records of <= 512 bytes) and <= 64 state words per group
+    const Spec& PS = h->spec;
+    const bool pp_fits = pp_direct_t(PS.pp_rw_raw) > 0 && pp_direct_t(PS.pp_rw_state) > 0 && PS.pp_sw <= 64;
+    if (strategy == DBG_STRATEGY_PARTITIONED && !pp_fits)
         return fail(DBG_ERR_UNSUPPORTED, "dbg_agg_set_strategy: records too wide for the partitioned payload");
     h->strategy = strategy;
     h->pp = strategy == DBG_STRATEGY_PARTITIONED;
@@ -1904,6 +1912,7 @@ static int fin_launch(dbg_agg_handle* h) {
         ff.seq = F.seq;
         ff.recycle = h->recycle;
         ff.on = 1;
+        ff.table_empty = h->def_clean ? 1 : 0;
         ff.trace = nullptr;
         static u64* x_trace = nullptr;  // EXPERIMENT (DBG_X_TRACE): 8 words per launch, 4096 launches
         static std::vector<u64> x_init;
@@ -1971,11 +1980,24 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
         // instead of a stream synchronisation (whose wake-up costs several microseconds); after
         // ~20 ms fall back to the blocking wait (long queued inserts)
         volatile u64* hseq = h->hcounters + CNT_WORDS + 2 + DBG_MAX_KEYS;
-        bool seen = false;
+        volatile u64* hcomp = h->hcounters + MIRROR_COMPACT;
+        bool seen = false, compact = false;
         auto t0 = std::chrono::steady_clock::now();
         for (u64 it = 0;; ++it) {
             if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == F.seq) {
                 seen = true;
+                break;
+            }
+            // the count-only fused finalize posts one word [seq | recycled | groups] when its
+            // counters are known (every group claimed in the launch, no overflow)
+            const u64 cw = __atomic_load_n(hcomp, __ATOMIC_ACQUIRE);
+            if ((cw >> 25) == (F.seq & ((1ULL << 39) - 1))) {
+                for (int w = 0; w < CNT_WORDS; ++w) h->hcounters[w] = 0;
+                h->hcounters[CNT_CLAIMS] = cw & 0xFFFFFF;
+                h->hcounters[CNT_WORDS] = cw & 0xFFFFFF;
+                for (int c = 0; c < DBG_MAX_KEYS; ++c) h->hcounters[CNT_WORDS + 1 + c] = 0;
+                h->hcounters[CNT_WORDS + 1 + DBG_MAX_KEYS] = (cw >> 24) & 1;
+                seen = compact = true;
                 break;
             }
             if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;

@@ -819,7 +819,7 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
 template <int MAXPER>
 __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDesc* batches, const TableDesc& t, const u64* view,
                                                     const OutDesc& out, u64* totals, u64* host_mirror, int recycle, u64 seq,
-                                                    u64* trace = nullptr) {
+                                                    u64* trace = nullptr, bool writeback = false) {
     __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
     __shared__ u64 cnts[CNT_WORDS];
     auto mark = [&](int k) { if (trace && threadIdx.x == 0) trace[k] = __builtin_amdgcn_s_memrealtime(); };
@@ -953,6 +953,8 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
         }
     }
     mark(10);
+    if (!rc && writeback)  // `view` is an LDS table the HBM table does not hold yet
+        for (u64 i = threadIdx.x; i < n_slots * t.stride_words; i += FIN_NT) t.slots[i] = view[i];
     if (rc) {  // table_init of the owned slots that were claimed (an EMPTY slot is still in its
                // initial state: state words are only written after the entry is claimed)
         const u32 sw = (u32)t.stride_words;
@@ -1012,6 +1014,315 @@ __device__ __forceinline__ void fused_finalize(const Spec& S, const BatchDesc* b
     if (ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
     finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq,
                                                   ff.trace);
+    if (ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
+}
+
+// merge_states of a parked partial state (sc1 loads) into a slot; COUNT(*) alone (CO): one add
+template <int AS, bool CO>
+__device__ __forceinline__ void merge_parked(const Spec& S, u64* st, const u64* r, u64 c1) {
+    if constexpr (CO) {  // c1: the parked count, loaded with the entry
+        if (c1) at_add<AS>(asp<AS>(st + 1), c1);
+    } else {
+        apply_state<AS, true>(S, asp<AS>(st), r);
+    }
+}
+
+// finalize_small_body for the COUNT(*)-only fast kernel (one non-null integer key of type T,
+// slots [key][count]): the same outputs, counters, recycle and host mirror in a fraction of the
+// code — this tail runs once per launch on whichever CU finishes last, from a cold instruction
+// cache, so its length is latency.
+template <typename T>
+__device__ __forceinline__ void finalize_count_only(const TableDesc& t, const u64* view, const FusedFin& ff, bool known) {
+    __shared__ u64 wsum[FIN_NT / 64];
+    __shared__ u64 cnts[CNT_WORDS];
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    const OutDesc& out = ff.out;
+    const u64 n_slots = t.cap + 1;
+    constexpr u32 PER = FUSED_FIN_SLOTS / FIN_NT;
+    const u64 base = (u64)threadIdx.x * PER;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 myc = (!known && threadIdx.x < CNT_WORDS) ? ld_sc1(t.counters + threadIdx.x) : 0;
+    u64 ent[PER];
+    u32 occ = 0, cnt = 0;
+#pragma unroll
+    for (u32 k = 0; k < PER; ++k) {
+        const u64 s = base + k;
+        ent[k] = s < n_slots ? view[s * 2] : SLOT_EMPTY;
+        if (ent[k] != SLOT_EMPTY) {
+            occ |= 1u << k;
+            cnt++;
+        }
+    }
+    u64 ic = cnt;
+    for (int off = 1; off < 64; off <<= 1) {
+        const u64 o = __shfl_up(ic, off, 64);
+        if (lane >= off) ic += o;
+    }
+    if (lane == 63) wsum[wave] = ic;
+    lds_barrier();
+    u64 p = ic - cnt, total = 0;
+    for (int w = 0; w < FIN_NT / 64; ++w) {
+        if (w < wave) p += wsum[w];
+        total += wsum[w];
+    }
+#pragma unroll
+    for (u32 k = 0; k < PER; ++k) {
+        if (!((occ >> k) & 1) || p >= out.cap_groups) continue;
+        const u64 s = base + k;
+        ((T*)out.key_data[0])[p] = (T)(s == t.cap ? SLOT_EMPTY : ent[k]);
+        ((u64*)out.agg_data[0])[p] = view[s * 2 + 1];
+        p++;
+    }
+    if (threadIdx.x == 0) ff.totals[0] = total;
+    // known: every group of the table was claimed in this launch, nothing overflowed
+    if (known) myc = threadIdx.x == CNT_CLAIMS ? total : 0;
+    if (threadIdx.x < CNT_WORDS) cnts[threadIdx.x] = myc;
+    lds_barrier();
+    const bool rc = ff.recycle && cnts[CNT_OVF_ROWS] == 0 && cnts[CNT_OVF_RECS] == 0 && total <= out.cap_groups;
+    if (rc && threadIdx.x < CNT_WORDS) t.counters[threadIdx.x] = 0;  // dbg_agg_reset
+    u64* hm = ff.host_mirror;
+    auto put = [&](int w, u64 v) { __hip_atomic_store(hm + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    // known counters: one self-validating word ([seq | recycled | groups], MIRROR_COMPACT) instead
+    // of the counter words and a seq posted behind a wait for them
+    const bool compact = known && total < (1u << 24);
+    if (hm && compact && threadIdx.x == 0)
+        put(MIRROR_COMPACT, (ff.seq << 25) | ((rc ? 1ULL : 0ULL) << 24) | total);
+    if (hm && !compact && threadIdx.x == 0) {
+        for (int w = 0; w < CNT_WORDS; ++w) put(w, cnts[w]);
+        put(CNT_WORDS, total);
+        put(CNT_WORDS + 1, 0);  // string bytes of the (integer) key column
+        put(CNT_WORDS + 1 + DBG_MAX_KEYS, rc ? 1 : 0);
+    }
+    if (!rc)  // the table outlives this finalize: the view holds groups the HBM table does not
+        for (u64 i = threadIdx.x; i < n_slots * 2; i += FIN_NT) t.slots[i] = view[i];
+    if (rc)  // table_init of the claimed slots of the view (the HBM copy may hold fewer: same values)
+#pragma unroll
+        for (u32 k = 0; k < PER; ++k)
+            if ((occ >> k) & 1) {
+                u64* d = t.slots + (base + k) * 2;
+                d[0] = SLOT_EMPTY;
+                d[1] = 0;
+            }
+    if (hm && !compact && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(hm + CNT_WORDS + 2 + DBG_MAX_KEYS, ff.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Find or claim `key` (inline) in an LDS copy of the HBM table (same slots, same probing as
+// g_find).  false: the probe limit was hit.
+__device__ __forceinline__ bool view_find(u64* view, const TableDesc& t, u64 key, u32& claims, u64& slot) {
+    const u32 sw = t.stride_words;
+    if (key == SLOT_EMPTY) {  // the all-ones 8-byte key: sentinel slot, entry 0 once claimed
+        slot = t.cap;
+        claims += at_cas<AS_LDS>(asp<AS_LDS>(view + t.cap * sw), SLOT_EMPTY, 0ULL) == SLOT_EMPTY ? 1u : 0u;
+        return true;
+    }
+    const u64 mask = t.cap - 1;
+    u64 s = slot_mix(key) & mask;
+    for (u32 p = 0; p < t.probe_limit; ++p) {
+        wptr<AS_LDS> e = asp<AS_LDS>(view + s * sw);
+        u64 ev = vld<AS_LDS>(e);
+        if (ev == SLOT_EMPTY) {
+            const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
+            if (old == SLOT_EMPTY) {
+                claims++;
+                slot = s;
+                return true;
+            }
+            ev = old;
+        }
+        if (ev == key) {
+            slot = s;
+            return true;
+        }
+        s = (s + 1) & mask;
+    }
+    return false;
+}
+
+// The low-cardinality end of a fused insert + finalize launch (ClickBench Q8: 32 groups in every
+// workgroup's LDS table).  The HBM table is not written on the way: partial tables travel as
+// parked rows up a two-level tree and are merged in LDS, and the last workgroup finalizes from
+// an LDS view of the table with the group tables merged in.
+//   1. every workgroup parks its LDS table (<= SCR_ENTRIES groups; a larger one flushes into the
+//      HBM table as block_flush does) and takes its group's ticket;
+//   2. the last workgroup of each group of SCR_GROUP merges the group's parked rows in LDS,
+//      parks the merged table in the group's row and takes the launch ticket;
+//   3. the last group leader copies the HBM table (groups of earlier launches and direct flushes)
+//      into LDS, merges every group row into that view and runs the finalize body on it.  The
+//      view goes back to HBM only when the table outlives the finalize (no recycle) or a key did
+//      not fit the view (overflow record: the host grows the table and finalizes again).
+// Each hand-off is a store drain + one ticket + sc1 loads (MI355X_MICROARCH.md, inter-workgroup
+// visibility); against block_flush + fused_finalize this saves the HBM probe / CAS / atomic
+// round trips of the group leaders' flush and one barrier + ticket level.
+template <typename T, bool CO>
+__device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots,
+                                            u32 sw, u32* lcount, u32 nt, const TableDesc& t, u32 my_claims, u32 my_ovf,
+                                            const FusedFin& ff) {
+    __shared__ u32 role, bad, vcl, wg_ovf;  // (the view overwrites lcount: the table copy extends past lds_slots)
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    u64* counts = t.scratch;
+    u64* tickets = t.scratch + t.scr_blocks;
+    u64* gmeta = tickets + t.scr_blocks / 2;  // [group] parked entries of the group row
+    u64* rows = t.scratch + 2 * (u64)t.scr_blocks;
+    u64* grows = rows + (u64)t.scr_blocks * SCR_ENTRIES * sw;
+    const u32 n_groups = (gridDim.x + SCR_GROUP - 1) / SCR_GROUP;
+    const u32 g = blockIdx.x / SCR_GROUP;
+    const u32 gsize = min((u32)SCR_GROUP, gridDim.x - g * SCR_GROUP);
+    if (threadIdx.x == 0) wg_ovf = 0;
+    __syncthreads();
+    // park the LDS table (compacted) in `dst` with sc1 stores, or flush it into the HBM table when
+    // it holds more than a row takes (counted as a possible overflow: the flush may push
+    // records); returns the parked entries (uniform)
+    auto park = [&](u64* dst) -> u64 {
+        if (lcount[0] > SCR_ENTRIES) {
+            flush_lds_direct<true, false>(S, batches, B, lds, lds_slots, sw, nt, t, my_claims);
+            my_ovf += threadIdx.x == 0 ? 1u : 0u;
+            return 0;
+        }
+        for (u32 s = threadIdx.x; s < lds_slots; s += nt) {
+            const u64* p = lds + (u64)s * sw;
+            if (p[0] == SLOT_EMPTY) continue;
+            const u32 k = atomicAdd(&lcount[2], 1u);
+            u64* d = dst + (u64)k * sw;
+            for (u32 w = 0; w <= (u32)S.n_words; ++w) st_sc1(d + w, p[w]);
+        }
+        __syncthreads();
+        return lcount[2];
+    };
+    // HBM claims of this workgroup into the table counter, then a ticket (thread 0; both device
+    // atomics complete in order: the ticket's taker sees the claims)
+    // A ticket word carries, besides the arrivals (bits [0, 16)), the HBM claims (bits [16, 40))
+    // and the possible overflow pushes (bits [40, 64)) of the workgroups that took it, so the last
+    // arrival knows without another load whether this launch created groups in HBM or pushed
+    // overflow records (the finalize then needs neither the table nor the counters).
+    auto claims_and_ticket = [&](u64* ticket, u64 carried_claims, u64 carried_ovf) -> u64 {
+        if (my_claims) atomicAdd(&lcount[1], my_claims);
+        if (my_ovf) atomicAdd(&wg_ovf, my_ovf);
+        my_claims = my_ovf = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        u64 tk = 0;
+        if (threadIdx.x == 0) {
+            if (lcount[1]) {
+                atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const u64 add = 1 + ((carried_claims + lcount[1]) << 16) + ((carried_ovf + wg_ovf) << 40);
+            tk = atomicAdd((unsigned long long*)ticket, (unsigned long long)add) + add;  // inclusive
+        }
+        return tk;
+    };
+    // 1. park, group ticket
+    const u64 np = park(rows + (u64)blockIdx.x * SCR_ENTRIES * sw);
+    if (threadIdx.x == 0) st_sc1(counts + blockIdx.x, np);
+    __shared__ u64 hbm_claims, ovf_seen;  // this launch's HBM claims / possible overflow pushes: the
+                                          // group's (leader), all (last leader)
+    {
+        const u64 tk = claims_and_ticket(tickets + g, 0, 0);
+        if (threadIdx.x == 0) {
+            role = (tk & 0xFFFF) == gsize ? 1u : 0u;
+            hbm_claims = (tk >> 16) & 0xFFFFFF;
+            ovf_seen = tk >> 40;
+            wg_ovf = 0;
+        }
+    }
+    __syncthreads();
+    if (!role) return;
+    // 2. group leader: merge the group's parked rows in LDS, park the result in the group row
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tickets[g] = 0;  // ready for the next launch on this table (all members have added)
+        lcount[0] = lcount[1] = lcount[2] = 0;
+    }
+    lds_table_init(S, lds, lds_slots, sw, nt);
+    __syncthreads();
+    for (u32 f = threadIdx.x; f < gsize * SCR_ENTRIES; f += nt) {
+        const u64 b = (u64)g * SCR_GROUP + f / SCR_ENTRIES, k = f % SCR_ENTRIES;
+        const u64* r = rows + (b * SCR_ENTRIES + k) * sw;
+        const u64 cnt = ld_sc1(counts + b);
+        const u64 e = ld_sc1(r);  // issued with the count: rows are allocated in full
+        const u64 c1 = CO ? ld_sc1(r + 1) : 0;  // COUNT(*): the whole state, in the same round trip
+        if (k >= cnt) continue;
+        const int ls = lds_find<true>(S, batches, B.keys, 0, e, 0, lds, lmask, sw, lcount, llimit);
+        if (ls >= 0) {
+            merge_parked<AS_LDS, CO>(S, lds + (u64)ls * sw, r, c1);
+            continue;
+        }
+        bool claimed;
+        const u64 gs = g_find<true>(S, batches, B.keys, 0, e, 0, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_rec<true>(S, t, e, r);
+            my_ovf++;
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        merge_parked<AS_GLB, CO>(S, t.slots + gs * t.stride_words, r, c1);
+    }
+    __syncthreads();
+    const u64 gp = park(grows + (u64)g * SCR_ENTRIES * sw);
+    if (threadIdx.x == 0) st_sc1(gmeta + g, gp);
+    {
+        const u64 tk = claims_and_ticket(t.counters + CNT_FIN_TICKET, hbm_claims, ovf_seen);
+        if (threadIdx.x == 0) {
+            role = (tk & 0xFFFF) == n_groups ? 2u : 0u;
+            hbm_claims = (tk >> 16) & 0xFFFFFF;
+            ovf_seen = tk >> 40;
+        }
+    }
+    __syncthreads();
+    if (ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (role != 2) return;
+    // 3. the last group leader: view of the HBM table, group rows merged into it, finalize
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
+        bad = 0;
+        vcl = 0;
+        if (ff.trace) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
+    }
+    // the view: the HBM table, or its initial state when it was empty at launch start (recycled
+    // by the previous finalize) and no workgroup of this launch created a group in it
+    const u64 n = (t.cap + 1) * sw;  // host: <= the launch's dynamic LDS
+    if (ff.table_empty && hbm_claims == 0)
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = S.slot_init[i % sw];
+    else
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = ld_sc1(t.slots + i);
+    __syncthreads();
+    u32 vclaims = 0;
+    for (u32 f = threadIdx.x; f < n_groups * SCR_ENTRIES; f += nt) {
+        const u64 gg = f / SCR_ENTRIES, k = f % SCR_ENTRIES;
+        const u64* r = grows + (gg * SCR_ENTRIES + k) * sw;
+        const u64 cnt = ld_sc1(gmeta + gg);
+        const u64 e = ld_sc1(r);
+        const u64 c1 = CO ? ld_sc1(r + 1) : 0;
+        if (k >= cnt) continue;
+        u64 slot;
+        if (view_find(lds, t, e, vclaims, slot)) {
+            merge_parked<AS_LDS, CO>(S, lds + slot * sw, r, c1);
+        } else {
+            push_ovf_rec<true>(S, t, e, r);
+            bad = 1;
+        }
+    }
+    if (vclaims) atomicAdd(&vcl, vclaims);
+    __syncthreads();
+    if (threadIdx.x == 0 && vcl) {
+        atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)vcl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
+    // the finalize writes the view back when the table outlives it (no recycle: short buffers, an
+    // overflow record, or a caller that keeps the table)
+    // counters known without a load: an empty table at launch start, no overflow anywhere
+    if constexpr (CO) finalize_count_only<T>(t, lds, ff, ff.table_empty && ovf_seen == 0 && !bad);
+    else finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq,
+                                                       ff.trace, true);
     if (ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -1088,6 +1399,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
     u32 my_claims = 0;
+    u32 my_ovf = 0;  // overflow rows pushed (the fused chain reports them through its tickets)
 
     // predicate in range form: lo <= v <= hi, xor negate (host maps =, <>, <, <=, >, >=)
     auto pass = [&](T v) -> bool { return ((v >= lo) & (v <= hi)) ^ (negate != 0); };
@@ -1105,6 +1417,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         u64 gs = g_find<true>(S, batches, nullptr, i, key, 0, t, t.probe_limit, claimed);
         if (gs == ~0ULL) {
             push_ovf_row(t, bid, i);
+            my_ovf++;
             return;
         }
         my_claims += claimed ? 1 : 0;
@@ -1339,6 +1652,10 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         const u64 tm = __builtin_amdgcn_s_memrealtime();
         atomicMin((unsigned long long*)ff.trace + 1, (unsigned long long)tm);
         atomicMax((unsigned long long*)ff.trace + 2, (unsigned long long)tm);
+    }
+    if (ff.on && t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks) {
+        fused_chain<T, CO>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims, my_ovf, ff);
+        return;
     }
     block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
     if (ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());

@@ -78,13 +78,17 @@ struct TableDesc {
     u64* ovf_recs;  // [keyref][words...] per record, stride = stride_words
     u64 ovf_recs_cap;
     // per-workgroup parking rows of small LDS tables (merged by the last workgroup of each group,
-    // see block_flush in agg.hip): [count u64 x scr_blocks][group tickets u64 x scr_blocks]
-    // [scr_blocks x SCR_ENTRIES x stride_words]
+    // see block_flush in agg.hip): [count u64 x scr_blocks][group tickets u64 x scr_blocks / 2]
+    // [group meta u64 x scr_blocks / 2][scr_blocks x SCR_ENTRIES x stride_words]
+    // [scr_blocks / SCR_GROUP group rows x SCR_ENTRIES x stride_words] (fused chain)
     u64* scratch;
     u32 scr_blocks;
 };
 #define SCR_ENTRIES 64
 #define SCR_GROUP 16
+inline size_t scr_words(u32 blocks, u32 stride_words) {
+    return (size_t)blocks * (2 + (size_t)SCR_ENTRIES * stride_words) + (size_t)(blocks / SCR_GROUP) * SCR_ENTRIES * stride_words;
+}
 #define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
 enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_FIN_TICKET = 6, CNT_WORDS = 8 };
@@ -238,6 +242,10 @@ void launch_ser_compact(hipStream_t s, const u8* lens, const u8* src, u32 stride
 // finalize_small fused into the fast insert: the last workgroup to finish runs it (one launch per
 // batch).  Tables of at most FUSED_FIN_SLOTS slots whose copy fits the insert's LDS.
 #define FUSED_FIN_SLOTS 2048
+// host mirror words: [0, CNT_WORDS) counters, CNT_WORDS totals (+ string bytes per key), then
+// recycled, seq, and the compact word [seq << 25 | recycled << 24 | groups] that the count-only
+// fused finalize posts alone when its counters are known (no wait between mirror stores)
+#define MIRROR_COMPACT (CNT_WORDS + 3 + DBG_MAX_KEYS)
 struct FusedFin {
     OutDesc out;
     u64* totals;
@@ -245,6 +253,7 @@ struct FusedFin {
     u64 seq;
     int recycle;
     int on;
+    int table_empty;  // the HBM table held no group when the launch started (fused chain)
     u64* trace;  // EXPERIMENT (DBG_X_TRACE): phase timestamps of this launch, s_memrealtime ticks
 };
 // host side: would launch_insert of this batch take the fast kernel (and so could fuse)?
@@ -269,6 +278,13 @@ struct PPChunk {
 };
 #define PP_L1_BITS 8
 #define PP_CHUNK 262144  // rows / records per scatter work unit
+// direct scatter tiles: rows whose records are built in a 32 KiB LDS scratch per step (pp.hip)
+#define PP_NT 512  // threads per workgroup of the partitioned-payload kernels
+#define PP_SCRATCH_BYTES (32 * 1024)
+__host__ __device__ __forceinline__ u32 pp_direct_t(u32 rw) {  // threads with a row per step (0: too wide)
+    const u32 t = PP_SCRATCH_BYTES / rw;
+    return t >= PP_NT ? PP_NT : (t & ~63u);
+}
 // sample probe: distinct group hashes among sampled selected rows -> out[0] selected, [1] distinct,
 // [2] singletons (f1), [3] doubletons (f2)
 void launch_pp_sample(hipStream_t s, const Spec* dspec, const BatchDesc* batches, u32 bid, u64 rows, u64 n_sample,

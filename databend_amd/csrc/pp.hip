@@ -20,7 +20,6 @@
 #include "agg.hpp"
 #include "agg_dev.hpp"
 
-#define PP_NT 512
 #define PP_AGG_NT 512
 #define PP_AGG_LDS (72 * 1024)  // two workgroups per CU
 #define PP_AU 4                  // raw records per thread in flight (aggregation)
@@ -556,11 +555,6 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* wtot, u32& total) {
 // per-thread LDS scratch slot where a raw row's record is built (W == 0).  Three barriers per tile;
 // the records of one bucket land contiguously within the tile, so the XCD's L2 merges them into
 // whole lines.  LDS: hist u32 [K] | run u64 [K] | scratch [T * U * rw] (W == 0).
-#define PP_SCRATCH_BYTES (32 * 1024)
-__host__ __device__ __forceinline__ u32 pp_direct_t(u32 rw) {  // threads with a row per step
-    const u32 t = PP_SCRATCH_BYTES / rw;
-    return t >= PP_NT ? PP_NT : (t & ~63u);
-}
 __host__ __device__ __forceinline__ u32 pp_direct_u(int W, u32 rw) {  // rows per thread per step
     if (W > 0) return W <= 2 ? 4 : (W <= 4 ? 2 : 1);
     const u32 u = PP_SCRATCH_BYTES / (PP_NT * rw);

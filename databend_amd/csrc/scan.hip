@@ -1,0 +1,945 @@
+// scan.hip — Parquet column chunks decoded into HBM columns (include/dbgpu_scan.h).
+//
+// The Fuse read path hands one leaf column chunk (page headers + pages) to arrow-rs's parquet
+// reader (BlockReader::deserialize_parquet_chunks -> column_chunks_to_record_batch,
+// storages/fuse/src/io/read/block/parquet/mod.rs:45-60, deserialize.rs:33-80).  Here the page
+// headers (Thrift compact, a few dozen bytes per page) are parsed on the host and every page is
+// decoded on the device, one workgroup per page:
+//
+//   pq_inflate   one wave per page: UNCOMPRESSED copy, or a SNAPPY / LZ4_RAW block decode.  The
+//                element stream is parsed by the whole wave in lockstep (uniform loads, no lane
+//                divergence); literals and back-references are copied 64 bytes per step, and
+//                back-references read a 64 KiB LDS ring of the page's recent output (both formats
+//                reference at most 64 KiB back — an offset beyond the ring is a decode error).
+//   pq_walk      one lane per BYTE_ARRAY page: the value starts of PLAIN byte arrays (u32 length
+//                prefixes) — a dependent chain inside a page, parallel across pages.
+//   pq_decode    one workgroup per data page: definition levels and dictionary indices through
+//                the RLE / bit-packed hybrid (thread 0 parses run headers into an LDS run table,
+//                all threads expand values by binary search over the runs), a block scan of the
+//                definition bits gives every row its value index, then PLAIN / dictionary values
+//                are converted to the Databend type and written at their row (arrow layout: NULL
+//                rows hold a zero slot, validity bytes packed afterwards).
+//   pq_strings   String payload gather after the offsets scan.
+// All integer / byte work, HBM- or latency-bound; every device read is bounds-checked against its
+// page (a malformed page sets an error bit, it never faults).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "agg.hpp"
+#include "../../include/dbgpu_scan.h"
+
+int abi_fail(int code, const std::string& msg);  // abi.hip: sets dbg_last_error
+void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);
+void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total);
+
+namespace {
+
+enum { PG_DATA_V1 = 0, PG_DATA_V2 = 1, PG_DICT = 2 };
+enum { ENC_PLAIN = 0, ENC_PLAIN_DICT = 2, ENC_RLE = 3, ENC_RLE_DICT = 8 };
+enum { SERR_MALFORMED = 1, SERR_COUNT = 2, SERR_NULL_IN_REQUIRED = 4, SERR_DICT_RANGE = 8 };
+
+struct ScanPage {
+    u64 src;          // payload offset in the chunk
+    u64 dst;          // decompressed page offset in the page buffer
+    u64 row0;         // first output row (data pages)
+    u64 vk0;          // first slot of this page's values in the index / value-start arrays
+    u32 comp, uncomp; // payload sizes (v2: levels included)
+    u32 num_values;
+    u32 lv;           // v2: repetition + definition level bytes (stored uncompressed in front)
+    u32 def_len;      // v2: definition level bytes
+    u8 kind;          // PG_*
+    u8 compressed;    // the payload after `lv` is compressed with the chunk's codec
+    u8 encoding;
+    u8 pad;
+};
+
+struct ScanArgs {
+    const u8* chunk;
+    u8* buf;           // decompressed pages
+    const ScanPage* pages;
+    u32 n_pages;
+    int32_t ptype, tlen, max_def, codec;
+    int32_t ttype;     // target dbg_type
+    u32 twidth;        // target value width (bytes)
+    int32_t dict_page; // index of the dictionary page, -1 none
+    u64 rows;
+    u8* vbytes;        // [rows] definition flags
+    u32* idx;          // [rows] dictionary indices / RLE booleans by value index
+    u64* vstart;       // [rows + dict values] BYTE_ARRAY value starts (page-relative)
+    u32* nwalk;        // [n_pages] values found by pq_walk
+    u64* sptr;         // [rows] String payload source offsets in buf
+    u8* out_data;      // target values (BOOLEAN: value bytes, packed afterwards)
+    u64* out_offs;     // String: lengths, then the scan
+    u64* err;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Decompression (one wave per page).  Loads of the compressed stream are wave-uniform.
+// ---------------------------------------------------------------------------------------------
+#define RING 65536
+__device__ __forceinline__ u32 ld_u8(const u8* p) { return *(const volatile u8*)p; }
+
+template <int CODEC>
+__global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
+    __shared__ u8 ring[RING];
+    const ScanPage pg = a.pages[blockIdx.x];
+    const u32 lane = threadIdx.x;
+    const u8* src = a.chunk + pg.src;
+    u8* dst = a.buf + pg.dst;
+    // v2 levels (uncompressed) first
+    for (u32 j = lane; j < pg.lv; j += 64) dst[j] = src[j];
+    const u8* s = src + pg.lv;
+    u8* o = dst + pg.lv;
+    const u32 sn = pg.comp - pg.lv, on = pg.uncomp - pg.lv;
+    if (CODEC == DBG_PQ_UNCOMPRESSED || !pg.compressed) {
+        if (sn != on) {
+            if (lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+            return;
+        }
+        for (u32 j = lane; j < on; j += 64) o[j] = s[j];
+        return;
+    }
+    bool bad = false;
+    u32 p = 0, w = 0;  // input / output cursors (uniform)
+    auto copy_lit = [&](u32 len) {
+        if (p + len > sn || w + len > on) { bad = true; return; }
+        for (u32 j = lane; j < len; j += 64) {
+            const u8 b = s[p + j];
+            o[w + j] = b;
+            ring[(w + j) & (RING - 1)] = b;
+        }
+        __builtin_amdgcn_wave_barrier();
+        p += len;
+        w += len;
+    };
+    auto copy_back = [&](u32 off, u32 len) {
+        if (off == 0 || off > w || off > RING || w + len > on) { bad = true; return; }
+        // byte j repeats the last `off` bytes: out[w + j] = out[w - off + j % off]; chunks of at
+        // most `off` bytes so that every source byte is in the ring before it is read
+        for (u32 c0 = 0; c0 < len; c0 += 64) {
+            const u32 j = c0 + lane;
+            u8 b = 0;
+            if (j < len) b = ring[(w - off + (j % off)) & (RING - 1)];
+            __builtin_amdgcn_wave_barrier();
+            if (j < len) {
+                o[w + j] = b;
+                ring[(w + j) & (RING - 1)] = b;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        w += len;
+    };
+    if (CODEC == DBG_PQ_SNAPPY) {
+        u32 n = 0, sh = 0;  // preamble: uncompressed length (varint)
+        for (;;) {
+            if (p >= sn || sh > 28) { bad = true; break; }
+            const u32 c = ld_u8(s + p++);
+            n |= (c & 0x7F) << sh;
+            sh += 7;
+            if (!(c & 0x80)) break;
+        }
+        if (n != on) bad = true;
+        while (!bad && p < sn) {
+            const u32 tag = ld_u8(s + p++);
+            const u32 kind = tag & 3;
+            if (kind == 0) {
+                u32 len = tag >> 2;
+                if (len >= 60) {
+                    const u32 nb = len - 59;
+                    if (p + nb > sn) { bad = true; break; }
+                    len = 0;
+                    for (u32 k = 0; k < nb; ++k) len |= ld_u8(s + p + k) << (8 * k);
+                    p += nb;
+                }
+                copy_lit(len + 1);
+            } else {
+                u32 len, off;
+                if (kind == 1) {
+                    if (p + 1 > sn) { bad = true; break; }
+                    len = ((tag >> 2) & 7) + 4;
+                    off = ((tag >> 5) << 8) | ld_u8(s + p);
+                    p += 1;
+                } else if (kind == 2) {
+                    if (p + 2 > sn) { bad = true; break; }
+                    len = (tag >> 2) + 1;
+                    off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8);
+                    p += 2;
+                } else {
+                    if (p + 4 > sn) { bad = true; break; }
+                    len = (tag >> 2) + 1;
+                    off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8) | (ld_u8(s + p + 2) << 16) | (ld_u8(s + p + 3) << 24);
+                    p += 4;
+                }
+                copy_back(off, len);
+            }
+        }
+    } else {  // LZ4 block: [token][literal length+][literals][offset u16][match length+]
+        while (!bad && p < sn) {
+            const u32 tok = ld_u8(s + p++);
+            u32 lit = tok >> 4;
+            if (lit == 15)
+                for (;;) {
+                    if (p >= sn) { bad = true; break; }
+                    const u32 c = ld_u8(s + p++);
+                    lit += c;
+                    if (c != 255) break;
+                }
+            if (bad) break;
+            copy_lit(lit);
+            if (bad || p >= sn) break;  // the last sequence has literals only
+            if (p + 2 > sn) { bad = true; break; }
+            const u32 off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8);
+            p += 2;
+            u32 ml = tok & 15;
+            if (ml == 15)
+                for (;;) {
+                    if (p >= sn) { bad = true; break; }
+                    const u32 c = ld_u8(s + p++);
+                    ml += c;
+                    if (c != 255) break;
+                }
+            if (bad) break;
+            copy_back(off, ml + 4);
+        }
+    }
+    if ((bad || w != on) && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Page-relative layout helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ u32 rd_u32(const u8* p) { return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24); }
+
+// start of the values section and the definition-level byte range [d0, d1) of a data page
+__device__ __forceinline__ bool page_sections(const ScanArgs& a, const ScanPage& pg, const u8* base, u32& d0, u32& d1, u32& vp) {
+    d0 = d1 = vp = 0;
+    if (pg.kind == PG_DICT) return true;
+    if (pg.kind == PG_DATA_V2) {
+        d0 = pg.lv - pg.def_len;
+        d1 = pg.lv;
+        vp = pg.lv;
+        return pg.lv <= pg.uncomp;
+    }
+    if (a.max_def) {
+        if (pg.uncomp < 4) return false;
+        const u32 ln = rd_u32(base);
+        if (ln > pg.uncomp - 4) return false;
+        d0 = 4;
+        d1 = 4 + ln;
+        vp = d1;
+    }
+    return true;
+}
+
+// one lane per BYTE_ARRAY page: starts of the PLAIN values (positions of their u32 length)
+__global__ void __launch_bounds__(64) pq_walk_kernel(ScanArgs a) {
+    const u32 pi = blockIdx.x * 64 + threadIdx.x;
+    if (pi >= a.n_pages) return;
+    const ScanPage pg = a.pages[pi];
+    if (pg.encoding != ENC_PLAIN && pg.kind != PG_DICT) return;
+    const u8* base = a.buf + pg.dst;
+    u32 d0, d1, vp;
+    if (!page_sections(a, pg, base, d0, d1, vp)) {
+        atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+        return;
+    }
+    u64 p = vp, k = 0;
+    const u64 end = pg.uncomp, cap = pg.num_values;
+    while (p + 4 <= end && k < cap) {
+        const u32 len = rd_u32(base + p);
+        if (p + 4 + len > end) break;
+        a.vstart[pg.vk0 + k] = p;
+        ++k;
+        p += 4 + (u64)len;
+    }
+    if (p != end && k < cap) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+    a.nwalk[pi] = (u32)k;
+}
+
+// ---------------------------------------------------------------------------------------------
+// RLE / bit-packed hybrid, expanded by a whole workgroup
+// ---------------------------------------------------------------------------------------------
+#define DEC_NT 256
+#define RMAX 512
+struct RunTable {
+    u32 start[RMAX + 1];  // first value index of each run (start[nr] = end of the last one)
+    u32 info[RMAX];       // bit-packed: byte offset of the packed values; RLE: the value
+    u8 packed[RMAX];
+    u32 nr, kend, pos, bad;
+};
+
+// Expand `n` values of bit width `bw` from [p0, p1) of `base`; put(k, v) for every k < n.
+template <typename PUT>
+__device__ __forceinline__ bool hybrid_expand(const u8* base, u32 p0, u32 p1, u32 bw, u32 n, RunTable& rt, PUT put) {
+    if (threadIdx.x == 0) {
+        rt.pos = p0;
+        rt.kend = 0;
+        rt.bad = bw > 32 ? 1u : 0u;
+    }
+    __syncthreads();
+    const u32 vb = (bw + 7) / 8;
+    while (true) {
+        const u32 k0 = rt.kend;
+        if (k0 >= n || rt.bad) break;
+        __syncthreads();
+        if (threadIdx.x == 0) {  // parse up to RMAX run headers
+            u32 pos = rt.pos, k = k0, nr = 0;
+            bool bad = false;
+            while (nr < RMAX && k < n) {
+                if (pos >= p1) { bad = true; break; }
+                u32 h = 0, sh = 0;
+                for (;;) {
+                    if (pos >= p1 || sh > 28) { bad = true; break; }
+                    const u32 c = base[pos++];
+                    h |= (c & 0x7F) << sh;
+                    sh += 7;
+                    if (!(c & 0x80)) break;
+                }
+                if (bad) break;
+                rt.start[nr] = k;
+                if (h & 1) {
+                    const u32 groups = h >> 1;
+                    const u64 bytes = (u64)groups * bw;
+                    if ((u64)pos + bytes > p1 && (u64)pos + (((u64)(n - k) * bw + 7) / 8) > p1) { bad = true; break; }
+                    rt.info[nr] = pos;
+                    rt.packed[nr] = 1;
+                    pos += (u32)min<u64>(bytes, (u64)(p1 - pos));
+                    k += groups * 8;
+                } else {
+                    if (pos + vb > p1) { bad = true; break; }
+                    u32 v = 0;
+                    for (u32 j = 0; j < vb; ++j) v |= (u32)base[pos + j] << (8 * j);
+                    pos += vb;
+                    rt.info[nr] = v;
+                    rt.packed[nr] = 0;
+                    k += h >> 1;
+                    if ((h >> 1) == 0) { bad = true; break; }
+                }
+                ++nr;
+            }
+            rt.start[nr] = k;
+            rt.nr = nr;
+            rt.kend = min(k, n);
+            rt.pos = pos;
+            if (bad) rt.bad = 1;
+        }
+        __syncthreads();
+        if (rt.bad) break;
+        const u32 nr = rt.nr, ke = rt.kend;
+        for (u32 k = k0 + threadIdx.x; k < ke; k += DEC_NT) {
+            u32 lo = 0, hi = nr;  // last run with start <= k
+            while (hi - lo > 1) {
+                const u32 mid = (lo + hi) >> 1;
+                if (rt.start[mid] <= k) lo = mid;
+                else hi = mid;
+            }
+            u32 v;
+            if (rt.packed[lo]) {
+                const u64 bit = (u64)(k - rt.start[lo]) * bw;
+                const u32 bp = rt.info[lo] + (u32)(bit >> 3);
+                u64 x = 0;
+                for (u32 j = 0; j < 5 && bp + j < p1; ++j) x |= (u64)base[bp + j] << (8 * j);
+                v = bw ? (u32)((x >> (bit & 7)) & ((bw == 32) ? 0xFFFFFFFFull : ((1ull << bw) - 1))) : 0u;
+            } else {
+                v = rt.info[lo];
+            }
+            put(k, v);
+        }
+    }
+    __syncthreads();
+    return !rt.bad;
+}
+
+// physical value at `p` (PLAIN layout) -> target bytes at `d`
+__device__ __forceinline__ void put_value(const ScanArgs& a, const u8* p, u8* d) {
+    switch (a.ptype) {
+        case DBG_PQ_INT32: {
+            const u32 v = rd_u32(p);
+            if (a.ttype == DBG_DECIMAL128) {
+                const i64 x = (i64)(int32_t)v;
+                ((u64*)d)[0] = (u64)x;
+                ((u64*)d)[1] = x < 0 ? ~0ULL : 0ULL;
+            } else {
+                for (u32 j = 0; j < a.twidth; ++j) d[j] = (u8)(v >> (8 * j));
+            }
+            return;
+        }
+        case DBG_PQ_INT64: case DBG_PQ_DOUBLE: {
+            u64 v = 0;
+            for (int j = 0; j < 8; ++j) v |= (u64)p[j] << (8 * j);
+            if (a.ttype == DBG_DECIMAL128) {
+                ((u64*)d)[0] = v;
+                ((u64*)d)[1] = (i64)v < 0 ? ~0ULL : 0ULL;
+            } else {
+                *(u64*)d = v;
+            }
+            return;
+        }
+        case DBG_PQ_FLOAT: *(u32*)d = rd_u32(p); return;
+        default: {  // FIXED_LEN_BYTE_ARRAY: big-endian two's complement -> i128 LE
+            u64 lo = 0, hi = 0;
+            const u32 n = (u32)a.tlen;
+            for (u32 j = 0; j < n; ++j) {
+                const u64 b = p[n - 1 - j];
+                if (j < 8) lo |= b << (8 * j);
+                else hi |= b << (8 * (j - 8));
+            }
+            if (n < 16 && (p[0] & 0x80)) {  // sign-extend
+                if (n < 8) {
+                    lo |= ~0ULL << (8 * n);
+                    hi = ~0ULL;
+                } else {
+                    hi |= n == 8 ? ~0ULL : (~0ULL << (8 * (n - 8)));
+                }
+            }
+            ((u64*)d)[0] = lo;
+            ((u64*)d)[1] = hi;
+            return;
+        }
+    }
+}
+
+__device__ __forceinline__ u32 phys_width(const ScanArgs& a) {
+    switch (a.ptype) {
+        case DBG_PQ_INT32: case DBG_PQ_FLOAT: return 4;
+        case DBG_PQ_INT64: case DBG_PQ_DOUBLE: return 8;
+        case DBG_PQ_FIXED_LEN_BYTE_ARRAY: return (u32)a.tlen;
+        default: return 0;
+    }
+}
+
+__global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
+    __shared__ RunTable rt;
+    __shared__ u32 wtot[DEC_NT / 64];
+    __shared__ u32 s_bad;
+    const ScanPage pg = a.pages[blockIdx.x];
+    if (pg.kind == PG_DICT) return;
+    const u8* base = a.buf + pg.dst;
+    const u32 n = pg.num_values;
+    auto fail = [&](u64 bit) {
+        if (threadIdx.x == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)bit);
+    };
+    u32 d0, d1, vp;
+    if (!page_sections(a, pg, base, d0, d1, vp)) return fail(SERR_MALFORMED);
+    u8* vb = a.vbytes + pg.row0;
+    // 1. definition levels -> one byte per row
+    if (a.max_def) {
+        if (!hybrid_expand(base, d0, d1, 1, n, rt, [&](u32 k, u32 v) { vb[k] = (u8)(v != 0); })) return fail(SERR_MALFORMED);
+    } else {
+        for (u32 k = threadIdx.x; k < n; k += DEC_NT) vb[k] = 1;
+        __syncthreads();
+    }
+    // 2. dictionary indices (or RLE booleans) by value index
+    const bool dict = pg.encoding == ENC_PLAIN_DICT || pg.encoding == ENC_RLE_DICT;
+    const bool rle_bool = pg.encoding == ENC_RLE && a.ptype == DBG_PQ_BOOLEAN;
+    u32* ix = a.idx + pg.vk0;
+    if (dict || rle_bool) {
+        u32 p0 = vp, bw = 1, p1 = pg.uncomp;
+        if (dict) {
+            if (vp >= pg.uncomp) {  // a page of NULLs may carry no index bytes
+                p0 = p1;
+                bw = 0;
+            } else {
+                bw = base[vp];
+                p0 = vp + 1;
+            }
+        } else {
+            if (vp + 4 > pg.uncomp) return fail(SERR_MALFORMED);
+            p0 = vp + 4;
+            p1 = min<u32>(pg.uncomp, p0 + rd_u32(base + vp));
+        }
+        // the non-null count bounds the indices; count it first (defs are in vb)
+        __shared__ u32 s_nn;
+        if (threadIdx.x == 0) s_nn = 0;
+        __syncthreads();
+        u32 c = 0;
+        for (u32 k = threadIdx.x; k < n; k += DEC_NT) c += vb[k];
+        if (c) atomicAdd(&s_nn, c);
+        __syncthreads();
+        const u32 nn = s_nn;
+        if (bw == 0) {
+            for (u32 k = threadIdx.x; k < nn; k += DEC_NT) ix[k] = 0;
+            __syncthreads();
+        } else if (!hybrid_expand(base, p0, p1, bw, nn, rt, [&](u32 k, u32 v) { ix[k] = v; })) {
+            return fail(SERR_MALFORMED);
+        }
+    }
+    // 3. values, 256 rows per round: block scan of the definition bytes -> value index
+    const ScanPage* dp = a.dict_page >= 0 ? &a.pages[a.dict_page] : nullptr;
+    const u8* dbase = dp ? a.buf + dp->dst : nullptr;
+    const u32 dn = dp ? dp->num_values : 0;
+    const u32 pw = phys_width(a);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_bad = 0;
+    u32 vbase = 0;
+    for (u32 r0 = 0; r0 < n; r0 += DEC_NT) {
+        const u32 k = r0 + threadIdx.x;
+        const u32 def = k < n ? vb[k] : 0u;
+        const u64 bal = __ballot(def);
+        const u32 pre_w = (u32)__popcll(bal & ((1ULL << lane) - 1));
+        if (lane == 0) wtot[wave] = (u32)__popcll(bal);
+        __syncthreads();
+        u32 pre = 0, tot = 0;
+        for (int w = 0; w < DEC_NT / 64; ++w) {
+            if (w < wave) pre += wtot[w];
+            tot += wtot[w];
+        }
+        const u32 vi = vbase + pre + pre_w;
+        if (k < n) {
+            const u64 row = pg.row0 + k;
+            bool bad = false;
+            if (a.ptype == DBG_PQ_BYTE_ARRAY) {
+                u64 len = 0, so = 0;
+                if (def) {
+                    if (dict) {
+                        const u32 i = ix[vi];
+                        if (i >= dn || i >= a.nwalk[a.dict_page]) {
+                            bad = true;
+                        } else {
+                            const u64 st = a.vstart[dp->vk0 + i];
+                            len = rd_u32(dbase + st);
+                            so = dp->dst + st + 4;
+                        }
+                    } else if (vi >= a.nwalk[blockIdx.x]) {
+                        bad = true;
+                    } else {
+                        const u64 st = a.vstart[pg.vk0 + vi];
+                        len = rd_u32(base + st);
+                        so = pg.dst + st + 4;
+                    }
+                }
+                a.out_offs[row] = bad ? 0 : len;
+                a.sptr[row] = so;
+            } else if (a.ptype == DBG_PQ_BOOLEAN) {
+                u8 v = 0;
+                if (def) {
+                    if (rle_bool) {
+                        v = (u8)(ix[vi] & 1);
+                    } else if (vp + (vi >> 3) < pg.uncomp) {
+                        v = (base[vp + (vi >> 3)] >> (vi & 7)) & 1;
+                    } else {
+                        bad = true;
+                    }
+                }
+                a.out_data[row] = v;
+            } else {
+                u8* d = a.out_data + row * a.twidth;
+                const u8* sp = nullptr;
+                if (def) {
+                    if (dict) {
+                        const u32 i = ix[vi];
+                        if (i < dn && (u64)(i + 1) * pw <= dp->uncomp) sp = dbase + (u64)i * pw;
+                    } else if ((u64)vp + (u64)(vi + 1) * pw <= pg.uncomp) {
+                        sp = base + vp + (u64)vi * pw;
+                    }
+                    if (!sp) bad = true;
+                }
+                if (sp) put_value(a, sp, d);
+                else for (u32 j = 0; j < a.twidth; ++j) d[j] = 0;
+            }
+            if (bad) s_bad = 1;
+        }
+        vbase += tot;
+        __syncthreads();
+    }
+    if (s_bad) fail(SERR_DICT_RANGE);
+    // PLAIN byte arrays: every value the walk found is consumed exactly once
+    if (a.ptype == DBG_PQ_BYTE_ARRAY && !dict && threadIdx.x == 0 && vbase != a.nwalk[blockIdx.x])
+        atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_COUNT);
+    if (a.max_def == 0 && threadIdx.x == 0 && vbase != n) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_COUNT);
+}
+
+// payload gather: one lane per row
+__global__ void __launch_bounds__(256) pq_strings_kernel(const u8* __restrict__ buf, const u64* __restrict__ sptr,
+                                                         const u64* __restrict__ offs, u64 rows, u8* __restrict__ out, u64 cap) {
+    const u64 r = blockIdx.x * 256ULL + threadIdx.x;
+    if (r >= rows) return;
+    const u64 o = offs[r], e = offs[r + 1];
+    if (e > cap) return;
+    const u8* s = buf + sptr[r];
+    for (u64 j = 0; j < e - o; ++j) out[o + j] = s[j];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host: Thrift compact PageHeader (parquet-format parquet.thrift, fields used by the reader)
+// ---------------------------------------------------------------------------------------------
+struct Compact {
+    const u8* b;
+    u64 n, p;
+    bool ok = true;
+    u32 byte() {
+        if (p >= n) { ok = false; return 0; }
+        return b[p++];
+    }
+    u64 varint() {
+        u64 v = 0;
+        for (int sh = 0; sh < 64 && ok; sh += 7) {
+            const u32 c = byte();
+            v |= (u64)(c & 0x7F) << sh;
+            if (!(c & 0x80)) return v;
+        }
+        ok = false;
+        return 0;
+    }
+    i64 zigzag() {
+        const u64 v = varint();
+        return (i64)(v >> 1) ^ -(i64)(v & 1);
+    }
+    void skip(int t, int depth = 0) {
+        if (depth > 16) { ok = false; return; }
+        switch (t) {
+            case 1: case 2: return;
+            case 3: p += 1; return;
+            case 4: case 5: case 6: varint(); return;
+            case 7: p += 8; return;
+            case 8: p += varint(); return;
+            case 9: case 10: {
+                const u32 h = byte();
+                u64 cnt = h >> 4;
+                if (cnt == 15) cnt = varint();
+                for (u64 i = 0; i < cnt && ok; ++i) skip(h & 15, depth + 1);
+                return;
+            }
+            case 12: {
+                i64 last = 0;
+                while (ok) {
+                    const u32 h = byte();
+                    if (h == 0) return;
+                    last = (h >> 4) ? last + (h >> 4) : zigzag();
+                    skip(h & 15, depth + 1);
+                }
+                return;
+            }
+            default: ok = false;
+        }
+    }
+    // walk a struct: f(fid, type) returns true when it consumed the value
+    template <typename F>
+    void fields(F f) {
+        i64 last = 0;
+        while (ok) {
+            const u32 h = byte();
+            if (h == 0 || !ok) return;
+            const int t = h & 15;
+            last = (h >> 4) ? last + (h >> 4) : zigzag();
+            if (!f(last, t)) skip(t);
+        }
+    }
+};
+
+struct HostPage {
+    int type;
+    i64 uncomp, comp;
+    u64 data_off;
+    i64 num_values = 0, encoding = 0, def_len = 0, rep_len = 0;
+    bool v2_compressed = true;
+};
+
+// page type 0 DATA_PAGE, 1 INDEX_PAGE, 2 DICTIONARY_PAGE, 3 DATA_PAGE_V2
+int parse_pages(const dbg_parquet_chunk& c, std::vector<HostPage>& out) {
+    out.clear();
+    u64 pos = 0;
+    while (pos < c.len) {
+        Compact r{c.host, c.len, pos};
+        HostPage pg{-1, -1, -1, 0};
+        auto sub = [&](std::vector<std::pair<i64, i64>>& kv) {
+            r.fields([&](i64 fid, int t) {
+                if (t == 5 || t == 6) { kv.push_back({fid, r.zigzag()}); return true; }
+                if (t == 1 || t == 2) { kv.push_back({fid, t == 1 ? 1 : 0}); return true; }
+                return false;
+            });
+        };
+        auto get = [](const std::vector<std::pair<i64, i64>>& kv, i64 f, i64 d) {
+            for (auto& x : kv) if (x.first == f) return x.second;
+            return d;
+        };
+        r.fields([&](i64 fid, int t) {
+            if (fid == 1 && t == 5) { pg.type = (int)r.zigzag(); return true; }
+            if (fid == 2 && t == 5) { pg.uncomp = r.zigzag(); return true; }
+            if (fid == 3 && t == 5) { pg.comp = r.zigzag(); return true; }
+            if ((fid == 5 || fid == 7 || fid == 8) && t == 12) {
+                std::vector<std::pair<i64, i64>> kv;
+                sub(kv);
+                if (fid == 5) { pg.num_values = get(kv, 1, -1); pg.encoding = get(kv, 2, -1); }
+                if (fid == 7) { pg.num_values = get(kv, 1, -1); pg.encoding = get(kv, 2, -1); }
+                if (fid == 8) {
+                    pg.num_values = get(kv, 1, -1);
+                    pg.encoding = get(kv, 4, -1);
+                    pg.def_len = get(kv, 5, -1);
+                    pg.rep_len = get(kv, 6, -1);
+                    pg.v2_compressed = get(kv, 7, 1) != 0;
+                }
+                return true;
+            }
+            return false;
+        });
+        if (!r.ok || pg.type < 0 || pg.uncomp < 0 || pg.comp < 0 || r.p + (u64)pg.comp > c.len)
+            return abi_fail(DBG_ERR_INVALID, "dbg_parquet: malformed page header at byte " + std::to_string(pos));
+        if (pg.uncomp > 0x7FFFFFFF || pg.num_values < 0 || pg.num_values > 0x7FFFFFFF)
+            return abi_fail(DBG_ERR_INVALID, "dbg_parquet: page header values out of range");
+        pg.data_off = r.p;
+        out.push_back(pg);
+        pos = r.p + (u64)pg.comp;
+    }
+    return DBG_OK;
+}
+
+}  // namespace
+
+struct dbg_scan_ctx {
+    hipStream_t stream = nullptr;
+    u8* chunk = nullptr;  // uploaded chunk bytes
+    u64 chunk_cap = 0;
+    u8* buf = nullptr;
+    u64 buf_cap = 0;
+    ScanPage* pages = nullptr;
+    u64 pages_cap = 0;
+    u8* vbytes = nullptr;
+    u64 vbytes_cap = 0;
+    u32* idx = nullptr;
+    u64 idx_cap = 0;
+    u64* vstart = nullptr;
+    u64 vstart_cap = 0;
+    u32* nwalk = nullptr;
+    u64 nwalk_cap = 0;
+    u64* sptr = nullptr;
+    u64 sptr_cap = 0;
+    u8* bools = nullptr;
+    u64 bools_cap = 0;
+    u64* err = nullptr;  // [0] error bits, [1] string total
+    u64* herr = nullptr; // pinned
+};
+
+namespace {
+template <typename T>
+int ensure(T** p, u64* cap, u64 n) {
+    if (*cap >= n && *p) return DBG_OK;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const u64 want = n < 64 ? 64 : n + n / 4;
+    if (hipMalloc((void**)p, want * sizeof(T)) != hipSuccess) return abi_fail(DBG_ERR_OOM, "dbg_parquet: device allocation");
+    *cap = want;
+    return DBG_OK;
+}
+
+bool target_ok(int ptype, int tlen, const dbg_datatype& t, u32& width) {
+    width = type_width(t.type);
+    switch (ptype) {
+        case DBG_PQ_BOOLEAN: return t.type == DBG_BOOLEAN;
+        case DBG_PQ_INT32:
+            return (t.type >= DBG_INT8 && t.type <= DBG_INT32) || (t.type >= DBG_UINT8 && t.type <= DBG_UINT32) || t.type == DBG_DATE ||
+                   (t.type == DBG_DECIMAL128 && t.precision <= 9);
+        case DBG_PQ_INT64:
+            return t.type == DBG_INT64 || t.type == DBG_UINT64 || t.type == DBG_TIMESTAMP || (t.type == DBG_DECIMAL128 && t.precision <= 18);
+        case DBG_PQ_FLOAT: return t.type == DBG_FLOAT32;
+        case DBG_PQ_DOUBLE: return t.type == DBG_FLOAT64;
+        case DBG_PQ_BYTE_ARRAY: return t.type == DBG_STRING;
+        case DBG_PQ_FIXED_LEN_BYTE_ARRAY: return t.type == DBG_DECIMAL128 && tlen >= 1 && tlen <= 16;
+        default: return false;
+    }
+}
+}  // namespace
+
+#define SCAN_HIP(expr)                                                                                     \
+    do {                                                                                                   \
+        hipError_t e_ = (expr);                                                                            \
+        if (e_ != hipSuccess) return abi_fail(DBG_ERR_DEVICE, std::string("dbg_parquet: ") + hipGetErrorString(e_)); \
+    } while (0)
+#define SCAN_RET(rc)              \
+    do {                          \
+        int r_ = (rc);            \
+        if (r_ != DBG_OK) return r_; \
+    } while (0)
+
+extern "C" {
+
+int dbg_scan_create(dbg_scan_ctx** out, void* stream) {
+    if (!out) return abi_fail(DBG_ERR_INVALID, "dbg_scan_create: null out");
+    auto* c = new dbg_scan_ctx();
+    c->stream = (hipStream_t)stream;
+    if (hipMalloc((void**)&c->err, 16) != hipSuccess || hipHostMalloc((void**)&c->herr, 16, hipHostMallocDefault) != hipSuccess) {
+        dbg_scan_destroy(c);
+        return abi_fail(DBG_ERR_OOM, "dbg_scan_create: allocation");
+    }
+    *out = c;
+    return DBG_OK;
+}
+
+int dbg_scan_destroy(dbg_scan_ctx* c) {
+    if (!c) return DBG_OK;
+    void* dev[] = {c->chunk, c->buf, c->pages, c->vbytes, c->idx, c->vstart, c->nwalk, c->sptr, c->bools, c->err};
+    for (void* p : dev)
+        if (p) hipFree(p);
+    if (c->herr) hipHostFree(c->herr);
+    delete c;
+    return DBG_OK;
+}
+
+int dbg_parquet_chunk_rows(const dbg_parquet_chunk* chunk, uint64_t* rows, uint32_t* n_pages) {
+    if (!chunk || !chunk->host || !rows) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_chunk_rows: null argument");
+    std::vector<HostPage> pg;
+    SCAN_RET(parse_pages(*chunk, pg));
+    u64 r = 0;
+    for (auto& p : pg)
+        if (p.type == 0 || p.type == 3) r += (u64)p.num_values;
+    *rows = r;
+    if (n_pages) *n_pages = (uint32_t)pg.size();
+    return DBG_OK;
+}
+
+int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_datatype target, dbg_out_column* out, uint64_t max_rows,
+                       uint64_t max_string_bytes, uint64_t* rows_out, uint64_t* string_bytes) {
+    if (!ctx || !chunk || !chunk->host || !out || !rows_out) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null argument");
+    *rows_out = 0;
+    if (string_bytes) *string_bytes = 0;
+    const dbg_parquet_chunk& c = *chunk;
+    u32 tw = 0;
+    if (c.max_def_level < 0 || c.max_def_level > 1) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: nested column (definition level > 1)");
+    if (c.codec != DBG_PQ_UNCOMPRESSED && c.codec != DBG_PQ_SNAPPY && c.codec != DBG_PQ_LZ4_RAW)
+        return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: codec " + std::to_string(c.codec) + " is decoded on the CPU");
+    if (!target_ok(c.physical_type, c.type_length, target, tw))
+        return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: physical type " + std::to_string(c.physical_type) + " -> target type " +
+                                                 std::to_string(target.type));
+    std::vector<HostPage> hp;
+    SCAN_RET(parse_pages(c, hp));
+    // page table
+    std::vector<ScanPage> pages;
+    u64 dst = 0, row = 0, vk = 0;
+    int dict = -1;
+    for (auto& p : hp) {
+        if (p.type == 1) continue;  // INDEX_PAGE
+        if (p.type != 0 && p.type != 2 && p.type != 3) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: page type " + std::to_string(p.type));
+        ScanPage s;
+        memset(&s, 0, sizeof(s));
+        s.src = p.data_off;
+        s.dst = dst;
+        s.comp = (u32)p.comp;
+        s.uncomp = (u32)p.uncomp;
+        s.num_values = (u32)p.num_values;
+        s.encoding = (u8)p.encoding;
+        s.compressed = (c.codec != DBG_PQ_UNCOMPRESSED) ? 1 : 0;
+        if (p.type == 2) {
+            if (dict >= 0) return abi_fail(DBG_ERR_INVALID, "dbg_parquet: two dictionary pages");
+            if (p.encoding != ENC_PLAIN && p.encoding != ENC_PLAIN_DICT) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: dictionary encoding");
+            s.kind = PG_DICT;
+            dict = (int)pages.size();
+        } else {
+            const bool dict_enc = p.encoding == ENC_PLAIN_DICT || p.encoding == ENC_RLE_DICT;
+            if (!(p.encoding == ENC_PLAIN || dict_enc || (p.encoding == ENC_RLE && c.physical_type == DBG_PQ_BOOLEAN)))
+                return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: encoding " + std::to_string(p.encoding));
+            if (dict_enc && dict < 0) return abi_fail(DBG_ERR_INVALID, "dbg_parquet: dictionary-encoded page without a dictionary");
+            s.kind = p.type == 3 ? PG_DATA_V2 : PG_DATA_V1;
+            s.row0 = row;
+            row += (u64)p.num_values;
+            if (p.type == 3) {
+                if (p.rep_len != 0) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: repeated column");
+                if (p.def_len < 0 || p.def_len > p.uncomp || p.def_len > p.comp) return abi_fail(DBG_ERR_INVALID, "dbg_parquet: v2 level lengths");
+                s.lv = (u32)p.def_len;
+                s.def_len = (u32)p.def_len;
+                s.compressed = s.compressed && p.v2_compressed;
+            }
+        }
+        s.vk0 = vk;
+        vk += (u64)p.num_values;
+        dst += ((u64)p.uncomp + 15) & ~15ULL;
+        pages.push_back(s);
+    }
+    *rows_out = row;
+    if (row > max_rows) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: " + std::to_string(row) + " rows exceed max_rows");
+    if (target.type != DBG_STRING && target.type != DBG_BOOLEAN && !out->data && row) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null data buffer");
+    hipStream_t s = ctx->stream;
+    const bool upload = c.device == nullptr;
+    if (upload) {
+        SCAN_RET(ensure(&ctx->chunk, &ctx->chunk_cap, c.len + 16));
+        SCAN_HIP(hipMemcpyAsync(ctx->chunk, c.host, c.len, hipMemcpyHostToDevice, s));
+    }
+    SCAN_RET(ensure(&ctx->buf, &ctx->buf_cap, dst + 16));
+    SCAN_RET(ensure(&ctx->pages, &ctx->pages_cap, pages.size() + 1));
+    SCAN_RET(ensure(&ctx->vbytes, &ctx->vbytes_cap, row + 1));
+    SCAN_RET(ensure(&ctx->idx, &ctx->idx_cap, vk + 1));
+    SCAN_RET(ensure(&ctx->nwalk, &ctx->nwalk_cap, pages.size() + 1));
+    const bool is_str = target.type == DBG_STRING, is_bool = target.type == DBG_BOOLEAN;
+    if (is_str) {
+        SCAN_RET(ensure(&ctx->vstart, &ctx->vstart_cap, vk + 1));
+        SCAN_RET(ensure(&ctx->sptr, &ctx->sptr_cap, row + 1));
+        if (!out->offsets) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: String output needs offsets");
+    }
+    if (is_bool) SCAN_RET(ensure(&ctx->bools, &ctx->bools_cap, row + 1));
+    if (target.nullable && c.max_def_level && !out->validity && row) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null validity buffer");
+    SCAN_HIP(hipMemcpyAsync(ctx->pages, pages.data(), pages.size() * sizeof(ScanPage), hipMemcpyHostToDevice, s));
+    SCAN_HIP(hipMemsetAsync(ctx->err, 0, 16, s));
+    SCAN_HIP(hipMemsetAsync(ctx->nwalk, 0, pages.size() * 4, s));
+    ScanArgs a;
+    memset(&a, 0, sizeof(a));
+    a.chunk = upload ? ctx->chunk : c.device;
+    a.buf = ctx->buf;
+    a.pages = ctx->pages;
+    a.n_pages = (u32)pages.size();
+    a.ptype = c.physical_type;
+    a.tlen = c.type_length;
+    a.max_def = c.max_def_level;
+    a.codec = c.codec;
+    a.ttype = target.type;
+    a.twidth = tw;
+    a.dict_page = dict;
+    a.rows = row;
+    a.vbytes = ctx->vbytes;
+    a.idx = ctx->idx;
+    a.vstart = ctx->vstart;
+    a.nwalk = ctx->nwalk;
+    a.sptr = ctx->sptr;
+    a.out_data = is_bool ? ctx->bools : (u8*)out->data;
+    a.out_offs = out->offsets;
+    a.err = ctx->err;
+    if (!pages.empty()) {
+        const dim3 g((u32)pages.size());
+        switch (c.codec) {
+            case DBG_PQ_SNAPPY: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_SNAPPY>, g, dim3(64), 0, s, a); break;
+            case DBG_PQ_LZ4_RAW: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_LZ4_RAW>, g, dim3(64), 0, s, a); break;
+            default: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_UNCOMPRESSED>, g, dim3(64), 0, s, a); break;
+        }
+        SCAN_HIP(hipGetLastError());
+        if (c.physical_type == DBG_PQ_BYTE_ARRAY) {
+            hipLaunchKernelGGL(pq_walk_kernel, dim3((u32)((pages.size() + 63) / 64)), dim3(64), 0, s, a);
+            SCAN_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(pq_decode_kernel, g, dim3(DEC_NT), 0, s, a);
+        SCAN_HIP(hipGetLastError());
+    }
+    if (is_str) {
+        // lengths -> offsets (exclusive scan, total into offsets[rows]), then the payload
+        if (row) launch_exclusive_scan(s, out->offsets, row, out->offsets + row);
+        else SCAN_HIP(hipMemsetAsync(out->offsets, 0, 8, s));
+        SCAN_HIP(hipMemcpyAsync(ctx->err + 1, out->offsets + row, 8, hipMemcpyDeviceToDevice, s));
+        if (row && out->data)
+            hipLaunchKernelGGL(pq_strings_kernel, dim3((u32)((row + 255) / 256)), dim3(256), 0, s, ctx->buf, ctx->sptr, out->offsets, row,
+                               (u8*)out->data, max_string_bytes);
+        SCAN_HIP(hipGetLastError());
+    }
+    if (is_bool && row) launch_pack_bits(s, ctx->bools, row, (u8*)out->data);
+    if (target.nullable && row && out->validity) launch_pack_bits(s, ctx->vbytes, row, out->validity);
+    SCAN_HIP(hipMemcpyAsync(ctx->herr, ctx->err, 16, hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipStreamSynchronize(s));
+    const u64 e = ctx->herr[0];
+    if (e & SERR_MALFORMED) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: malformed page data");
+    if (e & (SERR_COUNT | SERR_DICT_RANGE)) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: value count / dictionary index out of range");
+    if (is_str) {
+        if (string_bytes) *string_bytes = ctx->herr[1];
+        if (ctx->herr[1] > max_string_bytes)
+            return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: String payload needs " + std::to_string(ctx->herr[1]) + " bytes");
+    }
+    if (!target.nullable && c.max_def_level && row) {  // a NULL in a non-nullable target is an error
+        // (checked on the host from the validity bytes: one small read-back)
+        std::vector<u8> vb(row);
+        SCAN_HIP(hipMemcpy(vb.data(), ctx->vbytes, row, hipMemcpyDeviceToHost));
+        for (u64 i = 0; i < row; ++i)
+            if (!vb[i]) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: NULL in a non-nullable column");
+    }
+    return DBG_OK;
+}
+
+}  // extern "C"

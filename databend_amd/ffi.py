@@ -23,6 +23,7 @@ EXPORTED = [
     "dbg_prof_get", "dbg_prof_marker", "dbg_datagen", "dbg_agg_set_strategy", "dbg_agg_get_strategy",
     "dbg_agg_record_layout", "dbg_agg_set_host_staging",
     "dbg_take_string", "dbg_legacy_hash_method", "dbg_legacy_group_hash", "dbg_agg_serialized_stride", "dbg_agg_result_serialized", "dbg_agg_merge_serialized", "dbg_comm_get_unique_id", "dbg_comm_create", "dbg_comm_destroy", "dbg_agg_exchange",
+    "dbg_scan_create", "dbg_scan_destroy", "dbg_parquet_chunk_rows", "dbg_parquet_decode",
 ]
 
 
@@ -102,6 +103,11 @@ def lib():
         L.dbg_prof_enable.argtypes = [C.c_int]
         L.dbg_prof_get.argtypes = [C.c_int, P(C.c_char_p), P(C.c_double), P(U64)]
         L.dbg_prof_marker.argtypes = [VP]
+        L.dbg_scan_create.argtypes = [P(VP), VP]
+        L.dbg_scan_destroy.argtypes = [VP]
+        L.dbg_parquet_chunk_rows.argtypes = [P(abi.dbg_parquet_chunk), P(U64), P(C.c_uint32)]
+        L.dbg_parquet_decode.argtypes = [VP, P(abi.dbg_parquet_chunk), abi.dbg_datatype, P(abi.dbg_out_column), U64, U64, P(U64),
+                                         P(U64)]
         L.dbg_datagen.argtypes = [C.c_int, U64, U64, U64, P(VP), C.c_int, VP, VP]
         _LIB = L
     return _LIB

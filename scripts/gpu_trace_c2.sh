@@ -1,0 +1,9 @@
+#!/bin/bash
+# C2 phase trace: the fused insert+finalize launch's timestamps (DBG_X_TRACE, medians over launches).
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+DBG_X_TRACE=1 timeout -k 10 120 python -u bench.py --config 2 --steps 200 --warmup 10 --no-cpu-baseline --extra-configs none \
+  > gpurun_out/trace_c2.json 2> gpurun_out/trace_c2.err || { echo "trace failed"; tail -20 gpurun_out/trace_c2.err; exit 1; }
+grep trace gpurun_out/trace_c2.err
+cut -c1-300 gpurun_out/trace_c2.json

@@ -16,13 +16,15 @@ from databend_amd.ffi import EXPORTED, LIB_PATH, lib
 from oracle import oracle
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "dbgpu_agg.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("dbgpu_agg.h", "dbgpu_scan.h")]
 
 
 def header_functions():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(dbg_\w+)\s*\(", txt)))
+    names = set()
+    for h in HEADERS:
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(dbg_\w+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_struct_layout_matches_header():
-    src = '#include "dbgpu_agg.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){' + "".join(
+    src = '#include "dbgpu_scan.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){' + "".join(
         f'printf("{n} %zu\\n", sizeof({n}));' for n in abi.EXPECTED_SIZES) + \
         'printf("off_len %zu\\n", offsetof(dbg_column, len));printf("off_hint %zu\\n", offsetof(dbg_agg_params, capacity_hint));return 0;}'
     with tempfile.TemporaryDirectory() as d:
