@@ -385,6 +385,26 @@ class AggregateHashTable:
                                           dev_strings.data_ptr() if dev_strings is not None else None, n, sr, ss))
         self._retained.append((dev_records, dev_strings))
 
+    # ---- before-partial shuffle of the partitioned payload (dbg_agg_payload_*)
+    def payload_counts(self):
+        """(counts [2][256] numpy u64: raw / state records per level-1 partition, record widths)."""
+        import numpy as np
+        c = (C.c_uint64 * 512)()
+        w = (C.c_uint32 * 2)()
+        check(lib().dbg_agg_payload_counts(self.h, c, w))
+        return np.frombuffer(bytes(c), dtype=np.uint64).reshape(2, 256).copy(), (int(w[0]), int(w[1]))
+
+    def payload_export(self, n_ranks: int, dev_buf):
+        check(lib().dbg_agg_payload_export(self.h, n_ranks, dev_buf.data_ptr()))
+
+    def payload_import(self, n_ranks: int, rank: int, all_counts, raw, state):
+        """all_counts: numpy u64 [n_ranks][2][256]; raw / state: received records (source-major)."""
+        import numpy as np
+        arr = np.ascontiguousarray(all_counts, dtype=np.uint64)
+        ptr = arr.ctypes.data_as(C.POINTER(C.c_uint64))
+        check(lib().dbg_agg_payload_import(self.h, n_ranks, rank, ptr, raw.data_ptr() if raw is not None else None,
+                                           state.data_ptr() if state is not None else None))
+
     # ---- fixed-capacity exchange (low cardinality: replicas + gather)
     @property
     def capacity(self) -> int:

@@ -227,6 +227,7 @@ struct dbg_agg_handle {
     bool pp = false;          // batches go to the radix-partitioned payload, not the HBM table
     double pp_ratio = 1.0;    // estimated groups per selected row (cardinality probe)
     bool pp_probed = false;   // pp_ratio comes from a probe (not the default upper bound)
+    u64 probe_distinct = 0;   // distinct group hashes the last probe saw (0: no probe)
     struct Seg {
         u64 base, n;
         std::vector<u64> off;  // level-1 partition offsets (257), relative to base
@@ -421,6 +422,13 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     S.flags_word = flag_bits ? word++ : -1;
     S.n_words = word - 1;
     if (word > DBG_MAX_WORDS) return fail(DBG_ERR_UNSUPPORTED, "aggregate states too wide");
+    // key cache (agg.hip, one String key): [READY | len][32 key bytes] after the state words, so a
+    // probe compares a short key in the slot's own line instead of the representative row's
+    S.kc_off = -1;
+    if (!S.inline_keys && S.n_keys == 1 && S.key_types[0].type == DBG_STRING && word + KC_WORDS <= DBG_MAX_WORDS) {
+        S.kc_off = word;
+        word += KC_WORDS;
+    }
     int sw = 1;
     while (sw < word && sw < 8) sw <<= 1;
     if (word > 8) sw = (word + 7) & ~7;
@@ -459,6 +467,12 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     S.pp_rw_state = S.pp_kw + 8 * (u32)S.n_words;
     S.pp_sw = 1 + S.pp_kw / 8 + (u32)S.n_words;
     S.pp_ok = S.pp_rw_raw <= 256 && S.pp_rw_state <= 256 && vbits <= 64 && S.pp_sw <= 64;
+    S.reg_ok = S.n_aggs <= 8 && S.flags_word < 0;
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        if (A.kind != DBG_AGG_COUNT && A.kind != DBG_AGG_SUM && A.kind != DBG_AGG_AVG) S.reg_ok = 0;
+        if (A.arg_type >= 0 && A.arg_nullable) S.reg_ok = 0;
+    }
     return DBG_OK;
 }
 
@@ -989,6 +1003,7 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     HIPCHECK(hipMemcpyAsync(h->pp_hpart, out, 32, hipMemcpyDeviceToHost, h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));
     const double sel = (double)h->pp_hpart[0], D = (double)h->pp_hpart[1], f1 = (double)h->pp_hpart[2];
+    h->probe_distinct = (u64)D;  // the register-private insert takes tables the probe saw <= 4 keys of
     if (sel <= 0) return DBG_OK;
     const double nsel = (double)rows * sel / (double)ns;
     double gu = nsel;
@@ -1287,7 +1302,7 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     memset(&o, 0, sizeof(o));
     o.tot = h->pp_tot;
     static u64* x_pptrace = nullptr;  // EXPERIMENT (DBG_X_PPTRACE)
-    if (getenv("DBG_X_PPTRACE")) {
+    if (kPhaseTrace && getenv("DBG_X_PPTRACE")) {
         if (!x_pptrace) {
             RETURN_IF(dev_alloc((void**)&x_pptrace, 64));
             HIPCHECK(hipMemset(x_pptrace, 0, 64));
@@ -1436,7 +1451,8 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
     }
     {
         prof::Scope ps("agg_insert", h->stream);
-        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st);
+        const bool few = (h->probe_distinct && h->probe_distinct <= 4) || (h->hint_groups && h->hint_groups <= 4);
+        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st, nullptr, few);
     }
     HIPCHECK(hipGetLastError());
     if (!on_device) RETURN_IF(resolve_overflow(h));  // host path: synchronous like the reference processor
@@ -1916,7 +1932,7 @@ static int fin_launch(dbg_agg_handle* h) {
         ff.trace = nullptr;
         static u64* x_trace = nullptr;  // EXPERIMENT (DBG_X_TRACE): 8 words per launch, 4096 launches
         static std::vector<u64> x_init;
-        if (getenv("DBG_X_TRACE")) {
+        if (kPhaseTrace && getenv("DBG_X_TRACE")) {
             if (!x_trace) {
                 RETURN_IF(dev_alloc((void**)&x_trace, 4096 * 128));
                 x_init.assign(16, 0);
@@ -2753,6 +2769,196 @@ void dbg_comm_destroy(dbg_comm* c) {
     if (c->hsizes) hipHostFree(c->hsizes);
     if (c->sent) hipEventDestroy(c->sent);
     delete c;
+}
+
+// ---- before-partial shuffle of the partitioned payload (group_by_shuffle_mode = before_partial,
+//      settings_default.rs:469-473): level-1 partition p (of 2^PP_L1_BITS) belongs to rank
+//      p * n / 2^PP_L1_BITS, so every group's records meet on one rank and are aggregated once ----
+static void payload_owned(u32 d, u32 n, u32& lo, u32& hi) {
+    const u64 P = 1ull << PP_L1_BITS;
+    lo = (u32)((d * P + n - 1) / n);
+    hi = (u32)(((d + 1) * P + n - 1) / n);
+}
+
+static int payload_check(dbg_agg_handle* h) {
+    if (!h->pp) return fail(DBG_ERR_UNSUPPORTED, "payload exchange: the handle is not in partitioned mode (dbg_agg_set_strategy)");
+    if (h->spec.pp_str) return fail(DBG_ERR_UNSUPPORTED, "payload exchange: string keys (records may reference local rows)");
+    return DBG_OK;
+}
+
+int dbg_agg_payload_counts(dbg_agg_handle* h, uint64_t* part_counts, uint32_t* widths) {
+    if (!h || !part_counts) return fail(DBG_ERR_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    RETURN_IF(payload_check(h));
+    const u64 P = 1ull << PP_L1_BITS;
+    for (int k = 0; k < 2; ++k) {
+        for (u64 p = 0; p < P; ++p) part_counts[k * P + p] = 0;
+        for (const auto& sg : h->ppk[k].segs)
+            for (u64 p = 0; p < P; ++p) part_counts[k * P + p] += sg.off[p + 1] - sg.off[p];
+    }
+    if (widths) {
+        widths[0] = h->spec.pp_rw_raw;
+        widths[1] = h->spec.pp_rw_state;
+    }
+    return DBG_OK;
+}
+
+int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf) {
+    if (!h || !dev_buf || n_ranks == 0 || n_ranks > (1u << PP_L1_BITS)) return fail(DBG_ERR_INVALID, "dbg_agg_payload_export: bad argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    RETURN_IF(payload_check(h));
+    u64 dst = 0;
+    for (int k = 0; k < 2; ++k) {
+        const auto& K = h->ppk[k];
+        const u64 rw = k ? h->spec.pp_rw_state : h->spec.pp_rw_raw;
+        std::vector<CopyRange> rs;
+        for (u32 d = 0; d < n_ranks; ++d) {  // destination-major, partition-major within a destination
+            u32 lo, hi;
+            payload_owned(d, n_ranks, lo, hi);
+            for (u32 p = lo; p < hi; ++p)
+                for (const auto& sg : K.segs) {
+                    const u64 n = sg.off[p + 1] - sg.off[p];
+                    if (!n) continue;
+                    if (!rs.empty() && rs.back().src + rs.back().n == (sg.base + sg.off[p]) * rw && rs.back().dst + rs.back().n == dst)
+                        rs.back().n += n * rw;  // contiguous with the previous range (one segment)
+                    else
+                        rs.push_back(CopyRange{(sg.base + sg.off[p]) * rw, dst, n * rw});
+                    dst += n * rw;
+                }
+        }
+        if (rs.empty()) continue;
+        CopyRange* dr = nullptr;
+        RETURN_IF(dev_alloc((void**)&dr, rs.size() * sizeof(CopyRange)));
+        h->owned.push_back({dr, rs.size() * sizeof(CopyRange)});  // freed at the next reset
+        HIPCHECK(hipMemcpy(dr, rs.data(), rs.size() * sizeof(CopyRange), hipMemcpyHostToDevice));
+        launch_copy_ranges(h->stream, K.l1, (u8*)dev_buf, dr, (u32)rs.size());
+        HIPCHECK(hipGetLastError());
+    }
+    return DBG_OK;
+}
+
+int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts, const void* raw_records,
+                           const void* state_records) {
+    if (!h || !part_counts || n_ranks == 0 || rank >= n_ranks || n_ranks > (1u << PP_L1_BITS))
+        return fail(DBG_ERR_INVALID, "dbg_agg_payload_import: bad argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    RETURN_IF(payload_check(h));
+    const u64 P = 1ull << PP_L1_BITS;
+    u32 lo, hi;
+    payload_owned(rank, n_ranks, lo, hi);
+    for (int k = 0; k < 2; ++k) {
+        auto& K = h->ppk[k];
+        const u64 rw = k ? h->spec.pp_rw_state : h->spec.pp_rw_raw;
+        const void* src = k ? state_records : raw_records;
+        std::vector<dbg_agg_handle::Seg> segs;
+        u64 total = 0;
+        for (u32 s = 0; s < n_ranks; ++s) {  // one level-1 segment per source rank
+            const uint64_t* c = part_counts + ((u64)s * 2 + k) * P;
+            dbg_agg_handle::Seg sg{total, 0, std::vector<u64>(P + 1, 0)};
+            u64 run = 0;
+            for (u64 p = 0; p < P; ++p) {
+                sg.off[p] = run;
+                if (p >= lo && p < hi) run += c[p];
+            }
+            sg.off[P] = run;
+            sg.n = run;
+            total += run;
+            segs.push_back(std::move(sg));
+        }
+        if (total && !src) return fail(DBG_ERR_INVALID, "dbg_agg_payload_import: records missing");
+        HIPCHECK(hipStreamSynchronize(h->stream));  // the export has read the old payload
+        if (total > K.l1_cap) {
+            if (K.l1) HIPCHECK(hipFree(K.l1));
+            K.l1 = nullptr;
+            K.l1_cap = 0;
+            RETURN_IF(dev_alloc((void**)&K.l1, total * rw + 64));  // slack: the aggregation reads whole words
+            K.l1_cap = total;
+        }
+        if (total) HIPCHECK(hipMemcpyAsync(K.l1, src, total * rw, hipMemcpyDeviceToDevice, h->stream));
+        K.l1_n = total;
+        K.segs = std::move(segs);
+    }
+    h->pp_grec_ready = false;
+    h->finalized = false;
+    return DBG_OK;
+}
+
+int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats* stats) {
+    if (!c || !h) return fail(DBG_ERR_INVALID, "null argument");
+    if (h->device != c->device) return fail(DBG_ERR_INVALID, "communicator and table are on different devices");
+    RcclApi& R = rccl_api();
+    if (!R.ok) return fail(DBG_ERR_UNSUPPORTED, R.err);
+    HIPCHECK(hipSetDevice(c->device));
+    const u32 n = (u32)c->n, me = (u32)c->rank;
+    const u64 P = 1ull << PP_L1_BITS, W = 2 * P + 1;  // per rank: counts [2][P] + an eligibility flag
+    std::vector<u64> mine(W, 0);
+    uint32_t widths[2] = {0, 0};
+    const int rc0 = dbg_agg_payload_counts(h, mine.data(), widths);
+    mine[2 * P] = rc0 == DBG_OK ? 1 : 0;
+    hipStream_t s = h->stream;
+    // 1. every rank's counts (and whether it can take part), one all-gather
+    u64* dbuf = nullptr;
+    RETURN_IF(dev_alloc((void**)&dbuf, 8 * W * (n + 1)));
+    std::vector<u64> all(W * n);
+    HIPCHECK(hipMemcpyAsync(dbuf, mine.data(), 8 * W, hipMemcpyHostToDevice, s));
+    RCCLCHECK(R.AllGather(dbuf, dbuf + W, W, ncclUint64, c->comm, s));
+    HIPCHECK(hipMemcpyAsync(all.data(), dbuf + W, 8 * W * n, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    HIPCHECK(hipFree(dbuf));
+    for (u32 r = 0; r < n; ++r)
+        if (all[(u64)r * W + 2 * P] != 1)
+            return rc0 != DBG_OK ? rc0 : fail(DBG_ERR_UNSUPPORTED, "payload exchange: rank " + std::to_string(r) + " cannot take part");
+    // 2. pack this rank's records destination-major
+    u64 send_bytes[2][256] = {}, recv_bytes[2][256] = {}, kind_total[2] = {0, 0}, recv_total[2] = {0, 0};
+    u32 lo_me, hi_me;
+    payload_owned(me, n, lo_me, hi_me);
+    for (int k = 0; k < 2; ++k)
+        for (u32 d = 0; d < n; ++d) {
+            u32 lo, hi;
+            payload_owned(d, n, lo, hi);
+            for (u32 p = lo; p < hi; ++p) send_bytes[k][d] += mine[k * P + p] * widths[k];
+            for (u32 p = lo_me; p < hi_me; ++p) recv_bytes[k][d] += all[(u64)d * W + k * P + p] * widths[k];
+            kind_total[k] += send_bytes[k][d];
+            recv_total[k] += recv_bytes[k][d];
+        }
+    u8* sendb = nullptr;
+    u8* recvb[2] = {nullptr, nullptr};
+    RETURN_IF(dev_alloc((void**)&sendb, std::max<u64>(kind_total[0] + kind_total[1], 16)));
+    for (int k = 0; k < 2; ++k) RETURN_IF(dev_alloc((void**)&recvb[k], std::max<u64>(recv_total[k], 16)));
+    RETURN_IF(dbg_agg_payload_export(h, n, sendb));
+    // 3. grouped point-to-point over xGMI (self included)
+    RCCLCHECK(R.GroupStart());
+    for (int k = 0; k < 2; ++k) {
+        u64 so = k ? kind_total[0] : 0, ro = 0;
+        for (u32 p = 0; p < n; ++p) {
+            if (send_bytes[k][p]) RCCLCHECK(R.Send(sendb + so, send_bytes[k][p], ncclUint8, (int)p, c->comm, s));
+            if (recv_bytes[k][p]) RCCLCHECK(R.Recv(recvb[k] + ro, recv_bytes[k][p], ncclUint8, (int)p, c->comm, s));
+            so += send_bytes[k][p];
+            ro += recv_bytes[k][p];
+        }
+    }
+    RCCLCHECK(R.GroupEnd());
+    // 4. the received records become this rank's level-1 payload
+    std::vector<u64> pc(2 * P * n);
+    for (u32 r = 0; r < n; ++r)
+        for (u64 x = 0; x < 2 * P; ++x) pc[(u64)r * 2 * P + x] = all[(u64)r * W + x];
+    const int rc = dbg_agg_payload_import(h, n, me, pc.data(), recvb[0], recvb[1]);
+    HIPCHECK(hipStreamSynchronize(s));
+    hipFree(sendb);
+    hipFree(recvb[0]);
+    hipFree(recvb[1]);
+    if (rc != DBG_OK) return rc;
+    if (stats) {
+        stats->sent_bytes = kind_total[0] + kind_total[1];
+        stats->remote_bytes = stats->sent_bytes - send_bytes[0][me] - send_bytes[1][me];
+        stats->received_records = 0;
+        for (int k = 0; k < 2; ++k) stats->received_records += recv_total[k] / std::max<u32>(widths[k], 1);
+        stats->received_string_bytes = 0;
+    }
+    return DBG_OK;
 }
 
 int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final_h, dbg_exchange_stats* stats) {

@@ -70,6 +70,71 @@ __device__ __forceinline__ bool ref_equal(const Spec& S, const BatchDesc* batche
     return true;
 }
 
+// ------------------------------------------------------------------------------------------
+// Key cache (Spec::kc_off, one String key): a slot keeps a copy of its group's key — [READY | len]
+// and up to KC_BYTES bytes — next to its entry, written by the thread that claimed the slot.  A
+// probe whose salt matches compares the row's key with the copy (the slot's own line) instead of
+// reading the representative row (offsets + bytes: two dependent random reads, ClickBench Q13's
+// HBM traffic).  The copy is an optimisation only: a slot whose copy is not READY
+// yet (its claimer has not published it) or whose key is longer than KC_BYTES or NULL is compared
+// through the representative row as before — no reader ever waits.
+// ------------------------------------------------------------------------------------------
+struct RowKey {
+    u64 w[KC_WORDS];  // [len][bytes...] as the cache holds them (READY added on publish)
+    bool ok;          // non-NULL and short enough to be cached
+};
+__device__ __forceinline__ RowKey row_key(const DCol& c, u64 i) {
+    RowKey k;
+    k.ok = false;
+#pragma unroll
+    for (int w = 0; w < KC_WORDS; ++w) k.w[w] = 0;
+    if (!dcol_valid(c, i)) return k;
+    const StrRef s = dcol_str(c, i);
+    if (s.len > KC_BYTES) return k;
+    k.w[0] = s.len;
+#pragma unroll
+    for (int w = 0; w < KC_BYTES / 8; ++w) {
+        const u64 o = (u64)w * 8;
+        if (o < s.len) k.w[1 + w] = load_partial(s.p + o, s.len - o < 8 ? s.len - o : 8) &
+                                    (s.len - o >= 8 ? ~0ULL : ((1ULL << (8 * (s.len - o))) - 1));
+    }
+    k.ok = true;
+    return k;
+}
+// publish the claimed slot's key copy (LDS: workgroup order; HBM: agent-scope stores, the READY
+// word last behind a release fence)
+template <int AS>
+__device__ __forceinline__ void kc_publish(const Spec& S, u64* slot, const DCol* keys, u64 i) {
+    const RowKey k = row_key(keys[0], i);
+    if (!k.ok) return;
+    u64* c = slot + S.kc_off;
+#pragma unroll
+    for (int w = 1; w < KC_WORDS; ++w) __hip_atomic_store(asp<AS>(c + w), k.w[w], __ATOMIC_RELAXED, AT_SCOPE(AS));
+    __hip_atomic_store(asp<AS>(c), k.w[0] | KC_READY, __ATOMIC_RELEASE, AT_SCOPE(AS));
+}
+// 1: equal, 0: different, -1: no usable copy (compare the representative row)
+template <int AS>
+__device__ __forceinline__ int kc_compare(const Spec& S, const u64* slot, const DCol* keys, u64 i) {
+    const u64* c = slot + S.kc_off;
+    const u64 h = __hip_atomic_load(asp<AS>(c), __ATOMIC_ACQUIRE, AT_SCOPE(AS));
+    if (!(h & KC_READY)) return -1;
+    const RowKey k = row_key(keys[0], i);
+    if (!k.ok) return dcol_valid(keys[0], i) ? 0 : -1;  // longer than any cached key, or NULL
+    if ((h & ~KC_READY) != k.w[0]) return 0;
+#pragma unroll
+    for (int w = 1; w < KC_WORDS; ++w)
+        if (__hip_atomic_load(asp<AS>(c + w), __ATOMIC_RELAXED, AT_SCOPE(AS)) != k.w[w]) return 0;
+    return 1;
+}
+template <int AS>
+__device__ __forceinline__ bool key_equal(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 e, const u64* slot) {
+    if (S.kc_off >= 0) {
+        const int r = kc_compare<AS>(S, slot, keys, i);
+        if (r >= 0) return r == 1;
+    }
+    return ref_equal(S, batches, keys, i, e);
+}
+
 // Reference group hash of the group an entry stands for.
 __device__ __forceinline__ u64 entry_hash(const Spec& S, const BatchDesc* batches, u64 e, bool is_sentinel) {
     if (S.inline_keys) return hash_packed(S, is_sentinel ? SLOT_EMPTY : e);
@@ -100,13 +165,14 @@ __device__ __forceinline__ u64 g_find(const Spec& S, const BatchDesc* batches, c
             u64 old = at_cas<AS_GLB>(e, SLOT_EMPTY, key);
             if (old == SLOT_EMPTY) {
                 claimed = true;
+                if (!INLINE && S.kc_off >= 0 && keys) kc_publish<AS_GLB>(S, t.slots + s * t.stride_words, keys, i);
                 return s;
             }
             ev = old;
         }
         if (INLINE) {
             if (ev == key) return s;
-        } else if ((ev >> 48) == (key >> 48) && ref_equal(S, batches, keys, i, ev)) {
+        } else if ((ev >> 48) == (key >> 48) && key_equal<AS_GLB>(S, batches, keys, i, ev, t.slots + s * t.stride_words)) {
             return s;
         }
         s = (s + 1) & mask;
@@ -143,13 +209,14 @@ __device__ __forceinline__ int lds_find(const Spec& S, const BatchDesc* batches,
             if (old == SLOT_EMPTY) {
                 __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (!INLINE && S.kc_off >= 0 && keys) kc_publish<AS_LDS>(S, lds + (u64)s * sw, keys, i);
                 return (int)s;
             }
             ev = old;
         }
         if (INLINE) {
             if (ev == key) return (int)s;
-        } else if ((ev >> 48) == (key >> 48) && ref_equal(S, batches, keys, i, ev)) {
+        } else if ((ev >> 48) == (key >> 48) && key_equal<AS_LDS>(S, batches, keys, i, ev, lds + (u64)s * sw)) {
             return (int)s;
         }
         s = (s + 1) & lmask;
@@ -403,7 +470,23 @@ __device__ __forceinline__ void maybe_flush(const Spec& S, const BatchDesc* batc
     }
 }
 
-template <bool INLINE, bool RECORDS>
+// Register-private accumulation (REG): a table expected to hold at most RG groups (the
+// cardinality probe saw <= RG distinct keys: TPC-H Q1's four) gets no LDS atomics per row.  Each
+// thread keeps, per group, a row count and one 64-bit partial per aggregate in registers; the
+// row's group is its LDS-table slot (lds_find, as ever) mapped to a register index through a small
+// LDS map filled on first sight.  Partials go into the LDS table once, before the block flush.
+// Eligible (Spec::reg_ok): COUNT, and SUM / AVG of non-nullable arguments; a Decimal128 value that
+// does not fit the 64-bit partial (or would overflow it) takes the LDS atomic path for that row.
+// Keys beyond the first RG a workgroup sees take the generic path.
+#define RG 4
+#define RA 8
+template <bool REG>
+struct RegAcc {
+    u64 acc[REG ? RG : 1][REG ? RA : 1];
+    u32 rows[REG ? RG : 1];
+};
+
+template <bool INLINE, bool RECORDS, bool REG = false>
 __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
                                                           u32 lds_slots) {
@@ -417,7 +500,77 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
 
     lds_table_init(S, lds, lds_slots, sw, BLOCK);
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
+    // REG: LDS slot -> register group (0xFF none), register group -> LDS slot
+    __shared__ u8 slot2g[REG ? 4096 : 1];
+    __shared__ u32 g2slot[RG], reg_n;
+    RegAcc<REG> R;
+    if constexpr (REG) {
+        for (u32 k = threadIdx.x; k < lds_slots && k < 4096; k += BLOCK) slot2g[k] = 0xFF;
+        if (threadIdx.x == 0) reg_n = 0;
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+            R.rows[g] = 0;
+#pragma unroll
+            for (int a = 0; a < RA; ++a) R.acc[g][a] = 0;
+        }
+    }
     __syncthreads();
+    // one selected row through the register path; false: the caller takes the generic path
+    auto insert_reg = [&](u64 i) -> bool {
+        if constexpr (!REG) {
+            return false;
+        } else {
+            u64 h, key;
+            if (INLINE) {
+                h = 0;
+                key = pack_key(S, B.keys, i);
+            } else {
+                h = group_hash(B.keys, S.n_keys, i);
+                key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+            }
+            const int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
+            if (ls < 0 || ls >= 4096) return false;
+            u32 g = slot2g[ls];
+            if (g == 0xFF) {
+                g = atomicAdd(&reg_n, 1u);
+                if (g >= RG) return false;
+                g2slot[g] = (u32)ls;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is published before the map
+                slot2g[ls] = (u8)g;
+            }
+#pragma unroll
+            for (int gg = 0; gg < RG; ++gg) R.rows[gg] += gg == (int)g ? 1u : 0u;
+#pragma unroll
+            for (int a = 0; a < RA; ++a) {
+                if (a >= S.n_aggs) break;
+                const DAgg& A = S.aggs[a];
+                if (A.kind == DBG_AGG_COUNT) continue;
+                const DCol& c = B.args[a];
+                u64 cur = R.acc[0][a];
+#pragma unroll
+                for (int gg = 1; gg < RG; ++gg) cur = gg == (int)g ? R.acc[gg][a] : cur;
+                u64 nv = cur;
+                if (A.sumk == SUMK_I64) {
+                    nv = cur + (u64)dcol_i64(c, i);
+                } else if (A.sumk == SUMK_F64) {
+                    nv = (u64)__double_as_longlong(__longlong_as_double((long long)cur) + dcol_f64(c, i));
+                } else {
+                    const u64 lo = dcol_bits(c, i), hi = dcol_hi(c, i);
+                    long long r;
+                    if (hi == (u64)((i64)lo >> 63) && !__builtin_add_overflow((long long)cur, (long long)lo, &r)) nv = (u64)r;
+                    else add128<AS_LDS>(asp<AS_LDS>(lds + (u64)ls * sw + A.w0), lo, hi);  // the slot of this row's group
+                }
+#pragma unroll
+                for (int gg = 0; gg < RG; ++gg)
+                    if (gg == (int)g) R.acc[gg][a] = nv;
+            }
+            return true;
+        }
+    };
+    auto insert_row = [&](u64 i, u32& my_claims) {
+        if (REG && insert_reg(i)) return;
+        insert_one<INLINE, RECORDS>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+    };
 
     u64 r0 = (u64)blockIdx.x * rows_per_block;
     u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
@@ -435,7 +588,8 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         __syncthreads();
         const u32 lane = __lane_id();
         for (u64 it = 0; it < n_iter; ++it) {
-            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            // REG keeps LDS slots in its register map: the table is never restarted
+            if (!REG && it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
             const u64 i = r0 + it * BLOCK + threadIdx.x;
             const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
             const u64 m = __ballot(sel);
@@ -454,16 +608,16 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
                 __syncthreads();
                 if (threadIdx.x < rem) selq[threadIdx.x] = mv;
                 if (threadIdx.x == 0) qn = rem;
-                insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + off, lds, lmask, sw, lcount, llimit, t, my_claims);
+                insert_row(r0 + off, my_claims);
             }
             __syncthreads();  // the queue is settled before the next round appends
         }
         const u32 n = qn;  // < BLOCK
         if (threadIdx.x < n)
-            insert_one<INLINE, RECORDS>(S, batches, B, bid, r0 + selq[threadIdx.x], lds, lmask, sw, lcount, llimit, t, my_claims);
+            insert_row(r0 + selq[threadIdx.x], my_claims);
     } else {
         for (u64 it = 0; it < n_iter; ++it) {
-            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            if (!REG && it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
             const u64 i = r0 + it * BLOCK + threadIdx.x;
             if (i >= r1) continue;
             if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
@@ -476,7 +630,29 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
                 }
                 if (q > gld<u64>(hdr)) continue;
             }
-            insert_one<INLINE, RECORDS>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+            insert_row(i, my_claims);
+        }
+    }
+    if constexpr (REG) {  // register partials -> the groups' LDS slots (one add per state word)
+        __syncthreads();
+        const u32 ng = min(reg_n, (u32)RG);
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+            if ((u32)g >= ng || R.rows[g] == 0) continue;
+            u64* st = lds + (u64)g2slot[g] * sw;
+            for (int a = 0; a < RA && a < S.n_aggs; ++a) {
+                const DAgg& A = S.aggs[a];
+                wptr<AS_LDS> w = asp<AS_LDS>(st + A.w0);
+                const u64 v = R.acc[g][a];
+                if (A.kind == DBG_AGG_COUNT) {
+                    at_add<AS_LDS>(w, (u64)R.rows[g]);
+                    continue;
+                }
+                if (A.sumk == SUMK_I64) at_add<AS_LDS>(w, v);
+                else if (A.sumk == SUMK_F64) at_addf<AS_LDS>(w, __longlong_as_double((long long)v));
+                else add128<AS_LDS>(w, v, (u64)((i64)v >> 63));
+                if (A.kind == DBG_AGG_AVG) at_add<AS_LDS>(w + (A.sumk == SUMK_I128 ? 2 : 1), (u64)R.rows[g]);
+            }
         }
     }
     __syncthreads();
@@ -822,7 +998,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
                                                     u64* trace = nullptr, bool writeback = false) {
     __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
     __shared__ u64 cnts[CNT_WORDS];
-    auto mark = [&](int k) { if (trace && threadIdx.x == 0) trace[k] = __builtin_amdgcn_s_memrealtime(); };
+    auto mark = [&](int k) { if (kPhaseTrace && trace && threadIdx.x == 0) trace[k] = __builtin_amdgcn_s_memrealtime(); };
     // Barriers here are LDS-only (no wait for this workgroup's global stores) unless a later
     // phase reads what other threads stored to global memory: every __syncthreads costs a
     // store round trip (vmcnt 0, ~1 us).
@@ -1006,15 +1182,15 @@ __device__ __forceinline__ void fused_finalize(const Spec& S, const BatchDesc* b
     }
     __syncthreads();
     if (!is_last) return;
-    if (ff.trace && threadIdx.x == 0) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
     const u64 n = (t.cap + 1) * t.stride_words;  // host: <= the launch's dynamic LDS
     for (u64 i = threadIdx.x; i < n; i += FIN_NT) lds[i] = ld_sc1(t.slots + i);
     if (threadIdx.x == 0) atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
     __syncthreads();
-    if (ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
     finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq,
                                                   ff.trace);
-    if (ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // merge_states of a parked partial state (sc1 loads) into a slot; COUNT(*) alone (CO): one add
@@ -1032,7 +1208,8 @@ __device__ __forceinline__ void merge_parked(const Spec& S, u64* st, const u64* 
 // code — this tail runs once per launch on whichever CU finishes last, from a cold instruction
 // cache, so its length is latency.
 template <typename T>
-__device__ __forceinline__ void finalize_count_only(const TableDesc& t, const u64* view, const FusedFin& ff, bool known) {
+__device__ __forceinline__ void finalize_count_only(const TableDesc& t, const u64* view, const FusedFin& ff, bool known,
+                                                    u32 view_claims) {
     __shared__ u64 wsum[FIN_NT / 64];
     __shared__ u64 cnts[CNT_WORDS];
     auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
@@ -1080,6 +1257,10 @@ __device__ __forceinline__ void finalize_count_only(const TableDesc& t, const u6
     lds_barrier();
     const bool rc = ff.recycle && cnts[CNT_OVF_ROWS] == 0 && cnts[CNT_OVF_RECS] == 0 && total <= out.cap_groups;
     if (rc && threadIdx.x < CNT_WORDS) t.counters[threadIdx.x] = 0;  // dbg_agg_reset
+    // known counters: the view's claims were not added yet (fused_chain); a table that outlives
+    // this finalize needs them
+    if (known && !rc && threadIdx.x == 0 && view_claims)
+        atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)view_claims);
     u64* hm = ff.host_mirror;
     auto put = [&](int w, u64 v) { __hip_atomic_store(hm + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
     // known counters: one self-validating word ([seq | recycled | groups], MIRROR_COMPACT) instead
@@ -1274,7 +1455,7 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
         }
     }
     __syncthreads();
-    if (ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     if (role != 2) return;
     // 3. the last group leader: view of the HBM table, group rows merged into it, finalize
     if (threadIdx.x == 0) {
@@ -1283,7 +1464,7 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
         atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
         bad = 0;
         vcl = 0;
-        if (ff.trace) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
+        if (kPhaseTrace && ff.trace) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
     }
     // the view: the HBM table, or its initial state when it was empty at launch start (recycled
     // by the previous finalize) and no workgroup of this launch created a group in it
@@ -1311,19 +1492,22 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
     }
     if (vclaims) atomicAdd(&vcl, vclaims);
     __syncthreads();
-    if (threadIdx.x == 0 && vcl) {
+    const bool known = ff.table_empty && ovf_seen == 0 && !bad;
+    // the view's claims into the table counter: before the finalize reads the counters, or — when
+    // they are known (count-only) — only if the table outlives the finalize (finalize_count_only)
+    if (threadIdx.x == 0 && vcl && !(CO && known)) {
         atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)vcl);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
     // the finalize writes the view back when the table outlives it (no recycle: short buffers, an
     // overflow record, or a caller that keeps the table)
     // counters known without a load: an empty table at launch start, no overflow anywhere
-    if constexpr (CO) finalize_count_only<T>(t, lds, ff, ff.table_empty && ovf_seen == 0 && !bad);
+    if constexpr (CO) finalize_count_only<T>(t, lds, ff, known, vcl);
     else finalize_small_body<FUSED_FIN_SLOTS / FIN_NT>(S, batches, t, lds, ff.out, ff.totals, ff.host_mirror, ff.recycle, ff.seq,
                                                        ff.trace, true);
-    if (ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1394,7 +1578,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     // candidate-vector queue (the `<> c` path below) over the same per-wave space
     v4u* vq = (v4u*)qkey;
     u64* vqb = qkey + 2 * WQ;
-    if (ff.trace && threadIdx.x == 0) atomicMin((unsigned long long*)ff.trace, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) atomicMin((unsigned long long*)ff.trace, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     lds_table_init(S, lds, lds_slots, sw, NT);
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
     __syncthreads();
@@ -1648,7 +1832,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         if (!PRED || pass(v)) process((u64)(typename std::make_unsigned<T>::type)v, i);
     }
     __syncthreads();
-    if (ff.trace && threadIdx.x == 0) {
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) {
         const u64 tm = __builtin_amdgcn_s_memrealtime();
         atomicMin((unsigned long long*)ff.trace + 1, (unsigned long long)tm);
         atomicMax((unsigned long long*)ff.trace + 2, (unsigned long long)tm);
@@ -1658,7 +1842,7 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         return;
     }
     block_flush<true, false>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims);
-    if (ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     if (ff.on) fused_finalize(S, batches, t, lds, ff);
 }
 
@@ -1731,7 +1915,7 @@ bool insert_can_fuse(const Spec& S, const BatchDesc& hb, u64 cap) {
 }
 
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, u32 bid, u64 rows, bool records,
-                   const TableDesc& t, bool use_lds, const BatchDesc* hb, const FusedFin* fused) {
+                   const TableDesc& t, bool use_lds, const BatchDesc* hb, const FusedFin* fused, bool few_groups) {
     if (rows == 0) return;
     if (hb && use_lds && fast_eligible(S, *hb, records)) {
         u32 lslots = lds_slots_for(S, 16 * 1024);
@@ -1760,6 +1944,11 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     u64 rpb = (rows + blocks - 1) / blocks;
     blocks = (rows + rpb - 1) / rpb;
     size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
+    if (few_groups && !records && S.reg_ok && lslots <= 4096) {
+        if (S.inline_keys) hipLaunchKernelGGL((agg_insert_kernel<true, false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        else hipLaunchKernelGGL((agg_insert_kernel<false, false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        return;
+    }
     if (S.inline_keys) {
         if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
         else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);

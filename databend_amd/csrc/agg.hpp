@@ -38,6 +38,8 @@ struct Spec {
     //   raw record   = [key part][arg values, each aligned to its width][arg validity bits]
     //   state record = [key part][state words 1..n_words]
     int32_t pp_ok;          // the spec can run partitioned (record widths within bounds)
+    int32_t reg_ok;         // register-private accumulation applies (agg.hip REG: COUNT / SUM / AVG, non-null args)
+    int32_t kc_off;         // slot word of the key cache (one String key; -1 none): [READY | len][KC_BYTES bytes]
     int32_t pp_str;         // key part is [hash][klen][blob]
     uint32_t pp_kw;         // key part bytes (multiple of 8)
     uint32_t pp_rw_raw;     // raw record bytes (multiple of 8)
@@ -84,6 +86,9 @@ struct TableDesc {
     u64* scratch;
     u32 scr_blocks;
 };
+#define KC_BYTES 32
+#define KC_WORDS (1 + KC_BYTES / 8)
+#define KC_READY (1ULL << 63)
 #define SCR_ENTRIES 64
 #define SCR_GROUP 16
 inline size_t scr_words(u32 blocks, u32 stride_words) {
@@ -198,6 +203,14 @@ __device__ __forceinline__ u64 ld_sc1(const u64* p) {
     return __hip_atomic_load((wptr<AS_GLB>)(u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Phase timestamps inside kernels (experiments only): compiled in by `make TRACE=1`
+// (-DDBG_PHASE_TRACE, scripts/gpu_trace_c2.sh); the shipped library carries no trace code.
+#ifdef DBG_PHASE_TRACE
+constexpr bool kPhaseTrace = true;
+#else
+constexpr bool kPhaseTrace = false;
+#endif
+
 struct FusedFin;
 // ---- launch wrappers (agg.hip) ----
 // part.hip: radix-partitioned COUNT(*) insert for high-cardinality single integer keys
@@ -208,7 +221,7 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
                    bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr,
-                   const FusedFin* fused = nullptr);
+                   const FusedFin* fused = nullptr, bool few_groups = false);
 void launch_retry(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                   u64 n_rows, u64 n_recs, const u64* rows_list, const u64* recs_list);
 void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const u64* old_slots,
@@ -339,6 +352,10 @@ struct PPAggOut {
 // device totals of one partitioned finalize: groups, string bytes per key column, extra rounds, errors
 enum { PPT_GROUPS = 0, PPT_STR = 1, PPT_ROUNDS = 1 + DBG_MAX_KEYS, PPT_ERR = 2 + DBG_MAX_KEYS, PPT_WORDS = 4 + DBG_MAX_KEYS };
 u32 pp_agg_slots(const Spec& hspec);
+struct CopyRange {
+    u64 src, dst, n;  // byte offsets / length (multiples of 8)
+};
+void launch_copy_ranges(hipStream_t s, const u8* src, u8* dst, const CopyRange* dranges, u32 n);
 void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
                    const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out);
 // group records -> result columns (deterministic positions: block sums, scan, write)

@@ -1285,7 +1285,7 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     part_range(blockIdx.x + gridDim.x, b_r0, b_nr);
     load_tile(bufB, raw, b_r0, b_nr, 0);
     __syncthreads();
-    const bool tr = out.trace && (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+    const bool tr = kPhaseTrace && out.trace && (blockIdx.x & 63) == 0 && threadIdx.x == 0;
     u64 tm0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
     auto run_part = [&](u32 p, Tile& buf, u64& br0, u64& bnr) {
         const u64 r0 = br0, s0 = st_off ? st_off[p] : 0;
@@ -1664,4 +1664,23 @@ void launch_pp_grec_export(hipStream_t s, const Spec* dspec, const BatchDesc* ba
     if (!nblocks) return;
     hipLaunchKernelGGL(pp_grec_export_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, pos,
                        str_pos, nblocks, rec_out, str_out, part_str_base);
+}
+
+// ------------------------------------------------------------------------------------------
+// Byte-range gather (payload export / import, abi.hip dbg_agg_payload_*): one workgroup per
+// range, 8-byte words (records and their offsets are multiples of 8 bytes).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) copy_ranges_kernel(const u8* __restrict__ src, u8* __restrict__ dst,
+                                                          const CopyRange* __restrict__ r, u32 n) {
+    for (u32 k = blockIdx.x; k < n; k += gridDim.x) {
+        const CopyRange c = r[k];
+        const u64* a = (const u64*)(src + c.src);
+        u64* b = (u64*)(dst + c.dst);
+        for (u64 w = threadIdx.x; w < c.n / 8; w += 256) b[w] = a[w];
+    }
+}
+
+void launch_copy_ranges(hipStream_t s, const u8* src, u8* dst, const CopyRange* dranges, u32 n) {
+    if (!n) return;
+    hipLaunchKernelGGL(copy_ranges_kernel, dim3(n < 4096 ? n : 4096), dim3(256), 0, s, src, dst, dranges, n);
 }

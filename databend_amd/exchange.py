@@ -104,6 +104,56 @@ def exchange_partial(partial, final, device) -> dict:
     return dict(sent_bytes=sent, remote_bytes=sent - counts[me] * w - sbytes[me], received_records=sum(seg_records))
 
 
+def payload_owned(d: int, n: int, parts: int = 256):
+    """Level-1 partitions of rank d: p with p * n // parts == d (dbg_agg_payload_*, abi.hip)."""
+    return (d * parts + n - 1) // n, ((d + 1) * parts + n - 1) // n
+
+
+def payload_splits(counts, all_counts, widths, rank: int, world: int):
+    """Byte splits of the before-partial shuffle per record kind: send[k][d] (this rank's records of
+    the partitions rank d owns) and recv[k][s] (source s's records of this rank's partitions)."""
+    send = [[0] * world for _ in range(2)]
+    recv = [[0] * world for _ in range(2)]
+    lo_me, hi_me = payload_owned(rank, world)
+    for k in range(2):
+        for d in range(world):
+            lo, hi = payload_owned(d, world)
+            send[k][d] = int(counts[k][lo:hi].sum()) * widths[k]
+            recv[k][d] = int(all_counts[d][k][lo_me:hi_me].sum()) * widths[k]
+    return send, recv
+
+
+def exchange_payload(table, device) -> dict:
+    """Before-partial shuffle (group_by_shuffle_mode = before_partial, settings_default.rs:469-473)
+    of a partitioned-mode table over torch.distributed: every rank's level-1 records go to the rank
+    owning their level-1 partition (dbg_agg_payload_export), with one all-gather of the per-partition
+    counts and one all_to_all_single per record kind, and become that rank's payload
+    (dbg_agg_payload_import) — aggregated once, by its finalize."""
+    import numpy as np
+    import torch
+    dist = _dist()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    counts, widths = table.payload_counts()
+    mine = torch.from_numpy(counts.astype(np.int64).reshape(-1)).to(device)
+    allc = torch.empty(world * mine.numel(), dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(allc, mine)
+    all_counts = allc.cpu().numpy().astype(np.uint64).reshape(world, 2, 256)
+    send, recv = payload_splits(counts, all_counts, widths, rank, world)
+    tot = [sum(send[0]), sum(send[1])]
+    buf = torch.empty(max(1, tot[0] + tot[1]), dtype=torch.uint8, device=device)
+    table.payload_export(world, buf)
+    got = []
+    for k in range(2):
+        inp = buf[(tot[0] if k else 0):(tot[0] if k else 0) + tot[k]]
+        out = torch.empty(max(1, sum(recv[k])), dtype=torch.uint8, device=device)
+        dist.all_to_all_single(out[:sum(recv[k])], inp, output_split_sizes=recv[k], input_split_sizes=send[k])
+        got.append(out)
+    table.payload_import(world, rank, all_counts, got[0], got[1])
+    sent = tot[0] + tot[1]
+    return dict(sent_bytes=sent, remote_bytes=sent - send[0][rank] - send[1][rank],
+                received_records=sum(recv[0]) // max(1, widths[0]) + sum(recv[1]) // max(1, widths[1]))
+
+
 class AbiComm:
     """A communicator of the C ABI (dbg_comm_*): the exchange a Rust host drives without torch.
     `unique_id` is created by one rank and handed to every rank by the host's own channel (here
@@ -142,6 +192,15 @@ class AbiComm:
         check(lib().dbg_agg_exchange(self.h, partial.h, final.h, C.byref(st)))
         return dict(sent_bytes=st.sent_bytes, remote_bytes=st.remote_bytes, received_records=st.received_records,
                     received_string_bytes=st.received_string_bytes)
+
+    def exchange_payload(self, table) -> dict:
+        """dbg_agg_exchange_payload: the before-partial shuffle of a partitioned-mode table."""
+        import ctypes as C
+        from . import abi
+        from .ffi import check, lib
+        st = abi.dbg_exchange_stats()
+        check(lib().dbg_agg_exchange_payload(self.h, table.h, C.byref(st)))
+        return dict(sent_bytes=st.sent_bytes, remote_bytes=st.remote_bytes, received_records=st.received_records)
 
     def close(self):
         if getattr(self, "h", None):

@@ -366,6 +366,30 @@ void dbg_comm_destroy(dbg_comm* c);
  * all-gather; stats may be NULL. */
 int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final_table, dbg_exchange_stats* stats);
 
+/* ---- before-partial shuffle of the partitioned payload (mostly-unique keys) ----
+ * group_by_shuffle_mode = before_partial (src/query/settings/src/settings_default.rs:469-473;
+ * the rows are scattered before any aggregation, HashFlightScatter, servers/flight/v1/scatter/
+ * flight_scatter_hash.rs:133-200).  When every rank's handle is in partitioned mode
+ * (dbg_agg_set_strategy(PARTITIONED), fixed-width keys) its level-1 records — written by
+ * add_groups, not yet aggregated — are routed by level-1 partition: partition p of 256 (top 8 bits
+ * of the group hash) goes to rank p * n / 256, so every group's records meet on one rank and are
+ * aggregated once, by that rank's finalize.  Routing differs from HashFlightScatter's SipHash: the
+ * exchange is GPU-to-GPU only (a mixed CPU/GPU cluster uses dbg_agg_exchange, before_merge).
+ *   counts: part_counts[kind][p] (2 x 256: raw / state records per level-1 partition), widths[kind]
+ *           record bytes (host only);
+ *   export: the records packed destination-major (kind 0 for ranks 0..n-1, then kind 1), each
+ *           destination's records partition-major, into dev_buf (sum of counts x widths bytes);
+ *   import: replace the payload with records received from n_ranks sources: raw_records /
+ *           state_records source-major, each source's block holding the records of this rank's
+ *           partitions; part_counts[source][kind][p] are the sources' counts;
+ *   exchange_payload: the whole collective over RCCL (one all-gather of the counts, grouped
+ *           send/recv), then import.  DBG_ERR_UNSUPPORTED on every rank if any rank cannot take part. */
+int dbg_agg_payload_counts(dbg_agg_handle* h, uint64_t* part_counts /* 2 x 256 */, uint32_t* widths /* 2, may be NULL */);
+int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf);
+int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts /* n x 2 x 256 */,
+                           const void* raw_records, const void* state_records);
+int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats* stats);
+
 /* ---- fixed-capacity exchange: replicas + gather for low-cardinality tables ----
  * Replaces, for small inline-key partial tables, the Serialized/Flight hand-off of
  * TransformPartialAggregate::on_finish (AGG/transform_aggregate_partial.rs:449-465) to the final

@@ -1,5 +1,8 @@
 #!/bin/bash
 # C2 phase trace: the fused insert+finalize launch's timestamps (DBG_X_TRACE, medians over launches).
+# Needs a library built with phase tracing (here, before the GPU call):
+#   make -C databend_amd/csrc clean && make -C databend_amd/csrc TRACE=1
+# (the shipped build has none; rebuild without TRACE=1 afterwards).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out

@@ -1,0 +1,61 @@
+"""GPU parity of the register-private insert (agg.hip REG: tables the cardinality probe or the
+capacity hint puts at <= 4 groups, TPC-H Q1's shape) against the oracle: every eligible aggregate
+(COUNT, SUM, AVG, SQL avg over integers, floats, Decimal128 incl. values beyond the 64-bit
+partials), inline and string keys, a fifth key arriving late (generic path beside the registers),
+filters, and the ineligible shapes (nullable arguments, MIN/MAX) staying on the generic path."""
+import numpy as np
+import pytest
+
+from databend_amd import column as col
+from databend_amd.column import Column
+from databend_amd.filter import cmp
+from tests.test_gpu_parity import check_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(rng, n, kind):
+    if kind == "strings":
+        flags = np.array([b"A", b"N", b"R"])[rng.integers(0, 3, n)]
+        status = np.array([b"F", b"O"])[rng.integers(0, 2, n)]
+        return [Column.from_strings(list(flags)), Column.from_strings(list(status))]
+    return [Column.from_numbers(col.Int16, rng.integers(0, 4, n))]
+
+
+@pytest.mark.parametrize("kind", ["strings", "int"])
+@pytest.mark.parametrize("on_device", [False, True])
+def test_reg_q1_shape(kind, on_device):
+    rng = np.random.default_rng(11)
+    n = 600_000
+    keys = _inputs(rng, n, kind)
+    qty = Column.from_decimals(15, 2, [int(v) for v in rng.integers(100, 5001, n)])
+    price = Column.from_decimals(15, 2, [int(v) for v in rng.integers(90_000, 10_500_000, n)])
+    big = Column.from_decimals(38, 6, [int(v) * 10**22 for v in rng.integers(-10**6, 10**6, n)])  # beyond 64-bit partials
+    i64 = Column.from_numbers(col.Int64, rng.integers(-2**62, 2**62, n))  # wrapping sums
+    f64 = Column.from_numbers(col.Float64, rng.random(n) * 100)
+    ship = Column.from_numbers(col.Int32, rng.integers(0, 2600, n))
+    aggs = [("sum", qty), ("sum", price), ("sum", big), ("avg", qty), ("avg", price), ("sum", i64), ("avg", f64), ("count", None)]
+    ng = check_parity(keys, aggs, (cmp(0, "<=", 2500), [ship]), on_device=on_device, capacity_hint=4)
+    assert 4 <= ng <= 6
+
+
+def test_reg_late_fifth_key_and_batches():
+    """Keys beyond the four a workgroup registers take the generic LDS path in the same launch."""
+    rng = np.random.default_rng(12)
+    n = 400_000
+    k = rng.integers(0, 4, n)
+    k[rng.random(n) < 0.001] = 7  # rare fifth key, anywhere
+    keys = [Column.from_numbers(col.Int32, k)]
+    v = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n))
+    d = Column.from_decimals(15, 2, [int(x) for x in rng.integers(-10**12, 10**12, n)])
+    check_parity(keys, [("count", None), ("sum", v), ("avg", d), ("count", v)], capacity_hint=4, batches=3)
+
+
+def test_reg_ineligible_shapes_stay_generic():
+    rng = np.random.default_rng(13)
+    n = 200_000
+    keys = [Column.from_numbers(col.Int16, rng.integers(0, 3, n))]
+    vn = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n), validity=rng.random(n) > 0.3)
+    v = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n))
+    check_parity(keys, [("sum", vn), ("count", None)], capacity_hint=4)
+    check_parity(keys, [("min", v), ("max", v), ("sum", v)], capacity_hint=4)
