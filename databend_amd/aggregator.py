@@ -400,6 +400,8 @@ class AggregateHashTable:
     def payload_import(self, n_ranks: int, rank: int, all_counts, raw, state):
         """all_counts: numpy u64 [n_ranks][2][256]; raw / state: received records (source-major)."""
         import numpy as np
+        import torch
+        torch.cuda.current_stream().synchronize()  # the received buffers were written on torch's stream
         arr = np.ascontiguousarray(all_counts, dtype=np.uint64)
         ptr = arr.ctypes.data_as(C.POINTER(C.c_uint64))
         check(lib().dbg_agg_payload_import(self.h, n_ranks, rank, ptr, raw.data_ptr() if raw is not None else None,

@@ -227,7 +227,6 @@ struct dbg_agg_handle {
     bool pp = false;          // batches go to the radix-partitioned payload, not the HBM table
     double pp_ratio = 1.0;    // estimated groups per selected row (cardinality probe)
     bool pp_probed = false;   // pp_ratio comes from a probe (not the default upper bound)
-    u64 probe_distinct = 0;   // distinct group hashes the last probe saw (0: no probe)
     struct Seg {
         u64 base, n;
         std::vector<u64> off;  // level-1 partition offsets (257), relative to base
@@ -422,13 +421,6 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     S.flags_word = flag_bits ? word++ : -1;
     S.n_words = word - 1;
     if (word > DBG_MAX_WORDS) return fail(DBG_ERR_UNSUPPORTED, "aggregate states too wide");
-    // key cache (agg.hip, one String key): [READY | len][32 key bytes] after the state words, so a
-    // probe compares a short key in the slot's own line instead of the representative row's
-    S.kc_off = -1;
-    if (!S.inline_keys && S.n_keys == 1 && S.key_types[0].type == DBG_STRING && word + KC_WORDS <= DBG_MAX_WORDS) {
-        S.kc_off = word;
-        word += KC_WORDS;
-    }
     int sw = 1;
     while (sw < word && sw < 8) sw <<= 1;
     if (word > 8) sw = (word + 7) & ~7;
@@ -467,12 +459,6 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     S.pp_rw_state = S.pp_kw + 8 * (u32)S.n_words;
     S.pp_sw = 1 + S.pp_kw / 8 + (u32)S.n_words;
     S.pp_ok = S.pp_rw_raw <= 256 && S.pp_rw_state <= 256 && vbits <= 64 && S.pp_sw <= 64;
-    S.reg_ok = S.n_aggs <= 8 && S.flags_word < 0;
-    for (int a = 0; a < S.n_aggs; ++a) {
-        const DAgg& A = S.aggs[a];
-        if (A.kind != DBG_AGG_COUNT && A.kind != DBG_AGG_SUM && A.kind != DBG_AGG_AVG) S.reg_ok = 0;
-        if (A.arg_type >= 0 && A.arg_nullable) S.reg_ok = 0;
-    }
     return DBG_OK;
 }
 
@@ -1003,7 +989,6 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     HIPCHECK(hipMemcpyAsync(h->pp_hpart, out, 32, hipMemcpyDeviceToHost, h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));
     const double sel = (double)h->pp_hpart[0], D = (double)h->pp_hpart[1], f1 = (double)h->pp_hpart[2];
-    h->probe_distinct = (u64)D;  // the register-private insert takes tables the probe saw <= 4 keys of
     if (sel <= 0) return DBG_OK;
     const double nsel = (double)rows * sel / (double)ns;
     double gu = nsel;
@@ -1451,8 +1436,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
     }
     {
         prof::Scope ps("agg_insert", h->stream);
-        const bool few = (h->probe_distinct && h->probe_distinct <= 4) || (h->hint_groups && h->hint_groups <= 4);
-        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st, nullptr, few);
+        launch_insert(h->stream, h->dspec, S, h->dbatches, bid, rows, false, table_desc(h), true, st);
     }
     HIPCHECK(hipGetLastError());
     if (!on_device) RETURN_IF(resolve_overflow(h));  // host path: synchronous like the reference processor
@@ -2836,6 +2820,7 @@ int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf) {
         launch_copy_ranges(h->stream, K.l1, (u8*)dev_buf, dr, (u32)rs.size());
         HIPCHECK(hipGetLastError());
     }
+    HIPCHECK(hipStreamSynchronize(h->stream));  // dev_buf is complete when the call returns
     return DBG_OK;
 }
 
@@ -2881,6 +2866,7 @@ int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, c
         K.l1_n = total;
         K.segs = std::move(segs);
     }
+    HIPCHECK(hipStreamSynchronize(h->stream));  // the caller may release the received buffers
     h->pp_grec_ready = false;
     h->finalized = false;
     return DBG_OK;

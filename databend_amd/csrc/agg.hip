@@ -70,70 +70,6 @@ __device__ __forceinline__ bool ref_equal(const Spec& S, const BatchDesc* batche
     return true;
 }
 
-// ------------------------------------------------------------------------------------------
-// Key cache (Spec::kc_off, one String key): a slot keeps a copy of its group's key — [READY | len]
-// and up to KC_BYTES bytes — next to its entry, written by the thread that claimed the slot.  A
-// probe whose salt matches compares the row's key with the copy (the slot's own line) instead of
-// reading the representative row (offsets + bytes: two dependent random reads, ClickBench Q13's
-// HBM traffic).  The copy is an optimisation only: a slot whose copy is not READY
-// yet (its claimer has not published it) or whose key is longer than KC_BYTES or NULL is compared
-// through the representative row as before — no reader ever waits.
-// ------------------------------------------------------------------------------------------
-struct RowKey {
-    u64 w[KC_WORDS];  // [len][bytes...] as the cache holds them (READY added on publish)
-    bool ok;          // non-NULL and short enough to be cached
-};
-__device__ __forceinline__ RowKey row_key(const DCol& c, u64 i) {
-    RowKey k;
-    k.ok = false;
-#pragma unroll
-    for (int w = 0; w < KC_WORDS; ++w) k.w[w] = 0;
-    if (!dcol_valid(c, i)) return k;
-    const StrRef s = dcol_str(c, i);
-    if (s.len > KC_BYTES) return k;
-    k.w[0] = s.len;
-#pragma unroll
-    for (int w = 0; w < KC_BYTES / 8; ++w) {
-        const u64 o = (u64)w * 8;
-        if (o < s.len) k.w[1 + w] = load_partial(s.p + o, s.len - o < 8 ? s.len - o : 8) &
-                                    (s.len - o >= 8 ? ~0ULL : ((1ULL << (8 * (s.len - o))) - 1));
-    }
-    k.ok = true;
-    return k;
-}
-// publish the claimed slot's key copy (LDS: workgroup order; HBM: agent-scope stores, the READY
-// word last behind a release fence)
-template <int AS>
-__device__ __forceinline__ void kc_publish(const Spec& S, u64* slot, const DCol* keys, u64 i) {
-    const RowKey k = row_key(keys[0], i);
-    if (!k.ok) return;
-    u64* c = slot + S.kc_off;
-#pragma unroll
-    for (int w = 1; w < KC_WORDS; ++w) __hip_atomic_store(asp<AS>(c + w), k.w[w], __ATOMIC_RELAXED, AT_SCOPE(AS));
-    __hip_atomic_store(asp<AS>(c), k.w[0] | KC_READY, __ATOMIC_RELEASE, AT_SCOPE(AS));
-}
-// 1: equal, 0: different, -1: no usable copy (compare the representative row)
-template <int AS>
-__device__ __forceinline__ int kc_compare(const Spec& S, const u64* slot, const DCol* keys, u64 i) {
-    const u64* c = slot + S.kc_off;
-    const u64 h = __hip_atomic_load(asp<AS>(c), __ATOMIC_ACQUIRE, AT_SCOPE(AS));
-    if (!(h & KC_READY)) return -1;
-    const RowKey k = row_key(keys[0], i);
-    if (!k.ok) return dcol_valid(keys[0], i) ? 0 : -1;  // longer than any cached key, or NULL
-    if ((h & ~KC_READY) != k.w[0]) return 0;
-#pragma unroll
-    for (int w = 1; w < KC_WORDS; ++w)
-        if (__hip_atomic_load(asp<AS>(c + w), __ATOMIC_RELAXED, AT_SCOPE(AS)) != k.w[w]) return 0;
-    return 1;
-}
-template <int AS>
-__device__ __forceinline__ bool key_equal(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 e, const u64* slot) {
-    if (S.kc_off >= 0) {
-        const int r = kc_compare<AS>(S, slot, keys, i);
-        if (r >= 0) return r == 1;
-    }
-    return ref_equal(S, batches, keys, i, e);
-}
 
 // Reference group hash of the group an entry stands for.
 __device__ __forceinline__ u64 entry_hash(const Spec& S, const BatchDesc* batches, u64 e, bool is_sentinel) {
@@ -165,14 +101,13 @@ __device__ __forceinline__ u64 g_find(const Spec& S, const BatchDesc* batches, c
             u64 old = at_cas<AS_GLB>(e, SLOT_EMPTY, key);
             if (old == SLOT_EMPTY) {
                 claimed = true;
-                if (!INLINE && S.kc_off >= 0 && keys) kc_publish<AS_GLB>(S, t.slots + s * t.stride_words, keys, i);
                 return s;
             }
             ev = old;
         }
         if (INLINE) {
             if (ev == key) return s;
-        } else if ((ev >> 48) == (key >> 48) && key_equal<AS_GLB>(S, batches, keys, i, ev, t.slots + s * t.stride_words)) {
+        } else if ((ev >> 48) == (key >> 48) && ref_equal(S, batches, keys, i, ev)) {
             return s;
         }
         s = (s + 1) & mask;
@@ -209,14 +144,13 @@ __device__ __forceinline__ int lds_find(const Spec& S, const BatchDesc* batches,
             if (old == SLOT_EMPTY) {
                 __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (!INLINE && S.kc_off >= 0 && keys) kc_publish<AS_LDS>(S, lds + (u64)s * sw, keys, i);
                 return (int)s;
             }
             ev = old;
         }
         if (INLINE) {
             if (ev == key) return (int)s;
-        } else if ((ev >> 48) == (key >> 48) && key_equal<AS_LDS>(S, batches, keys, i, ev, lds + (u64)s * sw)) {
+        } else if ((ev >> 48) == (key >> 48) && ref_equal(S, batches, keys, i, ev)) {
             return (int)s;
         }
         s = (s + 1) & lmask;
@@ -470,23 +404,7 @@ __device__ __forceinline__ void maybe_flush(const Spec& S, const BatchDesc* batc
     }
 }
 
-// Register-private accumulation (REG): a table expected to hold at most RG groups (the
-// cardinality probe saw <= RG distinct keys: TPC-H Q1's four) gets no LDS atomics per row.  Each
-// thread keeps, per group, a row count and one 64-bit partial per aggregate in registers; the
-// row's group is its LDS-table slot (lds_find, as ever) mapped to a register index through a small
-// LDS map filled on first sight.  Partials go into the LDS table once, before the block flush.
-// Eligible (Spec::reg_ok): COUNT, and SUM / AVG of non-nullable arguments; a Decimal128 value that
-// does not fit the 64-bit partial (or would overflow it) takes the LDS atomic path for that row.
-// Keys beyond the first RG a workgroup sees take the generic path.
-#define RG 4
-#define RA 8
-template <bool REG>
-struct RegAcc {
-    u64 acc[REG ? RG : 1][REG ? RA : 1];
-    u32 rows[REG ? RG : 1];
-};
-
-template <bool INLINE, bool RECORDS, bool REG = false>
+template <bool INLINE, bool RECORDS>
 __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
                                                           u32 lds_slots) {
@@ -500,75 +418,8 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
 
     lds_table_init(S, lds, lds_slots, sw, BLOCK);
     if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
-    // REG: LDS slot -> register group (0xFF none), register group -> LDS slot
-    __shared__ u8 slot2g[REG ? 4096 : 1];
-    __shared__ u32 g2slot[RG], reg_n;
-    RegAcc<REG> R;
-    if constexpr (REG) {
-        for (u32 k = threadIdx.x; k < lds_slots && k < 4096; k += BLOCK) slot2g[k] = 0xFF;
-        if (threadIdx.x == 0) reg_n = 0;
-#pragma unroll
-        for (int g = 0; g < RG; ++g) {
-            R.rows[g] = 0;
-#pragma unroll
-            for (int a = 0; a < RA; ++a) R.acc[g][a] = 0;
-        }
-    }
     __syncthreads();
-    // one selected row through the register path; false: the caller takes the generic path
-    auto insert_reg = [&](u64 i) -> bool {
-        if constexpr (!REG) {
-            return false;
-        } else {
-            u64 h, key;
-            if (INLINE) {
-                h = 0;
-                key = pack_key(S, B.keys, i);
-            } else {
-                h = group_hash(B.keys, S.n_keys, i);
-                key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
-            }
-            const int ls = lds_find<INLINE>(S, batches, B.keys, i, key, h, lds, lmask, sw, lcount, llimit);
-            if (ls < 0 || ls >= 4096) return false;
-            u32 g = slot2g[ls];
-            if (g == 0xFF) {
-                g = atomicAdd(&reg_n, 1u);
-                if (g >= RG) return false;
-                g2slot[g] = (u32)ls;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is published before the map
-                slot2g[ls] = (u8)g;
-            }
-#pragma unroll
-            for (int gg = 0; gg < RG; ++gg) R.rows[gg] += gg == (int)g ? 1u : 0u;
-#pragma unroll
-            for (int a = 0; a < RA; ++a) {
-                if (a >= S.n_aggs) break;
-                const DAgg& A = S.aggs[a];
-                if (A.kind == DBG_AGG_COUNT) continue;
-                const DCol& c = B.args[a];
-                u64 cur = R.acc[0][a];
-#pragma unroll
-                for (int gg = 1; gg < RG; ++gg) cur = gg == (int)g ? R.acc[gg][a] : cur;
-                u64 nv = cur;
-                if (A.sumk == SUMK_I64) {
-                    nv = cur + (u64)dcol_i64(c, i);
-                } else if (A.sumk == SUMK_F64) {
-                    nv = (u64)__double_as_longlong(__longlong_as_double((long long)cur) + dcol_f64(c, i));
-                } else {
-                    const u64 lo = dcol_bits(c, i), hi = dcol_hi(c, i);
-                    long long r;
-                    if (hi == (u64)((i64)lo >> 63) && !__builtin_add_overflow((long long)cur, (long long)lo, &r)) nv = (u64)r;
-                    else add128<AS_LDS>(asp<AS_LDS>(lds + (u64)ls * sw + A.w0), lo, hi);  // the slot of this row's group
-                }
-#pragma unroll
-                for (int gg = 0; gg < RG; ++gg)
-                    if (gg == (int)g) R.acc[gg][a] = nv;
-            }
-            return true;
-        }
-    };
     auto insert_row = [&](u64 i, u32& my_claims) {
-        if (REG && insert_reg(i)) return;
         insert_one<INLINE, RECORDS>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
     };
 
@@ -588,8 +439,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         __syncthreads();
         const u32 lane = __lane_id();
         for (u64 it = 0; it < n_iter; ++it) {
-            // REG keeps LDS slots in its register map: the table is never restarted
-            if (!REG && it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
             const u64 i = r0 + it * BLOCK + threadIdx.x;
             const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
             const u64 m = __ballot(sel);
@@ -617,7 +467,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
             insert_row(r0 + selq[threadIdx.x], my_claims);
     } else {
         for (u64 it = 0; it < n_iter; ++it) {
-            if (!REG && it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
             const u64 i = r0 + it * BLOCK + threadIdx.x;
             if (i >= r1) continue;
             if (!RECORDS && B.n_nodes && !eval_pred(B.nodes, B.n_nodes, B.fcols, i)) continue;
@@ -631,28 +481,6 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
                 if (q > gld<u64>(hdr)) continue;
             }
             insert_row(i, my_claims);
-        }
-    }
-    if constexpr (REG) {  // register partials -> the groups' LDS slots (one add per state word)
-        __syncthreads();
-        const u32 ng = min(reg_n, (u32)RG);
-#pragma unroll
-        for (int g = 0; g < RG; ++g) {
-            if ((u32)g >= ng || R.rows[g] == 0) continue;
-            u64* st = lds + (u64)g2slot[g] * sw;
-            for (int a = 0; a < RA && a < S.n_aggs; ++a) {
-                const DAgg& A = S.aggs[a];
-                wptr<AS_LDS> w = asp<AS_LDS>(st + A.w0);
-                const u64 v = R.acc[g][a];
-                if (A.kind == DBG_AGG_COUNT) {
-                    at_add<AS_LDS>(w, (u64)R.rows[g]);
-                    continue;
-                }
-                if (A.sumk == SUMK_I64) at_add<AS_LDS>(w, v);
-                else if (A.sumk == SUMK_F64) at_addf<AS_LDS>(w, __longlong_as_double((long long)v));
-                else add128<AS_LDS>(w, v, (u64)((i64)v >> 63));
-                if (A.kind == DBG_AGG_AVG) at_add<AS_LDS>(w + (A.sumk == SUMK_I128 ? 2 : 1), (u64)R.rows[g]);
-            }
         }
     }
     __syncthreads();
@@ -1915,7 +1743,7 @@ bool insert_can_fuse(const Spec& S, const BatchDesc& hb, u64 cap) {
 }
 
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, u32 bid, u64 rows, bool records,
-                   const TableDesc& t, bool use_lds, const BatchDesc* hb, const FusedFin* fused, bool few_groups) {
+                   const TableDesc& t, bool use_lds, const BatchDesc* hb, const FusedFin* fused) {
     if (rows == 0) return;
     if (hb && use_lds && fast_eligible(S, *hb, records)) {
         u32 lslots = lds_slots_for(S, 16 * 1024);
@@ -1944,11 +1772,6 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     u64 rpb = (rows + blocks - 1) / blocks;
     blocks = (rows + rpb - 1) / rpb;
     size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
-    if (few_groups && !records && S.reg_ok && lslots <= 4096) {
-        if (S.inline_keys) hipLaunchKernelGGL((agg_insert_kernel<true, false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
-        else hipLaunchKernelGGL((agg_insert_kernel<false, false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
-        return;
-    }
     if (S.inline_keys) {
         if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
         else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);

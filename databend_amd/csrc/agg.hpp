@@ -38,8 +38,6 @@ struct Spec {
     //   raw record   = [key part][arg values, each aligned to its width][arg validity bits]
     //   state record = [key part][state words 1..n_words]
     int32_t pp_ok;          // the spec can run partitioned (record widths within bounds)
-    int32_t reg_ok;         // register-private accumulation applies (agg.hip REG: COUNT / SUM / AVG, non-null args)
-    int32_t kc_off;         // slot word of the key cache (one String key; -1 none): [READY | len][KC_BYTES bytes]
     int32_t pp_str;         // key part is [hash][klen][blob]
     uint32_t pp_kw;         // key part bytes (multiple of 8)
     uint32_t pp_rw_raw;     // raw record bytes (multiple of 8)
@@ -86,9 +84,6 @@ struct TableDesc {
     u64* scratch;
     u32 scr_blocks;
 };
-#define KC_BYTES 32
-#define KC_WORDS (1 + KC_BYTES / 8)
-#define KC_READY (1ULL << 63)
 #define SCR_ENTRIES 64
 #define SCR_GROUP 16
 inline size_t scr_words(u32 blocks, u32 stride_words) {
@@ -221,7 +216,7 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
                    bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr,
-                   const FusedFin* fused = nullptr, bool few_groups = false);
+                   const FusedFin* fused = nullptr);
 void launch_retry(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
                   u64 n_rows, u64 n_recs, const u64* rows_list, const u64* recs_list);
 void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const u64* old_slots,

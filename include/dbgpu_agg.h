@@ -383,7 +383,9 @@ int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final
  *           state_records source-major, each source's block holding the records of this rank's
  *           partitions; part_counts[source][kind][p] are the sources' counts;
  *   exchange_payload: the whole collective over RCCL (one all-gather of the counts, grouped
- *           send/recv), then import.  DBG_ERR_UNSUPPORTED on every rank if any rank cannot take part. */
+ *           send/recv), then import.  DBG_ERR_UNSUPPORTED on every rank if any rank cannot take part.
+ * export and import are synchronous (they return with dev_buf written / the records copied):
+ * buffers produced or released on another stream need no further ordering. */
 int dbg_agg_payload_counts(dbg_agg_handle* h, uint64_t* part_counts /* 2 x 256 */, uint32_t* widths /* 2, may be NULL */);
 int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf);
 int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts /* n x 2 x 256 */,

@@ -1,8 +1,8 @@
-"""GPU parity of the register-private insert (agg.hip REG: tables the cardinality probe or the
-capacity hint puts at <= 4 groups, TPC-H Q1's shape) against the oracle: every eligible aggregate
-(COUNT, SUM, AVG, SQL avg over integers, floats, Decimal128 incl. values beyond the 64-bit
-partials), inline and string keys, a fifth key arriving late (generic path beside the registers),
-filters, and the ineligible shapes (nullable arguments, MIN/MAX) staying on the generic path."""
+"""GPU parity of tables with very few groups (TPC-H Q1's shape: <= 4-6 groups, capacity hint 4)
+against the oracle: COUNT, SUM, AVG over integers, floats and Decimal128 (including sums beyond 64
+bits), inline and string keys, a rare fifth key arriving late, filters, nullable arguments and
+MIN/MAX.  (A register-private insert for such tables was built and measured slower than the LDS
+table — DESIGN.md §4.5 — so these cases run the generic insert.)"""
 import numpy as np
 import pytest
 
