@@ -49,6 +49,13 @@ def parse():
                    help="comma list of further configs timed in the same run (single GPU), reported under 'configs' "
                         "(default: 1,3,4,5 with the headline config 2 at N=1; none otherwise; 'none' disables)")
     p.add_argument("--extra-steps", type=int, default=3)
+    p.add_argument("--exchange", choices=["abi", "torch"], default="abi",
+                   help="N > 1, high cardinality: the library's RCCL exchange (dbg_agg_exchange / "
+                        "dbg_agg_exchange_payload, what a Rust host drives) or torch.distributed all-to-all")
+    p.add_argument("--shuffle", choices=["auto", "before_partial", "before_merge"], default="auto",
+                   help="N > 1, high cardinality: route level-1 records before any aggregation (group_by_shuffle_mode "
+                        "= before_partial, partitioned payload) or partial states after it; auto = before_partial when "
+                        "every rank's cardinality probe chose the partitioned payload")
     p.add_argument("--scaling", choices=["weak", "strong"], default=None,
                    help="weak: every GPU aggregates the config's rows; strong: the config's rows are split over "
                         "the GPUs (default: strong for the 1B-row configs 3-5, weak for 1-2)")
@@ -214,7 +221,7 @@ def main():
     from databend_amd import ffi
     from databend_amd.aggregator import AggregateHashTable, HashTableConfig
     from databend_amd import abi
-    from databend_amd.exchange import GatherPipeline, exchange_partial
+    from databend_amd.exchange import AbiComm, GatherPipeline, exchange_partial, exchange_payload
     from databend_amd.workloads import DEFAULT_ROWS, SHAPES, ConfigRunner, algorithmic_bytes
 
     cfg = args.config
@@ -259,6 +266,24 @@ def main():
     elif small:
         pipe = GatherPipeline(runner, final, dev, rank, world)
 
+    # High cardinality at N > 1: decide the shuffle once, the same on every rank (one untimed
+    # insert shows what each rank's cardinality probe chose), then keep the table in that mode.
+    comm = None
+    before_partial = False
+    if world > 1 and not small:
+        if args.exchange == "abi":
+            comm = AbiComm.from_process_group(local)
+        t = runner.table
+        t.reset()
+        t.add_groups(runner.key_abi[0], runner.arg_cols[0], rows=rows, filter_program=runner.programs[0], on_device=True)
+        fixed = all(runner.inputs[0][k].dtype.type_id != abi.STRING for k in shape.keys)
+        vote = torch.tensor([1 if (t.strategy()[0] and fixed) else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(vote, op=dist.ReduceOp.MIN)
+        before_partial = args.shuffle == "before_partial" or (args.shuffle == "auto" and int(vote.item()) == 1)
+        t.reset()
+        if before_partial:
+            t.set_strategy(abi.STRATEGY_PARTITIONED)
+
     def drain():
         if pipelined:
             return runner.pipe_drain()
@@ -277,8 +302,18 @@ def main():
         t = runner.table
         t.reset()
         t.add_groups(runner.key_abi[i], runner.arg_cols[i], rows=rows, filter_program=runner.programs[i], on_device=True)
+        if before_partial:  # level-1 records to their partition's owner, aggregated once there
+            if comm is not None:
+                comm.exchange_payload(t)
+            else:
+                exchange_payload(t, dev)
+            n, sb = t.finalize()
+            return n
         final.reset()
-        exchange_partial(t, final, dev)
+        if comm is not None:
+            comm.exchange(t, final)
+        else:
+            exchange_partial(t, final, dev)
         n, sb = final.finalize()
         return n
 
@@ -365,7 +400,9 @@ def main():
         "config": {"workload": shape.name + ("" if scaling == "weak" or world == 1 else f"_strong_{total_rows}_rows"),
                    "query": shape.sql, "rows_per_gpu": rows, "input_copies": copies,
                    "groups": n_groups, "selected_rows": sel, "parallelism": f"dp{world}" if world > 1 else "single",
-                   "strategy": "partitioned" if partitioned else "hbm_table"},
+                   "strategy": "partitioned" if partitioned else "hbm_table",
+                   "exchange": (("before_partial" if before_partial else "before_merge") + "/" + args.exchange)
+                   if world > 1 and not small else ("replicas+gather" if world > 1 else None)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": kernel_name, "kernel_avg_ms": avg_ms, "kernel_launches": ins_n,
