@@ -466,10 +466,78 @@ def main():
             except Exception as e:  # reported, never hidden: the headline line still prints
                 out["configs"][f"C{c}"] = {"error": f"{type(e).__name__}: {e}"}
             print(f"bench.py: C{c} done", file=sys.stderr, flush=True)
+        if extra == "1,3,4,5":  # the scan side beside the configurations
+            try:
+                out["scan"] = measure_scan(args.extra_steps + 2)
+            except Exception as e:
+                out["scan"] = {"error": f"{type(e).__name__}: {e}"}
+            print("bench.py: scan done", file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure_scan(steps: int, rows: int = 1 << 26) -> dict:
+    """Parquet -> HBM decode of C2's column as a Fuse block stores it (blocks_to_parquet: one row
+    group — 2^26 rows, pyarrow's row-group cap — PLAIN, no dictionary, 1 MiB pages, Int16 stored as
+    INT32 as arrow writers do; parquet_rs.rs:30-57), chunk bytes already resident in
+    HBM: dbg_parquet_decode per chunk (host page-header parse + the device decode + one read-back),
+    timed with events on the default stream.  Algorithmic bytes = the chunk's bytes read + the
+    column's bytes written (values and validity)."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    import io
+    import torch
+    import ctypes as C
+    from databend_amd import abi
+    from databend_amd import column as col
+    from databend_amd.ffi import check, lib
+    from databend_amd.scan import ParquetChunkDecoder
+    rng = np.random.default_rng(0xC2)
+    adv = np.where(rng.random(rows) < 0.9937, 0, rng.integers(1, 33, rows)).astype(np.int16)
+    res = {"workload": "clickbench AdvEngineID (Int16) column, 2^26 rows (one row group), Fuse parquet shape", "rows": rows}
+    dec = ParquetChunkDecoder()
+    for comp in ("NONE", "SNAPPY"):
+        t = pa.table({"a": pa.array(adv)}, schema=pa.schema([pa.field("a", pa.int16(), nullable=False)]))
+        bio = io.BytesIO()
+        pq.write_table(t, bio, compression=comp, use_dictionary=False, row_group_size=1 << 30, data_page_size=1 << 20)
+        buf = bio.getvalue()
+        md = pq.ParquetFile(io.BytesIO(buf)).metadata.row_group(0).column(0)
+        chunk = buf[md.data_page_offset:md.data_page_offset + md.total_compressed_size]
+        dchunk = torch.from_numpy(np.frombuffer(chunk, dtype=np.uint8).copy()).cuda()
+        hbuf = C.create_string_buffer(chunk, len(chunk))
+        c = abi.dbg_parquet_chunk()
+        c.host = C.cast(hbuf, C.c_void_p)
+        c.device = dchunk.data_ptr()
+        c.len = len(chunk)
+        c.physical_type = abi.PQ_INT32
+        c.max_def_level = 0
+        c.codec = abi.PQ_UNCOMPRESSED if comp == "NONE" else abi.PQ_SNAPPY
+        out_t = torch.empty(rows * 2, dtype=torch.uint8, device="cuda")
+        o = abi.dbg_out_column()
+        o.data = out_t.data_ptr()
+        nr, sb = C.c_uint64(), C.c_uint64()
+        call = lambda: check(lib().dbg_parquet_decode(dec.h, C.byref(c), col.Int16.to_abi(), C.byref(o), rows, 0,
+                                                     C.byref(nr), C.byref(sb)))
+        call()
+        assert nr.value == rows and torch.equal(out_t.view(torch.int16), torch.from_numpy(adv).cuda())
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record()
+        for _ in range(steps):
+            call()
+        ev1.record()
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / steps
+        alg = len(chunk) + rows * 2
+        res[comp.lower()] = {"chunk_bytes": len(chunk), "ms_per_chunk": ms, "rows_per_s": rows / (ms * 1e-3),
+                             "achieved_gbs": alg / (ms * 1e-3) / 1e9, "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "algorithmic_bytes": alg, "bit_exact": True}
+        del dchunk, out_t
+    dec.close()
+    return res
 
 
 if __name__ == "__main__":

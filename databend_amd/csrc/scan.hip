@@ -6,7 +6,8 @@
 // headers (Thrift compact, a few dozen bytes per page) are parsed on the host and every page is
 // decoded on the device, one workgroup per page:
 //
-//   pq_inflate   one wave per page: UNCOMPRESSED copy, or a SNAPPY / LZ4_RAW block decode.  The
+//   pq_inflate   one wave per compressed page: a SNAPPY / LZ4_RAW block decode (an UNCOMPRESSED
+//                page is decoded where it lies in the chunk, page_base).  The
 //                element stream is parsed by the whole wave in lockstep (uniform loads, no lane
 //                divergence); literals and back-references are copied 64 bytes per step, and
 //                back-references read a 64 KiB LDS ring of the page's recent output (both formats
@@ -70,7 +71,7 @@ struct ScanArgs {
     u32* idx;          // [rows] dictionary indices / RLE booleans by value index
     u64* vstart;       // [rows + dict values] BYTE_ARRAY value starts (page-relative)
     u32* nwalk;        // [n_pages] values found by pq_walk
-    u64* sptr;         // [rows] String payload source offsets in buf
+    u64* sptr;         // [rows] String payload source addresses (page buffer or chunk)
     u8* out_data;      // target values (BOOLEAN: value bytes, packed afterwards)
     u64* out_offs;     // String: lengths, then the scan
     u64* err;
@@ -87,6 +88,11 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     __shared__ u8 ring[RING];
     const ScanPage pg = a.pages[blockIdx.x];
     const u32 lane = threadIdx.x;
+    // an uncompressed page is decoded where it lies in the chunk (page_base): nothing to copy
+    if (CODEC == DBG_PQ_UNCOMPRESSED || !pg.compressed) {
+        if (pg.comp != pg.uncomp && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+        return;
+    }
     const u8* src = a.chunk + pg.src;
     u8* dst = a.buf + pg.dst;
     // v2 levels (uncompressed) first
@@ -94,14 +100,6 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     const u8* s = src + pg.lv;
     u8* o = dst + pg.lv;
     const u32 sn = pg.comp - pg.lv, on = pg.uncomp - pg.lv;
-    if (CODEC == DBG_PQ_UNCOMPRESSED || !pg.compressed) {
-        if (sn != on) {
-            if (lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
-            return;
-        }
-        for (u32 j = lane; j < on; j += 64) o[j] = s[j];
-        return;
-    }
     bool bad = false;
     u32 p = 0, w = 0;  // input / output cursors (uniform)
     auto copy_lit = [&](u32 len) {
@@ -211,6 +209,12 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Page-relative layout helpers
 // ---------------------------------------------------------------------------------------------
+// the page's uncompressed bytes: inflated into the page buffer, or in place in the chunk
+__device__ __forceinline__ const u8* page_base(const ScanArgs& a, const ScanPage& pg) {
+    return pg.compressed ? a.buf + pg.dst : a.chunk + pg.src;
+}
+// ---------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ u32 rd_u32(const u8* p) { return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24); }
 
 // start of the values section and the definition-level byte range [d0, d1) of a data page
@@ -240,7 +244,7 @@ __global__ void __launch_bounds__(64) pq_walk_kernel(ScanArgs a) {
     if (pi >= a.n_pages) return;
     const ScanPage pg = a.pages[pi];
     if (pg.encoding != ENC_PLAIN && pg.kind != PG_DICT) return;
-    const u8* base = a.buf + pg.dst;
+    const u8* base = page_base(a, pg);
     u32 d0, d1, vp;
     if (!page_sections(a, pg, base, d0, d1, vp)) {
         atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
@@ -417,7 +421,9 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
     __shared__ u32 s_bad;
     const ScanPage pg = a.pages[blockIdx.x];
     if (pg.kind == PG_DICT) return;
-    const u8* base = a.buf + pg.dst;
+    if (threadIdx.x == 0) s_bad = 0;
+    __syncthreads();
+    const u8* base = page_base(a, pg);
     const u32 n = pg.num_values;
     auto fail = [&](u64 bit) {
         if (threadIdx.x == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)bit);
@@ -425,16 +431,23 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
     u32 d0, d1, vp;
     if (!page_sections(a, pg, base, d0, d1, vp)) return fail(SERR_MALFORMED);
     u8* vb = a.vbytes + pg.row0;
+    const bool dict = pg.encoding == ENC_PLAIN_DICT || pg.encoding == ENC_RLE_DICT;
+    const bool rle_bool = pg.encoding == ENC_RLE && a.ptype == DBG_PQ_BOOLEAN;
+    // a required PLAIN page is elementwise (value index = row index): its rows are split over the
+    // grid's y dimension; every other page is decoded by its y = 0 workgroup alone
+    const bool split = !a.max_def && !dict && !rle_bool;
+    if (!split && blockIdx.y) return;
     // 1. definition levels -> one byte per row
-    if (a.max_def) {
+    if (split) {
+        const u32 per = (n + gridDim.y - 1) / gridDim.y, lo = blockIdx.y * per, hi = min(n, lo + per);
+        for (u32 k = lo + threadIdx.x; k < hi; k += DEC_NT) vb[k] = 1;
+    } else if (a.max_def) {
         if (!hybrid_expand(base, d0, d1, 1, n, rt, [&](u32 k, u32 v) { vb[k] = (u8)(v != 0); })) return fail(SERR_MALFORMED);
     } else {
         for (u32 k = threadIdx.x; k < n; k += DEC_NT) vb[k] = 1;
         __syncthreads();
     }
     // 2. dictionary indices (or RLE booleans) by value index
-    const bool dict = pg.encoding == ENC_PLAIN_DICT || pg.encoding == ENC_RLE_DICT;
-    const bool rle_bool = pg.encoding == ENC_RLE && a.ptype == DBG_PQ_BOOLEAN;
     u32* ix = a.idx + pg.vk0;
     if (dict || rle_bool) {
         u32 p0 = vp, bw = 1, p1 = pg.uncomp;
@@ -469,11 +482,76 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
     }
     // 3. values, 256 rows per round: block scan of the definition bytes -> value index
     const ScanPage* dp = a.dict_page >= 0 ? &a.pages[a.dict_page] : nullptr;
-    const u8* dbase = dp ? a.buf + dp->dst : nullptr;
+    const u8* dbase = dp ? page_base(a, *dp) : nullptr;
     const u32 dn = dp ? dp->num_values : 0;
     const u32 pw = phys_width(a);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_bad = 0;
+    // one row: its value (value index vi when def) converted and written; true = out of range
+    auto emit = [&](u32 k, u32 vi, u32 def) -> bool {
+        const u64 row = pg.row0 + k;
+        bool bad = false;
+        if (a.ptype == DBG_PQ_BYTE_ARRAY) {
+            u64 len = 0, so = 0;
+            if (def) {
+                if (dict) {
+                    const u32 i = ix[vi];
+                    if (i >= dn || i >= a.nwalk[a.dict_page]) {
+                        bad = true;
+                    } else {
+                        const u64 st = a.vstart[dp->vk0 + i];
+                        len = rd_u32(dbase + st);
+                        so = (u64)(dbase + st + 4);
+                    }
+                } else if (vi >= a.nwalk[blockIdx.x]) {
+                    bad = true;
+                } else {
+                    const u64 st = a.vstart[pg.vk0 + vi];
+                    len = rd_u32(base + st);
+                    so = (u64)(base + st + 4);
+                }
+            }
+            a.out_offs[row] = bad ? 0 : len;
+            a.sptr[row] = so;
+        } else if (a.ptype == DBG_PQ_BOOLEAN) {
+            u8 v = 0;
+            if (def) {
+                if (rle_bool) {
+                    v = (u8)(ix[vi] & 1);
+                } else if (vp + (vi >> 3) < pg.uncomp) {
+                    v = (base[vp + (vi >> 3)] >> (vi & 7)) & 1;
+                } else {
+                    bad = true;
+                }
+            }
+            a.out_data[row] = v;
+        } else {
+            u8* d = a.out_data + row * a.twidth;
+            const u8* sp = nullptr;
+            if (def) {
+                if (dict) {
+                    const u32 i = ix[vi];
+                    if (i < dn && (u64)(i + 1) * pw <= dp->uncomp) sp = dbase + (u64)i * pw;
+                } else if ((u64)vp + (u64)(vi + 1) * pw <= pg.uncomp) {
+                    sp = base + vp + (u64)vi * pw;
+                }
+                if (!sp) bad = true;
+            }
+            if (sp) put_value(a, sp, d);
+            else for (u32 j = 0; j < a.twidth; ++j) d[j] = 0;
+        }
+        return bad;
+    };
+    if (split) {
+        const u32 per = (n + gridDim.y - 1) / gridDim.y, lo = blockIdx.y * per, hi = min(n, lo + per);
+        bool bad = false;
+        for (u32 k = lo + threadIdx.x; k < hi; k += DEC_NT) bad |= emit(k, k, 1);
+        if (bad) s_bad = 1;
+        __syncthreads();
+        if (s_bad) fail(SERR_DICT_RANGE);
+        if (a.ptype == DBG_PQ_BYTE_ARRAY && blockIdx.y == 0 && threadIdx.x == 0 && n != a.nwalk[blockIdx.x])
+            atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_COUNT);
+        return;
+    }
     u32 vbase = 0;
     for (u32 r0 = 0; r0 < n; r0 += DEC_NT) {
         const u32 k = r0 + threadIdx.x;
@@ -487,61 +565,7 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
             if (w < wave) pre += wtot[w];
             tot += wtot[w];
         }
-        const u32 vi = vbase + pre + pre_w;
-        if (k < n) {
-            const u64 row = pg.row0 + k;
-            bool bad = false;
-            if (a.ptype == DBG_PQ_BYTE_ARRAY) {
-                u64 len = 0, so = 0;
-                if (def) {
-                    if (dict) {
-                        const u32 i = ix[vi];
-                        if (i >= dn || i >= a.nwalk[a.dict_page]) {
-                            bad = true;
-                        } else {
-                            const u64 st = a.vstart[dp->vk0 + i];
-                            len = rd_u32(dbase + st);
-                            so = dp->dst + st + 4;
-                        }
-                    } else if (vi >= a.nwalk[blockIdx.x]) {
-                        bad = true;
-                    } else {
-                        const u64 st = a.vstart[pg.vk0 + vi];
-                        len = rd_u32(base + st);
-                        so = pg.dst + st + 4;
-                    }
-                }
-                a.out_offs[row] = bad ? 0 : len;
-                a.sptr[row] = so;
-            } else if (a.ptype == DBG_PQ_BOOLEAN) {
-                u8 v = 0;
-                if (def) {
-                    if (rle_bool) {
-                        v = (u8)(ix[vi] & 1);
-                    } else if (vp + (vi >> 3) < pg.uncomp) {
-                        v = (base[vp + (vi >> 3)] >> (vi & 7)) & 1;
-                    } else {
-                        bad = true;
-                    }
-                }
-                a.out_data[row] = v;
-            } else {
-                u8* d = a.out_data + row * a.twidth;
-                const u8* sp = nullptr;
-                if (def) {
-                    if (dict) {
-                        const u32 i = ix[vi];
-                        if (i < dn && (u64)(i + 1) * pw <= dp->uncomp) sp = dbase + (u64)i * pw;
-                    } else if ((u64)vp + (u64)(vi + 1) * pw <= pg.uncomp) {
-                        sp = base + vp + (u64)vi * pw;
-                    }
-                    if (!sp) bad = true;
-                }
-                if (sp) put_value(a, sp, d);
-                else for (u32 j = 0; j < a.twidth; ++j) d[j] = 0;
-            }
-            if (bad) s_bad = 1;
-        }
+        if (k < n && emit(k, vbase + pre + pre_w, def)) s_bad = 1;
         vbase += tot;
         __syncthreads();
     }
@@ -553,13 +577,13 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
 }
 
 // payload gather: one lane per row
-__global__ void __launch_bounds__(256) pq_strings_kernel(const u8* __restrict__ buf, const u64* __restrict__ sptr,
-                                                         const u64* __restrict__ offs, u64 rows, u8* __restrict__ out, u64 cap) {
+__global__ void __launch_bounds__(256) pq_strings_kernel(const u64* __restrict__ sptr, const u64* __restrict__ offs, u64 rows,
+                                                         u8* __restrict__ out, u64 cap) {
     const u64 r = blockIdx.x * 256ULL + threadIdx.x;
     if (r >= rows) return;
     const u64 o = offs[r], e = offs[r + 1];
-    if (e > cap) return;
-    const u8* s = buf + sptr[r];
+    if (e > cap || e == o) return;
+    const u8* s = (const u8*)sptr[r];  // the value's bytes: page buffer or chunk
     for (u64 j = 0; j < e - o; ++j) out[o + j] = s[j];
 }
 
@@ -907,7 +931,8 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
             hipLaunchKernelGGL(pq_walk_kernel, dim3((u32)((pages.size() + 63) / 64)), dim3(64), 0, s, a);
             SCAN_HIP(hipGetLastError());
         }
-        hipLaunchKernelGGL(pq_decode_kernel, g, dim3(DEC_NT), 0, s, a);
+        // required PLAIN pages are split 16 ways (1 MiB pages of 2-byte values: 500 K rows each)
+        hipLaunchKernelGGL(pq_decode_kernel, dim3((u32)pages.size(), c.max_def_level ? 1 : 16), dim3(DEC_NT), 0, s, a);
         SCAN_HIP(hipGetLastError());
     }
     if (is_str) {
@@ -916,7 +941,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         else SCAN_HIP(hipMemsetAsync(out->offsets, 0, 8, s));
         SCAN_HIP(hipMemcpyAsync(ctx->err + 1, out->offsets + row, 8, hipMemcpyDeviceToDevice, s));
         if (row && out->data)
-            hipLaunchKernelGGL(pq_strings_kernel, dim3((u32)((row + 255) / 256)), dim3(256), 0, s, ctx->buf, ctx->sptr, out->offsets, row,
+            hipLaunchKernelGGL(pq_strings_kernel, dim3((u32)((row + 255) / 256)), dim3(256), 0, s, ctx->sptr, out->offsets, row,
                                (u8*)out->data, max_string_bytes);
         SCAN_HIP(hipGetLastError());
     }
