@@ -34,6 +34,12 @@ class AggregatorParams:
     group_data_types: List[DataType]
     aggregate_functions: List[AggregateFunction]
     max_block_size: int = 65536
+    # enable_experimental_aggregate_hashtable (settings_default.rs); False selects the legacy
+    # HashMethod path's buckets: single-level (-1) below group_by_two_level_threshold groups, else
+    # 256 buckets hash2bucket<8, true> of FastHash (AGG/transform_aggregate_partial.rs:330-350,
+    # 415-447)
+    enable_experimental_aggregate_hashtable: bool = True
+    group_by_two_level_threshold: int = 20000
 
     def to_abi(self, partial: bool, capacity_hint: int, device: int):
         # a DISTINCT aggregate raises here (AggregateFunction.to_abi): DistinctAggregator runs it
@@ -452,6 +458,7 @@ class AggregateMeta:
     max_partition_count: int = 1
     data: Optional[List["AggregateMeta"]] = None
     serialized: Optional[DataBlock] = None
+    legacy: bool = False  # a legacy HashMethod partial's bucket (-1 = single-level, else 0..255)
 
     @staticmethod
     def create_agg_payload(bucket: int, payload: Payload, max_partition_count: int) -> "AggregateMeta":
@@ -477,10 +484,16 @@ def _cuda_device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+SINGLE_LEVEL_BUCKET = -1  # SINGLE_LEVEL_BUCKET_NUM (AGG/transform_partition_bucket.rs)
+LEGACY_BUCKETS = 256      # PartitionedHashtable<_, 8> (HT/partitioned_hashtable.rs)
+LEGACY_SCHEME = 2
+
+
 def export_buckets(table: AggregateHashTable, n_parts: int, scheme: int = 1) -> List[Payload]:
     """All groups of `table` as n_parts bucket payloads (dbg_agg_partition + export_records), in
     bucket order; scheme 1 = radix bits [48 - r, 48) (EAGG/partitioned_payload.rs:121, 267-275),
-    scheme 0 = hash % n_parts (EAGG/payload.rs:377-383)."""
+    scheme 0 = hash % n_parts (EAGG/payload.rs:377-383), scheme 2 = the legacy buckets
+    hash2bucket<log2 n, true>(FastHash(key)) (HT/partitioned_hashtable.rs:77-83)."""
     import torch
     counts, sbytes = table.partition(n_parts, scheme)
     w = table.record_width()
@@ -525,8 +538,22 @@ class TransformPartialAggregate:
 
     def on_finish(self) -> List[AggregateMeta]:
         """on_finish (:449-465): one AggregatePayload per non-empty radix bucket, bucket = hash bits
-        [48 - r, 48), with r from the shared radix hint and this table's payload size."""
+        [48 - r, 48), with r from the shared radix hint and this table's payload size.
+
+        Legacy path (enable_experimental_aggregate_hashtable = 0, :415-447): the table stays
+        single-level (bucket -1) until it holds group_by_two_level_threshold groups (the
+        reference converts after the block that reaches it, :330-350; groups only grow, so the
+        final count decides the same), then emits the non-empty of 256 buckets
+        hash2bucket<8, true>(FastHash(key)) (HT/partitioned_hashtable.rs:77-83)."""
         n_groups = sum(self.hashtable.partition(1, 1)[0])
+        if not self.params.enable_experimental_aggregate_hashtable:
+            if not n_groups:
+                return []
+            if n_groups < self.params.group_by_two_level_threshold:
+                payloads = export_buckets(self.hashtable, 1, LEGACY_SCHEME)
+                return [AggregateMeta(SINGLE_LEVEL_BUCKET, payloads[0], 1, legacy=True)]
+            payloads = export_buckets(self.hashtable, LEGACY_BUCKETS, LEGACY_SCHEME)
+            return [AggregateMeta(b, p, LEGACY_BUCKETS, legacy=True) for b, p in enumerate(payloads) if len(p)]
         tuple_size = payload_tuple_size(self.params.group_data_types, len(self.params.aggregate_functions))
         bits = partial_bucket_bits(self.config, n_groups, tuple_size)
         payloads = export_buckets(self.hashtable, 1 << bits)
@@ -551,7 +578,7 @@ class TransformPartitionBucket:
     def push(self, metas: Sequence[AggregateMeta]) -> None:
         self.inputs.extend(metas)
 
-    def _partition_payload(self, meta: AggregateMeta, max_partition_count: int) -> List[AggregateMeta]:
+    def _partition_payload(self, meta: AggregateMeta, max_partition_count: int, scheme: int = 1) -> List[AggregateMeta]:
         """partition_payload (:389-429) for AggregatePayload, partition_block (:341-387) for
         Serialized: the rows re-inserted into a scratch table (merge_states / batch_merge), then
         exported as records at the larger radix."""
@@ -562,16 +589,34 @@ class TransformPartitionBucket:
             else:
                 p = meta.payload
                 scratch.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
-            out = export_buckets(scratch, max_partition_count)
+            out = export_buckets(scratch, max_partition_count, scheme)
             import torch
             torch.cuda.current_stream().synchronize()  # exports complete before the scratch goes
         finally:
             scratch.close()
-        return [AggregateMeta.create_agg_payload(b, q, max_partition_count) for b, q in enumerate(out) if len(q)]
+        return [AggregateMeta(b, q, max_partition_count, legacy=meta.legacy) for b, q in enumerate(out) if len(q)]
+
+    def _finish_legacy(self) -> List[AggregateMeta]:
+        """TransformPartitionBucket (AGG/transform_partition_bucket.rs:140-300): with only
+        single-level inputs, one Partitioned meta of bucket -1 (try_push_single_level); once any
+        input is two-level, every single-level one is split into the 256 buckets
+        (partition_hashtable / partition_block: hash2bucket<8, true> of the key's FastHash) and
+        the buckets go out in ascending order (try_push_two_level)."""
+        inputs, self.inputs = self.inputs, []
+        if all(m.bucket == SINGLE_LEVEL_BUCKET for m in inputs):
+            return [AggregateMeta(SINGLE_LEVEL_BUCKET, None, 0, inputs, legacy=True)]
+        buckets = {}
+        for m in inputs:
+            split = [m] if m.bucket != SINGLE_LEVEL_BUCKET else self._partition_payload(m, LEGACY_BUCKETS, LEGACY_SCHEME)
+            for a in split:
+                buckets.setdefault(a.bucket, []).append(a)
+        return [AggregateMeta(b, None, 0, buckets[b], legacy=True) for b in sorted(buckets)]
 
     def finish(self) -> List[AggregateMeta]:
         if not self.inputs:
             return []
+        if any(m.legacy for m in self.inputs):
+            return self._finish_legacy()
         maxp = max(m.max_partition_count for m in self.inputs)
         buckets = {}
         for m in self.inputs:

@@ -200,6 +200,8 @@ struct dbg_agg_handle {
     u64* d_part_str_pos = nullptr;
     u64* d_part_str_base = nullptr;
     u64 part_cap = 0, part_str_cap = 0;
+    u64* d_lpart = nullptr;   // scheme 2: legacy bucket per slot / group record (u32)
+    u64 lpart_cap = 0;
     std::vector<u64> part_counts, part_strings;
     // fused finalize: validity bytes staging
     u8* vbytes = nullptr;
@@ -840,7 +842,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     for (auto& b : h->owned) hipFree(b.p);
     for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
-                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->vbytes, h->part_sorted, h->part_bounds,
+                    h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->d_lpart, h->vbytes, h->part_sorted, h->part_bounds,
                     h->part_temp, h->ser_err};
     for (void* p : bufs)
         if (p) hipFree(p);
@@ -1530,7 +1532,7 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
         TableDesc t = table_desc(h);
         {
             prof::Scope ps("count_groups", h->stream);
-            launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+            launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, nullptr, h->d_pos, h->d_str_pos);
         }
         u64* totals = h->d_pos + nb;  // [0] groups, [1 + c] string bytes of key column c
         launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
@@ -1866,7 +1868,7 @@ static int fin_launch(dbg_agg_handle* h) {
     u64* totals = h->d_pos + nb;
     if (!small && !h->pp) {
         prof::Scope ps("count_groups", h->stream);
-        launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, h->d_pos, h->d_str_pos);
+        launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, nullptr, h->d_pos, h->d_str_pos);
         launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
         if (S.has_strings && !S.inline_keys)
             for (int c = 0; c < S.n_keys; ++c)
@@ -2131,16 +2133,59 @@ int dbg_agg_record_layout(const dbg_agg_params* params, dbg_record_layout* out) 
     return DBG_OK;
 }
 
+static int legacy_method(const dbg_datatype* types, int n, int* kind, uint32_t* key_bytes);
+
+// The group key's legacy layout (legacy_method's FixedKeys packing or SingleBinary) by key column.
+static int legacy_layout(const Spec& S, u32 bits, LegacyLayout* L) {
+    memset(L, 0, sizeof(*L));
+    int kind = 0;
+    uint32_t kb = 0;
+    RETURN_IF(legacy_method(S.key_types, S.n_keys, &kind, &kb));
+    if (kind == DBG_LEGACY_SERIALIZER) return fail(DBG_ERR_UNSUPPORTED, "legacy HashMethodSerializer keys stay on the CPU path");
+    L->bits = bits;
+    if (kind == DBG_LEGACY_SINGLE_BINARY) {
+        L->binary = 1;
+        return DBG_OK;
+    }
+    L->words = kb <= 8 ? 1 : (kb <= 16 ? 2 : 4);
+    // build_keys_vec: stable order by value width, widest first; null bytes after all values
+    std::vector<int> order(S.n_keys);
+    for (int j = 0; j < S.n_keys; ++j) order[j] = j;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return type_width(S.key_types[a].type) > type_width(S.key_types[b].type); });
+    u32 off = 0, noff = 0;
+    for (int j = 0; j < S.n_keys; ++j) noff += type_width(S.key_types[j].type);
+    for (int j = 0; j < S.n_keys; ++j) {
+        const int c = order[j];
+        L->off[c] = off;
+        off += type_width(S.key_types[c].type);
+        L->null_off[c] = S.key_types[c].nullable ? (int32_t)noff++ : -1;
+    }
+    return DBG_OK;
+}
+
 int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t* rec_counts, uint64_t* string_bytes) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     if (n_parts < 1 || n_parts > 256) return fail(DBG_ERR_UNSUPPORTED, "1..256 partitions");
-    if (scheme == 1 && (n_parts & (n_parts - 1))) return fail(DBG_ERR_INVALID, "radix partitions must be a power of two");
+    if (scheme < 0 || scheme > 2) return fail(DBG_ERR_INVALID, "scheme 0 (hash % n), 1 (radix bits) or 2 (legacy buckets)");
+    if (scheme >= 1 && (n_parts & (n_parts - 1))) return fail(DBG_ERR_INVALID, "radix partitions must be a power of two");
+    LegacyLayout L;
+    if (scheme == 2) RETURN_IF(legacy_layout(h->spec, 31 - __builtin_clz(n_parts), &L));
     HIPCHECK(hipSetDevice(h->device));
     RETURN_IF(flush_pending(h));
     if (h->pp) RETURN_IF(pp_finalize(h, nullptr, nullptr));
     else RETURN_IF(resolve_overflow(h));
     const Spec& S = h->spec;
     u64 nb = h->pp ? pp_grec_blocks(std::max<u64>(h->n_groups, 1)) : finalize_blocks(h->cap);
+    const u32* lpart = nullptr;
+    if (scheme == 2 && n_parts > 1) {  // hash2bucket<bits, true> of each group's FastHash
+        const u64 n = h->pp ? h->n_groups : h->cap + 1;
+        RETURN_IF(ensure_buf(&h->d_lpart, &h->lpart_cap, n / 2 + 1));
+        prof::Scope ps("legacy_bucket", h->stream);
+        if (h->pp) launch_pp_grec_legacy_bucket(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, L, (u32*)h->d_lpart);
+        else launch_legacy_slot_bucket(h->stream, h->dspec, h->dbatches, table_desc(h), L, (u32*)h->d_lpart);
+        lpart = (const u32*)h->d_lpart;
+    }
     u64 nflat = (u64)n_parts * nb;
     RETURN_IF(ensure_buf(&h->d_part_pos, &h->part_cap, nflat + 8));
     RETURN_IF(ensure_buf(&h->d_part_str_pos, &h->part_str_cap, nflat * S.n_keys + 8));
@@ -2149,10 +2194,10 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
     {
         prof::Scope ps("count_groups", h->stream);
         if (h->pp)
-            launch_pp_grec_count_parts(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, n_parts, scheme, h->d_part_pos,
-                                       h->d_part_str_pos, nb);
+            launch_pp_grec_count_parts(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, n_parts, scheme, lpart,
+                                       h->d_part_pos, h->d_part_str_pos, nb);
         else
-            launch_count_groups(h->stream, h->dspec, S, h->dbatches, table_desc(h), n_parts, scheme, h->d_part_pos,
+            launch_count_groups(h->stream, h->dspec, S, h->dbatches, table_desc(h), n_parts, scheme, lpart, h->d_part_pos,
                                 h->d_part_str_pos);
     }
     h->part_nb = nb;
@@ -2188,11 +2233,12 @@ int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strin
     RETURN_IF(flush_pending(h));
     prof::Scope ps("export_records", h->stream);
     if (h->pp)
-        launch_pp_grec_export(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, h->part_n, h->part_scheme, h->d_part_pos,
-                              h->d_part_str_pos, h->part_nb, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
+        launch_pp_grec_export(h->stream, h->dspec, h->dbatches, h->pp_grec, h->n_groups, h->part_n, h->part_scheme,
+                              (const u32*)h->d_lpart, h->d_part_pos, h->d_part_str_pos, h->part_nb, (u8*)dev_records,
+                              (u8*)dev_strings, h->d_part_str_base);
     else
-        launch_export(h->stream, h->dspec, h->spec, h->dbatches, table_desc(h), h->part_n, h->part_scheme, h->d_part_pos,
-                      h->d_part_str_pos, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
+        launch_export(h->stream, h->dspec, h->spec, h->dbatches, table_desc(h), h->part_n, h->part_scheme, (const u32*)h->d_lpart,
+                      h->d_part_pos, h->d_part_str_pos, (u8*)dev_records, (u8*)dev_strings, h->d_part_str_base);
     HIPCHECK(hipGetLastError());
     return DBG_OK;
 }

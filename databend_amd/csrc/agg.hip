@@ -17,6 +17,7 @@
 #include <limits>
 #include <type_traits>
 
+#include "legacy.hpp"
 #include "agg.hpp"
 #include "agg_dev.hpp"
 
@@ -597,8 +598,10 @@ void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
 // ------------------------------------------------------------------------------------------
 u64 finalize_blocks(u64 cap) { return (cap + 1 + SLOTS_PER_BLOCK - 1) / SLOTS_PER_BLOCK; }
 
-__device__ __forceinline__ u32 part_of(u64 h, u32 n_parts, int scheme) {
+// scheme 2: the slot's legacy bucket, computed beforehand by legacy_slot_bucket_kernel
+__device__ __forceinline__ u32 part_of(u64 h, u32 n_parts, int scheme, const u32* lpart, u64 s) {
     if (n_parts <= 1) return 0;
+    if (scheme == 2) return lpart[s];
     if (scheme == 0) return (u32)(h % n_parts);  // Payload::scatter: hash % n (payload.rs:383)
     u32 rb = 31 - __clz(n_parts);                // radix bits [48 - r, 48) (partitioned_payload.rs:121)
     return (u32)((h >> (48 - rb)) & (n_parts - 1));
@@ -612,8 +615,8 @@ __device__ __forceinline__ u64 key_str_len(const Spec& S, const BatchDesc* batch
 #define MAX_PARTS_LDS 256
 
 __global__ void __launch_bounds__(BLOCK) count_groups_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                            TableDesc t, u32 n_parts, int scheme, u64* hist, u64* str_hist,
-                                                            u64 nblocks) {
+                                                            TableDesc t, u32 n_parts, int scheme, const u32* __restrict__ lpart,
+                                                            u64* hist, u64* str_hist, u64 nblocks) {
     const Spec& S = *spec;
     __shared__ unsigned long long lh[MAX_PARTS_LDS];
     __shared__ unsigned long long ls[DBG_MAX_KEYS][MAX_PARTS_LDS];
@@ -630,7 +633,7 @@ __global__ void __launch_bounds__(BLOCK) count_groups_kernel(const Spec* __restr
         if (e == SLOT_EMPTY) continue;
         u32 p = 0;
         if (n_parts > 1) {
-            p = part_of(entry_hash(S, batches, e, s == t.cap), n_parts, scheme);
+            p = part_of(scheme == 2 ? 0 : entry_hash(S, batches, e, s == t.cap), n_parts, scheme, lpart, s);
             atomicAdd(&lh[p], 1ULL);
         } else {
             mine++;
@@ -653,9 +656,61 @@ __global__ void __launch_bounds__(BLOCK) count_groups_kernel(const Spec* __restr
 }
 
 void launch_count_groups(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t, u32 n_parts,
-                         int scheme, u64* hist, u64* str_hist) {
+                         int scheme, const u32* lpart, u64* hist, u64* str_hist) {
     u64 nb = finalize_blocks(t.cap);
-    hipLaunchKernelGGL(count_groups_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, n_parts, scheme, hist, str_hist, nb);
+    hipLaunchKernelGGL(count_groups_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, n_parts, scheme, lpart, hist, str_hist, nb);
+}
+
+// Legacy bucket of every occupied slot (enable_experimental_aggregate_hashtable = 0): the
+// FastHash of the group's FixedKeys / SingleBinary key (legacy.hpp), hash2bucket<bits, true>.
+__global__ void __launch_bounds__(BLOCK) legacy_slot_bucket_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                  TableDesc t, LegacyLayout L, u32* __restrict__ out) {
+    const Spec& S = *spec;
+    __shared__ u32 tab[256];
+    crc_table_init(tab);
+    for (u64 s = blockIdx.x * (u64)BLOCK + threadIdx.x; s <= t.cap; s += (u64)gridDim.x * BLOCK) {
+        const u64 e = t.slots[s * t.stride_words];
+        if (e == SLOT_EMPTY) continue;
+        u64 h;
+        if (L.binary) {
+            const StrRef sr = dcol_str(batches[ref_bid(e)].keys[0], ref_row(e));
+            h = legacy_bytes_hash(tab, sr.p, sr.len);
+        } else {
+            u64 k[4] = {0, 0, 0, 0};
+            const u64 key = s == t.cap ? SLOT_EMPTY : e;
+            for (int c = 0; c < S.n_keys; ++c) {
+                const dbg_datatype& ty = S.key_types[c];
+                const u32 w = type_width(ty.type);
+                bool v;
+                u64 lo, hi = 0;
+                if (S.inline_keys) {
+                    v = !ty.nullable || ((key >> (8 * S.voff[c])) & 0xff) != 0;
+                    lo = (key >> (8 * S.koff[c])) & width_mask(w);
+                } else {
+                    const DCol& kc = batches[ref_bid(e)].keys[c];
+                    const u64 row = ref_row(e);
+                    v = dcol_valid(kc, row);
+                    lo = dcol_bits(kc, row);
+                    if (w == 16) hi = dcol_hi(kc, row);
+                }
+                if (!v) {  // null byte 1, value bytes 0
+                    const u32 o = (u32)L.null_off[c];
+                    k[o >> 3] |= 1ULL << (8 * (o & 7));
+                } else {
+                    legacy_put(k, L.off[c], lo, hi, w);
+                }
+            }
+            h = legacy_fixed_crc(tab, k, L.words);
+        }
+        out[s] = legacy_bucket(h, L.bits);
+    }
+}
+
+void launch_legacy_slot_bucket(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const LegacyLayout& L,
+                               u32* out) {
+    u64 blocks = (t.cap + 1 + BLOCK - 1) / BLOCK;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(legacy_slot_bucket_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, batches, t, L, out);
 }
 
 // Single-workgroup exclusive scan (in place) over n u64; *total = sum.
@@ -1854,8 +1909,9 @@ __device__ __forceinline__ void write_inline_key_part(const Spec& S, u64 key, u8
 }
 
 __global__ void __launch_bounds__(BLOCK) export_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                      TableDesc t, u32 n_parts, int scheme, const u64* pos, const u64* str_pos,
-                                                      u64 nblocks, u8* rec_out, u8* str_out, const u64* part_str_base) {
+                                                      TableDesc t, u32 n_parts, int scheme, const u32* __restrict__ lpart,
+                                                      const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out, u8* str_out,
+                                                      const u64* part_str_base) {
     const Spec& S = *spec;
     __shared__ unsigned long long cur[MAX_PARTS_LDS];
     __shared__ unsigned long long scur[DBG_MAX_KEYS][MAX_PARTS_LDS];
@@ -1874,7 +1930,7 @@ __global__ void __launch_bounds__(BLOCK) export_kernel(const Spec* __restrict__ 
         u64 e = st[0];
         if (e == SLOT_EMPTY) continue;
         u64 h = entry_hash(S, batches, e, s == t.cap);
-        u32 p = part_of(h, n_parts, scheme);
+        u32 p = part_of(h, n_parts, scheme, lpart, s);
         u64 r = atomicAdd(&cur[p], 1ULL);
         u8* rec = rec_out + r * S.rec_width;
         *(u64*)rec = h;
@@ -1909,9 +1965,10 @@ __global__ void __launch_bounds__(BLOCK) export_kernel(const Spec* __restrict__ 
 }
 
 void launch_export(hipStream_t s, const Spec* dspec, const Spec& S, const BatchDesc* batches, const TableDesc& t, u32 n_parts,
-                   int scheme, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out, const u64* part_str_base) {
+                   int scheme, const u32* lpart, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out,
+                   const u64* part_str_base) {
     u64 nb = finalize_blocks(t.cap);
-    hipLaunchKernelGGL(export_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, n_parts, scheme, pos, str_pos, nb,
+    hipLaunchKernelGGL(export_kernel, dim3((u32)nb), dim3(BLOCK), 0, s, dspec, batches, t, n_parts, scheme, lpart, pos, str_pos, nb,
                        rec_out, str_out, part_str_base);
 }
 

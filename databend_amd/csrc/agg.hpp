@@ -223,8 +223,14 @@ void launch_rehash(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
                    u64 old_cap, const TableDesc& t);
 // finalize: counts per block of occupied slots (and string bytes per key col); returns blocks used
 u64 finalize_blocks(u64 cap);
+// scheme 0: hash % n; 1: radix bits [48 - r, 48); 2: lpart[slot] (legacy buckets, launch_legacy_slot_bucket)
+struct LegacyLayout;
+void launch_legacy_slot_bucket(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const LegacyLayout& L,
+                               u32* out);
+void launch_pp_grec_legacy_bucket(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n,
+                                  const LegacyLayout& L, u32* out);
 void launch_count_groups(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
-                         u32 n_parts, int scheme, u64* hist /* [n_parts][blocks] */, u64* str_hist /* [n_parts][n_keys][blocks] */);
+                         u32 n_parts, int scheme, const u32* lpart, u64* hist /* [n_parts][blocks] */, u64* str_hist /* [n_parts][n_keys][blocks] */);
 void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total);
 struct OutDesc {
     void* key_data[DBG_MAX_KEYS];
@@ -272,7 +278,7 @@ void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);
 void launch_export_fixed(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, u8* buf, u64 cap_records,
                          int recycle);
 void launch_export(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, const TableDesc& t,
-                   u32 n_parts, int scheme, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out,
+                   u32 n_parts, int scheme, const u32* lpart, const u64* pos, const u64* str_pos, u8* rec_out, u8* str_out,
                    const u64* part_str_base);
 
 // ---- partitioned payload (pp.hip) ----
@@ -361,8 +367,8 @@ void launch_pp_grec_write(hipStream_t s, const Spec* dspec, const BatchDesc* bat
                           const u64* str_pos /* [n_keys][blocks] scanned */, u64 nblocks, const OutDesc& out, u64* err);
 // group records -> exchange records partitioned by hash % n (scheme 0) or radix bits (scheme 1)
 void launch_pp_grec_count_parts(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n,
-                                u32 n_parts, int scheme, u64* hist /* [n_parts][blocks] */,
+                                u32 n_parts, int scheme, const u32* lpart, u64* hist /* [n_parts][blocks] */,
                                 u64* str_hist /* [n_parts][n_keys][blocks] */, u64 nblocks);
 void launch_pp_grec_export(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n, u32 n_parts,
-                           int scheme, const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out, u8* str_out,
+                           int scheme, const u32* lpart, const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out, u8* str_out,
                            const u64* part_str_base);

@@ -17,22 +17,6 @@
 #include "device.hpp"
 #include "legacy.hpp"
 
-// CRC32C (Castagnoli, reflected 0x82F63B78) of 8 little-endian bytes, table-driven from LDS
-__device__ __forceinline__ u32 crc32c_u64(const u32* tab, u32 crc, u64 v) {
-#pragma unroll
-    for (int b = 0; b < 8; ++b) crc = tab[(crc ^ (u32)(v >> (8 * b))) & 0xffu] ^ (crc >> 8);
-    return crc;
-}
-
-__device__ __forceinline__ void crc_table_init(u32* tab) {
-    for (u32 i = threadIdx.x; i < 256; i += blockDim.x) {
-        u32 c = i;
-        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
-        tab[i] = c;
-    }
-    __syncthreads();
-}
-
 __global__ void __launch_bounds__(256) legacy_fixed_hash_kernel(LegacyKeyDesc d, u64 rows, u64* __restrict__ hash,
                                                                u32* __restrict__ bucket, u32 bits) {
     __shared__ u32 tab[256];
@@ -48,19 +32,11 @@ __global__ void __launch_bounds__(256) legacy_fixed_hash_kernel(LegacyKeyDesc d,
             }
             const u32 w = c.width, o = d.off[j];
             const u64 lo = dcol_bits(c, i), hi = w == 16 ? dcol_hi(c, i) : 0;
-            // value bytes at offset o (little-endian; may straddle words)
-            const u32 wi = o >> 3, sh = 8 * (o & 7);
-            k[wi] |= lo << sh;
-            if (sh && wi + 1 < 4) k[wi + 1] |= lo >> (64 - sh);
-            if (w == 16) {
-                k[wi + 1] |= hi << sh;
-                if (sh && wi + 2 < 4) k[wi + 2] |= hi >> (64 - sh);
-            }
+            legacy_put(k, o, lo, hi, w);
         }
-        u32 crc = 0xFFFFFFFFu;
-        for (u32 w = 0; w < d.words; ++w) crc = crc32c_u64(tab, crc, k[w]);
+        const u64 crc = legacy_fixed_crc(tab, k, d.words);
         hash[i] = crc;
-        if (bucket) bucket[i] = (crc >> (32 - bits)) & ((1u << bits) - 1);
+        if (bucket) bucket[i] = legacy_bucket(crc, bits);
     }
 }
 
@@ -72,19 +48,9 @@ __global__ void __launch_bounds__(256) legacy_binary_hash_kernel(DCol c, u64 row
         // a NULL of a nullable String key hashes as its (empty) value bytes — NullableColumn keeps
         // the inner column's bytes; the reference hashes what the column holds at the row
         const StrRef s = dcol_str(c, i);
-        u64 v = ~0ULL;
-        if (s.len) {
-            u32 crc = 0xFFFFFFFFu;
-            for (u64 o = 0; o < s.len; o += 8) {
-                const u64 n = s.len - o < 8 ? s.len - o : 8;
-                u64 w = 0;
-                for (u64 b = 0; b < n; ++b) w |= (u64)s.p[o + b] << (8 * b);
-                crc = crc32c_u64(tab, crc, w);
-            }
-            v = crc;
-        }
+        const u64 v = legacy_bytes_hash(tab, s.p, s.len);
         hash[i] = v;
-        if (bucket) bucket[i] = (u32)((v >> (32 - bits)) & ((1ULL << bits) - 1));
+        if (bucket) bucket[i] = legacy_bucket(v, bits);
     }
 }
 

@@ -13,5 +13,64 @@ struct LegacyKeyDesc {
     u32 null_off[DBG_MAX_KEYS];
 };
 
+// Layout of a table's group key under the legacy method, indexed by key column (abi.hip
+// legacy_layout): FixedKeys value offset off[c] and null byte null_off[c] (-1: not nullable), or
+// SingleBinary (binary = 1).  Buckets are hash2bucket<bits, true>.
+struct LegacyLayout {
+    int32_t binary;
+    u32 words;
+    u32 bits;
+    u32 off[DBG_MAX_KEYS];
+    int32_t null_off[DBG_MAX_KEYS];
+};
+
+// CRC32C (Castagnoli, reflected 0x82F63B78) of 8 little-endian bytes, table-driven from LDS
+__device__ __forceinline__ u32 crc32c_u64(const u32* tab, u32 crc, u64 v) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) crc = tab[(crc ^ (u32)(v >> (8 * b))) & 0xffu] ^ (crc >> 8);
+    return crc;
+}
+
+__device__ __forceinline__ void crc_table_init(u32* tab) {
+    for (u32 i = threadIdx.x; i < 256; i += blockDim.x) {
+        u32 c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+        tab[i] = c;
+    }
+    __syncthreads();
+}
+
+// value bytes (w <= 16, little-endian lo/hi) at byte offset o of the packed key k[4]
+__device__ __forceinline__ void legacy_put(u64* k, u32 o, u64 lo, u64 hi, u32 w) {
+    const u32 wi = o >> 3, sh = 8 * (o & 7);
+    k[wi] |= lo << sh;
+    if (sh && wi + 1 < 4) k[wi + 1] |= lo >> (64 - sh);
+    if (w == 16) {
+        k[wi + 1] |= hi << sh;
+        if (sh && wi + 2 < 4) k[wi + 2] |= hi >> (64 - sh);
+    }
+}
+
+__device__ __forceinline__ u64 legacy_fixed_crc(const u32* tab, const u64* k, u32 words) {
+    u32 crc = 0xFFFFFFFFu;
+    for (u32 w = 0; w < words; ++w) crc = crc32c_u64(tab, crc, k[w]);
+    return crc;
+}
+
+// [u8] FastHash: 8-byte little-endian words, the last one zero-padded; empty -> u64::MAX
+__device__ __forceinline__ u64 legacy_bytes_hash(const u32* tab, const u8* p, u64 len) {
+    if (!len) return ~0ULL;
+    u32 crc = 0xFFFFFFFFu;
+    for (u64 o = 0; o < len; o += 8) {
+        const u64 n = len - o < 8 ? len - o : 8;
+        u64 w = 0;
+        for (u64 b = 0; b < n; ++b) w |= (u64)p[o + b] << (8 * b);
+        crc = crc32c_u64(tab, crc, w);
+    }
+    return crc;
+}
+
+__device__ __forceinline__ u32 legacy_bucket(u64 h, u32 bits) { return (u32)((h >> (32 - bits)) & ((1ULL << bits) - 1)); }
+
 void launch_legacy_fixed_hash(hipStream_t s, const LegacyKeyDesc& d, u64 rows, u64* hash, u32* bucket, u32 bits);
 void launch_legacy_binary_hash(hipStream_t s, const DCol& c, u64 rows, u64* hash, u32* bucket, u32 bits);

@@ -17,6 +17,7 @@
 // histograms, one workgroup scans them in (source partition, bucket, unit) order, and the scatter
 // pass stages records in LDS, sorts each tile by bucket and writes whole runs.  No device-scope
 // atomics touch the data: HBM traffic is record streams only.
+#include "legacy.hpp"
 #include "agg.hpp"
 #include "agg_dev.hpp"
 
@@ -1567,8 +1568,9 @@ void launch_pp_grec_write(hipStream_t s, const Spec* dspec, const BatchDesc* bat
 // (PartitionedPayload) — the same record format as the HBM table's export.
 // ------------------------------------------------------------------------------------------
 #define PP_MAX_PARTS 256
-__device__ __forceinline__ u32 pp_part_of(u64 h, u32 n_parts, int scheme) {
+__device__ __forceinline__ u32 pp_part_of(u64 h, u32 n_parts, int scheme, const u32* lpart, u64 r) {
     if (n_parts <= 1) return 0;
+    if (scheme == 2) return lpart[r];  // legacy bucket (pp_grec_legacy_bucket_kernel)
     if (scheme == 0) return (u32)(h % n_parts);
     const u32 rb = 31 - __clz(n_parts);
     return (u32)((h >> (48 - rb)) & (n_parts - 1));
@@ -1577,7 +1579,8 @@ __device__ __forceinline__ u64 pp_grec_hash(const Spec& S, const u8* k) { return
 
 __global__ void __launch_bounds__(PP_GNT) pp_grec_count_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                               const u8* __restrict__ grec, u64 n, u32 n_parts, int scheme,
-                                                              u64* __restrict__ hist, u64* __restrict__ str_hist, u64 nblocks) {
+                                                              const u32* __restrict__ lpart, u64* __restrict__ hist,
+                                                              u64* __restrict__ str_hist, u64 nblocks) {
     const Spec& S = *spec;
     __shared__ unsigned long long lh[PP_MAX_PARTS];
     __shared__ unsigned long long ls[DBG_MAX_KEYS][PP_MAX_PARTS];
@@ -1589,7 +1592,7 @@ __global__ void __launch_bounds__(PP_GNT) pp_grec_count_kernel(const Spec* __res
     const u64 r0 = (u64)blockIdx.x * PP_GB;
     for (u64 r = r0 + threadIdx.x; r < r0 + PP_GB && r < n; r += PP_GNT) {
         const u8* k = grec + r * S.pp_rw_state;
-        const u32 p = pp_part_of(pp_grec_hash(S, k), n_parts, scheme);
+        const u32 p = pp_part_of(scheme == 2 ? 0 : pp_grec_hash(S, k), n_parts, scheme, lpart, r);
         atomicAdd(&lh[p], 1ULL);
         for (int c = 0; c < S.n_keys; ++c)
             if (S.key_types[c].type == DBG_STRING) {
@@ -1605,14 +1608,15 @@ __global__ void __launch_bounds__(PP_GNT) pp_grec_count_kernel(const Spec* __res
 }
 
 void launch_pp_grec_count_parts(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n, u32 n_parts,
-                                int scheme, u64* hist, u64* str_hist, u64 nblocks) {
+                                int scheme, const u32* lpart, u64* hist, u64* str_hist, u64 nblocks) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(pp_grec_count_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, hist,
+    hipLaunchKernelGGL(pp_grec_count_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, lpart, hist,
                        str_hist, nblocks);
 }
 
 __global__ void __launch_bounds__(PP_GNT) pp_grec_export_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                const u8* __restrict__ grec, u64 n, u32 n_parts, int scheme,
+                                                               const u32* __restrict__ lpart,
                                                                const u64* __restrict__ pos, const u64* __restrict__ str_pos,
                                                                u64 nblocks, u8* rec_out, u8* str_out,
                                                                const u64* __restrict__ part_str_base) {
@@ -1628,7 +1632,7 @@ __global__ void __launch_bounds__(PP_GNT) pp_grec_export_kernel(const Spec* __re
     for (u64 r = r0 + threadIdx.x; r < r0 + PP_GB && r < n; r += PP_GNT) {
         const u8* k = grec + r * S.pp_rw_state;
         const u64 h = pp_grec_hash(S, k);
-        const u32 p = pp_part_of(h, n_parts, scheme);
+        const u32 p = pp_part_of(h, n_parts, scheme, lpart, r);
         const u64 ri = atomicAdd(&cur[p], 1ULL);
         u8* rec = rec_out + ri * S.rec_width;
         *(u64*)rec = h;
@@ -1658,11 +1662,52 @@ __global__ void __launch_bounds__(PP_GNT) pp_grec_export_kernel(const Spec* __re
     }
 }
 
+// Legacy bucket of every group record (enable_experimental_aggregate_hashtable = 0), as
+// agg.hip legacy_slot_bucket_kernel does for the HBM table's slots.
+__global__ void __launch_bounds__(PP_GNT) pp_grec_legacy_bucket_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                      const u8* __restrict__ grec, u64 n, LegacyLayout L,
+                                                                      u32* __restrict__ out) {
+    const Spec& S = *spec;
+    __shared__ u32 tab[256];
+    crc_table_init(tab);
+    for (u64 r = blockIdx.x * (u64)PP_GNT + threadIdx.x; r < n; r += (u64)gridDim.x * PP_GNT) {
+        const u8* k = grec + r * S.pp_rw_state;
+        u64 h;
+        if (L.binary) {
+            bool v;
+            const StrRef sr = pp_key_str(S, batches, k, 0, v);
+            h = legacy_bytes_hash(tab, sr.p, sr.len);
+        } else {
+            u64 kw[4] = {0, 0, 0, 0};
+            for (int c = 0; c < S.n_keys; ++c) {
+                u64 lo, hi;
+                if (!pp_key_fixed(S, batches, k, c, lo, hi)) {
+                    const u32 o = (u32)L.null_off[c];
+                    kw[o >> 3] |= 1ULL << (8 * (o & 7));
+                } else {
+                    const u32 w = type_width(S.key_types[c].type);
+                    legacy_put(kw, L.off[c], lo, w == 16 ? hi : 0, w);
+                }
+            }
+            h = legacy_fixed_crc(tab, kw, L.words);
+        }
+        out[r] = legacy_bucket(h, L.bits);
+    }
+}
+
+void launch_pp_grec_legacy_bucket(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n,
+                                  const LegacyLayout& L, u32* out) {
+    if (!n) return;
+    u64 blocks = (n + PP_GNT - 1) / PP_GNT;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(pp_grec_legacy_bucket_kernel, dim3((u32)blocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, L, out);
+}
+
 void launch_pp_grec_export(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const u8* grec, u64 n, u32 n_parts,
-                           int scheme, const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out, u8* str_out,
-                           const u64* part_str_base) {
+                           int scheme, const u32* lpart, const u64* pos, const u64* str_pos, u64 nblocks, u8* rec_out,
+                           u8* str_out, const u64* part_str_base) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(pp_grec_export_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, pos,
+    hipLaunchKernelGGL(pp_grec_export_kernel, dim3((u32)nblocks), dim3(PP_GNT), 0, s, dspec, batches, grec, n, n_parts, scheme, lpart, pos,
                        str_pos, nblocks, rec_out, str_out, part_str_base);
 }
 

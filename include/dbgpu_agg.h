@@ -304,7 +304,13 @@ int dbg_agg_get_strategy(dbg_agg_handle* h, int* partitioned, uint64_t* extra_ro
  * A record = [hash u64][group keys, fixed part][state words]; string keys are (u64 offset, u64 len)
  * into a per-partition string blob.  scheme 0: partition = hash % n_parts (cluster routing,
  * StrengthReducedU64); scheme 1: partition = (hash & mask) >> (48 - r) with n_parts = 2^r
- * (radix buckets). */
+ * (radix buckets); scheme 2: the legacy HashMethod path's buckets (enable_experimental_aggregate_
+ * hashtable = 0), partition = hash2bucket<r, true>(FastHash(key)) = bits [32 - r, 32) of the
+ * CRC32C FastHash of the group's FixedKeys / SingleBinary key (HT/partitioned_hashtable.rs:77-83,
+ * HT/traits.rs:172-330; the key packing as dbg_legacy_group_hash), n_parts = 2^r — 256 for the
+ * reference's PartitionedHashtable<_, 8>.  Scheme 2 with HashMethodSerializer keys (String +
+ * anything, Boolean, > 32 packed bytes) returns DBG_ERR_UNSUPPORTED.  Records still carry the new
+ * group hash at offset 0 whatever the scheme. */
 int dbg_agg_record_width(dbg_agg_handle* h, uint32_t* width);
 /* The record layout of a handle built from `params`, computed on the host (no device needed): a
  * mixed CPU/GPU exchange or a test packs and unpacks records with it.  Offsets are in bytes from
