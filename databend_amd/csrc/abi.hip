@@ -334,7 +334,9 @@ static int result_type_of(const dbg_agg_spec& s, dbg_datatype* out) {
             else return fail(DBG_ERR_UNSUPPORTED, "avg: unsupported argument type");
             break;
         case DBG_AGG_MIN: case DBG_AGG_MAX:
-            if (t == DBG_STRING || t == DBG_BOOLEAN) return fail(DBG_ERR_UNSUPPORTED, "min/max: String/Boolean arguments stay on the CPU path");
+            // Boolean: MinMaxAnyState<BooleanType> (false < true; the 0/1 value in an i64 state word,
+            // one byte per row in results and borsh Option<bool>); String stays on the CPU path
+            if (t == DBG_STRING) return fail(DBG_ERR_UNSUPPORTED, "min/max: String arguments stay on the CPU path");
             r = dbg_datatype{t, s.arg.precision, s.arg.scale, 0, 0};
             break;
         default: return fail(DBG_ERR_INVALID, "unknown aggregate kind");
@@ -2631,6 +2633,39 @@ int dbg_sort_limit_indices(const dbg_column* col, uint64_t rows, int asc, int nu
     d.data_offset = col->data_offset;
     std::string err;
     int rc = sort_limit_run((hipStream_t)stream, d, rows, asc, nulls_first, limit, idx_out, n_out, err);
+    return rc == DBG_OK ? rc : fail(rc, err);
+}
+
+int dbg_sort_limit_multi(const dbg_column* cols, int n_cols, const int* asc, const int* nulls_first, uint64_t rows,
+                         uint64_t limit, uint32_t* idx_out, uint64_t* n_out, void* stream) {
+    if (!cols || !asc || !nulls_first || !n_out || (!idx_out && limit && rows)) return fail(DBG_ERR_INVALID, "null argument");
+    if (n_cols < 1 || n_cols > SORT_MAX_COLS) return fail(DBG_ERR_UNSUPPORTED, "dbg_sort_limit_multi: 1..8 sort columns");
+    MKeyDesc K;
+    memset(&K, 0, sizeof(K));
+    K.n = n_cols;
+    for (int c = 0; c < n_cols; ++c) {
+        const dbg_column& col = cols[c];
+        const int t = col.dt.type;
+        if (!valid_type(t) || (t != DBG_STRING && type_width(t) == 0))
+            return fail(DBG_ERR_UNSUPPORTED, "dbg_sort_limit_multi: number, Decimal128 and String columns");
+        if (col.len < rows) return fail(DBG_ERR_INVALID, "column shorter than rows");
+        if (t == DBG_STRING && !col.offsets) return fail(DBG_ERR_INVALID, "String column without offsets");
+        DCol& d = K.cols[c];
+        d.type = t;
+        d.nullable = col.dt.nullable;
+        d.layout = LAYOUT_ARROW;
+        d.width = type_width(t);
+        d.stride = d.width;
+        d.data = (const u8*)col.data;
+        d.offsets = col.offsets;
+        d.validity = col.dt.nullable ? col.validity : nullptr;
+        d.validity_offset = col.validity_offset;
+        d.data_offset = col.data_offset;
+        K.desc[c] = asc[c] ? 0 : 1;
+        K.nulls_first[c] = nulls_first[c] ? 1 : 0;
+    }
+    std::string err;
+    int rc = sort_multi_limit_run((hipStream_t)stream, K, rows, limit, idx_out, n_out, err);
     return rc == DBG_OK ? rc : fail(rc, err);
 }
 

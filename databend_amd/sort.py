@@ -1,4 +1,4 @@
-"""ORDER BY <one column> [ASC|DESC] [NULLS FIRST|LAST] LIMIT k on device.
+"""ORDER BY <columns> [ASC|DESC] [NULLS FIRST|LAST] LIMIT k on device.
 
 Host mirror of `DataBlock::sort(block, descriptions, limit)` (EXP/kernels/sort.rs:79-107) for one
 sort column — the shape that ends every ClickBench GROUP BY query (`ORDER BY c DESC LIMIT 10`),
@@ -65,11 +65,35 @@ def take(col: DeviceColumn, idx) -> DeviceColumn:
     return out
 
 
+def sort_multi_limit_indices(columns: Sequence[DeviceColumn], descriptions: Sequence[SortColumnDescription],
+                             limit: Optional[int]):
+    """Row indices (torch int32) of the first min(limit, rows) rows in the order of several sort
+    columns — numbers, Decimal128 or String, each with its own direction (dbg_sort_limit_multi)."""
+    import torch
+
+    cols = [columns[d.offset] for d in descriptions]
+    n = len(cols[0])
+    k = n if limit is None else min(int(limit), n)
+    arr = (abi.dbg_column * len(cols))(*[c.to_abi() for c in cols])
+    asc = (C.c_int * len(cols))(*[1 if d.asc else 0 for d in descriptions])
+    nf = (C.c_int * len(cols))(*[1 if d.nulls_first else 0 for d in descriptions])
+    out = torch.empty(max(1, k), dtype=torch.int32, device=cols[0].data.device)
+    got = C.c_uint64()
+    check(lib().dbg_sort_limit_multi(arr, len(cols), asc, nf, n, k, out.data_ptr(), C.byref(got), None))
+    return out[:got.value]
+
+
 def sort(columns: Sequence[DeviceColumn], descriptions: Sequence[SortColumnDescription],
          limit: Optional[int]) -> List[DeviceColumn]:
-    """DataBlock::sort for one sort description over fixed-width columns."""
-    if len(descriptions) != 1:
-        raise NotImplementedError("device sort: one sort column")
+    """DataBlock::sort (EXP/kernels/sort.rs:79-107): one fixed-width number column takes the
+    radix-select path of dbg_sort_limit_indices; several columns, or a String / Decimal128 one,
+    the composite-key path of dbg_sort_limit_multi."""
+    if not descriptions:
+        raise ValueError("sort: no sort description")
     d = descriptions[0]
-    idx = sort_limit_indices(columns[d.offset], d.asc, d.nulls_first, limit)
+    one_number = len(descriptions) == 1 and columns[d.offset].dtype.type_id not in (abi.STRING, abi.DECIMAL128)
+    if one_number:
+        idx = sort_limit_indices(columns[d.offset], d.asc, d.nulls_first, limit)
+    else:
+        idx = sort_multi_limit_indices(columns, descriptions, limit)
     return [take(c, idx) for c in columns]

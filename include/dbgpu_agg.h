@@ -465,6 +465,16 @@ int dbg_legacy_group_hash(const dbg_column* cols, int n, uint64_t rows, uint64_t
  * columns return DBG_ERR_UNSUPPORTED.  Synchronous on hip_stream. */
 int dbg_sort_limit_indices(const dbg_column* col, uint64_t rows, int asc, int nulls_first, uint64_t limit,
                            uint32_t* idx_out, uint64_t* n_out, void* hip_stream);
+/* ORDER BY several columns LIMIT k: DataBlock::sort with n_cols descriptions (EXP/kernels/sort.rs:
+ * 79-107 -> arrow lexsort_to_indices with a limit) over device-resident number, Decimal128 and
+ * String columns (1..8, each its own asc / nulls_first).  Rows compare column by column: NULLs
+ * first or last per the column's nulls_first; values by ord::total_cmp (integers, i128 decimals),
+ * IEEE totalOrder (floats), byte-wise then by length (strings), reversed when asc[c] == 0.  Rows
+ * equal on every column come out in ascending row order (the reference leaves them unspecified).
+ * idx_out (device, >= min(limit, rows) u32) receives the row indices in order; *n_out =
+ * min(limit, rows).  limit > 2048 returns DBG_ERR_UNSUPPORTED.  Synchronous on hip_stream. */
+int dbg_sort_limit_multi(const dbg_column* cols, int n_cols, const int* asc, const int* nulls_first, uint64_t rows,
+                         uint64_t limit, uint32_t* idx_out, uint64_t* n_out, void* hip_stream);
 
 /* ---- in-library kernel timing (HIP events around each launch; off by default) ---- */
 int dbg_prof_enable(int on);

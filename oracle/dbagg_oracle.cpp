@@ -352,6 +352,7 @@ template <> inline u64 arg_as<u64>(const dbg_column& c, u64 i) {
         case DBG_UINT8: return val<uint8_t>(c, i);
         case DBG_UINT16: return val<uint16_t>(c, i);
         case DBG_UINT32: return val<uint32_t>(c, i);
+        case DBG_BOOLEAN: return bool_val(c, i) ? 1 : 0;
         default: return val<uint64_t>(c, i);
     }
 }
@@ -832,7 +833,7 @@ static AggFn* make_fn(const dbg_agg_spec& s) {
         bool mn = s.kind == DBG_AGG_MIN;
         dbg_datatype rt{t, s.arg.precision, s.arg.scale, 0, 0};
         if (is_signed_int(t) || t == DBG_DATE || t == DBG_TIMESTAMP) base = new MinMaxFn<i64>(mn, rt);
-        else if (is_unsigned_int(t)) base = new MinMaxFn<u64>(mn, rt);
+        else if (is_unsigned_int(t) || t == DBG_BOOLEAN) base = new MinMaxFn<u64>(mn, rt);  // bool: false < true
         else if (is_float(t)) base = new MinMaxFn<double>(mn, rt);
         else if (t == DBG_DECIMAL128) base = new MinMaxFn<i128>(mn, rt);
     }

@@ -273,3 +273,55 @@ def sort_limit_indices(col: Column, asc: bool, nulls_first: bool, limit) -> np.n
     vsorted = vrows[np.argsort(key[valid], kind="stable")]
     order = np.concatenate([nulls, vsorted]) if nulls_first else np.concatenate([vsorted, nulls])
     return order[:k]
+
+
+def _order_rank(col: Column) -> np.ndarray:
+    """Per-row rank of the value in the column's ascending value order (equal values, equal rank):
+    ord::total_cmp for integers, IEEE totalOrder for floats (array/ord.rs:36-56), i128 order for
+    Decimal128, byte-wise (then shorter first) for strings."""
+    t = col.dtype.type_id
+    n = len(col)
+    if t == abi.STRING:
+        o = np.asarray(col.offsets, np.int64)
+        d = bytes(np.asarray(col.data, np.uint8))
+        vals = np.empty(n, dtype=object)
+        for i in range(n):
+            vals[i] = d[o[i]:o[i + 1]]
+    elif t == abi.DECIMAL128:
+        raw = bytes(np.asarray(col.data, np.uint8))
+        vals = np.empty(n, dtype=object)
+        for i in range(n):
+            vals[i] = int.from_bytes(raw[16 * i:16 * i + 16], "little", signed=True)
+    else:
+        v = np.asarray(col.data)
+        if t == abi.FLOAT64:
+            b = v.astype(np.float64).view(np.uint64)
+            vals = np.where(b >> np.uint64(63) != 0, ~b, b | np.uint64(1 << 63))
+        elif t == abi.FLOAT32:
+            b = v.astype(np.float32).view(np.uint32).astype(np.uint64)
+            vals = np.where(b >> np.uint64(31) != 0, (~b) & np.uint64(0xFFFFFFFF), b | np.uint64(0x80000000))
+        elif t in (abi.UINT8, abi.UINT16, abi.UINT32, abi.UINT64, abi.BOOLEAN):
+            vals = v.astype(np.uint64)
+        else:
+            vals = v.astype(np.int64)
+    _, inv = np.unique(vals, return_inverse=True)
+    return inv.astype(np.int64).reshape(-1)
+
+
+def sort_multi_limit_indices(cols: Sequence[Column], asc: Sequence[bool], nulls_first: Sequence[bool], limit) -> np.ndarray:
+    """DataBlock::sort with several descriptions (EXP/kernels/sort.rs:79-107) -> arrow
+    lexsort_to_indices: rows compare column by column — NULLs first or last per the column's
+    nulls_first, values in the column's order reversed for DESC (NULL placement is not reversed);
+    rows equal on every column in ascending row order (one of the orders the reference's
+    unstable sort may produce)."""
+    n = len(cols[0])
+    k = n if limit is None else min(int(limit), n)
+    keys = [np.arange(n, dtype=np.int64)]  # least significant: row index
+    for c, a, nf in reversed(list(zip(cols, asc, nulls_first))):
+        valid = np.ones(n, bool) if c.validity is None or not c.dtype.nullable else np.asarray(c.validity, bool)
+        rank = _order_rank(c)
+        rank = np.where(valid, rank if a else -rank, 0)
+        null_rank = np.where(valid, 1 if nf else 0, 0 if nf else 1)
+        keys.append(rank)
+        keys.append(null_rank)
+    return np.lexsort(keys)[:k]

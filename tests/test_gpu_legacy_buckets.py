@@ -14,6 +14,7 @@ HashMethodSerializer keys (two Strings), which are UNSUPPORTED."""
 import numpy as np
 import pytest
 
+from databend_amd import abi
 from databend_amd import column as col
 from databend_amd.aggregates import AggregateFunctionFactory
 from databend_amd.aggregator import (LEGACY_BUCKETS, SINGLE_LEVEL_BUCKET, AggregatorParams, HashTableConfig,
@@ -43,13 +44,15 @@ def _data(case, n, groups, rng):
     return keys, [("count", None), ("sum", v), ("max", v), ("sql_avg", d)]
 
 
-def _partial(params, keys, aggs, lo, hi):
+def _partial(params, keys, aggs, lo, hi, strategy=None):
     nk = len(keys)
     arg_idx, j = [], nk
     for _, c in aggs:
         arg_idx.append(None if c is None else j)
         j += c is not None
     p = TransformPartialAggregate(params, HashTableConfig(), staging_rows=1 << 20)
+    if strategy is not None:
+        p.hashtable.set_strategy(strategy)
     for s in range(lo, hi, BLOCK):
         e = min(hi, s + BLOCK)
         cols = [slice_col(k, s, e) for k in keys] + [slice_col(c, s, e) for _, c in aggs if c is not None]
@@ -73,10 +76,12 @@ def _final_all(params, parts, nk, na):
     return [concat(c) for c in out_k], [concat(c) for c in out_a]
 
 
-@pytest.mark.parametrize("case", ["fixed", "binary"])
-def test_legacy_two_level_and_split(case):
+@pytest.mark.parametrize("case,strategy", [("fixed", None), ("binary", None), ("fixed", abi.STRATEGY_PARTITIONED),
+                                           ("binary", abi.STRATEGY_PARTITIONED)])
+def test_legacy_two_level_and_split(case, strategy):
     """One partial above the threshold (two-level), one below (single-level, split by the bucket
-    transform)."""
+    transform); the two-level partial on the HBM table or on the partitioned payload (its buckets
+    come from the payload's group records)."""
     rng = np.random.default_rng(21 if case == "fixed" else 22)
     n_a, n_b = 400_000, 5_000
     keys_a, aggs = _data(case, n_a, 60_000, rng)
@@ -85,7 +90,7 @@ def test_legacy_two_level_and_split(case):
     aggs = [(f, None if c is None else concat([c, cb])) for (f, c), (_, cb) in zip(aggs, aggs_b)]
     fns = [F.get(f, [], [c.dtype] if c is not None else []) for f, c in aggs]
     params = AggregatorParams([k.dtype for k in keys], fns, enable_experimental_aggregate_hashtable=False)
-    pa = _partial(params, keys, aggs, 0, n_a)
+    pa = _partial(params, keys, aggs, 0, n_a, strategy)
     pb = _partial(params, keys, aggs, n_a, n_a + n_b)
     try:
         ma, mb = pa.on_finish(), pb.on_finish()
