@@ -1755,7 +1755,7 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
     const int nt = 1024;
     static_assert(FIN_NT == 1024, "the fused finalize runs on the insert's workgroup");
-    const u64 max_blocks = 256;  // one 1024-lane workgroup per CU
+    const u64 max_blocks = 256;  // one 1024-lane workgroup per CU (512 / 768 / 1024 / 2048 measured: 52 / 55 / 63 / 90 us a C2 step)
     size_t shmem = fast_shmem(table_bytes);
     FusedFin ff;
     if (fused) ff = *fused;
