@@ -213,6 +213,22 @@ class AggregateHashTable:
         # every launch that reads them (the handle runs on torch's current stream)
         self._retained.clear()
 
+    def compact(self) -> bool:
+        """dbg_agg_compact: the table rewritten to reference one record batch of its groups, so the
+        inputs of earlier add_groups calls are released (the reference's payload arena holds only
+        new groups' keys, EAGG/payload_row.rs:111-130).  True when it rewrote the table."""
+        done = C.c_int(0)
+        check(lib().dbg_agg_compact(self.h, C.byref(done)))
+        if done.value:
+            self._retained.clear()  # no entry points at them any more (stream-ordered reuse)
+        return bool(done.value)
+
+    def retained_bytes(self) -> int:
+        """Device bytes the handle keeps for referenced inputs (dbg_agg_retained_bytes)."""
+        b = C.c_uint64()
+        check(lib().dbg_agg_retained_bytes(self.h, C.byref(b)))
+        return b.value
+
     def set_host_staging(self, rows: int):
         """Gather host blocks into launches of `rows` rows (dbg_agg_set_host_staging); 0 = off."""
         check(lib().dbg_agg_set_host_staging(self.h, rows))
@@ -514,14 +530,18 @@ class TransformPartialAggregate:
     host staging into launches of `staging_rows` rows (dbg_agg_set_host_staging)."""
 
     DEFAULT_STAGING_ROWS = 1 << 23
+    DEFAULT_COMPACT_BYTES = 1 << 30
 
     def __init__(self, params: AggregatorParams, config: HashTableConfig = None, device: int = -1,
-                 staging_rows: int = DEFAULT_STAGING_ROWS):
+                 staging_rows: int = DEFAULT_STAGING_ROWS, compact_bytes: int = DEFAULT_COMPACT_BYTES):
         self.params = params
         self.config = (config or HashTableConfig()).with_partial(True)
         self.hashtable = AggregateHashTable(params, self.config, device)
         if staging_rows:
             self.hashtable.set_host_staging(staging_rows)
+        # once the copies of host blocks a referenced-key table keeps exceed this, the table is
+        # compacted to its groups (0 = never)
+        self.compact_bytes = compact_bytes
 
     @classmethod
     def try_create(cls, params: AggregatorParams, config: HashTableConfig = None, device: int = -1, **kw):
@@ -534,6 +554,8 @@ class TransformPartialAggregate:
         groups = [block.columns[i] for i in group_indices]
         args = [None if i is None else block.columns[i] for i in arg_indices]
         self.hashtable.add_groups(groups, args, rows=block.num_rows(), filter_program=filter_program)
+        if self.compact_bytes and self.hashtable.retained_bytes() > self.compact_bytes:
+            self.hashtable.compact()
         return []
 
     def on_finish(self) -> List[AggregateMeta]:

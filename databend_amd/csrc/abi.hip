@@ -290,6 +290,7 @@ static int dev_alloc(void** p, size_t bytes) {
 
 static int own_copy(dbg_agg_handle* h, const void* src, size_t bytes, const void** out) {
     DevBuf b;
+    b.bytes = bytes;
     RETURN_IF(dev_alloc(&b.p, bytes));
     h->owned.push_back(b);
     if (bytes) HIPCHECK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, h->stream));
@@ -2376,6 +2377,56 @@ int dbg_agg_merge_records(dbg_agg_handle* h, const void* dev_records, const void
     return DBG_OK;
 }
 
+// Key compaction (the reference copies only a new group's key into its payload arena,
+// EAGG/payload_row.rs:111-130, so a partial's memory follows its groups, not the rows it saw):
+// every group leaves as an exchange record (keys, string blob, states), the table restarts empty
+// and merges the records back, so its ref-key entries point at one record batch of exactly the
+// groups, and the inputs seen so far — the library's copies of host blocks and the caller's
+// device columns — are no longer referenced.  O(groups); a no-op for inline keys (no references)
+// and the partitioned payload (its records already hold the keys).
+int dbg_agg_compact(dbg_agg_handle* h, int* compacted) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    if (compacted) *compacted = 0;
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    const Spec& S = h->spec;
+    if (h->pp || S.inline_keys) return DBG_OK;
+    u64 n = 0, sb = 0;
+    RETURN_IF(dbg_agg_partition(h, 1, 0, &n, &sb));
+    DevBuf rb, strb;
+    rb.bytes = std::max<u64>(n * S.rec_width, 16);
+    strb.bytes = std::max<u64>(sb, 16);
+    RETURN_IF(dev_alloc(&rb.p, rb.bytes));
+    int rc = dev_alloc(&strb.p, strb.bytes);
+    if (rc == DBG_OK) rc = dbg_agg_export_records(h, rb.p, strb.p);
+    if (rc == DBG_OK && hipStreamSynchronize(h->stream) != hipSuccess) rc = fail(DBG_ERR_DEVICE, "compact: export failed");
+    if (rc == DBG_OK) rc = dbg_agg_reset(h);  // frees the copies of earlier inputs
+    if (rc != DBG_OK) {
+        hipFree(rb.p);
+        if (strb.p) hipFree(strb.p);
+        return rc;
+    }
+    h->owned.push_back(rb);
+    h->owned.push_back(strb);
+    h->finalized = false;
+    h->clean = false;
+    const u8* per_col[DBG_MAX_KEYS];
+    for (int c = 0; c < DBG_MAX_KEYS; ++c) per_col[c] = (const u8*)strb.p;
+    RETURN_IF(merge_record_batch(h, (const u8*)rb.p, n, per_col));
+    if (compacted) *compacted = 1;
+    return DBG_OK;
+}
+
+// Device bytes the handle keeps for the inputs its table references: copies of host blocks and
+// received / compacted records (the caller's own device columns are not counted).
+int dbg_agg_retained_bytes(dbg_agg_handle* h, uint64_t* bytes) {
+    if (!h || !bytes) return fail(DBG_ERR_INVALID, "null argument");
+    u64 t = 0;
+    for (const auto& b : h->owned) t += b.bytes;
+    *bytes = t;
+    return DBG_OK;
+}
+
 // AggregateMeta::Serialized -> this table (SerializedPayload::convert_to_aggregate_table,
 // AGG/aggregate_meta.rs:57-101; AggregateFunction::batch_merge, EAGG/aggregate_function.rs:96-103).
 int dbg_agg_merge_serialized(dbg_agg_handle* h, const dbg_column* state_cols, const dbg_column* group_cols, uint64_t rows,
@@ -2409,6 +2460,7 @@ int dbg_agg_merge_serialized(dbg_agg_handle* h, const dbg_column* state_cols, co
     }
     // records are retained (the table's ref-key entries point at them) until reset
     DevBuf rb;
+    rb.bytes = rows * S.rec_width;
     RETURN_IF(dev_alloc(&rb.p, rows * S.rec_width));
     h->owned.push_back(rb);
     if (!h->ser_err) RETURN_IF(dev_alloc((void**)&h->ser_err, 8));

@@ -85,7 +85,9 @@ struct TableDesc {
     u32 scr_blocks;
 };
 #define SCR_ENTRIES 64
+#ifndef SCR_GROUP
 #define SCR_GROUP 16
+#endif
 inline size_t scr_words(u32 blocks, u32 stride_words) {
     return (size_t)blocks * (2 + (size_t)SCR_ENTRIES * stride_words) + (size_t)(blocks / SCR_GROUP) * SCR_ENTRIES * stride_words;
 }

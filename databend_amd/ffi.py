@@ -12,14 +12,15 @@ import os
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdbgpu_agg.so")
+# DBGPU_LIB: another in-tree build of the same library (e.g. `make TRACE=1` into a side path)
+LIB_PATH = os.environ.get("DBGPU_LIB") or os.path.join(_HERE, "libdbgpu_agg.so")
 _LIB = None
 
 EXPORTED = [
     "dbg_version", "dbg_last_error", "dbg_device_count", "dbg_agg_result_type", "dbg_agg_create",
     "dbg_agg_destroy", "dbg_agg_set_stream", "dbg_agg_reset", "dbg_agg_add_groups", "dbg_agg_finalize",
     "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_set_recycle", "dbg_agg_finalize_into_async", "dbg_agg_finalize_wait", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
-    "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_sort_limit_indices", "dbg_sort_limit_multi", "dbg_prof_enable", "dbg_prof_reset",
+    "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_sort_limit_indices", "dbg_sort_limit_multi", "dbg_agg_compact", "dbg_agg_retained_bytes", "dbg_prof_enable", "dbg_prof_reset",
     "dbg_prof_get", "dbg_prof_marker", "dbg_datagen", "dbg_agg_set_strategy", "dbg_agg_get_strategy",
     "dbg_agg_record_layout", "dbg_agg_set_host_staging",
     "dbg_take_string", "dbg_legacy_hash_method", "dbg_legacy_group_hash", "dbg_agg_serialized_stride", "dbg_agg_result_serialized", "dbg_agg_merge_serialized", "dbg_comm_get_unique_id", "dbg_comm_create", "dbg_comm_destroy", "dbg_agg_exchange",
@@ -101,6 +102,8 @@ def lib():
         L.dbg_legacy_group_hash.argtypes = [P(abi.dbg_column), C.c_int, U64, VP, VP, C.c_int, VP]
         L.dbg_take_string.argtypes = [P(abi.dbg_column), VP, U64, VP, VP, U64, VP, P(U64), VP]
         L.dbg_sort_limit_indices.argtypes = [P(abi.dbg_column), U64, C.c_int, C.c_int, U64, VP, P(U64), VP]
+        L.dbg_agg_compact.argtypes = [VP, P(C.c_int)]
+        L.dbg_agg_retained_bytes.argtypes = [VP, P(U64)]
         L.dbg_sort_limit_multi.argtypes = [P(abi.dbg_column), C.c_int, P(C.c_int), P(C.c_int), U64, U64, VP, P(U64), VP]
         L.dbg_prof_enable.argtypes = [C.c_int]
         L.dbg_prof_get.argtypes = [C.c_int, P(C.c_char_p), P(C.c_double), P(U64)]

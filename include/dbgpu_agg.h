@@ -337,6 +337,18 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
  * into dev_strings (string_bytes[p] bytes each, same order; record string offsets are relative to
  * the partition's blob).  Device buffers; asynchronous.  Call after dbg_agg_partition. */
 int dbg_agg_export_records(dbg_agg_handle* h, void* dev_records, void* dev_strings);
+/* Key compaction: a table with referenced keys (String, Decimal128, wide tuples) points at the
+ * input rows that created its groups, so by default the inputs stay resident until
+ * dbg_agg_reset.  dbg_agg_compact rewrites the table so that it references one record batch of
+ * exactly its groups (keys, string bytes, states) — the reference's payload arena holds only new
+ * groups' keys too (EAGG/payload_row.rs:111-130) — after which the caller's device input columns
+ * of earlier dbg_agg_add_groups calls may be freed and the library's copies of host blocks are
+ * released.  O(groups) device work, synchronous.  A no-op for inline keys and in partitioned mode
+ * (*compacted, may be NULL: 1 when the table was rewritten).
+ * dbg_agg_retained_bytes reports the device bytes the handle keeps for its inputs (copies of host
+ * blocks, received and compacted records; not the caller's own device columns). */
+int dbg_agg_compact(dbg_agg_handle* h, int* compacted);
+int dbg_agg_retained_bytes(dbg_agg_handle* h, uint64_t* bytes);
 /* merge_states of received records into this table (combine_payload,
  * EAGG/aggregate_hashtable.rs:383-425).  The buffers hold n_segments concatenated segments
  * (one per source, each as written by dbg_agg_export_records for one partition);
