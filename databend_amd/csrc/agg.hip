@@ -258,13 +258,15 @@ __device__ __forceinline__ void block_flush(const Spec& S, const BatchDesc* batc
         // Hand-off without release fences (MI355X_MICROARCH.md, inter-workgroup visibility, valid
         // forms): parked words are stored sc1 (write-through past the XCD's L2); every storing
         // wave drains them and the barrier orders all waves before lane 0's ticket add; the last
-        // workgroup of each group of SCR_GROUP reads them back with sc1 loads behind one
+        // workgroup of each group of FLUSH_GROUP reads them back with sc1 loads behind one
         // agent-scope acquire.  Groups keep the merge tail short and parallel, and cut the
-        // same-address atomics on the HBM table by SCR_GROUP.
+        // same-address atomics on the HBM table by FLUSH_GROUP (C1, 1464 workgroups of 4 groups:
+        // FLUSH_GROUP 2 / 4 / 8 / 16 / 64 -> insert 0.470 / 0.432 / 0.439 / 0.467 / 0.649 ms: a
+        // leader's serial merge of many parked tables costs more than the HBM atomics it saves).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        const u32 g = blockIdx.x / SCR_GROUP;
-        const u32 gsize = min((u32)SCR_GROUP, gridDim.x - g * SCR_GROUP);
+        const u32 g = blockIdx.x / FLUSH_GROUP;
+        const u32 gsize = min((u32)FLUSH_GROUP, gridDim.x - g * FLUSH_GROUP);
         if (threadIdx.x == 0) {
             u64 tk = atomicAdd((unsigned long long*)(tickets + g), 1ULL);
             lcount[3] = tk == (u64)gsize - 1 ? 1u : 0u;
@@ -281,7 +283,7 @@ __device__ __forceinline__ void block_flush(const Spec& S, const BatchDesc* batc
             __syncthreads();
             const u32 total = gsize * SCR_ENTRIES;
             for (u32 f = threadIdx.x; f < total; f += nt) {
-                u64 b = (u64)g * SCR_GROUP + f / SCR_ENTRIES, k = f % SCR_ENTRIES;
+                u64 b = (u64)g * FLUSH_GROUP + f / SCR_ENTRIES, k = f % SCR_ENTRIES;
                 const u64* r = rows + (b * SCR_ENTRIES + k) * sw;
                 u64 cnt = ld_sc1(counts + b);
                 u64 e = ld_sc1(r);  // issued with the count: rows are allocated in full
