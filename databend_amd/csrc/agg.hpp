@@ -86,7 +86,7 @@ struct TableDesc {
 };
 #define SCR_ENTRIES 64
 #ifndef SCR_GROUP
-#define SCR_GROUP 16  // workgroups per group of the fused chain (C2: 4 / 16 / 64 -> 47.1 / 45.0 / 47.8 us)
+#define SCR_GROUP 16  // workgroups per group of the fused chain (C2: 4 / 8 / 16 / 32 / 64 -> 47.1 / 45.5 / 45.0 / 46.0 / 47.8 us)
 #endif
 #ifndef FLUSH_GROUP
 #define FLUSH_GROUP 4  // workgroups per group of the generic insert's parked flush (<= SCR_GROUP)
