@@ -65,7 +65,7 @@ def parse():
 def cpu_baseline(cfg, sample_rows, gpu_check=None):
     """Restated Databend CPU aggregator (oracle/, the reference's algorithm: per-thread partial
     AggregateHashTable over 65536-row blocks -> partition bucket -> final) on the host's cores,
-    on a bounded sample of the same workload; median of 3 timed runs after 1 warm-up."""
+    on a bounded sample of the same workload; median of 5 timed runs after 1 warm-up."""
     from oracle import oracle
     from databend_amd.workloads import SHAPES, F
     from databend_amd.filter import FilterProgram, cmp
@@ -84,17 +84,20 @@ def cpu_baseline(cfg, sample_rows, gpu_check=None):
         prog = FilterProgram(cmp(0, op, const), [cols[name].to_abi()])
     times = []
     result = None
-    for it in range(4):
+    for it in range(6):
         t0 = time.perf_counter()
         result = oracle.aggregate(keys, aggs, filter_program=prog, threads=threads)
         dt = time.perf_counter() - t0
         if it:
             times.append(dt)
     med = statistics.median(times)
+    n_groups = len(result[0][0]) if result and result[0] else 0
     return dict(value=sample_rows / med, unit="rows/s", cores=threads, kind="port",
-                sample=f"{sample_rows} rows of the same synthetic workload (rows 0..{sample_rows - 1}), "
-                       f"median of {len(times)} runs after 1 warm-up, {threads} threads",
-                seconds_per_run=med), result, cols
+                label="restated Databend CPU aggregator (oracle/dbagg_oracle.cpp: per-thread partial "
+                      "AggregateHashTable -> partition bucket -> final)",
+                sample=f"{sample_rows} rows of the same synthetic workload (rows 0..{sample_rows - 1}, "
+                       f"{n_groups} groups), median of {len(times)} runs after 1 warm-up, {threads} threads",
+                sample_groups=n_groups, seconds_per_run=med), result, cols
 
 
 def spawn_ranks(args) -> int:
@@ -182,7 +185,9 @@ def measure_extra(cfg, steps, warmup, with_cpu):
     if with_cpu:
         sample = {1: 6_001_215, 3: 20_000_000, 4: 10_000_000, 5: 20_000_000}[cfg]
         cb, _, _ = cpu_baseline(cfg, sample)
-        rec["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        rec["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "label", "sample", "sample_groups")}
+        # the GPU's groups beside the sample's: a sample holds fewer groups than the full config
+        rec["cpu_baseline"]["full_config_groups"] = n_groups
         rec["gpu_vs_cpu"] = rec["rows_per_s"] / cb["value"]
     return rec
 
@@ -437,7 +442,8 @@ def main():
         sample = args.cpu_sample_rows or {1: 6_001_215, 2: 100_000_000, 3: 20_000_000, 4: 10_000_000, 5: 20_000_000}[cfg]
         sample = min(sample, rows)
         cb, cres, _ = cpu_baseline(cfg, sample)
-        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "label", "sample", "sample_groups")}
+        out["cpu_baseline"]["full_config_groups"] = n_groups
         out["gpu_vs_cpu"] = value / cb["value"]
         # parity of this bench's own GPU result against the CPU run when they cover the same rows
         if sample == rows and copies >= 1:

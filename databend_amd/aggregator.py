@@ -505,6 +505,18 @@ LEGACY_BUCKETS = 256      # PartitionedHashtable<_, 8> (HT/partitioned_hashtable
 LEGACY_SCHEME = 2
 
 
+LEGACY_KEYS_U8, LEGACY_KEYS_U16 = 1, 2  # DBG_LEGACY_KEYS_U8 / _U16 (include/dbgpu_agg.h)
+
+
+def legacy_hash_method(types: Sequence[DataType]):
+    """dbg_legacy_hash_method: (kind, key bytes) of HashMethodKind::choose_hash_method_with_types
+    (EXP/kernels/group_by.rs:48-95)."""
+    arr = (abi.dbg_datatype * len(types))(*[t.to_abi() for t in types])
+    k, kb = C.c_int(), C.c_uint32()
+    check(lib().dbg_legacy_hash_method(arr, len(types), C.byref(k), C.byref(kb)))
+    return k.value, kb.value
+
+
 def export_buckets(table: AggregateHashTable, n_parts: int, scheme: int = 1) -> List[Payload]:
     """All groups of `table` as n_parts bucket payloads (dbg_agg_partition + export_records), in
     bucket order; scheme 1 = radix bits [48 - r, 48) (EAGG/partitioned_payload.rs:121, 267-275),
@@ -542,6 +554,7 @@ class TransformPartialAggregate:
         # once the copies of host blocks a referenced-key table keeps exceed this, the table is
         # compacted to its groups (0 = never)
         self.compact_bytes = compact_bytes
+        self._compacted_bytes = 0  # retained bytes right after the last compaction (its group records)
 
     @classmethod
     def try_create(cls, params: AggregatorParams, config: HashTableConfig = None, device: int = -1, **kw):
@@ -554,8 +567,12 @@ class TransformPartialAggregate:
         groups = [block.columns[i] for i in group_indices]
         args = [None if i is None else block.columns[i] for i in arg_indices]
         self.hashtable.add_groups(groups, args, rows=block.num_rows(), filter_program=filter_program)
-        if self.compact_bytes and self.hashtable.retained_bytes() > self.compact_bytes:
+        # compact on the bytes retained since the last compaction, not on the total: the compacted
+        # group records themselves count towards the total, and once they alone pass the limit a
+        # total-based trigger would compact again after every block
+        if self.compact_bytes and self.hashtable.retained_bytes() - self._compacted_bytes > self.compact_bytes:
             self.hashtable.compact()
+            self._compacted_bytes = self.hashtable.retained_bytes()
         return []
 
     def on_finish(self) -> List[AggregateMeta]:
@@ -571,7 +588,10 @@ class TransformPartialAggregate:
         if not self.params.enable_experimental_aggregate_hashtable:
             if not n_groups:
                 return []
-            if n_groups < self.params.group_by_two_level_threshold:
+            # HashMethodFixedKeys<u8> / <u16> never convert to two-level: SUPPORT_PARTITIONED is
+            # false for them (aggregator_polymorphic_keys.rs:149,189; transform_aggregate_partial.rs:337)
+            if n_groups < self.params.group_by_two_level_threshold or \
+                    legacy_hash_method(self.params.group_data_types)[0] in (LEGACY_KEYS_U8, LEGACY_KEYS_U16):
                 payloads = export_buckets(self.hashtable, 1, LEGACY_SCHEME)
                 return [AggregateMeta(SINGLE_LEVEL_BUCKET, payloads[0], 1, legacy=True)]
             payloads = export_buckets(self.hashtable, LEGACY_BUCKETS, LEGACY_SCHEME)

@@ -212,6 +212,10 @@ struct dbg_agg_handle {
     // recycle mode (dbg_agg_set_recycle): a small-table finalize_into leaves the table empty
     int recycle = 0;
     bool clean = false;           // table already re-initialised by the last finalize
+    // dbg_agg_reset deferred the table's initialisation (counters and the sentinel slot are
+    // initialised): table_desc() runs it before any kernel touches the table, except a
+    // partitioned insert, whose slice kernel starts every slice EMPTY and writes the whole table
+    bool init_pending = false;
     u64 fin_seq = 0;              // sequence number the finalize kernel posts to host_mirror
     bool uploads_pending = false; // descriptor uploads from pinned staging since the last sync
     // radix-partitioned insert (part.hip): sorted mixed keys, slice bounds, rocPRIM scratch
@@ -224,6 +228,10 @@ struct dbg_agg_handle {
     u64 table_rows = 0;  // rows / records inserted into the HBM table since the last reset
     int strategy = DBG_STRATEGY_AUTO;
     u64 hint_groups = 0;  // dbg_agg_params.capacity_hint
+    // cardinality the last table-mode finalize observed (kept across reset): rows / records
+    // inserted and the groups they formed.  A handle reused for the next batch of the same query
+    // shape decides its strategy from it instead of probing again (no probe kernel, no host sync)
+    u64 obs_rows = 0, obs_groups = 0;
 
     // ---- partitioned payload (pp.hip): high-cardinality mode ----
     bool pp = false;          // batches go to the radix-partitioned payload, not the HBM table
@@ -470,7 +478,16 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
 // ------------------------------------------------------------------------------------------
 // table allocation / growth
 // ------------------------------------------------------------------------------------------
+static void table_init_now(dbg_agg_handle* h) {
+    if (!h->init_pending) return;
+    h->init_pending = false;
+    prof::Scope ps("table_init", h->stream);
+    launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap, nullptr);
+}
+
+// The table as the kernels see it; a deferred initialisation is launched first (stream order).
 static TableDesc table_desc(dbg_agg_handle* h) {
+    table_init_now(h);
     TableDesc t;
     t.slots = h->slots;
     t.cap = h->cap;
@@ -513,6 +530,7 @@ static int alloc_table(dbg_agg_handle* h, u64 cap, u64** out) {
 }
 
 static int grow_table(dbg_agg_handle* h, u64 new_cap) {
+    table_init_now(h);  // the old table is rehashed below
     u64* ns = nullptr;
     RETURN_IF(alloc_table(h, new_cap, &ns));
     u64* old = h->slots;
@@ -905,8 +923,11 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     }
     h->pp_grec_ready = false;
     if (h->clean) return DBG_OK;  // the recycling finalize already re-initialised table + counters
+    // the counters and the sentinel slot now; the slots when a kernel first touches the table
+    // (table_desc), or never if a partitioned insert rewrites every slice first
     prof::Scope ps("table_init", h->stream);
-    launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap, h->counters);
+    launch_table_init(h->stream, h->dspec, h->spec, h->slots + h->cap * (u64)h->spec.stride_words, 0, h->counters);
+    h->init_pending = true;
     h->clean = true;
     return DBG_OK;
 }
@@ -930,8 +951,11 @@ static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows
     RETURN_IF(ensure_buf(&h->part_bounds, &h->part_bounds_cap, (h->cap >> sb) + 1));
     prof::Scope ps("agg_insert", h->stream);
     const char* step = "";
+    // an empty table whose initialisation is still deferred: the slice kernel writes every slot
+    const bool empty = h->init_pending;
+    h->init_pending = false;
     hipError_t e = launch_part_insert(h->stream, *st, rows, table_desc(h), sb, h->part_temp, h->part_temp_cap, h->part_sorted,
-                                      h->part_bounds, &step);
+                                      h->part_bounds, empty, &step);
     if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("partitioned insert (") + step + "): " + hipGetErrorString(e));
     return DBG_OK;
 }
@@ -970,7 +994,13 @@ extern "C" {
 
 #define PP_MIN_ROWS (1ULL << 22)
 #define PP_MIN_GROUPS (1ULL << 20)
-#define PP_SET_CAP (1ULL << 21)  // 2^20 samples at most: <= 50 % load
+#define PP_SET_CAP (1ULL << 19)  // 2^18 samples at most: <= 50 % load
+
+static void note_observed(dbg_agg_handle* h) {
+    if (h->pp || !h->table_rows) return;
+    h->obs_rows = h->table_rows;
+    h->obs_groups = h->n_groups;
+}
 
 // Cardinality probe of the first batch into an empty handle (AggregateHashTable decides its
 // partial strategy by observed cardinality too: clear_ht / maybe_repartition,
@@ -982,12 +1012,22 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     const int mode = h->strategy == DBG_STRATEGY_TABLE ? 0 : (h->strategy == DBG_STRATEGY_PARTITIONED ? 2 : 1);
     if (h->pp || !mode || !S.pp_ok || h->table_rows) return DBG_OK;
     if (mode == 1 && (rows < PP_MIN_ROWS || (!S.has_strings && S.inline_width <= 2))) return DBG_OK;
+    if (mode == 1 && h->obs_rows >= PP_MIN_ROWS) {
+        // the handle's last finalize saw this query's cardinality (groups per inserted row)
+        const double ratio = std::min(1.0, (double)h->obs_groups / (double)h->obs_rows);
+        h->pp_ratio = std::max(ratio, 1e-9);
+        h->pp_probed = true;
+        if (ratio * (double)rows > (double)PP_MIN_GROUPS && ratio > 0.5) h->pp = true;
+        return DBG_OK;
+    }
     if (!h->pp_set) RETURN_IF(dev_alloc((void**)&h->pp_set, PP_SET_CAP * 16 + 64));
     u64* out = h->pp_set + 2 * PP_SET_CAP;
-    const u64 ns = std::min<u64>(rows, 1ULL << 20);
+    // 1/64 of the rows, between 2^16 and 2^18 samples; the set sized for them (<= 50 % load)
+    const u64 ns = std::min<u64>(rows, std::max<u64>(1ULL << 16, std::min<u64>(rows / 64, 1ULL << 18)));
+    const u64 set_cap = std::min<u64>(PP_SET_CAP, pow2_at_least(2 * ns));
     {
         prof::Scope ps("pp_probe", h->stream);
-        launch_pp_sample(h->stream, h->dspec, h->dbatches, bid, rows, ns, h->pp_set, PP_SET_CAP, out);
+        launch_pp_sample(h->stream, h->dspec, h->dbatches, bid, rows, ns, h->pp_set, set_cap, out);
     }
     HIPCHECK(hipGetLastError());
     RETURN_IF(ensure_pinned(h, &h->pp_hpart, &h->pp_hpart_cap, 1024));
@@ -1557,6 +1597,7 @@ int dbg_agg_finalize(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* string_byt
         h->pending_rows = h->pending_recs = 0;
         const u64* tot = h->hcounters + CNT_WORDS;
         h->n_groups = tot[0];
+        note_observed(h);
         h->string_bytes.assign(S.n_keys, 0);
         for (int c = 0; c < S.n_keys; ++c)
             h->string_bytes[c] = (S.key_types[c].type == DBG_STRING && !S.inline_keys) ? tot[1 + c] : 0;
@@ -2026,6 +2067,7 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
     h->pending_rows = h->pending_recs = 0;
     const u64* tot = h->hcounters + CNT_WORDS;
     h->n_groups = tot[0];
+    note_observed(h);
     h->string_bytes.assign(S.n_keys, 0);
     bool short_buf = h->n_groups > F.max_groups;
     for (int c = 0; c < S.n_keys; ++c) {
@@ -2400,7 +2442,12 @@ int dbg_agg_compact(dbg_agg_handle* h, int* compacted) {
     int rc = dev_alloc(&strb.p, strb.bytes);
     if (rc == DBG_OK) rc = dbg_agg_export_records(h, rb.p, strb.p);
     if (rc == DBG_OK && hipStreamSynchronize(h->stream) != hipSuccess) rc = fail(DBG_ERR_DEVICE, "compact: export failed");
+    // the handle keeps its strategy: the re-merged batch (one record per group) must not be
+    // probed again — on an AUTO handle with many groups the probe would see ratio ~1 and switch
+    // to the partitioned payload, after which compaction does nothing
+    const u64 rows_before = h->table_rows;
     if (rc == DBG_OK) rc = dbg_agg_reset(h);  // frees the copies of earlier inputs
+    h->table_rows = rows_before ? rows_before : 1;
     if (rc != DBG_OK) {
         hipFree(rb.p);
         if (strb.p) hipFree(strb.p);
@@ -2833,6 +2880,12 @@ struct dbg_comm {
     u64 send_recs_cap = 0, send_strs_cap = 0;
     hipEvent_t sent = nullptr;  // the last exchange's sends: the next export into the buffers waits
     bool sent_valid = false;
+    // before-partial payload exchange: send and receive buffers kept between calls (grown only)
+    u8* pay_send = nullptr;
+    u8* pay_recv[2] = {nullptr, nullptr};
+    u64 pay_send_cap = 0, pay_recv_cap[2] = {0, 0};
+    u64* pay_dbuf = nullptr;  // counts all-gather: own row, then n rows
+    u64 pay_dbuf_cap = 0;
 };
 
 extern "C" {
@@ -2883,6 +2936,10 @@ void dbg_comm_destroy(dbg_comm* c) {
     if (c->dsizes) hipFree(c->dsizes);
     if (c->send_recs) hipFree(c->send_recs);
     if (c->send_strs) hipFree(c->send_strs);
+    if (c->pay_send) hipFree(c->pay_send);
+    for (int k = 0; k < 2; ++k)
+        if (c->pay_recv[k]) hipFree(c->pay_recv[k]);
+    if (c->pay_dbuf) hipFree(c->pay_dbuf);
     if (c->hsizes) hipHostFree(c->hsizes);
     if (c->sent) hipEventDestroy(c->sent);
     delete c;
@@ -3005,6 +3062,73 @@ int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, c
     return DBG_OK;
 }
 
+// Byte plan of the before-partial shuffle for one rank (host only): send_bytes[k * n + d] = this
+// rank's kind-k records of the partitions rank d owns, recv_bytes[k * n + s] = source s's kind-k
+// records of this rank's partitions; widths from the params' payload record formats.
+static void payload_plan(u32 n, u32 me, const uint32_t widths[2], const uint64_t* all_counts, u64* send_bytes, u64* recv_bytes) {
+    const u64 P = 1ull << PP_L1_BITS;
+    u32 lo_me, hi_me;
+    payload_owned(me, n, lo_me, hi_me);
+    for (int k = 0; k < 2; ++k)
+        for (u32 d = 0; d < n; ++d) {
+            u32 lo, hi;
+            payload_owned(d, n, lo, hi);
+            u64 sb = 0, rb = 0;
+            for (u32 p = lo; p < hi; ++p) sb += all_counts[((u64)me * 2 + k) * P + p];
+            for (u32 p = lo_me; p < hi_me; ++p) rb += all_counts[((u64)d * 2 + k) * P + p];
+            send_bytes[(u64)k * n + d] = sb * widths[k];
+            recv_bytes[(u64)k * n + d] = rb * widths[k];
+        }
+}
+
+int dbg_payload_exchange_plan(const dbg_agg_params* params, uint32_t n_ranks, uint32_t rank, const uint64_t* all_counts,
+                              uint32_t* widths, uint64_t* send_bytes, uint64_t* recv_bytes) {
+    if (!params || !all_counts || !send_bytes || !recv_bytes || n_ranks == 0 || rank >= n_ranks || n_ranks > (1u << PP_L1_BITS))
+        return fail(DBG_ERR_INVALID, "dbg_payload_exchange_plan: bad argument");
+    Spec S;
+    std::vector<dbg_datatype> rt;
+    RETURN_IF(build_spec(params, S, rt));
+    const uint32_t w[2] = {S.pp_rw_raw, S.pp_rw_state};
+    if (widths) {
+        widths[0] = w[0];
+        widths[1] = w[1];
+    }
+    payload_plan(n_ranks, rank, w, all_counts, send_bytes, recv_bytes);
+    return DBG_OK;
+}
+
+static int grow_dev(u8** p, u64* cap, u64 need) {
+    if (need <= *cap && *p) return DBG_OK;
+    if (*p) HIPCHECK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    const u64 c = std::max<u64>(need, 1 << 20);
+    RETURN_IF(dev_alloc((void**)p, c));
+    *cap = c;
+    return DBG_OK;
+}
+
+// One all-gather of a per-rank word (every rank calls it): true when every rank passed `ok`.
+// A rank that failed locally after the counts all-gather still takes part in this one, so no peer
+// is left waiting in a send / receive the failed rank never posts.
+static int all_ok(dbg_comm* c, RcclApi& R, hipStream_t s, bool ok, int* bad_rank) {
+    const u32 n = (u32)c->n;
+    u64* d = c->dsizes;  // >= 2n (n + 1) words
+    u64* hh = c->hsizes;
+    hh[0] = ok ? 1 : 0;
+    HIPCHECK(hipMemcpyAsync(d, hh, 8, hipMemcpyHostToDevice, s));
+    RCCLCHECK(R.AllGather(d, d + 1, 1, ncclUint64, c->comm, s));
+    HIPCHECK(hipMemcpyAsync(hh + 1, d + 1, 8ull * n, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    *bad_rank = -1;
+    for (u32 r = 0; r < n; ++r)
+        if (hh[1 + r] != 1) {
+            *bad_rank = (int)r;
+            break;
+        }
+    return DBG_OK;
+}
+
 int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats* stats) {
     if (!c || !h) return fail(DBG_ERR_INVALID, "null argument");
     if (h->device != c->device) return fail(DBG_ERR_INVALID, "communicator and table are on different devices");
@@ -3018,61 +3142,71 @@ int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats*
     const int rc0 = dbg_agg_payload_counts(h, mine.data(), widths);
     mine[2 * P] = rc0 == DBG_OK ? 1 : 0;
     hipStream_t s = h->stream;
-    // 1. every rank's counts (and whether it can take part), one all-gather
-    u64* dbuf = nullptr;
-    RETURN_IF(dev_alloc((void**)&dbuf, 8 * W * (n + 1)));
+    // buffers of the last call are reused once its sends have left them
+    if (c->sent_valid) HIPCHECK(hipEventSynchronize(c->sent));
+    c->sent_valid = false;
+    // 1. every rank's counts (and whether it can take part), one all-gather into a cached buffer
+    if (c->pay_dbuf_cap < W * (n + 1)) {
+        if (c->pay_dbuf) HIPCHECK(hipFree(c->pay_dbuf));
+        c->pay_dbuf = nullptr;
+        c->pay_dbuf_cap = 0;
+        RETURN_IF(dev_alloc((void**)&c->pay_dbuf, 8 * W * (n + 1)));
+        c->pay_dbuf_cap = W * (n + 1);
+    }
+    u64* dbuf = c->pay_dbuf;
     std::vector<u64> all(W * n);
     HIPCHECK(hipMemcpyAsync(dbuf, mine.data(), 8 * W, hipMemcpyHostToDevice, s));
     RCCLCHECK(R.AllGather(dbuf, dbuf + W, W, ncclUint64, c->comm, s));
     HIPCHECK(hipMemcpyAsync(all.data(), dbuf + W, 8 * W * n, hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
-    HIPCHECK(hipFree(dbuf));
     for (u32 r = 0; r < n; ++r)
-        if (all[(u64)r * W + 2 * P] != 1)
+        if (all[(u64)r * W + 2 * P] != 1)  // every rank sees the same flags: all return here
             return rc0 != DBG_OK ? rc0 : fail(DBG_ERR_UNSUPPORTED, "payload exchange: rank " + std::to_string(r) + " cannot take part");
-    // 2. pack this rank's records destination-major
-    u64 send_bytes[2][256] = {}, recv_bytes[2][256] = {}, kind_total[2] = {0, 0}, recv_total[2] = {0, 0};
-    u32 lo_me, hi_me;
-    payload_owned(me, n, lo_me, hi_me);
+    // 2. the byte plan, the buffers and this rank's records packed destination-major.  A local
+    //    failure here is made collective (all_ok) before any rank posts a send or receive.
+    std::vector<u64> pc(2 * P * n);
+    for (u32 r = 0; r < n; ++r)
+        for (u64 x = 0; x < 2 * P; ++x) pc[(u64)r * 2 * P + x] = all[(u64)r * W + x];
+    std::vector<u64> send_bytes(2 * n), recv_bytes(2 * n);
+    payload_plan(n, me, widths, pc.data(), send_bytes.data(), recv_bytes.data());
+    u64 kind_total[2] = {0, 0}, recv_total[2] = {0, 0};
     for (int k = 0; k < 2; ++k)
         for (u32 d = 0; d < n; ++d) {
-            u32 lo, hi;
-            payload_owned(d, n, lo, hi);
-            for (u32 p = lo; p < hi; ++p) send_bytes[k][d] += mine[k * P + p] * widths[k];
-            for (u32 p = lo_me; p < hi_me; ++p) recv_bytes[k][d] += all[(u64)d * W + k * P + p] * widths[k];
-            kind_total[k] += send_bytes[k][d];
-            recv_total[k] += recv_bytes[k][d];
+            kind_total[k] += send_bytes[(u64)k * n + d];
+            recv_total[k] += recv_bytes[(u64)k * n + d];
         }
-    u8* sendb = nullptr;
-    u8* recvb[2] = {nullptr, nullptr};
-    RETURN_IF(dev_alloc((void**)&sendb, std::max<u64>(kind_total[0] + kind_total[1], 16)));
-    for (int k = 0; k < 2; ++k) RETURN_IF(dev_alloc((void**)&recvb[k], std::max<u64>(recv_total[k], 16)));
-    RETURN_IF(dbg_agg_payload_export(h, n, sendb));
+    int rc = grow_dev(&c->pay_send, &c->pay_send_cap, kind_total[0] + kind_total[1]);
+    for (int k = 0; k < 2 && rc == DBG_OK; ++k) rc = grow_dev(&c->pay_recv[k], &c->pay_recv_cap[k], recv_total[k]);
+    if (rc == DBG_OK) rc = dbg_agg_payload_export(h, n, c->pay_send);
+    const std::string local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
+    int bad = -1;
+    RETURN_IF(all_ok(c, R, s, rc == DBG_OK, &bad));
+    if (bad >= 0) {
+        if (rc != DBG_OK) return fail(rc, local_err);
+        return fail(DBG_ERR_DEVICE, "payload exchange: rank " + std::to_string(bad) + " failed before the transfer");
+    }
     // 3. grouped point-to-point over xGMI (self included)
     RCCLCHECK(R.GroupStart());
     for (int k = 0; k < 2; ++k) {
         u64 so = k ? kind_total[0] : 0, ro = 0;
         for (u32 p = 0; p < n; ++p) {
-            if (send_bytes[k][p]) RCCLCHECK(R.Send(sendb + so, send_bytes[k][p], ncclUint8, (int)p, c->comm, s));
-            if (recv_bytes[k][p]) RCCLCHECK(R.Recv(recvb[k] + ro, recv_bytes[k][p], ncclUint8, (int)p, c->comm, s));
-            so += send_bytes[k][p];
-            ro += recv_bytes[k][p];
+            const u64 sb = send_bytes[(u64)k * n + p], rb = recv_bytes[(u64)k * n + p];
+            if (sb) RCCLCHECK(R.Send(c->pay_send + so, sb, ncclUint8, (int)p, c->comm, s));
+            if (rb) RCCLCHECK(R.Recv(c->pay_recv[k] + ro, rb, ncclUint8, (int)p, c->comm, s));
+            so += sb;
+            ro += rb;
         }
     }
     RCCLCHECK(R.GroupEnd());
-    // 4. the received records become this rank's level-1 payload
-    std::vector<u64> pc(2 * P * n);
-    for (u32 r = 0; r < n; ++r)
-        for (u64 x = 0; x < 2 * P; ++x) pc[(u64)r * 2 * P + x] = all[(u64)r * W + x];
-    const int rc = dbg_agg_payload_import(h, n, me, pc.data(), recvb[0], recvb[1]);
-    HIPCHECK(hipStreamSynchronize(s));
-    hipFree(sendb);
-    hipFree(recvb[0]);
-    hipFree(recvb[1]);
+    // 4. the received records become this rank's level-1 payload (import copies them: the
+    //    communicator's buffers are free again when it returns)
+    rc = dbg_agg_payload_import(h, n, me, pc.data(), c->pay_recv[0], c->pay_recv[1]);
+    HIPCHECK(hipEventRecord(c->sent, s));
+    c->sent_valid = true;
     if (rc != DBG_OK) return rc;
     if (stats) {
         stats->sent_bytes = kind_total[0] + kind_total[1];
-        stats->remote_bytes = stats->sent_bytes - send_bytes[0][me] - send_bytes[1][me];
+        stats->remote_bytes = stats->sent_bytes - send_bytes[me] - send_bytes[(u64)n + me];
         stats->received_records = 0;
         for (int k = 0; k < 2; ++k) stats->received_records += recv_total[k] / std::max<u32>(widths[k], 1);
         stats->received_string_bytes = 0;
@@ -3106,7 +3240,9 @@ int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final
     HIPCHECK(hipMemcpyAsync(c->dsizes, own, 16ull * n, hipMemcpyHostToDevice, s));
     RCCLCHECK(R.AllGather(c->dsizes, c->dsizes + 2 * n, 2 * n, ncclUint64, c->comm, s));
     HIPCHECK(hipMemcpyAsync(c->hsizes + 2 * n, c->dsizes + 2 * n, 16ull * n * n, hipMemcpyDeviceToHost, s));
-    // 2. records + blobs, partition-major, into the communicator's send buffers
+    // 2. records + blobs, partition-major, into the communicator's send buffers; the receive
+    //    buffers.  A local failure from here on is made collective (all_ok) before any rank posts a
+    //    send or receive, so no peer waits for transfers this rank never starts.
     u64 tot_r = 0, tot_s = 0;
     for (int d = 0; d < n; ++d) {
         tot_r += counts[d];
@@ -3114,20 +3250,10 @@ int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final
     }
     if (c->sent_valid) HIPCHECK(hipEventSynchronize(c->sent));
     c->sent_valid = false;
-    if (tot_r * w > c->send_recs_cap) {
-        if (c->send_recs) HIPCHECK(hipFree(c->send_recs));
-        c->send_recs_cap = std::max<u64>(tot_r * w, 1 << 20);
-        RETURN_IF(dev_alloc((void**)&c->send_recs, c->send_recs_cap));
-    }
-    if (tot_s > c->send_strs_cap) {
-        if (c->send_strs) HIPCHECK(hipFree(c->send_strs));
-        c->send_strs_cap = std::max<u64>(tot_s, 1 << 16);
-        RETURN_IF(dev_alloc((void**)&c->send_strs, c->send_strs_cap));
-    }
-    if (!c->send_recs) RETURN_IF(dev_alloc((void**)&c->send_recs, c->send_recs_cap = 1 << 20));
-    if (!c->send_strs) RETURN_IF(dev_alloc((void**)&c->send_strs, c->send_strs_cap = 1 << 16));
-    RETURN_IF(dbg_agg_export_records(partial, c->send_recs, c->send_strs));
-    HIPCHECK(hipStreamSynchronize(s));  // gathered sizes on the host (the one host round trip)
+    int rc = grow_dev(&c->send_recs, &c->send_recs_cap, tot_r * w);
+    if (rc == DBG_OK) rc = grow_dev(&c->send_strs, &c->send_strs_cap, tot_s);
+    if (rc == DBG_OK) rc = dbg_agg_export_records(partial, c->send_recs, c->send_strs);
+    if (hipStreamSynchronize(s) != hipSuccess && rc == DBG_OK) rc = fail(DBG_ERR_DEVICE, "exchange: size all-gather");
     const u64* g = c->hsizes + 2 * n;   // g[src * 2n + 2 * dst + {0, 1}]
     std::vector<u64> seg_r(n), seg_s(n);
     u64 rr = 0, rs = 0;
@@ -3137,13 +3263,18 @@ int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final
         rr += seg_r[src];
         rs += seg_s[src];
     }
-    if (seg_r[me] != counts[me] || seg_s[me] != sbytes[me]) return fail(DBG_ERR_INTERNAL, "exchange sizes disagree");
+    if (rc == DBG_OK && (seg_r[me] != counts[me] || seg_s[me] != sbytes[me])) rc = fail(DBG_ERR_INTERNAL, "exchange sizes disagree");
     // receive buffers belong to the final table: merge_records retains them until its reset
     void *rrec = nullptr, *rstr = nullptr;
-    RETURN_IF(dev_alloc(&rrec, rr * w));
-    final_h->owned.push_back({rrec, (size_t)std::max<u64>(rr * w, 16)});
-    RETURN_IF(dev_alloc(&rstr, rs));
-    final_h->owned.push_back({rstr, (size_t)std::max<u64>(rs, 16)});
+    if (rc == DBG_OK && (rc = dev_alloc(&rrec, rr * w)) == DBG_OK) final_h->owned.push_back({rrec, (size_t)std::max<u64>(rr * w, 16)});
+    if (rc == DBG_OK && (rc = dev_alloc(&rstr, rs)) == DBG_OK) final_h->owned.push_back({rstr, (size_t)std::max<u64>(rs, 16)});
+    const std::string local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
+    int bad = -1;
+    RETURN_IF(all_ok(c, R, s, rc == DBG_OK, &bad));
+    if (bad >= 0) {
+        if (rc != DBG_OK) return fail(rc, local_err);
+        return fail(DBG_ERR_DEVICE, "exchange: rank " + std::to_string(bad) + " failed before the transfer");
+    }
     // 3. grouped point-to-point over xGMI (records and blobs; self included)
     RCCLCHECK(R.GroupStart());
     u64 so_r = 0, so_s = 0, ro_r = 0, ro_s = 0;

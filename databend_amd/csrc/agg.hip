@@ -436,34 +436,78 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         // ballot + one LDS add per wave), and the hash / probe / state update runs on BLOCK queued
         // rows at a time with every lane busy — at 13% selectivity (ClickBench Q13) the
         // row-per-lane loop would run the long dependent chain of a string key with 1 lane in 8.
-        __shared__ u32 selq[2 * BLOCK];
+        // PU rounds of BLOCK rows are evaluated per step with all their loads issued together (one
+        // row per lane per round, a single round in flight left the stream latency-bound: C5's
+        // predicate pass ran at ~1.2 TB/s), queued together, and inserted BLOCK at a time.
+        constexpr int PU = 4;  // (PU + 1) KB of queue beside the 32 KB table: 4 workgroups per CU
+        static_assert(FLUSH_ROUND % PU == 0, "flush checks fall on step boundaries");
+        __shared__ u32 selq[(PU + 1) * BLOCK];
         __shared__ u32 qn;
         if (threadIdx.x == 0) qn = 0;
         __syncthreads();
         const u32 lane = __lane_id();
-        for (u64 it = 0; it < n_iter; ++it) {
+        // `s <op> ''` on one non-null String column (ClickBench Q13: SearchPhrase <> ''): the
+        // selection is a function of the row's length alone, read from the offsets
+        const DNode& n0 = B.nodes[0];
+        const DCol& c0 = B.fcols[n0.col];
+        const bool lenpred = B.n_nodes == 1 && n0.op == DBG_PRED_CMP_CONST && n0.str_len == 0 && c0.type == DBG_STRING &&
+                             !c0.nullable && c0.layout == LAYOUT_ARROW;
+        const u64* __restrict__ offs = c0.offsets;
+        for (u64 it = 0; it < n_iter; it += PU) {
             if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
-            const u64 i = r0 + it * BLOCK + threadIdx.x;
-            const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
-            const u64 m = __ballot(sel);
-            if (m) {
+            bool sel[PU];
+            if (lenpred) {
+                u64 a[PU], b[PU];
+#pragma unroll
+                for (int k = 0; k < PU; ++k) {
+                    const u64 i = r0 + (it + k) * BLOCK + threadIdx.x;
+                    const u64 j = i < r1 ? i : r0;
+                    a[k] = gld<u64>(offs + j);
+                    b[k] = gld<u64>(offs + j + 1);
+                }
+#pragma unroll
+                for (int k = 0; k < PU; ++k) {
+                    const u64 i = r0 + (it + k) * BLOCK + threadIdx.x;
+                    sel[k] = i < r1 && apply_cmp(n0.cmp, b[k] != a[k] ? 1 : 0);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < PU; ++k) {
+                    const u64 i = r0 + (it + k) * BLOCK + threadIdx.x;
+                    sel[k] = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+                }
+            }
+            // queue the step's selected rows: one LDS add per wave
+            u32 cnt = 0;
+            u64 mk[PU];
+#pragma unroll
+            for (int k = 0; k < PU; ++k) {
+                mk[k] = __ballot(sel[k]);
+                cnt += (u32)__popcll(mk[k]);
+            }
+            if (cnt) {
                 u32 wbase = 0;
-                if (lane == 0) wbase = atomicAdd(&qn, (u32)__popcll(m));
+                if (lane == 0) wbase = atomicAdd(&qn, cnt);
                 wbase = __shfl(wbase, 0);
-                if (sel) selq[wbase + (u32)__popcll(m & ((1ULL << lane) - 1))] = (u32)(i - r0);
+                const u64 lt = (1ULL << lane) - 1;
+#pragma unroll
+                for (int k = 0; k < PU; ++k) {
+                    if (sel[k]) selq[wbase + (u32)__popcll(mk[k] & lt)] = (u32)((it + k) * BLOCK + threadIdx.x);
+                    wbase += (u32)__popcll(mk[k]);
+                }
             }
             __syncthreads();
-            const u32 n = qn;  // < 2 * BLOCK
+            const u32 n = qn;  // < (PU + 1) * BLOCK
             if (n >= BLOCK) {
-                const u32 off = selq[threadIdx.x];
-                const u32 rem = n - BLOCK;  // < BLOCK
-                const u32 mv = threadIdx.x < rem ? selq[BLOCK + threadIdx.x] : 0u;
+                const u32 full = n / BLOCK;
+                for (u32 c = 0; c < full; ++c) insert_row(r0 + selq[c * BLOCK + threadIdx.x], my_claims);
+                const u32 rem = n - full * BLOCK;  // < BLOCK: moved to the front
+                const u32 mv = threadIdx.x < rem ? selq[full * BLOCK + threadIdx.x] : 0u;
                 __syncthreads();
                 if (threadIdx.x < rem) selq[threadIdx.x] = mv;
                 if (threadIdx.x == 0) qn = rem;
-                insert_row(r0 + off, my_claims);
             }
-            __syncthreads();  // the queue is settled before the next round appends
+            __syncthreads();  // the queue is settled before the next step appends
         }
         const u32 n = qn;  // < BLOCK
         if (threadIdx.x < n)

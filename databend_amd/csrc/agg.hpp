@@ -217,7 +217,7 @@ struct FusedFin;
 u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap);  // 0 = not eligible
 size_t part_temp_bytes(int width, u64 rows, u32 sb, u64 cap);
 hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, const TableDesc& t, u32 sb, void* temp,
-                              size_t temp_bytes, u64* sorted, u64* bounds, const char** step);
+                              size_t temp_bytes, u64* sorted, u64* bounds, bool table_empty, const char** step);
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
                    bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr,

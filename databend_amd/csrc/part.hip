@@ -6,24 +6,27 @@
 // reordered first so that the table is touched slice by slice:
 //
 //   1. m = slot_mix(key) for every row (slot_mix is a bijection of u64), radix-partitioned on
-//      the slot bits above the slice size — rocPRIM's onesweep radix sort over bits
-//      [slice_bits, log2 cap), input read through a transform iterator (no staging pass);
+//      the slot bits above the slice size by this file's own LSD radix partition (rp_*): one
+//      histogram pass over the keys counts the digits of every pass, then each pass scatters
+//      8192-row tiles through LDS — a stable wave-level ranking (8 ballots per digit), the
+//      tile's digit counts published for a decoupled look-back over earlier tiles, and the
+//      tile written out digit run by digit run;
 //   2. part_bounds: the first sorted position of every slice (one binary search per slice);
-//   3. part_slice: one workgroup per table slice: slice HBM -> LDS (64 KB), every row of the
-//      slice probes and counts in LDS (same linear probing as g_find, so the table stays a valid
-//      HBM table for every other kernel), LDS -> HBM.  A probe that would leave the slice (its
-//      run continues in the next slice, owned by another workgroup) becomes an overflow record
-//      [key][1] that agg_retry merges after the launch — the deferred-overflow protocol of the
-//      streaming insert.
+//   3. part_slice: one workgroup per table slice: slice HBM -> LDS (64 KB) — or, when the table is
+//      empty at launch (a reset whose initialisation was deferred), the slice starts EMPTY in
+//      LDS and the table is not read at all — every row of the slice probes and counts in LDS
+//      (same linear probing as g_find, so the table stays a valid HBM table for every other
+//      kernel), LDS -> HBM.  A probe that would leave the slice (its run continues in the next
+//      slice, owned by another workgroup) becomes an overflow record [key][1] that part_fixup
+//      merges right after — the deferred-overflow protocol of the streaming insert.
 //
 // This is the reference's own answer to the same problem — AggregateHashTable radix-partitions
 // its payload (EAGG/partitioned_payload.rs:100-143) so the final merge works partition by
 // partition on cache-sized tables (AGG/transform_aggregate_final.rs:71-156) — applied to the
 // 64 KB LDS of a CDNA4 workgroup instead of a CPU core's cache.
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
-
+#include <algorithm>
 #include <cstdio>
+#include <cstring>
 
 #include "agg.hpp"
 
@@ -35,10 +38,201 @@
 
 namespace {
 
-template <typename U>
-struct MixOf {
-    __host__ __device__ u64 operator()(U v) const { return slot_mix((u64)v); }
+// ---------------------------------------------------------------------------------------------
+// LSD radix partition of m = slot_mix(key) on bits [sb, log2 cap) — 1 to 3 passes of <= 8 bits
+// ---------------------------------------------------------------------------------------------
+#define RP_NT 512                      // threads per scatter workgroup (2 per CU: 72 KB of LDS each)
+#define RP_IPT 16                      // rows per thread and tile
+#define RP_TILE (RP_NT * RP_IPT)       // 8192 rows per tile
+#define RP_WAVES (RP_NT / 64)
+#define RP_WROWS (64 * RP_IPT)         // rows of one wave's share of a tile
+#define RP_MAXP 3
+#define RP_HIST_NT 256
+#define RP_HIST_BLOCKS 2048
+// look-back status words: [flag 2 b | count 62 b]; flag 1 = this tile's count, 2 = inclusive prefix
+#define RP_AGG (1ULL << 62)
+#define RP_INC (2ULL << 62)
+#define RP_VAL ((1ULL << 62) - 1)
+
+struct RadixPlan {
+    u32 npass;
+    u32 shift[RP_MAXP];
+    u32 bits[RP_MAXP];
 };
+
+template <int W>
+__device__ __forceinline__ u64 rp_key(const u8* p, u64 i) {
+    if (W == 1) return gld<u8>(p + i);
+    if (W == 2) return gld<uint16_t>(p + 2 * i);
+    if (W == 4) return gld<uint32_t>(p + 4 * i);
+    return gld<u64>(p + 8 * i);
+}
+
+// Digit counts of every pass in one read of the keys: per-workgroup LDS histograms, then one
+// device atomic per non-empty bin.  hist[p * 256 + d] (u32: a batch holds < 2^32 rows).
+template <int W>
+__global__ void __launch_bounds__(RP_HIST_NT) rp_hist_kernel(const u8* __restrict__ keys, u64 rows, RadixPlan P,
+                                                             u32* __restrict__ hist) {
+    __shared__ u32 h[RP_MAXP][256];
+    for (u32 i = threadIdx.x; i < RP_MAXP * 256; i += RP_HIST_NT) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const u64 per = (rows + gridDim.x - 1) / gridDim.x;
+    const u64 lo = min<u64>(rows, (u64)blockIdx.x * per), hi = min<u64>(rows, lo + per);
+    constexpr int U = 8;  // independent loads in flight per lane
+    u64 i = lo + threadIdx.x;
+    for (; i + (u64)(U - 1) * RP_HIST_NT < hi; i += (u64)U * RP_HIST_NT) {
+        u64 v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = rp_key<W>(keys, i + (u64)k * RP_HIST_NT);
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const u64 m = slot_mix(v[k]);
+            for (u32 p = 0; p < P.npass; ++p) atomicAdd(&h[p][(m >> P.shift[p]) & ((1u << P.bits[p]) - 1)], 1u);
+        }
+    }
+    for (; i < hi; i += RP_HIST_NT) {
+        const u64 m = slot_mix(rp_key<W>(keys, i));
+        for (u32 p = 0; p < P.npass; ++p) atomicAdd(&h[p][(m >> P.shift[p]) & ((1u << P.bits[p]) - 1)], 1u);
+    }
+    __syncthreads();
+    for (u32 x = threadIdx.x; x < P.npass * 256; x += RP_HIST_NT) {
+        const u32 c = (&h[0][0])[x];
+        if (c) atomicAdd(hist + x, c);
+    }
+}
+
+// Exclusive prefix sum of one value per thread over threads 0..255 (the first four waves; other
+// threads pass 0 and get a meaningless result).  Called by every thread of the workgroup (it
+// synchronises); tmp: 8 words of LDS.
+__device__ __forceinline__ u64 scan256(u64 v, u64* tmp) {
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u64 x = v;  // inclusive scan inside the wave
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u64 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63 && w < 4) tmp[w] = x;
+    __syncthreads();
+    u64 add = 0;
+    for (u32 k = 0; k < w && k < 4; ++k) add += tmp[k];
+    __syncthreads();  // tmp may be reused by the caller
+    return add + x - v;
+}
+
+// One scatter pass.  RAW: the source is the key column (width W; m = slot_mix(key) on the fly),
+// else the previous pass's m.  Tiles are taken in order from a device counter, so every tile's
+// predecessors are running or done when it looks back (no circular wait).  Rows keep their
+// relative order within a digit (LSD needs a stable pass): a wave ranks its 16 rounds of 64
+// rows in order, lanes ranked among equal digits by ballot, wave counts prefixed in wave order.
+template <int W, bool RAW>
+__global__ void __launch_bounds__(RP_NT) rp_scatter_kernel(const u8* __restrict__ src, u64 rows, u32 shift, u32 bits,
+                                                           const u32* __restrict__ hist, u64* __restrict__ status,
+                                                           u32* __restrict__ tile_ctr, u64* __restrict__ dst) {
+    __shared__ __attribute__((aligned(16))) u64 stage[RP_TILE];
+    __shared__ u32 wcnt[RP_WAVES][256];  // per wave: digit counts, then their exclusive prefix over waves
+    __shared__ u32 lstart[256];           // tile-local start of every digit
+    __shared__ u64 gstart[256];           // global start of every digit's run of this tile
+    __shared__ u32 s_tile;
+    __shared__ u64 scan_tmp[16];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u32 nb = 1u << bits, dmask = nb - 1;
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    for (u32 i = tid; i < RP_WAVES * 256; i += RP_NT) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const u32 tile = s_tile;
+    const u64 base = (u64)tile * RP_TILE;
+    const u64 e0 = base + (u64)w * RP_WROWS + lane;  // this lane's row of round 0
+    u64 m[RP_IPT];
+#pragma unroll
+    for (int r = 0; r < RP_IPT; ++r) {
+        const u64 e = e0 + (u64)r * 64;
+        if (e < rows) {
+            if (RAW) m[r] = rp_key<W>(src, e);
+            else m[r] = gld<u64>(src + 8 * e);
+        }
+    }
+    // stable ranking, round by round
+    u32 rank[RP_IPT];
+    const u64 lt = (1ULL << lane) - 1;
+#pragma unroll
+    for (int r = 0; r < RP_IPT; ++r) {
+        const u64 e = e0 + (u64)r * 64;
+        const bool ok = e < rows;
+        if (RAW && ok) m[r] = slot_mix(m[r]);
+        const u32 d = ok ? (u32)(m[r] >> shift) & dmask : 0;
+        u64 peers = __ballot(ok);
+        for (u32 b = 0; b < bits; ++b) {
+            const u64 bb = __ballot((d >> b) & 1);
+            peers &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        u32 old = 0;
+        if (ok) old = wcnt[w][d];
+        __builtin_amdgcn_wave_barrier();
+        const bool leader = ok && (peers & lt) == 0;
+        if (leader) wcnt[w][d] = old + (u32)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        rank[r] = old + (u32)__popcll(peers & lt);
+    }
+    __syncthreads();
+    // digit totals of the tile, per-wave exclusive prefixes, local digit starts
+    u32 tot = 0;
+    if (tid < 256) {
+        for (u32 x = 0; x < RP_WAVES; ++x) {
+            const u32 c = wcnt[x][tid];
+            wcnt[x][tid] = tot;
+            tot += c;
+        }
+        if (tid >= nb) tot = 0;
+    }
+    // publish this tile's counts (a tile without predecessors publishes its inclusive prefix)
+    if (tid < nb) {
+        u64* st = status + (u64)tile * 256 + tid;
+        __hip_atomic_store(st, (tile == 0 ? RP_INC : RP_AGG) | (u64)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // exclusive scans over the 256 digits: the tile's counts (local starts) and the pass
+    // histogram (the digit's first row in the output)
+    const u32 lst = scan256(tid < 256 ? tot : 0u, scan_tmp);
+    const u64 hst = scan256(tid < nb ? hist[tid] : 0u, scan_tmp + 8);
+    if (tid < 256) lstart[tid] = lst;
+    // decoupled look-back: the rows of digit d in every earlier tile
+    if (tid < nb) {
+        u64 acc = 0;
+        if (tile > 0) {
+            const u64* sp = status + (u64)(tile - 1) * 256 + tid;
+            for (;;) {
+                const u64 v = __hip_atomic_load((u64*)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                acc += v & RP_VAL;
+                if (v & RP_INC) break;
+                sp -= 256;
+            }
+            __hip_atomic_store(status + (u64)tile * 256 + tid, RP_INC | (acc + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        gstart[tid] = hst + acc;
+    }
+    __syncthreads();
+    // rows to LDS in digit order
+#pragma unroll
+    for (int r = 0; r < RP_IPT; ++r) {
+        const u64 e = e0 + (u64)r * 64;
+        if (e < rows) {
+            const u32 d = (u32)(m[r] >> shift) & dmask;
+            stage[lstart[d] + wcnt[w][d] + rank[r]] = m[r];
+        }
+    }
+    __syncthreads();
+    // LDS -> HBM: consecutive lanes write consecutive words of one digit's run
+    const u32 n = (u32)min<u64>(RP_TILE, rows - base);
+    for (u32 j = tid; j < n; j += RP_NT) {
+        const u64 v = stage[j];
+        const u32 d = (u32)(v >> shift) & dmask;
+        dst[gstart[d] + (j - lstart[d])] = v;
+    }
+}
 
 __device__ __forceinline__ u64 bucket_of(u64 m, u64 mask, u32 sb) { return (m & mask) >> sb; }
 
@@ -62,7 +256,9 @@ typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 // [entry][count].  The slice size is a compile-time constant so that the slice's loads (S / NT
 // 16-byte vectors per lane) are all in flight together before the first LDS store waits on
 // them: one memory latency per workgroup, not one per load.
-template <int SB>
+// EMPTY: the table holds no group and was not initialised (a deferred reset): the slice starts
+// as EMPTY entries with zero counts in LDS, and the kernel writes every slot of it.
+template <int SB, bool EMPTY>
 __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restrict__ sorted, const u64* __restrict__ bounds,
                                                              TableDesc t) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
@@ -81,7 +277,10 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     v2u64* lsl = (v2u64*)lds;
     v2u64 sv[PER];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) sv[k] = gsl[threadIdx.x + k * PART_NT];
+    for (int k = 0; k < PER; ++k) {
+        if (EMPTY) sv[k] = v2u64{SLOT_EMPTY, 0ULL};
+        else sv[k] = gsl[threadIdx.x + k * PART_NT];
+    }
     // the slice's first sorted keys are loaded before the slice reaches LDS (independent loads,
     // all in flight together); later batches are loaded one batch ahead of their processing
     const u64 __attribute__((address_space(1)))* src = (const u64 __attribute__((address_space(1)))*)sorted;
@@ -237,24 +436,72 @@ __global__ void __launch_bounds__(256) part_fixup_kernel(TableDesc t) {
     }
 }
 
-template <typename U>
-hipError_t sort_t(void* temp, size_t& temp_bytes, const void* keys, u64* out, u64 rows, u32 b0, u32 b1, hipStream_t s) {
-    auto it = rocprim::make_transform_iterator((const U*)keys, MixOf<U>());
-    hipError_t e = rocprim::radix_sort_keys(temp, temp_bytes, it, out, (size_t)rows, b0, b1, s);
-    return e;
-}
-
-hipError_t sort_any(int width, void* temp, size_t& temp_bytes, const void* keys, u64* out, u64 rows, u32 b0, u32 b1,
-                    hipStream_t s) {
-    switch (width) {
-        case 1: return sort_t<uint8_t>(temp, temp_bytes, keys, out, rows, b0, b1, s);
-        case 2: return sort_t<uint16_t>(temp, temp_bytes, keys, out, rows, b0, b1, s);
-        case 4: return sort_t<uint32_t>(temp, temp_bytes, keys, out, rows, b0, b1, s);
-        default: return sort_t<u64>(temp, temp_bytes, keys, out, rows, b0, b1, s);
-    }
-}
-
 u32 log2u(u64 x) { return 63 - __builtin_clzll(x); }
+
+// Passes over the digit bits [sb, log2 cap): at most 8 bits each, low digit first (LSD).
+RadixPlan rp_plan(u32 sb, u64 cap) {
+    RadixPlan P;
+    memset(&P, 0, sizeof(P));
+    const u32 D = log2u(cap) - sb;
+    P.npass = (D + 7) / 8;
+    u32 sh = sb;
+    for (u32 p = 0; p < P.npass; ++p) {
+        const u32 left = D - (sh - sb);
+        P.bits[p] = (left + (P.npass - p) - 1) / (P.npass - p);  // as even as possible
+        P.shift[p] = sh;
+        sh += P.bits[p];
+    }
+    return P;
+}
+
+u64 rp_tiles(u64 rows) { return (rows + RP_TILE - 1) / RP_TILE; }
+
+// temp layout: [alt rows u64][status tiles x 256 u64][hist RP_MAXP x 256 u32][tile counters RP_MAXP u32]
+size_t rp_status_off(u64 rows) { return (size_t)rows * 8; }
+size_t rp_hist_off(u64 rows) { return rp_status_off(rows) + (size_t)rp_tiles(rows) * 256 * 8; }
+size_t rp_temp_bytes(u64 rows) { return rp_hist_off(rows) + RP_MAXP * 256 * 4 + RP_MAXP * 4 + 64; }
+
+template <int W>
+void rp_launch_hist(hipStream_t s, const u8* keys, u64 rows, const RadixPlan& P, u32* hist) {
+    const u32 blocks = (u32)std::max<u64>(1, std::min<u64>(RP_HIST_BLOCKS, (rows + 8191) / 8192));
+    hipLaunchKernelGGL(rp_hist_kernel<W>, dim3(blocks), dim3(RP_HIST_NT), 0, s, keys, rows, P, hist);
+}
+
+hipError_t rp_sort(hipStream_t s, int width, const u8* keys, u64 rows, const RadixPlan& P, u8* temp, u64* out,
+                   const char** step) {
+    u64* alt = (u64*)temp;
+    u64* status = (u64*)(temp + rp_status_off(rows));
+    u32* hist = (u32*)(temp + rp_hist_off(rows));
+    u32* ctr = hist + RP_MAXP * 256;
+    const u64 tiles = rp_tiles(rows);
+    hipError_t e;
+    *step = "rp_hist";
+    if ((e = hipMemsetAsync(hist, 0, RP_MAXP * 256 * 4 + RP_MAXP * 4, s)) != hipSuccess) return e;
+    switch (width) {
+        case 1: rp_launch_hist<1>(s, keys, rows, P, hist); break;
+        case 2: rp_launch_hist<2>(s, keys, rows, P, hist); break;
+        case 4: rp_launch_hist<4>(s, keys, rows, P, hist); break;
+        default: rp_launch_hist<8>(s, keys, rows, P, hist); break;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the last pass writes `out`: passes alternate between out and alt backwards from it
+    for (u32 p = 0; p < P.npass; ++p) {
+        *step = "rp_scatter";
+        u64* dst = ((P.npass - 1 - p) % 2 == 0) ? out : alt;
+        const u8* src = p == 0 ? keys : (const u8*)(((P.npass - p) % 2 == 0) ? out : alt);
+        if ((e = hipMemsetAsync(status, 0, (size_t)tiles * 256 * 8, s)) != hipSuccess) return e;
+        const dim3 g((u32)tiles), b(RP_NT);
+        u32* h = hist + p * 256;
+        u32* tc = ctr + p;
+        if (p > 0) hipLaunchKernelGGL((rp_scatter_kernel<8, false>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
+        else if (width == 1) hipLaunchKernelGGL((rp_scatter_kernel<1, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
+        else if (width == 2) hipLaunchKernelGGL((rp_scatter_kernel<2, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
+        else if (width == 4) hipLaunchKernelGGL((rp_scatter_kernel<4, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
+        else hipLaunchKernelGGL((rp_scatter_kernel<8, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 }  // namespace
 
@@ -276,33 +523,35 @@ u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap) {
 }
 
 size_t part_temp_bytes(int width, u64 rows, u32 sb, u64 cap) {
-    size_t bytes = 0;
-    if (sort_any(width, nullptr, bytes, nullptr, nullptr, rows, sb, log2u(cap), 0) != hipSuccess) return 0;
-    return bytes;
+    (void)width;
+    (void)sb;
+    (void)cap;
+    return rp_temp_bytes(rows);
 }
 
-// sorted: rows u64; bounds: (cap >> sb) + 1 u64; temp: part_temp_bytes.  *step names the
-// failing step on error.
+// sorted: rows u64; bounds: (cap >> sb) + 1 u64; temp: part_temp_bytes.  table_empty: the table
+// holds no group and its initialisation was deferred (part_slice writes every slot).  *step
+// names the failing step on error.
 hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, const TableDesc& t, u32 sb, void* temp,
-                              size_t temp_bytes, u64* sorted, u64* bounds, const char** step) {
+                              size_t temp_bytes, u64* sorted, u64* bounds, bool table_empty, const char** step) {
     const int width = (int)hb.keys[0].width;
-    const u32 cb = log2u(t.cap);
-    // rocPRIM's return code is authoritative: it makes calls whose failure it tolerates (HIP's
-    // last-error slot then holds a stale code), so the slot is not consulted for the sort
-    *step = "rocprim radix_sort_keys";
-    (void)hipGetLastError();  // rocPRIM reads the last-error slot after its launches: start it clean
-    hipError_t e = sort_any(width, temp, temp_bytes, hb.keys[0].data, sorted, rows, sb, cb, s);
+    if (sb != PART_SB || temp_bytes < rp_temp_bytes(rows) || rows >= (1ULL << 32)) return hipErrorInvalidValue;
+    const RadixPlan P = rp_plan(sb, t.cap);
+    if (P.npass < 1 || P.npass > RP_MAXP) return hipErrorInvalidValue;
+    hipError_t e = rp_sort(s, width, hb.keys[0].data, rows, P, (u8*)temp, sorted, step);
     if (e != hipSuccess) return e;
-    (void)hipGetLastError();
     const u64 n_slices = t.cap >> sb;
     *step = "part_bounds";
     hipLaunchKernelGGL(part_bounds_kernel, dim3((u32)((n_slices + 1 + 255) / 256)), dim3(256), 0, s, sorted, rows, t.cap - 1, sb,
                        n_slices, bounds);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_slice";
-    if (sb != PART_SB) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(part_slice_kernel<PART_SB>, dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << PART_SB), s, sorted, bounds,
-                       t);
+    if (table_empty)
+        hipLaunchKernelGGL((part_slice_kernel<PART_SB, true>), dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << PART_SB), s,
+                           sorted, bounds, t);
+    else
+        hipLaunchKernelGGL((part_slice_kernel<PART_SB, false>), dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << PART_SB), s,
+                           sorted, bounds, t);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_fixup";
     hipLaunchKernelGGL(part_fixup_kernel, dim3(512), dim3(256), 0, s, t);

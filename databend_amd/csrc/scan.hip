@@ -102,19 +102,21 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     const u32 sn = pg.comp - pg.lv, on = pg.uncomp - pg.lv;
     bool bad = false;
     u32 p = 0, w = 0;  // input / output cursors (uniform)
-    auto copy_lit = [&](u32 len) {
-        if (p + len > sn || w + len > on) { bad = true; return; }
-        for (u32 j = lane; j < len; j += 64) {
+    // bounds are compared without wrapping (p <= sn and w <= on hold throughout): a 4-byte
+    // Snappy literal length near 2^32 must fail here, not wrap past the check
+    auto copy_lit = [&](u64 len) {
+        if (len > (u64)(sn - p) || len > (u64)(on - w)) { bad = true; return; }
+        for (u32 j = lane; j < (u32)len; j += 64) {
             const u8 b = s[p + j];
             o[w + j] = b;
             ring[(w + j) & (RING - 1)] = b;
         }
         __builtin_amdgcn_wave_barrier();
-        p += len;
-        w += len;
+        p += (u32)len;
+        w += (u32)len;
     };
-    auto copy_back = [&](u32 off, u32 len) {
-        if (off == 0 || off > w || off > RING || w + len > on) { bad = true; return; }
+    auto copy_back = [&](u32 off, u64 len) {
+        if (off == 0 || off > w || off > RING || len > (u64)(on - w)) { bad = true; return; }
         // byte j repeats the last `off` bytes: out[w + j] = out[w - off + j % off]; chunks of at
         // most `off` bytes so that every source byte is in the ring before it is read
         for (u32 c0 = 0; c0 < len; c0 += 64) {
@@ -152,7 +154,7 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
                     for (u32 k = 0; k < nb; ++k) len |= ld_u8(s + p + k) << (8 * k);
                     p += nb;
                 }
-                copy_lit(len + 1);
+                copy_lit((u64)len + 1);
             } else {
                 u32 len, off;
                 if (kind == 1) {
@@ -177,7 +179,7 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     } else {  // LZ4 block: [token][literal length+][literals][offset u16][match length+]
         while (!bad && p < sn) {
             const u32 tok = ld_u8(s + p++);
-            u32 lit = tok >> 4;
+            u64 lit = tok >> 4;
             if (lit == 15)
                 for (;;) {
                     if (p >= sn) { bad = true; break; }
@@ -191,7 +193,7 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
             if (p + 2 > sn) { bad = true; break; }
             const u32 off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8);
             p += 2;
-            u32 ml = tok & 15;
+            u64 ml = tok & 15;
             if (ml == 15)
                 for (;;) {
                     if (p >= sn) { bad = true; break; }
@@ -200,7 +202,7 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
                     if (c != 255) break;
                 }
             if (bad) break;
-            copy_back(off, ml + 4);
+            copy_back(off, (u64)ml + 4);
         }
     }
     if ((bad || w != on) && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);

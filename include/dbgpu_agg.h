@@ -409,6 +409,13 @@ int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf);
 int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts /* n x 2 x 256 */,
                            const void* raw_records, const void* state_records);
 int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats* stats);
+/* The byte plan dbg_agg_exchange_payload follows on rank `rank` (host only, no device work):
+ * all_counts[source][kind][p] (n x 2 x 256) as gathered; widths[kind] receives the params' payload
+ * record bytes (may be NULL); send_bytes[kind * n + d] = this rank's kind records of the partitions
+ * rank d owns (export order), recv_bytes[kind * n + s] = source s's kind records of this rank's
+ * partitions (import order). */
+int dbg_payload_exchange_plan(const dbg_agg_params* params, uint32_t n_ranks, uint32_t rank, const uint64_t* all_counts,
+                              uint32_t* widths, uint64_t* send_bytes, uint64_t* recv_bytes);
 
 /* ---- fixed-capacity exchange: replicas + gather for low-cardinality tables ----
  * Replaces, for small inline-key partial tables, the Serialized/Flight hand-off of

@@ -50,9 +50,13 @@ def main():
     w_kib, w_by = per_step(_csv(d, "write"), "WRITE_SIZE")
     read_b = 2.0 * f_kib * 1024.0 / steps
     write_b = w_kib * 1024.0 / steps
+    # keyed by the FULL kernel name: template instantiations (and library kernels) share long
+    # prefixes, and a truncated key let one overwrite another (round 3: rocPRIM's passes)
     kernels = {}
     for name in sorted(set(f_by) | set(w_by), key=lambda n: -(2 * f_by.get(n, 0) + w_by.get(n, 0))):
-        kernels[name[:160]] = {"read": 2.0 * f_by.get(name, 0.0) * 1024.0 / steps, "write": w_by.get(name, 0.0) * 1024.0 / steps}
+        kernels[name] = {"read": 2.0 * f_by.get(name, 0.0) * 1024.0 / steps, "write": w_by.get(name, 0.0) * 1024.0 / steps}
+    attributed = sum(v["read"] + v["write"] for v in kernels.values())
+    assert abs(attributed - (read_b + write_b)) <= 1e-6 * max(1.0, read_b + write_b), (attributed, read_b + write_b)
     res = {
         "scope": "every dispatch of one step (between dbg_marker_kernel dispatches of scripts/pmc_run.py)",
         "steps": steps,

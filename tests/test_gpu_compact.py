@@ -139,3 +139,27 @@ def test_compact_inline_keys_is_noop():
         assert sorted(gk[0].data.tolist()) == list(range(7))
     finally:
         ht.close()
+
+
+def test_compact_keeps_strategy_many_groups():
+    """the re-merged batch (one record per group) must not re-run the cardinality
+    probe — with more than 2^20 groups it would see ratio ~1 and switch an AUTO handle to the
+    partitioned payload, after which compact() does nothing."""
+    rng = np.random.default_rng(44)
+    n, groups = 4_400_000, 1_300_000
+    g = rng.integers(0, groups, n)
+    s = Column.from_strings(["k%07d" % i for i in g])
+    keys, aggs = [s], [("count", None)]
+    fns = [F.get("count", [], [])]
+    ht = AggregateHashTable(AggregatorParams([s.dtype], fns), HashTableConfig(True))
+    try:
+        ht.add_groups(keys, [None], rows=n)
+        assert ht.strategy()[0] == 0  # moderate cardinality (~0.3 groups per row): the HBM table
+        assert ht.compact()
+        assert ht.strategy()[0] == 0
+        assert ht.compact()  # still a table that compaction rewrites
+        gk, ga = _result(ht, 1)
+    finally:
+        ht.close()
+    ok, oa = oracle_aggregate(keys, aggs, threads=8)
+    assert_results_equal(gk, ga, ok, oa)

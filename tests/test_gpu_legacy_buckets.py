@@ -157,3 +157,33 @@ def test_legacy_threshold_setting_and_serializer_keys():
             p.on_finish()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("ktype", [col.UInt16, col.Int8.wrap_nullable()])
+def test_legacy_small_keys_stay_single_level(ktype):
+    """HashMethodFixedKeys<u8> / <u16> (a UInt16 key, a nullable Int8 key = 2 key bytes) never go
+    two-level (SUPPORT_PARTITIONED = false, aggregator_polymorphic_keys.rs:149,189), whatever the
+    group count: one bucket -1 meta, as the reference emits."""
+    rng = np.random.default_rng(25)
+    n = 200_000
+    if ktype == col.UInt16:
+        k = Column.from_numbers(col.UInt16, rng.integers(0, 65536, n))
+    else:
+        k = Column.from_numbers(col.Int8, rng.integers(-128, 128, n), validity=rng.random(n) > 0.1)
+    v = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n))
+    aggs = [("count", None), ("sum", v)]
+    fns = [F.get(f, [], [c.dtype] if c is not None else []) for f, c in aggs]
+    params = AggregatorParams([k.dtype], fns, enable_experimental_aggregate_hashtable=False,
+                              group_by_two_level_threshold=100)
+    p = _partial(params, [k], aggs, 0, n)
+    try:
+        metas = p.on_finish()
+        assert [m.bucket for m in metas] == [SINGLE_LEVEL_BUCKET]
+        bt = TransformPartitionBucket(params)
+        bt.push(metas)
+        parts = bt.finish()
+        gk, ga = _final_all(params, parts, 1, len(aggs))
+        ok, oa = oracle_aggregate([k], aggs, None, threads=8)
+        assert_results_equal(gk, ga, ok, oa)
+    finally:
+        p.close()

@@ -520,13 +520,15 @@ PART_CASES = [
     ("i32", 400_000, 3_300_000, 1 << 19, 3),
     ("i16", 65_536, 2_000_000, 1 << 19, 1),       # every i16 value, including -1 (all-ones key)
     ("u8", 256, 1_200_000, 1 << 19, 1),
+    ("i64", 600_000, 3_000_000, 1 << 26, 2),      # cap 2^27: two radix passes (8 + 7 bits); batch 2 into a used table
+    ("i64", 700_000, 2_000_000, 1 << 28, 1),      # cap 2^29: three radix passes (6 + 6 + 5 bits)
 ]
 
 
 @pytest.mark.parametrize("kind,distinct,n,hint,batches", PART_CASES, ids=lambda x: str(x))
 def test_partitioned_insert(kind, distinct, n, hint, batches):
-    """part.hip: radix-partitioned COUNT(*) insert (rocPRIM sort of mixed keys + one workgroup per
-    64 KB table slice in LDS).  Every batch holds >= 2^20 rows (the path's threshold); the
+    """part.hip: radix-partitioned COUNT(*) insert (the LSD radix partition of mixed keys + one
+    workgroup per 64 KB table slice in LDS).  Every batch holds >= 2^20 rows (the path's threshold); the
     sentinel key (all-ones), runs that leave a slice (overflow records -> agg_retry), growth,
     and several batches into one table are all covered."""
     rng = np.random.default_rng(distinct)

@@ -163,6 +163,15 @@ def test_errors_not_faults(dec):
         bad[j] = 0x7F
     with pytest.raises(DbgError):
         dec.decode(ColumnChunk(bytes(bad), chs.physical_type, chs.max_def_level, 0, chs.codec), target_of(ats))
+    # a Snappy literal whose 4-byte length is near 2^32: the bounds checks must not wrap (an
+    # out-of-bounds device write otherwise), the page is rejected as malformed
+    bad = bytearray(ch.data)
+    q = p.data_off
+    while bad[q] & 0x80:  # skip the uncompressed-length varint
+        q += 1
+    bad[q + 1:q + 6] = bytes([0xFC, 0xFE, 0xFF, 0xFF, 0xFF])
+    with pytest.raises(DbgError):
+        dec.decode(ColumnChunk(bytes(bad), ch.physical_type, ch.max_def_level, 0, ch.codec), target_of(at))
     # codecs the GPU does not take: the caller keeps the CPU reader
     with pytest.raises(Unsupported):
         dec.decode(ColumnChunk(ch.data, ch.physical_type, ch.max_def_level, 0, 6), target_of(at))  # ZSTD
