@@ -254,6 +254,8 @@ struct dbg_agg_handle {
         u8* alt = nullptr;
     } ppk[2];
     u32 pp_bits = 0;  // final partition bits
+    u32 pp_rc_sub = 0;  // > 0: record-centric aggregation in 2^pp_rc_sub rounds per partition (pp.hip)
+    u32* pp_spill = nullptr;  // [count, partition ids...] spilled by the record-centric kernel
     u32* pp_cnt = nullptr;
     u64 pp_cnt_cap = 0;
     u64* pp_off = nullptr;
@@ -872,7 +874,8 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
         for (void* q : kb)
             if (q) hipFree(q);
     }
-    void* pb[] = {h->pp_cnt, h->pp_off, h->pp_scan_tmp, h->pp_mid, h->pp_dchunks, h->pp_dc0, h->pp_tot, h->pp_set, h->pp_grec, h->pp_blk};
+    void* pb[] = {h->pp_cnt, h->pp_off, h->pp_scan_tmp, h->pp_mid, h->pp_dchunks, h->pp_dc0, h->pp_tot, h->pp_set, h->pp_grec, h->pp_blk,
+                  h->pp_spill};
     for (void* q : pb)
         if (q) hipFree(q);
     void* ph[] = {h->pp_hchunks, h->pp_hc0, h->pp_hpart, h->pp_htot};
@@ -1242,7 +1245,30 @@ static int pp_prepare(dbg_agg_handle* h) {
     u32 B = PP_L1_BITS + 1;
     while ((double)(1ULL << B) < need && B < PP_L1_BITS + 16) ++B;
     // level 2 takes up to 10 bits (one pass instead of a 1-2 bit third level), level 3 the rest
-    const u32 k2 = std::min<u32>(B - PP_L1_BITS <= 10 ? 10 : 8, B - PP_L1_BITS), k3 = B - PP_L1_BITS - k2;
+    u32 k2 = std::min<u32>(B - PP_L1_BITS <= 10 ? 10 : 8, B - PP_L1_BITS), k3 = B - PP_L1_BITS - k2;
+    // Record-centric aggregation (raw records only): one workgroup per level-2 partition (sized
+    // here for ~PP_RC_PART records on average), aggregated in 2^sub rounds of at most ~0.7 of one
+    // LDS round's records — no level 3.
+    h->pp_rc_sub = 0;
+    // measured slower than the slot-table kernel on C4 (pp_agg 74 vs 58 ms): opt-in (DBG_X_PPRC=1)
+    static const bool rc_on = getenv("DBG_X_PPRC") && getenv("DBG_X_PPRC")[0] == '1';
+    if (rc_on && pp_rc_ok(S) && nsr == 0 && nr > 0) {
+        const double per_part = (double)PP_RC_PART;
+        u32 b2 = PP_L1_BITS + 1;
+        while ((double)nr / (double)(1ULL << b2) > per_part && b2 < PP_L1_BITS + 10) ++b2;
+        const double avg = (double)nr / (double)(1ULL << b2);
+        const double round_cap = 0.7 * (double)pp_rc_records(S);
+        u32 sub = 0;
+        while (avg / (double)(1u << sub) > round_cap && sub < 5) ++sub;
+        // (a capacity hint asking for fewer partitions than this sizing — e.g. one group — keeps
+        // the slot-table kernel and its LDS overflow rounds)
+        if (avg <= per_part && avg / (double)(1u << sub) <= round_cap && B >= b2) {
+            B = b2;
+            k2 = B - PP_L1_BITS;
+            k3 = 0;
+            h->pp_rc_sub = std::max<u32>(sub, 1);  // >= 1 round bit: the flag doubles as "record-centric"
+        }
+    }
     h->pp_bits = B;
     for (int kind = 0; kind < 2; ++kind) {
         auto& K = h->ppk[kind];
@@ -1357,7 +1383,17 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     }
     auto& R = h->ppk[0];
     auto& T = h->ppk[1];
-    {
+    if (h->pp_rc_sub) {
+        constexpr u32 SPILL_CAP = 4096;
+        if (!h->pp_spill) RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + SPILL_CAP) * 4));
+        HIPCHECK(hipMemsetAsync(h->pp_spill, 0, 4, h->stream));
+        prof::Scope ps("pp_agg", h->stream);
+        launch_pp_agg_rc(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.part, R.fin, 64 - h->pp_bits - h->pp_rc_sub,
+                         h->pp_rc_sub, o, h->pp_spill, SPILL_CAP);
+        // partitions too large for it (skewed keys): the slot-table kernel, over the spilled ids only
+        launch_pp_agg(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.part, nullptr, R.fin, R.alt, nullptr, nullptr,
+                      o, h->pp_spill, SPILL_CAP);
+    } else {
         prof::Scope ps("pp_agg", h->stream);
         launch_pp_agg(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.l1_n ? R.part : nullptr,
                       T.l1_n ? T.part : nullptr, R.fin, R.alt, T.fin, T.alt, o);
@@ -1388,6 +1424,7 @@ static int pp_read_tot(dbg_agg_handle* h) {
     HIPCHECK(hipMemcpyAsync(h->pp_htot, h->pp_tot, PPT_WORDS * 8, hipMemcpyDeviceToHost, h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));
     h->pp_stat_rounds = h->pp_htot[PPT_ROUNDS];
+    if (h->pp_htot[PPT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "partitioned aggregate: spill list exhausted");
     return DBG_OK;
 }
 
@@ -1891,6 +1928,7 @@ static int pp_fin_complete(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* stri
     h->pp_grec_ready = S.has_strings != 0;
     h->finalized = h->pp_grec_ready;
     if (t[PPT_ERR] & ERR_DEC_OVERFLOW) return fail(DBG_ERR_OVERFLOW, "Decimal overflow");
+    if (t[PPT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "partitioned aggregate: spill list exhausted");
     RETURN_IF(check_minmax_spin(h));
     if (short_buf) return fail(DBG_ERR_INVALID, "output buffers too small: " + std::to_string(h->n_groups) + " groups");
     return DBG_OK;
@@ -2186,8 +2224,11 @@ static int legacy_layout(const Spec& S, u32 bits, LegacyLayout* L) {
     int kind = 0;
     uint32_t kb = 0;
     RETURN_IF(legacy_method(S.key_types, S.n_keys, &kind, &kb));
-    if (kind == DBG_LEGACY_SERIALIZER) return fail(DBG_ERR_UNSUPPORTED, "legacy HashMethodSerializer keys stay on the CPU path");
     L->bits = bits;
+    if (kind == DBG_LEGACY_SERIALIZER) {  // FastHash of the serialized key bytes (SerCrc, legacy.hpp)
+        L->serializer = 1;
+        return DBG_OK;
+    }
     if (kind == DBG_LEGACY_SINGLE_BINARY) {
         L->binary = 1;
         return DBG_OK;
@@ -2686,7 +2727,11 @@ int dbg_legacy_group_hash(const dbg_column* cols, int n, uint64_t rows, uint64_t
     if (kind == DBG_LEGACY_SINGLE_BINARY) {
         launch_legacy_binary_hash(s, dcol(cols[0]), rows, out_hash, out_bucket, (u32)bucket_bits);
     } else if (kind == DBG_LEGACY_SERIALIZER) {
-        return fail(DBG_ERR_UNSUPPORTED, "legacy HashMethodSerializer keys stay on the CPU path");
+        LegacyKeyDesc d;
+        memset(&d, 0, sizeof(d));
+        d.n = n;
+        for (int j = 0; j < n; ++j) d.cols[j] = dcol(cols[j]);  // key order: the serialized row
+        launch_legacy_serializer_hash(s, d, rows, out_hash, out_bucket, (u32)bucket_bits);
     } else {
         LegacyKeyDesc d;
         memset(&d, 0, sizeof(d));

@@ -410,7 +410,7 @@ __device__ __forceinline__ void maybe_flush(const Spec& S, const BatchDesc* batc
 template <bool INLINE, bool RECORDS>
 __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 bid, u64 rows, u64 rows_per_block, TableDesc t,
-                                                          u32 lds_slots) {
+                                                          u32 lds_slots, u32 lenq) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
@@ -439,24 +439,31 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
         // PU rounds of BLOCK rows are evaluated per step with all their loads issued together (one
         // row per lane per round, a single round in flight left the stream latency-bound: C5's
         // predicate pass ran at ~1.2 TB/s), queued together, and inserted BLOCK at a time.
-        constexpr int PU = 4;  // (PU + 1) KB of queue beside the 32 KB table: 4 workgroups per CU
+        // `s <op> ''` on one non-null String column (ClickBench Q13: SearchPhrase <> ''): the
+        // selection is a function of the row's length alone, read from the offsets; PU rounds of
+        // BLOCK rows are evaluated per step with all their offset loads issued together (one row
+        // per lane per round left C5's predicate pass latency-bound, ~1.2 TB/s)
+        constexpr int PU = 4;
         static_assert(FLUSH_ROUND % PU == 0, "flush checks fall on step boundaries");
-        __shared__ u32 selq[(PU + 1) * BLOCK];
+        __shared__ u32 selq[2 * BLOCK];
         __shared__ u32 qn;
         if (threadIdx.x == 0) qn = 0;
         __syncthreads();
         const u32 lane = __lane_id();
-        // `s <op> ''` on one non-null String column (ClickBench Q13: SearchPhrase <> ''): the
-        // selection is a function of the row's length alone, read from the offsets
         const DNode& n0 = B.nodes[0];
         const DCol& c0 = B.fcols[n0.col];
-        const bool lenpred = B.n_nodes == 1 && n0.op == DBG_PRED_CMP_CONST && n0.str_len == 0 && c0.type == DBG_STRING &&
-                             !c0.nullable && c0.layout == LAYOUT_ARROW;
-        const u64* __restrict__ offs = c0.offsets;
-        for (u64 it = 0; it < n_iter; it += PU) {
-            if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
-            bool sel[PU];
-            if (lenpred) {
+        // its (PU + 1)-round queue lives in dynamic LDS after the table (lenq entries, host-sized
+        // only for such a predicate: the other predicates keep the static 2-round queue and the
+        // occupancy it allows — C1: 6 workgroups per CU, all 1464 resident at once)
+        const bool lenpred = lenq >= (PU + 1) * BLOCK && B.n_nodes == 1 && n0.op == DBG_PRED_CMP_CONST && n0.str_len == 0 &&
+                             c0.type == DBG_STRING && !c0.nullable && c0.layout == LAYOUT_ARROW;
+        // the queue in use: the static one, or the multi-round one after the table (lenpred)
+        u32* qbuf = lenpred ? (u32*)(lds + (u64)lds_slots * sw + 2) : selq;
+        if (lenpred) {
+            u32* selq = qbuf;
+            const u64* __restrict__ offs = c0.offsets;
+            for (u64 it = 0; it < n_iter; it += PU) {
+                if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
                 u64 a[PU], b[PU];
 #pragma unroll
                 for (int k = 0; k < PU; ++k) {
@@ -465,53 +472,69 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
                     a[k] = gld<u64>(offs + j);
                     b[k] = gld<u64>(offs + j + 1);
                 }
+                bool sel[PU];
+                u32 cnt = 0;
+                u64 mk[PU];
 #pragma unroll
                 for (int k = 0; k < PU; ++k) {
                     const u64 i = r0 + (it + k) * BLOCK + threadIdx.x;
                     sel[k] = i < r1 && apply_cmp(n0.cmp, b[k] != a[k] ? 1 : 0);
+                    mk[k] = __ballot(sel[k]);
+                    cnt += (u32)__popcll(mk[k]);
                 }
-            } else {
+                if (cnt) {  // queue the step's selected rows: one LDS add per wave
+                    u32 wbase = 0;
+                    if (lane == 0) wbase = atomicAdd(&qn, cnt);
+                    wbase = __shfl(wbase, 0);
+                    const u64 lt = (1ULL << lane) - 1;
 #pragma unroll
-                for (int k = 0; k < PU; ++k) {
-                    const u64 i = r0 + (it + k) * BLOCK + threadIdx.x;
-                    sel[k] = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+                    for (int k = 0; k < PU; ++k) {
+                        if (sel[k]) selq[wbase + (u32)__popcll(mk[k] & lt)] = (u32)((it + k) * BLOCK + threadIdx.x);
+                        wbase += (u32)__popcll(mk[k]);
+                    }
                 }
-            }
-            // queue the step's selected rows: one LDS add per wave
-            u32 cnt = 0;
-            u64 mk[PU];
-#pragma unroll
-            for (int k = 0; k < PU; ++k) {
-                mk[k] = __ballot(sel[k]);
-                cnt += (u32)__popcll(mk[k]);
-            }
-            if (cnt) {
-                u32 wbase = 0;
-                if (lane == 0) wbase = atomicAdd(&qn, cnt);
-                wbase = __shfl(wbase, 0);
-                const u64 lt = (1ULL << lane) - 1;
-#pragma unroll
-                for (int k = 0; k < PU; ++k) {
-                    if (sel[k]) selq[wbase + (u32)__popcll(mk[k] & lt)] = (u32)((it + k) * BLOCK + threadIdx.x);
-                    wbase += (u32)__popcll(mk[k]);
-                }
-            }
-            __syncthreads();
-            const u32 n = qn;  // < (PU + 1) * BLOCK
-            if (n >= BLOCK) {
-                const u32 full = n / BLOCK;
-                for (u32 c = 0; c < full; ++c) insert_row(r0 + selq[c * BLOCK + threadIdx.x], my_claims);
-                const u32 rem = n - full * BLOCK;  // < BLOCK: moved to the front
-                const u32 mv = threadIdx.x < rem ? selq[full * BLOCK + threadIdx.x] : 0u;
                 __syncthreads();
-                if (threadIdx.x < rem) selq[threadIdx.x] = mv;
-                if (threadIdx.x == 0) qn = rem;
+                const u32 n = qn;  // < (PU + 1) * BLOCK
+                if (n >= BLOCK) {
+                    const u32 full = n / BLOCK;
+                    for (u32 c = 0; c < full; ++c) insert_row(r0 + selq[c * BLOCK + threadIdx.x], my_claims);
+                    const u32 rem = n - full * BLOCK;  // < BLOCK: moved to the front
+                    const u32 mv = threadIdx.x < rem ? selq[full * BLOCK + threadIdx.x] : 0u;
+                    __syncthreads();
+                    if (threadIdx.x < rem) selq[threadIdx.x] = mv;
+                    if (threadIdx.x == 0) qn = rem;
+                }
+                __syncthreads();  // the queue is settled before the next step appends
             }
-            __syncthreads();  // the queue is settled before the next step appends
+        } else {
+            for (u64 it = 0; it < n_iter; ++it) {
+                if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
+                const u64 i = r0 + it * BLOCK + threadIdx.x;
+                const bool sel = i < r1 && eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+                const u64 m = __ballot(sel);
+                if (m) {
+                    u32 wbase = 0;
+                    if (lane == 0) wbase = atomicAdd(&qn, (u32)__popcll(m));
+                    wbase = __shfl(wbase, 0);
+                    if (sel) selq[wbase + (u32)__popcll(m & ((1ULL << lane) - 1))] = (u32)(i - r0);
+                }
+                __syncthreads();
+                const u32 n = qn;  // < 2 * BLOCK
+                if (n >= BLOCK) {
+                    const u32 off = selq[threadIdx.x];
+                    const u32 rem = n - BLOCK;  // < BLOCK
+                    const u32 mv = threadIdx.x < rem ? selq[BLOCK + threadIdx.x] : 0u;
+                    __syncthreads();
+                    if (threadIdx.x < rem) selq[threadIdx.x] = mv;
+                    if (threadIdx.x == 0) qn = rem;
+                    insert_row(r0 + off, my_claims);
+                }
+                __syncthreads();  // the queue is settled before the next round appends
+            }
         }
         const u32 n = qn;  // < BLOCK
         if (threadIdx.x < n)
-            insert_row(r0 + selq[threadIdx.x], my_claims);
+            insert_row(r0 + qbuf[threadIdx.x], my_claims);
     } else {
         for (u64 it = 0; it < n_iter; ++it) {
             if (it && (it % FLUSH_ROUND) == 0) maybe_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, llimit, t, my_claims);
@@ -721,6 +744,30 @@ __global__ void __launch_bounds__(BLOCK) legacy_slot_bucket_kernel(const Spec* _
         if (L.binary) {
             const StrRef sr = dcol_str(batches[ref_bid(e)].keys[0], ref_row(e));
             h = legacy_bytes_hash(tab, sr.p, sr.len);
+        } else if (L.serializer) {
+            SerCrc sc;
+            const u64 key = s == t.cap ? SLOT_EMPTY : e;
+            for (int c = 0; c < S.n_keys; ++c) {
+                const dbg_datatype& ty = S.key_types[c];
+                bool v;
+                u64 lo = 0, hi = 0;
+                StrRef sr{nullptr, 0};
+                if (S.inline_keys) {
+                    v = !ty.nullable || ((key >> (8 * S.voff[c])) & 0xff) != 0;
+                    lo = (key >> (8 * S.koff[c])) & width_mask(type_width(ty.type));
+                } else {
+                    const DCol& kc = batches[ref_bid(e)].keys[c];
+                    const u64 row = ref_row(e);
+                    v = dcol_valid(kc, row);
+                    if (v && ty.type == DBG_STRING) sr = dcol_str(kc, row);
+                    else if (v) {
+                        lo = dcol_bits(kc, row);
+                        if (ty.type == DBG_DECIMAL128) hi = dcol_hi(kc, row);
+                    }
+                }
+                sc.column(tab, ty.type, ty.nullable, v, lo, hi, sr.p, sr.len);
+            }
+            h = sc.finish(tab);
         } else {
             u64 k[4] = {0, 0, 0, 0};
             const u64 key = s == t.cap ? SLOT_EMPTY : e;
@@ -1391,6 +1438,7 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
+        atomicExch((unsigned long long*)(t.counters + CNT_TAIL), 0ULL);  // every workgroup has left its tail
         bad = 0;
         vcl = 0;
         if (kPhaseTrace && ff.trace) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
@@ -1446,6 +1494,9 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
 // and stages the selected rows in the LDS table exactly like agg_insert.
 // ------------------------------------------------------------------------------------------
 #define FAST_UNROLL 4
+#ifndef TAIL_ON
+#define TAIL_ON 1  // dynamic stream tail of fused-chain launches (make TAIL=0: off, for A/B runs)
+#endif
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // Column data reached through a descriptor is a generic pointer to the compiler, which then
 // emits flat loads: those count against lgkmcnt too and retire out of order, so every LDS wait
@@ -1716,6 +1767,21 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
     u64 k = (u64)blockIdx.x * NT + threadIdx.x;
     const u64 step = (u64)FAST_UNROLL * gstride;
     const u64 lastv = nvec ? nvec - 1 : 0;
+    // Dynamic tail (fused-chain launches): the grid-strided static part covers ~80 % of the
+    // vectors in whole rounds of the grid; the rest is cut into chunks of NT x FAST_UNROLL vectors
+    // that workgroups done with their static share take from a device counter — so the chip's
+    // fast CUs absorb the end of the stream instead of waiting for its slow ones (workgroups
+    // finished streaming between 27.8 and 35.0 us of a C2 launch).  The counter
+    // (CNT_TAIL) is reset by the launch's last group leader.
+    constexpr u64 TAIL_CH = (u64)NT * FAST_UNROLL;
+    const bool dyn = TAIL_ON && ff.on && t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks;
+    u64 nstat = nvec, nch = 0;
+    if (dyn) {
+        nstat = ((nvec * 4 / 5) / step) * step;
+        nch = (nvec - nstat + TAIL_CH - 1) / TAIL_CH;
+    }
+    u64 tail_grab = 0;  // thread 0: the first tail chunk, taken now (its latency hides behind the stream)
+    if (dyn && nch && threadIdx.x == 0) tail_grab = atomicAdd((unsigned long long*)(t.counters + CNT_TAIL), 1ULL);
     // Software pipeline: the next round's FAST_UNROLL loads are issued before this round is
     // filtered and queued, so a wave busy with its ballots and LDS queue writes still has
     // 64 B/lane in flight (without it the per-round processing sits on the load critical path).
@@ -1723,28 +1789,76 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
 #pragma unroll
     for (int u = 0; u < FAST_UNROLL; ++u) {
         u64 idx = k + u * gstride;
-        y[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+        y[u] = __builtin_nontemporal_load(vp + (idx < nstat ? idx : lastv));
     }
-    while (__ballot(k < nvec) != 0) {
+    while (__ballot(k < nstat) != 0) {
         const u64 kn = k + step;
         v4u yn[FAST_UNROLL];
 #pragma unroll
         for (int u = 0; u < FAST_UNROLL; ++u) {
             u64 idx = kn + u * gstride;
-            yn[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+            yn[u] = __builtin_nontemporal_load(vp + (idx < nstat ? idx : lastv));
         }
         u64 bases[FAST_UNROLL];
         u32 actm = 0;
 #pragma unroll
         for (int u = 0; u < FAST_UNROLL; ++u) {
             u64 idx = k + u * gstride;
-            actm |= (idx < nvec ? 1u : 0u) << u;
+            actm |= (idx < nstat ? 1u : 0u) << u;
             bases[u] = idx * V;
         }
         handle_group(y, bases, FAST_UNROLL, actm);
 #pragma unroll
         for (int u = 0; u < FAST_UNROLL; ++u) y[u] = yn[u];
         k = kn;
+    }
+    if (dyn && nch) {
+        // chunk ids pass through LDS behind a bare s_barrier (no fence: the loads in flight are
+        // not drained); the next chunk's loads are issued, and the chunk after it taken, before
+        // the current chunk is filtered
+        __shared__ u32 tail_id[2];
+        auto load_chunk = [&](u32 c, v4u* yy) {
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                const u64 idx = nstat + (u64)c * TAIL_CH + (u64)u * NT + threadIdx.x;
+                yy[u] = __builtin_nontemporal_load(vp + (idx < nvec ? idx : lastv));
+            }
+        };
+        auto publish = [&](u32 slot, u64 v) -> u32 {
+            if (threadIdx.x == 0) tail_id[slot] = (u32)min<u64>(v, nch);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            return tail_id[slot];
+        };
+        u32 par = 0;
+        u32 cur = publish(par, tail_grab);
+        par ^= 1;
+        v4u yc[FAST_UNROLL];
+        if (cur < nch) {
+            load_chunk(cur, yc);
+            if (threadIdx.x == 0) tail_grab = atomicAdd((unsigned long long*)(t.counters + CNT_TAIL), 1ULL);
+        }
+        while (cur < nch) {
+            const u32 nxt = publish(par, tail_grab);
+            par ^= 1;
+            v4u yn[FAST_UNROLL];
+            if (nxt < nch) {
+                load_chunk(nxt, yn);
+                if (threadIdx.x == 0) tail_grab = atomicAdd((unsigned long long*)(t.counters + CNT_TAIL), 1ULL);
+            }
+            u64 bases[FAST_UNROLL];
+            u32 actm = 0;
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) {
+                const u64 idx = nstat + (u64)cur * TAIL_CH + (u64)u * NT + threadIdx.x;
+                actm |= (idx < nvec ? 1u : 0u) << u;
+                bases[u] = idx * V;
+            }
+            handle_group(yc, bases, FAST_UNROLL, actm);
+#pragma unroll
+            for (int u = 0; u < FAST_UNROLL; ++u) yc[u] = yn[u];
+            cur = nxt;
+        }
     }
     if (PRED && vqn) {
         __builtin_amdgcn_wave_barrier();
@@ -1873,12 +1987,20 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     u64 rpb = (rows + blocks - 1) / blocks;
     blocks = (rows + rpb - 1) / rpb;
     size_t shmem = (size_t)lslots * S.stride_words * 8 + 16;
+    // `string <op> ''` filter (one node on a non-null arrow String column): the kernel's
+    // multi-round queue (5 rounds of BLOCK row indices) after the table
+    u32 lenq = 0;
+    if (hb && !records && hb->n_nodes == 1 && hb->nodes[0].op == DBG_PRED_CMP_CONST && hb->nodes[0].str_len == 0) {
+        const DCol& c = hb->fcols[hb->nodes[0].col];
+        if (c.type == DBG_STRING && !c.nullable && c.layout == LAYOUT_ARROW) lenq = 5 * BLOCK;
+    }
+    shmem += (size_t)lenq * 4;
     if (S.inline_keys) {
-        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
-        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<true, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, lenq);
+        else hipLaunchKernelGGL((agg_insert_kernel<true, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, lenq);
     } else {
-        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
-        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        if (records) hipLaunchKernelGGL((agg_insert_kernel<false, true>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, lenq);
+        else hipLaunchKernelGGL((agg_insert_kernel<false, false>), dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots, lenq);
     }
 }
 

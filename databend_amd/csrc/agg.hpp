@@ -96,7 +96,8 @@ inline size_t scr_words(u32 blocks, u32 stride_words) {
 }
 #define DBG_INSERT_MAX_BLOCKS 2048  // grid cap of every insert launch (scratch rows are sized by it)
 
-enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_FIN_TICKET = 6, CNT_WORDS = 8 };
+enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_FIN_TICKET = 6,
+       CNT_TAIL = 7, CNT_WORDS = 8 };
 enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4, ERR_MINMAX_SPIN = 8 };
 
 // ---- device helpers shared by agg.hip and part.hip ----
@@ -362,8 +363,23 @@ struct CopyRange {
     u64 src, dst, n;  // byte offsets / length (multiples of 8)
 };
 void launch_copy_ranges(hipStream_t s, const u8* src, u8* dst, const CopyRange* dranges, u32 n);
+// plist (device): [count, partition ids...] — aggregate only those partitions (nullptr: all); plist_cap
+// bounds the count (grid size)
 void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
-                   const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out);
+                   const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out,
+                   const u32* plist = nullptr, u32 plist_cap = 0);
+// Record-centric aggregation (raw records only, <= PP_RC_W words): one workgroup per partition,
+// aggregated in 2^sub_bits LDS rounds by the hash bits [sub_shift, sub_shift + sub_bits) — a round's
+// records in LDS, a table of record indices, states beside the records.  A partition of more than
+// PP_RC_MAXN records, or with a round larger than one LDS table, is listed in spill ([count,
+// ids...], spill_cap ids at most) for launch_pp_agg.
+#define PP_RC_W 4
+#define PP_RC_PART 4096  // records per partition the level sizes aim at (PP_RC_MAXN = 8192 at most)
+u32 pp_rc_records(const Spec& hspec);  // records one LDS round holds
+bool pp_rc_ok(const Spec& hspec);
+void launch_pp_agg_rc(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
+                      const u64* raw_off, const u8* raw, u32 sub_shift, u32 sub_bits, const PPAggOut& out, u32* spill,
+                      u32 spill_cap);
 // group records -> result columns (deterministic positions: block sums, scan, write)
 void launch_pp_grec_lengths(hipStream_t s, const Spec* dspec, const u8* grec, const u64* n_dev, u64* blk_len /* [n_keys][blocks] */,
                             u64 nblocks, const BatchDesc* batches);

@@ -4,7 +4,7 @@
 // HashMethodKind::choose_hash_method_with_types (EXP/kernels/group_by.rs:48-97) picks
 //   SingleBinary for one String/Binary key, FixedKeys<T> when every key is a number, date,
 //   timestamp or decimal (T = u8 / u16 / u32 / u64 / u128 / U256 by the packed width: value bytes
-//   plus one null byte per nullable key), Serializer otherwise (not on this path: UNSUPPORTED).
+//   plus one null byte per nullable key), Serializer otherwise (the serialized key bytes, SerCrc).
 // FixedKeys packs a row (build_keys_vec / fixed_hash, EXP/kernels/group_by_hash/
 // method_fixed_keys.rs:74-100, 366-470): columns stably sorted by byte width, widest first, values
 // little-endian from offset 0, each nullable column's null byte after all the values (1 = NULL, the
@@ -54,6 +54,30 @@ __global__ void __launch_bounds__(256) legacy_binary_hash_kernel(DCol c, u64 row
     }
 }
 
+// HashMethodSerializer: d.cols in key order (d.n columns), hashed as their serialized bytes
+__global__ void __launch_bounds__(256) legacy_serializer_hash_kernel(LegacyKeyDesc d, u64 rows, u64* __restrict__ hash,
+                                                                    u32* __restrict__ bucket, u32 bits) {
+    __shared__ u32 tab[256];
+    crc_table_init(tab);
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < rows; i += (u64)gridDim.x * blockDim.x) {
+        SerCrc sc;
+        for (int j = 0; j < d.n; ++j) {
+            const DCol& c = d.cols[j];
+            const bool v = dcol_valid(c, i);
+            if (c.type == DBG_STRING) {
+                const StrRef sr = v ? dcol_str(c, i) : StrRef{nullptr, 0};
+                sc.column(tab, c.type, c.nullable, v, 0, 0, sr.p, sr.len);
+            } else {
+                const u64 lo = v ? dcol_bits(c, i) : 0, hi = (v && c.type == DBG_DECIMAL128) ? dcol_hi(c, i) : 0;
+                sc.column(tab, c.type, c.nullable, v, lo, hi, nullptr, 0);
+            }
+        }
+        const u64 h = sc.finish(tab);
+        hash[i] = h;
+        if (bucket) bucket[i] = legacy_bucket(h, bits);
+    }
+}
+
 static u32 grid_of(u64 rows) {
     u64 b = (rows + 255) / 256;
     return (u32)(b > 8192 ? 8192 : (b ? b : 1));
@@ -67,4 +91,9 @@ void launch_legacy_fixed_hash(hipStream_t s, const LegacyKeyDesc& d, u64 rows, u
 void launch_legacy_binary_hash(hipStream_t s, const DCol& c, u64 rows, u64* hash, u32* bucket, u32 bits) {
     if (!rows) return;
     hipLaunchKernelGGL(legacy_binary_hash_kernel, dim3(grid_of(rows)), dim3(256), 0, s, c, rows, hash, bucket, bits);
+}
+
+void launch_legacy_serializer_hash(hipStream_t s, const LegacyKeyDesc& d, u64 rows, u64* hash, u32* bucket, u32 bits) {
+    if (!rows) return;
+    hipLaunchKernelGGL(legacy_serializer_hash_kernel, dim3(grid_of(rows)), dim3(256), 0, s, d, rows, hash, bucket, bits);
 }

@@ -18,6 +18,7 @@ struct LegacyKeyDesc {
 // SingleBinary (binary = 1).  Buckets are hash2bucket<bits, true>.
 struct LegacyLayout {
     int32_t binary;
+    int32_t serializer;  // HashMethodSerializer: FastHash of the serialized key bytes
     u32 words;
     u32 bits;
     u32 off[DBG_MAX_KEYS];
@@ -70,7 +71,70 @@ __device__ __forceinline__ u64 legacy_bytes_hash(const u32* tab, const u8* p, u6
     return crc;
 }
 
+// HashMethodSerializer (EXP/kernels/group_by_hash/method_serializer.rs:39-70): the key is the
+// serialize_column_binary bytes of every group column in order (utils.rs:64-121): a nullable
+// column's validity byte, then — valid rows only — the value: numbers / Date / Timestamp
+// little-endian in their width, Decimal128 16 bytes, Boolean one byte, String its length as u64
+// then its bytes.  The [u8] FastHash of that byte string, fed incrementally (8-byte words, the last
+// one zero-padded, empty -> u64::MAX), equals legacy_bytes_hash of the concatenation.
+struct SerCrc {
+    u32 crc = 0xFFFFFFFFu;
+    u64 w = 0;
+    u32 n = 0;  // bytes in w (< 8)
+    u64 total = 0;
+    __device__ __forceinline__ void push(const u32* tab, u64 v, u32 nb) {  // nb in 1..8: v's low bytes
+        total += nb;
+        if (nb < 8) v &= (1ULL << (8 * nb)) - 1;
+        w |= n ? (v << (8 * n)) : v;
+        const u32 room = 8 - n;
+        if (nb < room) {
+            n += nb;
+            return;
+        }
+        crc = crc32c_u64(tab, crc, w);
+        const u32 rest = nb - room;
+        w = rest ? (v >> (8 * room)) : 0;
+        n = rest;
+    }
+    __device__ __forceinline__ void bytes(const u32* tab, const u8* p, u64 len) {
+        u64 o = 0;
+        for (; o + 8 <= len; o += 8) {
+            u64 x = 0;
+            for (int b = 0; b < 8; ++b) x |= (u64)gld<u8>(p + o + b) << (8 * b);
+            push(tab, x, 8);
+        }
+        if (o < len) {
+            u64 x = 0;
+            for (u64 b = 0; b < len - o; ++b) x |= (u64)gld<u8>(p + o + b) << (8 * b);
+            push(tab, x, (u32)(len - o));
+        }
+    }
+    // one key column: validity byte (nullable), then the value of a valid row
+    __device__ __forceinline__ void column(const u32* tab, int type, bool nullable, bool valid, u64 lo, u64 hi, const u8* sp,
+                                           u64 slen) {
+        if (nullable) push(tab, valid ? 1 : 0, 1);
+        if (!valid) return;
+        if (type == DBG_STRING) {
+            push(tab, slen, 8);
+            bytes(tab, sp, slen);
+        } else if (type == DBG_BOOLEAN) {
+            push(tab, lo & 1, 1);
+        } else if (type == DBG_DECIMAL128) {
+            push(tab, lo, 8);
+            push(tab, hi, 8);
+        } else {
+            push(tab, lo, type_width(type));
+        }
+    }
+    __device__ __forceinline__ u64 finish(const u32* tab) {
+        if (!total) return ~0ULL;
+        if (n) crc = crc32c_u64(tab, crc, w);
+        return crc;
+    }
+};
+
 __device__ __forceinline__ u32 legacy_bucket(u64 h, u32 bits) { return (u32)((h >> (32 - bits)) & ((1ULL << bits) - 1)); }
 
 void launch_legacy_fixed_hash(hipStream_t s, const LegacyKeyDesc& d, u64 rows, u64* hash, u32* bucket, u32 bits);
 void launch_legacy_binary_hash(hipStream_t s, const DCol& c, u64 rows, u64* hash, u32* bucket, u32 bits);
+void launch_legacy_serializer_hash(hipStream_t s, const LegacyKeyDesc& d, u64 rows, u64* hash, u32* bucket, u32 bits);

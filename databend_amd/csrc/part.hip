@@ -30,7 +30,7 @@
 
 #include "agg.hpp"
 
-#define PART_NT 1024
+#define PART_NT_DEFAULT 512  // slice-kernel workgroup: 48 KB of LDS, three per CU (DBG_X_SLICE_NT=1024: two)
 #define PART_SB 12  // slice = 4096 slots x 16 B = 64 KB of LDS
 #define PART_PROBE_CAP 64
 #define PART_OVF_LDS 512  // overflow keys gathered per workgroup before one device atomic
@@ -41,11 +41,7 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // LSD radix partition of m = slot_mix(key) on bits [sb, log2 cap) — 1 to 3 passes of <= 8 bits
 // ---------------------------------------------------------------------------------------------
-#define RP_NT 512                      // threads per scatter workgroup (2 per CU: 72 KB of LDS each)
-#define RP_IPT 16                      // rows per thread and tile
-#define RP_TILE (RP_NT * RP_IPT)       // 8192 rows per tile
-#define RP_WAVES (RP_NT / 64)
-#define RP_WROWS (64 * RP_IPT)         // rows of one wave's share of a tile
+// scatter tile shapes (threads x rows per thread) are template parameters; rp_shape() picks one
 #define RP_MAXP 3
 #define RP_HIST_NT 256
 #define RP_HIST_BLOCKS 2048
@@ -125,10 +121,11 @@ __device__ __forceinline__ u64 scan256(u64 v, u64* tmp) {
 // predecessors are running or done when it looks back (no circular wait).  Rows keep their
 // relative order within a digit (LSD needs a stable pass): a wave ranks its 16 rounds of 64
 // rows in order, lanes ranked among equal digits by ballot, wave counts prefixed in wave order.
-template <int W, bool RAW>
+template <int W, bool RAW, int RP_NT, int RP_IPT>
 __global__ void __launch_bounds__(RP_NT) rp_scatter_kernel(const u8* __restrict__ src, u64 rows, u32 shift, u32 bits,
                                                            const u32* __restrict__ hist, u64* __restrict__ status,
                                                            u32* __restrict__ tile_ctr, u64* __restrict__ dst) {
+    constexpr int RP_TILE = RP_NT * RP_IPT, RP_WAVES = RP_NT / 64, RP_WROWS = 64 * RP_IPT;
     __shared__ __attribute__((aligned(16))) u64 stage[RP_TILE];
     __shared__ u32 wcnt[RP_WAVES][256];  // per wave: digit counts, then their exclusive prefix over waves
     __shared__ u32 lstart[256];           // tile-local start of every digit
@@ -137,10 +134,18 @@ __global__ void __launch_bounds__(RP_NT) rp_scatter_kernel(const u8* __restrict_
     __shared__ u64 scan_tmp[16];
     const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u32 nb = 1u << bits, dmask = nb - 1;
+    const u32 ntiles = (u32)((rows + RP_TILE - 1) / RP_TILE);
+    // persistent: each workgroup takes tiles in order from the counter, the next one while it
+    // works on the current (the grab's latency off the tile's critical path); tiles only ever
+    // wait on smaller tiles, so holding a not-yet-started tile cannot deadlock
     if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    u32 tile = s_tile;
+    while (tile < ntiles) {
+    u32 next_tile = 0;
+    if (tid == 0) next_tile = atomicAdd(tile_ctr, 1u);
     for (u32 i = tid; i < RP_WAVES * 256; i += RP_NT) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const u32 tile = s_tile;
     const u64 base = (u64)tile * RP_TILE;
     const u64 e0 = base + (u64)w * RP_WROWS + lane;  // this lane's row of round 0
     u64 m[RP_IPT];
@@ -232,6 +237,10 @@ __global__ void __launch_bounds__(RP_NT) rp_scatter_kernel(const u8* __restrict_
         const u32 d = (u32)(v >> shift) & dmask;
         dst[gstart[d] + (j - lstart[d])] = v;
     }
+    if (tid == 0) s_tile = next_tile;
+    __syncthreads();  // stage / lstart / gstart are rewritten by the next tile
+    tile = s_tile;
+    }
 }
 
 __device__ __forceinline__ u64 bucket_of(u64 m, u64 mask, u32 sb) { return (m & mask) >> sb; }
@@ -258,7 +267,7 @@ typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 // them: one memory latency per workgroup, not one per load.
 // EMPTY: the table holds no group and was not initialised (a deferred reset): the slice starts
 // as EMPTY entries with zero counts in LDS, and the kernel writes every slot of it.
-template <int SB, bool EMPTY>
+template <int SB, bool EMPTY, int PART_NT>
 __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restrict__ sorted, const u64* __restrict__ bounds,
                                                              TableDesc t) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
@@ -272,9 +281,12 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     const u64 s0 = b * S;
     const u64 mask = t.cap - 1;
     const u64 lo = bounds[b], hi = bounds[b + 1];
-    // slice -> LDS (16-byte loads; the slot stride is 2 words)
+    // slice -> LDS: keys [S] u64, then this launch's counts [S] u32 (a slice receives < 2^32 rows;
+    // the table's own counts stay in registers and are added back at write-out), 48 KB: three
+    // workgroups per CU
     const v2u64 __attribute__((address_space(1)))* gsl = (const v2u64 __attribute__((address_space(1)))*)(t.slots + s0 * 2);
-    v2u64* lsl = (v2u64*)lds;
+    u64* lkey = lds;
+    u32* lcnt = (u32*)(lds + S);
     v2u64 sv[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -291,7 +303,10 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     for (int k = 0; k < RB; ++k) cur[k] = src[min<u64>(r + (u64)k * PART_NT, last)];
     if (threadIdx.x == 0) lclaims = novf = 0;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) lsl[threadIdx.x + k * PART_NT] = sv[k];
+    for (int k = 0; k < PER; ++k) {
+        lkey[threadIdx.x + k * PART_NT] = sv[k].x;
+        lcnt[threadIdx.x + k * PART_NT] = 0;
+    }
     __syncthreads();
     u32 my_claims = 0;
     auto push_rec = [&](u64 key) {
@@ -314,7 +329,7 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
         const u32 lim = (u32)min<u64>(S, (u64)ls + PART_PROBE_CAP);
         int st = key == SLOT_EMPTY ? 2 : 0;  // 0 probing, 1 found at ls, 2 sentinel key, 3 overflow
         while (st == 0) {
-            wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)ls * 2);
+            wptr<AS_LDS> e = asp<AS_LDS>(lkey + ls);
             u64 ev = *e;
             if (ev == SLOT_EMPTY) {
                 const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
@@ -325,7 +340,7 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
             else if (++ls >= lim) st = 3;
         }
         if (st == 1) {
-            at_add<AS_LDS>(asp<AS_LDS>(lds + (u64)ls * 2 + 1), 1ULL);
+            __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)(lcnt + ls), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (st == 2) {  // the sentinel slot (index cap) is outside every slice
             wptr<AS_GLB> sent = asp<AS_GLB>(t.slots + t.cap * 2);
             u64 old = at_cas<AS_GLB>(sent, SLOT_EMPTY, 0ULL);
@@ -375,7 +390,10 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     }
     v2u64 __attribute__((address_space(1)))* osl = (v2u64 __attribute__((address_space(1)))*)(t.slots + s0 * 2);
 #pragma unroll
-    for (int k = 0; k < PER; ++k) osl[threadIdx.x + k * PART_NT] = lsl[threadIdx.x + k * PART_NT];
+    for (int k = 0; k < PER; ++k) {
+        const u32 i = threadIdx.x + k * PART_NT;
+        osl[i] = v2u64{lkey[i], sv[k].y + (u64)lcnt[i]};
+    }
     if (threadIdx.x == 0 && lclaims) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lclaims);
 }
 
@@ -454,7 +472,23 @@ RadixPlan rp_plan(u32 sb, u64 cap) {
     return P;
 }
 
-u64 rp_tiles(u64 rows) { return (rows + RP_TILE - 1) / RP_TILE; }
+// scatter tile shape: (threads, rows per thread); DBG_X_RP="NT,IPT" overrides it (experiments)
+struct RpShape {
+    int nt, ipt;
+};
+RpShape rp_shape() {
+    static RpShape sh = [] {
+        RpShape r{512, 16};
+        if (const char* e = getenv("DBG_X_RP")) {
+            int a = 0, b = 0;
+            if (sscanf(e, "%d,%d", &a, &b) == 2) r = RpShape{a, b};
+        }
+        return r;
+    }();
+    return sh;
+}
+u64 rp_tile_rows() { return (u64)rp_shape().nt * rp_shape().ipt; }
+u64 rp_tiles(u64 rows) { return (rows + rp_tile_rows() - 1) / rp_tile_rows(); }
 
 // temp layout: [alt rows u64][status tiles x 256 u64][hist RP_MAXP x 256 u32][tile counters RP_MAXP u32]
 size_t rp_status_off(u64 rows) { return (size_t)rows * 8; }
@@ -490,14 +524,25 @@ hipError_t rp_sort(hipStream_t s, int width, const u8* keys, u64 rows, const Rad
         u64* dst = ((P.npass - 1 - p) % 2 == 0) ? out : alt;
         const u8* src = p == 0 ? keys : (const u8*)(((P.npass - p) % 2 == 0) ? out : alt);
         if ((e = hipMemsetAsync(status, 0, (size_t)tiles * 256 * 8, s)) != hipSuccess) return e;
-        const dim3 g((u32)tiles), b(RP_NT);
+        const dim3 g((u32)std::min<u64>(tiles, 2 * 256));  // persistent: two workgroups per CU
         u32* h = hist + p * 256;
         u32* tc = ctr + p;
-        if (p > 0) hipLaunchKernelGGL((rp_scatter_kernel<8, false>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
-        else if (width == 1) hipLaunchKernelGGL((rp_scatter_kernel<1, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
-        else if (width == 2) hipLaunchKernelGGL((rp_scatter_kernel<2, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
-        else if (width == 4) hipLaunchKernelGGL((rp_scatter_kernel<4, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
-        else hipLaunchKernelGGL((rp_scatter_kernel<8, true>), g, b, 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst);
+        const RpShape sh = rp_shape();
+#define RP_GO(WW, RAWF, NTT, IPTT) \
+    hipLaunchKernelGGL((rp_scatter_kernel<WW, RAWF, NTT, IPTT>), g, dim3(NTT), 0, s, src, rows, P.shift[p], P.bits[p], h, status, tc, dst)
+#define RP_SHAPES(WW, RAWF)                                                      \
+    if (sh.nt == 1024 && sh.ipt == 8) RP_GO(WW, RAWF, 1024, 8);                   \
+    else if (sh.nt == 256 && sh.ipt == 16) RP_GO(WW, RAWF, 256, 16);              \
+    else if (sh.nt == 512 && sh.ipt == 8) RP_GO(WW, RAWF, 512, 8);                \
+    else if (sh.nt == 256 && sh.ipt == 32) RP_GO(WW, RAWF, 256, 32);              \
+    else RP_GO(WW, RAWF, 512, 16);
+        if (p > 0) { RP_SHAPES(8, false) }
+        else if (width == 1) { RP_SHAPES(1, true) }
+        else if (width == 2) { RP_SHAPES(2, true) }
+        else if (width == 4) { RP_SHAPES(4, true) }
+        else { RP_SHAPES(8, true) }
+#undef RP_SHAPES
+#undef RP_GO
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -546,12 +591,16 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
                        n_slices, bounds);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_slice";
-    if (table_empty)
-        hipLaunchKernelGGL((part_slice_kernel<PART_SB, true>), dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << PART_SB), s,
-                           sorted, bounds, t);
-    else
-        hipLaunchKernelGGL((part_slice_kernel<PART_SB, false>), dim3((u32)n_slices), dim3(PART_NT), (size_t)(16ULL << PART_SB), s,
-                           sorted, bounds, t);
+    static const int slice_nt = getenv("DBG_X_SLICE_NT") ? atoi(getenv("DBG_X_SLICE_NT")) : PART_NT_DEFAULT;
+    const size_t sh = (size_t)(12ULL << PART_SB);
+#define SLICE_GO(EM, NTT) \
+    hipLaunchKernelGGL((part_slice_kernel<PART_SB, EM, NTT>), dim3((u32)n_slices), dim3(NTT), sh, s, sorted, bounds, t)
+    if (slice_nt == 1024) {
+        if (table_empty) SLICE_GO(true, 1024); else SLICE_GO(false, 1024);
+    } else {
+        if (table_empty) SLICE_GO(true, 512); else SLICE_GO(false, 512);
+    }
+#undef SLICE_GO
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_fixup";
     hipLaunchKernelGGL(part_fixup_kernel, dim3(512), dim3(256), 0, s, t);

@@ -1244,9 +1244,14 @@ __device__ __forceinline__ void pp_store_rec(u8* dst, const R& rk, u32 rw) {
 template <int MODE, int W>
 __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 n_parts, const u64* __restrict__ raw_off, const u64* __restrict__ st_off,
-                                                          u8* raw, u8* raw_alt, u8* st, u8* st_alt, u32 cap, PPAggOut out) {
+                                                          u8* raw, u8* raw_alt, u8* st, u8* st_alt, u32 cap, PPAggOut out,
+                                                          const u32* __restrict__ plist) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     const Spec& S = *spec;
+    // plist: aggregate only the partitions plist[1 .. plist[0]] (those the record-centric kernel
+    // spilled), numbered 0 .. plist[0] - 1 here
+    if (plist) n_parts = min(n_parts, plist[0]);
+    auto pid = [&](u32 q) -> u32 { return plist ? plist[1 + q] : q; };
     const u32 sw = S.pp_sw, kw8 = S.pp_kw / 8, rwr = S.pp_rw_raw, rws = S.pp_rw_state;
     l64* slots = (l64*)lds_raw;
     l16* list = (l16*)(slots + (size_t)cap * sw);
@@ -1263,8 +1268,8 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     constexpr int AU = W > 0 ? (W <= 2 ? 2 : 1) : 1;
     typedef RegRec<(W > 0 ? W : 1)> Tile[AU];
     auto part_range = [&](u32 q, u64& o0, u64& n) {
-        o0 = (raw_off && q < n_parts) ? raw_off[q] : 0;
-        n = (raw_off && q < n_parts) ? raw_off[q + 1] - o0 : 0;
+        o0 = (raw_off && q < n_parts) ? raw_off[pid(q)] : 0;
+        n = (raw_off && q < n_parts) ? raw_off[pid(q) + 1] - o0 : 0;
     };
     auto load_tile = [&](RegRec<(W > 0 ? W : 1)>* rr, const u8* src, u64 o0, u64 n, u64 base) {
         if constexpr (W > 0) {
@@ -1288,14 +1293,15 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     __syncthreads();
     const bool tr = kPhaseTrace && out.trace && (blockIdx.x & 63) == 0 && threadIdx.x == 0;
     u64 tm0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
-    auto run_part = [&](u32 p, Tile& buf, u64& br0, u64& bnr) {
+    auto run_part = [&](u32 q, Tile& buf, u64& br0, u64& bnr) {
+        const u32 p = pid(q);
         const u64 r0 = br0, s0 = st_off ? st_off[p] : 0;
         u64 nr = bnr, ns = st_off ? st_off[p + 1] - s0 : 0;
         u8 *rin = raw, *rout = raw_alt, *sin = st, *sout = st_alt;
         Tile cur;
 #pragma unroll
         for (int u = 0; u < AU; ++u) cur[u] = buf[u];
-        part_range(p + 2 * gridDim.x, br0, bnr);  // the buffer's next partition, loaded now
+        part_range(q + 2 * gridDim.x, br0, bnr);  // the buffer's next partition, loaded now
         load_tile(buf, raw, br0, bnr, 0);
         for (int round = 0;; ++round) {
             auto raw_one = [&](const auto& rk) {
@@ -1372,17 +1378,233 @@ __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restric
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Record-centric aggregation of raw records (mostly-unique keys, ClickBench Q33).  The slot
+// table above claims a slot per group — CAS, key copy, state init, publish, list append, and
+// readers spinning on the publish — which for ~one record per group is all overhead.  Here a
+// round's records sit in LDS first; a table of record indices (u32, 0 = empty) groups them: a
+// record whose CAS wins leads its group, one that finds an equal key (compared in LDS, already
+// there: no publish to wait for) joins that group; every record adds its contribution into the
+// leader's state words, kept beside the records.  Leaders are then written out in LDS order.
+// One workgroup per partition holds the partition's records in registers (PP_RC_RPT per thread)
+// and aggregates it in 2^sub_bits rounds by the next hash bits, so partitions are 2^sub_bits
+// times larger than one LDS table and the level-3 scatter disappears.
+// ------------------------------------------------------------------------------------------
+#define PP_RC_LDS (72 * 1024)  // two workgroups per CU
+static u32 rc_tcap(u32 n) {
+    u32 t = 64;
+    while (t < 2 * n) t <<= 1;
+    return t;
+}
+#define PP_RC_MAXN 8192  // records of one partition (its round bytes)
+u32 pp_rc_records(const Spec& S) {
+    const u32 per = 8 * (S.pp_rw_raw / 8) + 8 * (u32)S.n_words + 1 + 8;  // record + states + leader flag + 2 tags
+    const u32 budget = PP_RC_LDS - 256 - PP_RC_MAXN;
+    u32 n = budget / per;
+    while (n > 64 && n * (8 * (S.pp_rw_raw / 8) + 8 * (u32)S.n_words + 1) + 4 * rc_tcap(n) > budget) --n;
+    return n;
+}
+bool pp_rc_ok(const Spec& S) { return !S.pp_str && S.pp_rw_raw / 8 <= PP_RC_W && S.pp_rw_raw % 8 == 0; }
+
+template <int W>
+__device__ __forceinline__ bool rc_key_eq(const Spec& S, const RegRec<W>& a, const l64* b, u32 kw8) {
+    bool eq = true;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        if ((u32)w + 1 < kw8) eq &= a.r[w] == b[w];
+        else if ((u32)w + 1 == kw8) eq &= ((a.r[w] ^ b[w]) & S.pp_klast_mask) == 0;
+    }
+    return eq;
+}
+
+template <int MODE, int W>
+__global__ void __launch_bounds__(PP_AGG_NT) pp_agg_rc_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                             u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
+                                                             u32 sub_shift, u32 sub_bits, u32 rcap, u32 tcap, PPAggOut out,
+                                                             u32* __restrict__ spill, u32 spill_cap) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    const Spec& S = *spec;
+    const u32 kw8 = S.pp_kw / 8, nw = (u32)S.n_words;
+    l64* recs = (l64*)lds_raw;                       // [rcap][W]
+    l64* acc = recs + (size_t)rcap * W;              // [rcap][nw]
+    l32* tags = (l32*)(acc + (size_t)rcap * nw);     // [tcap]
+    l8* lead = (l8*)(tags + tcap);                   // [rcap]
+    l8* subid = lead + rcap;                         // [PP_RC_MAXN] round of every record of the partition
+    __shared__ u32 cnt, nlead, rcnt[32];
+    __shared__ u32 wsum[PP_AGG_NT / 64];
+    __shared__ u64 gbase;
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u32 smask = (1u << sub_bits) - 1;
+    auto spill_part = [&](u32 p) {
+        const u32 k = atomicAdd(spill, 1u);
+        if (k < spill_cap) spill[1 + k] = p;
+        else atomicOr((unsigned long long*)(out.tot + PPT_ERR), (unsigned long long)ERR_OVF_LOST);
+    };
+    for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
+        const u64 o0 = raw_off[p], n = raw_off[p + 1] - o0;
+        const u8* base = raw + o0 * (8 * W);
+        if (n > PP_RC_MAXN) {  // larger than the round table can index: the slot-table kernel
+            if (tid == 0) spill_part(p);
+            continue;
+        }
+        // every record's round (hash bits below the partition's), counted per round
+        if (tid < 32) rcnt[tid] = 0;
+        __syncthreads();
+        for (u32 i = tid; i < (u32)n; i += PP_AGG_NT) {
+            RegRec<W> rk;
+#pragma unroll
+            for (int w = 0; w < W; ++w) rk.r[w] = gld<u64>(base + (u64)i * (8 * W) + 8 * w);
+            const u32 sb = (u32)(pp_mix(pp_hash_of(S, rk)) >> sub_shift) & smask;
+            subid[i] = (u8)sb;
+            atomicAdd(&rcnt[sb], 1u);
+        }
+        __syncthreads();
+        u32 mx = 0;
+        for (u32 x = 0; x <= smask; ++x) mx = max(mx, rcnt[x]);
+        if (mx > rcap) {  // a round does not fit one LDS table: decided before any group is written
+            if (tid == 0) spill_part(p);
+            __syncthreads();
+            continue;
+        }
+        for (u32 sb = 0; sb <= smask; ++sb) {
+            if (tid == 0) cnt = nlead = 0;
+            for (u32 j = tid; j < tcap; j += PP_AGG_NT) tags[j] = 0;
+            __syncthreads();
+            // this round's records -> LDS (re-read: the partition was just streamed, L2 / MALL)
+            for (u32 i = tid; i < (u32)n; i += PP_AGG_NT) {
+                if (subid[i] != sb) continue;
+                const u32 k = atomicAdd(&cnt, 1u);
+#pragma unroll
+                for (int w = 0; w < W; ++w) recs[(size_t)k * W + w] = gld<u64>(base + (u64)i * (8 * W) + 8 * w);
+                for (u32 w = 0; w < nw; ++w) acc[(size_t)k * nw + w] = S.slot_init[1 + w];
+                lead[k] = 0;
+            }
+            __syncthreads();
+            const u32 m = cnt;  // <= rcap (checked above)
+            // group: the table holds record indices + 1; placement mixes the key words only
+            for (u32 me = tid; me < m; me += PP_AGG_NT) {
+                RegRec<W> rk;
+#pragma unroll
+                for (int w = 0; w < W; ++w) rk.r[w] = recs[(size_t)me * W + w];
+                u64 hm = 0;
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if ((u32)w < kw8) hm = slot_mix(hm ^ ((u32)w + 1 == kw8 ? rk.r[w] & S.pp_klast_mask : rk.r[w]));
+                u32 pos = (u32)hm & (tcap - 1);
+                u32 leader = me;
+                for (u32 probe = 0; probe < tcap; ++probe) {
+                    u32 old = 0;
+                    __hip_atomic_compare_exchange_strong(tags + pos, &old, me + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (old == 0) {
+                        lead[me] = 1;
+                        break;
+                    }
+                    if (rc_key_eq<W>(S, rk, recs + (size_t)(old - 1) * W, kw8)) {
+                        leader = old - 1;
+                        break;
+                    }
+                    pos = (pos + 1) & (tcap - 1);
+                }
+                pp_apply_rec(S, (wptr<AS_LDS>)(acc + (size_t)leader * nw) - 1, rk);
+            }
+            __syncthreads();
+            u32 mine = 0;
+            for (u32 j = tid; j < m; j += PP_AGG_NT) mine += lead[j];
+            if (mine) atomicAdd(&nlead, mine);
+            __syncthreads();
+            if (tid == 0) gbase = nlead ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlead) : 0;
+            __syncthreads();
+            // leaders out in slot order: row = gbase + leaders among smaller slots
+            u32 carry = 0;
+            for (u32 j0 = 0; j0 < m; j0 += PP_AGG_NT) {
+                const u32 j = j0 + tid;
+                const bool isl = j < m && lead[j];
+                const u64 bl = __ballot(isl);
+                if (lane == 0) wsum[wv] = (u32)__popcll(bl);
+                __syncthreads();
+                u32 before = carry, all = 0;
+                for (u32 x = 0; x < PP_AGG_NT / 64; ++x) {
+                    if (x < wv) before += wsum[x];
+                    all += wsum[x];
+                }
+                before += (u32)__popcll(bl & ((1ULL << lane) - 1));
+                if (isl) {
+                    const u64 row = gbase + before;
+                    const l64* kp = recs + (size_t)j * W;
+                    const u64* st = (const u64*)(acc + (size_t)j * nw) - 1;  // st[w0] = first state word
+                    if (MODE == 0) {
+                        if (row < out.cols.cap_groups) {
+                            const l8* k = (const l8*)kp;
+                            for (int c = 0; c < S.n_keys; ++c) {
+                                const dbg_datatype& t = S.key_types[c];
+                                const u32 wd = type_width(t.type);
+                                const bool v = !t.nullable || k[S.voff[c]] != 0;
+                                u64 lo = 0, hi = 0;
+                                if (t.type == DBG_DECIMAL128) {
+                                    lo = lget(k, S.koff[c], 8);
+                                    hi = lget(k, S.koff[c] + 8, 8);
+                                } else {
+                                    lo = lget(k, S.koff[c], wd);
+                                }
+                                write_bytes(out.cols.key_data[c], row, wd, lo, hi);
+                                if (out.cols.key_valid[c]) out.cols.key_valid[c][row] = v ? 1 : 0;
+                            }
+                            for (int a = 0; a < S.n_aggs; ++a) write_agg(S, a, st, row, out.cols, out.tot + PPT_ERR);
+                        }
+                    } else if (row < out.grec_cap) {
+                        u64* d = (u64*)(out.grec + row * S.pp_rw_state);
+                        for (u32 w = 0; w < kw8; ++w) d[w] = (w + 1 == kw8) ? (kp[w] & S.pp_klast_mask) : kp[w];
+                        for (u32 w = 0; w < nw; ++w) d[kw8 + w] = acc[(size_t)j * nw + w];
+                    }
+                }
+                carry += all;
+                __syncthreads();
+            }
+        }
+    }
+}
+
+void launch_pp_agg_rc(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
+                      const u64* raw_off, const u8* raw, u32 sub_shift, u32 sub_bits, const PPAggOut& out, u32* spill,
+                      u32 spill_cap) {
+    if (!n_parts) return;
+    const u32 rcap = pp_rc_records(hspec), tcap = rc_tcap(rcap);
+    const u32 W = hspec.pp_rw_raw / 8;
+    const size_t lds = (size_t)rcap * (8 * W + 8 * (u32)hspec.n_words + 1) + 4 * (size_t)tcap + PP_RC_MAXN + 16;
+    const u32 grid = n_parts < 16384 ? n_parts : 16384;
+#define PP_RC_LAUNCH(M, WW)                                                                                                  \
+    hipLaunchKernelGGL((pp_agg_rc_kernel<M, WW>), dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, raw, \
+                       sub_shift, sub_bits, rcap, tcap, out, spill, spill_cap)
+#define PP_RC_W_(M)                          \
+    switch (W) {                            \
+        case 1: PP_RC_LAUNCH(M, 1); break;  \
+        case 2: PP_RC_LAUNCH(M, 2); break;  \
+        case 3: PP_RC_LAUNCH(M, 3); break;  \
+        default: PP_RC_LAUNCH(M, 4); break; \
+    }
+    if (mode == 0) {
+        PP_RC_W_(0)
+    } else {
+        PP_RC_W_(1)
+    }
+#undef PP_RC_W_
+#undef PP_RC_LAUNCH
+}
+
 void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,
-                   const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out) {
+                   const u64* raw_off, const u64* st_off, u8* raw, u8* raw_alt, u8* st, u8* st_alt, const PPAggOut& out,
+                   const u32* plist, u32 plist_cap) {
     if (!n_parts) return;
     const u32 cap = pp_agg_slots(hspec);
     const size_t lds = (size_t)cap * (hspec.pp_sw * 8 + 2);
-    const u32 grid = n_parts < 8192 ? n_parts : 8192;
+    u32 grid = n_parts < 8192 ? n_parts : 8192;
+    if (plist) grid = std::min<u32>(grid, std::max<u32>(plist_cap, 1));
     const u32 wpr = hspec.pp_rw_raw / 8;  // record buffers carry >= 64 bytes of slack: W may round up
     const int W = wpr <= 1 ? 1 : wpr <= 2 ? 2 : wpr <= 4 ? 4 : wpr <= 6 ? 6 : wpr <= 8 ? 8 : 0;
 #define PP_AGG_LAUNCH(M, WW)                                                                                        \
     hipLaunchKernelGGL((pp_agg_kernel<M, WW>), dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, \
-                       st_off, raw, raw_alt, st, st_alt, cap, out)
+                       st_off, raw, raw_alt, st, st_alt, cap, out, plist)
 #define PP_AGG_W(M)                                  \
     switch (W) {                                     \
         case 1: PP_AGG_LAUNCH(M, 1); break;          \
@@ -1677,6 +1899,21 @@ __global__ void __launch_bounds__(PP_GNT) pp_grec_legacy_bucket_kernel(const Spe
             bool v;
             const StrRef sr = pp_key_str(S, batches, k, 0, v);
             h = legacy_bytes_hash(tab, sr.p, sr.len);
+        } else if (L.serializer) {
+            SerCrc sc;
+            for (int c = 0; c < S.n_keys; ++c) {
+                const dbg_datatype& ty = S.key_types[c];
+                if (ty.type == DBG_STRING) {
+                    bool v;
+                    const StrRef sr = pp_key_str(S, batches, k, c, v);
+                    sc.column(tab, ty.type, ty.nullable, v, 0, 0, sr.p, sr.len);
+                } else {
+                    u64 lo, hi;
+                    const bool v = pp_key_fixed(S, batches, k, c, lo, hi);
+                    sc.column(tab, ty.type, ty.nullable, v, lo, hi, nullptr, 0);
+                }
+            }
+            h = sc.finish(tab);
         } else {
             u64 kw[4] = {0, 0, 0, 0};
             for (int c = 0; c < S.n_keys; ++c) {

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "agg.hpp"
+#include "zstd_dev.hpp"
 #include "../../include/dbgpu_scan.h"
 
 int abi_fail(int code, const std::string& msg);  // abi.hip: sets dbg_last_error
@@ -206,6 +207,33 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
         }
     }
     if ((bad || w != on) && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+}
+
+// ZSTD pages (Fuse's default TableCompression, table_compression.rs:24-31): one wave per page,
+// zstd_dev.hpp.  lit: ZS_MAX_BLOCK bytes of literal scratch per page.
+__global__ void __launch_bounds__(64) pq_zstd_kernel(ScanArgs a, u8* lit) {
+    __shared__ ZsTables T;
+    const ScanPage pg = a.pages[blockIdx.x];
+    const u32 lane = threadIdx.x;
+    if (!pg.compressed) {
+        if (pg.comp != pg.uncomp && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+        return;
+    }
+    const u8* src = a.chunk + pg.src;
+    u8* dst = a.buf + pg.dst;
+    for (u32 j = lane; j < pg.lv; j += 64) dst[j] = src[j];  // v2 levels (uncompressed) first
+    __builtin_amdgcn_wave_barrier();
+    const bool ok = pg.comp >= pg.lv && pg.uncomp >= pg.lv &&
+                    zs_decode(src + pg.lv, pg.comp - pg.lv, dst + pg.lv, pg.uncomp - pg.lv, lit + (u64)blockIdx.x * ZS_MAX_BLOCK, T);
+    if (!ok && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
+}
+
+// a NULL decoded into a non-nullable target: one flag, raised on the device (no read-back of the
+// validity bytes)
+__global__ void __launch_bounds__(256) pq_null_check_kernel(const u8* __restrict__ vb, u64 n, u64* err) {
+    bool any = false;
+    for (u64 i = blockIdx.x * 256ULL + threadIdx.x; i < n; i += (u64)gridDim.x * 256) any |= vb[i] == 0;
+    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)err, (unsigned long long)SERR_NULL_IN_REQUIRED);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -737,6 +765,8 @@ struct dbg_scan_ctx {
     u64 bools_cap = 0;
     u64* err = nullptr;  // [0] error bits, [1] string total
     u64* herr = nullptr; // pinned
+    u8* zlit = nullptr;  // ZSTD literal scratch, ZS_MAX_BLOCK per page
+    u64 zlit_cap = 0;
 };
 
 namespace {
@@ -825,7 +855,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     const dbg_parquet_chunk& c = *chunk;
     u32 tw = 0;
     if (c.max_def_level < 0 || c.max_def_level > 1) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: nested column (definition level > 1)");
-    if (c.codec != DBG_PQ_UNCOMPRESSED && c.codec != DBG_PQ_SNAPPY && c.codec != DBG_PQ_LZ4_RAW)
+    if (c.codec != DBG_PQ_UNCOMPRESSED && c.codec != DBG_PQ_SNAPPY && c.codec != DBG_PQ_LZ4_RAW && c.codec != DBG_PQ_ZSTD)
         return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: codec " + std::to_string(c.codec) + " is decoded on the CPU");
     if (!target_ok(c.physical_type, c.type_length, target, tw))
         return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: physical type " + std::to_string(c.physical_type) + " -> target type " +
@@ -895,6 +925,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         if (!out->offsets) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: String output needs offsets");
     }
     if (is_bool) SCAN_RET(ensure(&ctx->bools, &ctx->bools_cap, row + 1));
+    if (c.codec == DBG_PQ_ZSTD) SCAN_RET(ensure(&ctx->zlit, &ctx->zlit_cap, (u64)pages.size() * ZS_MAX_BLOCK + 16));
     if (target.nullable && c.max_def_level && !out->validity && row) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null validity buffer");
     SCAN_HIP(hipMemcpyAsync(ctx->pages, pages.data(), pages.size() * sizeof(ScanPage), hipMemcpyHostToDevice, s));
     SCAN_HIP(hipMemsetAsync(ctx->err, 0, 16, s));
@@ -926,6 +957,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         switch (c.codec) {
             case DBG_PQ_SNAPPY: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_SNAPPY>, g, dim3(64), 0, s, a); break;
             case DBG_PQ_LZ4_RAW: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_LZ4_RAW>, g, dim3(64), 0, s, a); break;
+            case DBG_PQ_ZSTD: hipLaunchKernelGGL(pq_zstd_kernel, g, dim3(64), 0, s, a, ctx->zlit); break;
             default: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_UNCOMPRESSED>, g, dim3(64), 0, s, a); break;
         }
         SCAN_HIP(hipGetLastError());
@@ -949,6 +981,11 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     }
     if (is_bool && row) launch_pack_bits(s, ctx->bools, row, (u8*)out->data);
     if (target.nullable && row && out->validity) launch_pack_bits(s, ctx->vbytes, row, out->validity);
+    if (!target.nullable && c.max_def_level && row) {
+        hipLaunchKernelGGL(pq_null_check_kernel, dim3((u32)std::min<u64>(1024, (row + 255) / 256)), dim3(256), 0, s, ctx->vbytes, row,
+                           ctx->err);
+        SCAN_HIP(hipGetLastError());
+    }
     SCAN_HIP(hipMemcpyAsync(ctx->herr, ctx->err, 16, hipMemcpyDeviceToHost, s));
     SCAN_HIP(hipStreamSynchronize(s));
     const u64 e = ctx->herr[0];
@@ -959,13 +996,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         if (ctx->herr[1] > max_string_bytes)
             return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: String payload needs " + std::to_string(ctx->herr[1]) + " bytes");
     }
-    if (!target.nullable && c.max_def_level && row) {  // a NULL in a non-nullable target is an error
-        // (checked on the host from the validity bytes: one small read-back)
-        std::vector<u8> vb(row);
-        SCAN_HIP(hipMemcpy(vb.data(), ctx->vbytes, row, hipMemcpyDeviceToHost));
-        for (u64 i = 0; i < row; ++i)
-            if (!vb[i]) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: NULL in a non-nullable column");
-    }
+    if (e & SERR_NULL_IN_REQUIRED) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: NULL in a non-nullable column");
     return DBG_OK;
 }
 

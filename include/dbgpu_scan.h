@@ -30,7 +30,7 @@ extern "C" {
 /* parquet::format::Type / CompressionCodec values */
 enum { DBG_PQ_BOOLEAN = 0, DBG_PQ_INT32 = 1, DBG_PQ_INT64 = 2, DBG_PQ_INT96 = 3, DBG_PQ_FLOAT = 4, DBG_PQ_DOUBLE = 5,
        DBG_PQ_BYTE_ARRAY = 6, DBG_PQ_FIXED_LEN_BYTE_ARRAY = 7 };
-enum { DBG_PQ_UNCOMPRESSED = 0, DBG_PQ_SNAPPY = 1, DBG_PQ_LZ4_RAW = 7 };
+enum { DBG_PQ_UNCOMPRESSED = 0, DBG_PQ_SNAPPY = 1, DBG_PQ_ZSTD = 6, DBG_PQ_LZ4_RAW = 7 };
 
 /* One column chunk: the bytes from its first page header (dictionary page if any) to the end of
  * its last page — ColumnMeta::offset_length of the Fuse block (DataItem::RawData, mod.rs:88-104). */

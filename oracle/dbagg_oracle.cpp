@@ -1746,12 +1746,49 @@ static void legacy_group_hash(const dbg_column* cols, int n, u64 rows, u64* out)
         return;
     }
     u64 len = 0;
+    bool serializer = false;
     for (int j = 0; j < n; ++j) {
         const int t = cols[j].dt.type;
-        if (t == DBG_STRING || t == DBG_BOOLEAN) throw UnsupportedError("legacy Serializer keys");
+        if (t == DBG_STRING || t == DBG_BOOLEAN) serializer = true;
         len += fixed_width(t) + (cols[j].dt.nullable ? 1 : 0);
     }
-    if (len > 32) throw UnsupportedError("legacy Serializer keys");
+    if (serializer || len > 32) {
+        // HashMethodSerializer (EXP/kernels/group_by_hash/method_serializer.rs:39-70): the key is
+        // serialize_column_binary of every column in order (utils.rs:64-121) — a nullable column's
+        // validity byte, then for a valid row the value (numbers / dates in their width, Decimal128
+        // 16 bytes, Boolean one byte, String u64 length + bytes) — hashed as [u8]
+        std::vector<u8> key;
+        for (u64 i = 0; i < rows; ++i) {
+            key.clear();
+            for (int j = 0; j < n; ++j) {
+                const dbg_column& c = cols[j];
+                const bool v = is_valid(c, i);
+                if (c.dt.nullable) key.push_back(v ? 1 : 0);
+                if (!v) continue;
+                if (c.dt.type == DBG_STRING) {
+                    const u64 sl = str_len(c, i);
+                    for (int b = 0; b < 8; ++b) key.push_back((u8)(sl >> (8 * b)));
+                    const u8* p = str_ptr(c, i);
+                    key.insert(key.end(), p, p + sl);
+                } else if (c.dt.type == DBG_BOOLEAN) {
+                    key.push_back(bool_val(c, i) ? 1 : 0);
+                } else {
+                    const u64 w = fixed_width(c.dt.type);
+                    const u8* p = (const u8*)c.data + i * w;
+                    key.insert(key.end(), p, p + w);
+                }
+            }
+            u64 value = ~0ULL;
+            for (u64 o = 0; o < key.size(); o += 8) {
+                u64 w = 0;
+                const u64 k = std::min<u64>(8, key.size() - o);
+                for (u64 b = 0; b < k; ++b) w |= (u64)key[o + b] << (8 * b);
+                value = crc32c_u64_ref((u32)value, w);
+            }
+            out[i] = value;
+        }
+        return;
+    }
     const u64 step = len == 1 ? 1 : len == 2 ? 2 : len <= 4 ? 4 : len <= 8 ? 8 : len <= 16 ? 16 : 32;
     // build_keys_vec: sort_by (stable) widest first; null bytes start after every value byte
     std::vector<int> order(n);

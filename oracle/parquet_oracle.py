@@ -258,6 +258,15 @@ def decompress(codec: int, b: bytes, n: int) -> bytes:
         return snappy_decompress(b)
     if codec == LZ4_RAW:
         return lz4_raw_decompress(b, n)
+    if codec == ZSTD:
+        # Fuse's default page codec.  The reference decodes it with the `zstd` crate (0.12.4 /
+        # 0.13.2 over zstd-sys, i.e. libzstd; Cargo.lock); not restated here: the checker is
+        # libzstd itself, as pyarrow 25 bundles it.  The device decoder (scan.hip,
+        # zstd_dev.hpp) is the independent restatement of RFC 8878 under test.
+        import pyarrow as pa
+        out = pa.decompress(b, decompressed_size=n, codec="zstd", asbytes=True)
+        assert len(out) == n, "zstd: length mismatch"
+        return out
     raise NotImplementedError(f"codec {codec}")
 
 

@@ -10,7 +10,7 @@ SURVEY.md §8f-3) through partial -> bucket -> final, against the oracle:
 * every group of bucket b has the oracle's legacy FastHash bucket b, and the final results over
   all buckets equal the oracle's aggregate.
 Keys cover FixedKeys (Int32 + nullable Int16 -> u64 packing), a single String (SingleBinary), and
-HashMethodSerializer keys (two Strings), which are UNSUPPORTED."""
+HashMethodSerializer keys (two Strings, String + nullable Int32, Boolean + Int16)."""
 import numpy as np
 import pytest
 
@@ -147,14 +147,40 @@ def test_legacy_threshold_setting_and_serializer_keys():
         assert all(m.bucket >= 0 for m in metas) and sum(len(m.payload) for m in metas) == 1_000
     finally:
         p.close()
-    # two String keys: HashMethodSerializer, not served on the device
-    s1 = Column.from_strings(["a%d" % (i % 7) for i in range(1000)])
-    s2 = Column.from_strings(["b%d" % (i % 3) for i in range(1000)])
-    params = AggregatorParams([s1.dtype, s2.dtype], [F.get("count", [], [])], enable_experimental_aggregate_hashtable=False)
-    p = _partial(params, [s1, s2], [("count", None)], 0, 1000)
+
+
+
+@pytest.mark.parametrize("case", ["two_strings", "string_nullable_int", "bool_int"])
+def test_legacy_serializer_keys(case):
+    """HashMethodSerializer keys (EXP/kernels/group_by.rs:48-95): two Strings (TPC-H Q1's
+    l_returnflag, l_linestatus), a String with a nullable Int32, a Boolean with an Int16 — the
+    buckets are hash2bucket<8> of the FastHash of the serialized key bytes (serialize_column_binary,
+    group_by_hash/utils.rs:64-121), checked group by group against the oracle's restatement."""
+    rng = np.random.default_rng(31)
+    n = 300_000
+    if case == "two_strings":
+        g = rng.integers(0, 40_000, n)
+        keys = [Column.from_strings(["a%d" % (x % 4000) for x in g]), Column.from_strings(["b" * (x % 13) for x in g])]
+    elif case == "string_nullable_int":
+        g = rng.integers(0, 30_000, n)
+        keys = [Column.from_strings(["k%05d" % (x % 7000) for x in g]),
+                Column.from_numbers(col.Int32, g % 11, validity=(g % 7) != 0)]
+    else:
+        g = rng.integers(0, 60_000, n)
+        keys = [Column.from_bools(g % 2 == 0), Column.from_numbers(col.Int16, g % 30_000)]
+    v = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n))
+    aggs = [("count", None), ("sum", v)]
+    fns = [F.get(f, [], [c.dtype] if c is not None else []) for f, c in aggs]
+    params = AggregatorParams([k.dtype for k in keys], fns, enable_experimental_aggregate_hashtable=False)
+    p = _partial(params, keys, aggs, 0, n)
     try:
-        with pytest.raises(Unsupported):
-            p.on_finish()
+        metas = p.on_finish()
+        assert len(metas) > 100 and all(0 <= m.bucket < LEGACY_BUCKETS for m in metas)
+        bt = TransformPartitionBucket(params)
+        bt.push(metas)
+        gk, ga = _final_all(params, bt.finish(), len(keys), len(aggs))
+        ok, oa = oracle_aggregate(keys, aggs, None, threads=8)
+        assert_results_equal(gk, ga, ok, oa)
     finally:
         p.close()
 

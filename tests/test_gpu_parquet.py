@@ -48,7 +48,7 @@ def check_file(dec, buf, names=None):
     return n
 
 
-@pytest.mark.parametrize("comp", ["NONE", "SNAPPY", "LZ4"])
+@pytest.mark.parametrize("comp", ["NONE", "SNAPPY", "LZ4", "ZSTD"])
 @pytest.mark.parametrize("dictionary", [False, True])
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
 def test_decode_matches_oracle(dec, comp, dictionary, version):
@@ -61,7 +61,7 @@ def test_fuse_writer_shape_large(dec):
     """blocks_to_parquet's shape (one row group, PLAIN, no dictionary; parquet_rs.rs:36-44) at
     several hundred pages per chunk, every codec the GPU takes."""
     t = sample_table(400_000, seed=3).select(["i16", "i64", "s", "d20", "b"])
-    for comp in ["NONE", "SNAPPY", "LZ4"]:
+    for comp in ["NONE", "SNAPPY", "LZ4", "ZSTD"]:
         buf = write(t, compression=comp, use_dictionary=False, row_group_size=1 << 30)
         n = 0
         for name, _, ch, at in file_chunks(buf):  # at this size against pyarrow (which pins the oracle)
@@ -174,7 +174,17 @@ def test_errors_not_faults(dec):
         dec.decode(ColumnChunk(bytes(bad), ch.physical_type, ch.max_def_level, 0, ch.codec), target_of(at))
     # codecs the GPU does not take: the caller keeps the CPU reader
     with pytest.raises(Unsupported):
-        dec.decode(ColumnChunk(ch.data, ch.physical_type, ch.max_def_level, 0, 6), target_of(at))  # ZSTD
+        dec.decode(ColumnChunk(ch.data, ch.physical_type, ch.max_def_level, 0, 4), target_of(at))  # BROTLI
+    # a corrupted ZSTD page: an error, no fault
+    tz = sample_table(3000).select(["i64", "s"])
+    bz = write(tz, compression="ZSTD", use_dictionary=False, data_page_size=4096)
+    (_, _, chz, atz), _ = file_chunks(bz)
+    pz = __import__("oracle.parquet_oracle", fromlist=["x"]).parse_pages(chz.data)
+    bad = bytearray(chz.data)
+    for j in range(pz[0].data_off + 6, pz[0].data_off + min(pz[0].compressed, 60)):
+        bad[j] ^= 0x5A
+    with pytest.raises(DbgError):
+        dec.decode(ColumnChunk(bytes(bad), chz.physical_type, chz.max_def_level, 0, chz.codec), target_of(atz))
     # a physical type that does not convert to the target
     with pytest.raises(Unsupported):
         dec.decode(ch, col.String)

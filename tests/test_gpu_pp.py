@@ -221,3 +221,27 @@ def test_pp_auto_probe_selects_partitioned_for_c4():
     assert r4["partitioned"] and r4["n_groups"] == 5_000_000
     r2 = workloads.run_config(2, 5_000_000, steps=1)
     assert not r2["partitioned"]
+
+
+@pytest.mark.parametrize("kind", ["i64", "i64_i32", "dup_heavy", "skewed"])
+def test_pp_record_centric(kind):
+    """Record-centric aggregation of raw records (pp.hip pp_agg_rc_kernel): level-2 partitions of
+    ~PP_RC_PART records aggregated in LDS rounds.  Mostly-unique keys (its target), keys with a few
+    records each, and a skewed key holding a large share of the rows — whose partition exceeds one
+    round's LDS and is spilled to the slot-table kernel — all against the oracle."""
+    rng = np.random.default_rng(len(kind))
+    n = 6_000_000
+    if kind == "i64":
+        keys = [Column.from_numbers(col.Int64, rng.permutation(n).astype(np.int64) * 7919 - 3)]
+    elif kind == "i64_i32":
+        keys = [Column.from_numbers(col.Int64, rng.integers(0, n, n)), Column.from_numbers(col.Int32, rng.integers(0, 2**31 - 1, n))]
+    elif kind == "dup_heavy":
+        keys = [Column.from_numbers(col.Int64, rng.integers(0, n // 3, n))]
+    else:
+        k = rng.integers(0, n, n)
+        k[rng.random(n) < 0.3] = 42  # 30 % of the rows in one group
+        keys = [Column.from_numbers(col.Int64, k)]
+    i16 = Column.from_numbers(col.Int16, rng.integers(-3, 3, n))
+    w = Column.from_numbers(col.Int16, rng.integers(0, 2560, n))
+    g, info = check_pp(keys, [("count", None), ("sum", i16), ("sql_avg", w), ("min", w)], on_device=True)
+    assert g > 1_000_000

@@ -41,6 +41,31 @@ def legacy_py(cols, i):
         return v
     widths = [c.dtype.width for c in cols]
     total = sum(w + (1 if c.dtype.nullable else 0) for w, c in zip(widths, cols))
+    if any(c.dtype.type_id in (abi.STRING, abi.BOOLEAN) for c in cols) or total > 32:
+        # HashMethodSerializer: serialize_column_binary of every column, in order, as [u8]
+        key = bytearray()
+        for c in cols:
+            valid = c.validity is None or not c.dtype.nullable or bool(c.validity[i])
+            if c.dtype.nullable:
+                key.append(1 if valid else 0)
+            if not valid:
+                continue
+            if c.dtype.type_id == abi.STRING:
+                s = c.values()[i]
+                key += struct.pack("<Q", len(s)) + s
+            elif c.dtype.type_id == abi.BOOLEAN:
+                key.append(1 if c.values()[i] else 0)
+            elif c.dtype.type_id == abi.DECIMAL128:
+                key += bytes(np.asarray(c.data, np.uint8)[i * 16:(i + 1) * 16])
+            else:
+                w = c.dtype.width
+                key += bytes(np.asarray(c.data).view(np.uint8).reshape(-1)[i * w:(i + 1) * w])
+        if not key:
+            return (1 << 64) - 1
+        v = 0xFFFFFFFF
+        for o in range(0, len(key), 8):
+            v = crc_py(v, bytes(key[o:o + 8]).ljust(8, b"\0"))
+        return v
     step = 1 if total == 1 else 2 if total == 2 else 4 if total <= 4 else 8 if total <= 8 else 16 if total <= 16 else 32
     key = bytearray(32)
     order = sorted(range(len(cols)), key=lambda j: -widths[j])  # stable
@@ -78,8 +103,15 @@ def _cases(rng, n):
     d = Column.from_decimals(20, 2, [int(x) * (1 << 40) for x in rng.integers(-1000, 1000, n)])
     dt = Column.from_numbers(col.Date, rng.integers(0, 20000, n))
     s = Column.from_strings([("abcdefghij"[: int(k)] * (1 + int(k) % 3)) for k in rng.integers(0, 11, n)])
+    s2 = Column.from_strings(["RANF"[int(k) % 4] for k in rng.integers(0, 4, n)])
+    sn = Column.from_strings([("xy" * int(k)) for k in rng.integers(0, 9, n)], validity=rng.random(n) > 0.25)
+    b = Column.from_bools(rng.random(n) > 0.5)
+    bn = Column.from_bools(rng.random(n) > 0.5, validity=rng.random(n) > 0.3)
+    d38 = Column.from_decimals(38, 2, [int(x) * (1 << 70) for x in rng.integers(-1000, 1000, n)])
+    # FixedKeys, SingleBinary, then HashMethodSerializer keys: two Strings (TPC-H Q1), String +
+    # nullable Int32, one nullable String, Booleans, and more than 32 packed bytes
     return [[i16], [u8], [i16, u8], [i32n, u8, i16], [i64], [i64, i32n], [d], [d, i16], [f64, dt], [i64, d, u8],
-            [d, i64, i32n], [s]]
+            [d, i64, i32n], [s], [s, s2], [s2, i32n], [sn], [b], [bn, i16], [d38, d38, u8]]
 
 
 def test_oracle_matches_python_restatement():
