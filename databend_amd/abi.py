@@ -86,7 +86,7 @@ class dbg_parquet_chunk(C.Structure):  # include/dbgpu_scan.h
 
 # parquet physical types / codecs (dbgpu_scan.h)
 PQ_BOOLEAN, PQ_INT32, PQ_INT64, PQ_INT96, PQ_FLOAT, PQ_DOUBLE, PQ_BYTE_ARRAY, PQ_FIXED_LEN_BYTE_ARRAY = range(8)
-PQ_UNCOMPRESSED, PQ_SNAPPY, PQ_LZ4_RAW = 0, 1, 7
+PQ_UNCOMPRESSED, PQ_SNAPPY, PQ_ZSTD, PQ_LZ4_RAW = 0, 1, 6, 7
 
 DBG_COMM_ID_BYTES = 128
 

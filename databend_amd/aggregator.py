@@ -243,6 +243,17 @@ class AggregateHashTable:
         check(lib().dbg_agg_get_strategy(self.h, C.byref(p), C.byref(r)))
         return bool(p.value), r.value
 
+    def set_partition_keys(self, n_keys: int):
+        """Bucket groups (partition schemes 0 / 1) by the hash of their first n_keys key columns
+        (0 = all): a DISTINCT pair table's buckets follow its group's keys."""
+        check(lib().dbg_agg_set_partition_keys(self.h, n_keys))
+
+    def pp_specialised(self) -> bool:
+        """Whether the last partitioned finalize ran the compile-time specialised aggregation."""
+        p, r = C.c_int(), C.c_uint64()
+        check(lib().dbg_agg_get_strategy(self.h, C.byref(p), C.byref(r)))
+        return p.value == 2
+
     # ---- AggregateHashTable::add_groups (+ fused filter)
     def add_groups(self, group_columns: Sequence[ColumnLike], params: Sequence[Optional[ColumnLike]],
                    rows: Optional[int] = None, filter_program=None, on_device: Optional[bool] = None) -> None:

@@ -195,6 +195,7 @@ struct dbg_agg_handle {
     // partition state
     u32 part_n = 0;
     int part_scheme = 0;
+    int part_keys = 0;  // dbg_agg_set_partition_keys: buckets by the first part_keys key columns (0 = all)
     u64 part_nb = 0;  // blocks of the partition histogram
     u64* d_part_pos = nullptr;
     u64* d_part_str_pos = nullptr;
@@ -255,6 +256,8 @@ struct dbg_agg_handle {
     } ppk[2];
     u32 pp_bits = 0;  // final partition bits
     u32 pp_rc_sub = 0;  // > 0: record-centric aggregation in 2^pp_rc_sub rounds per partition (pp.hip)
+    int pp_spec = -1;   // >= 0: the compile-time specialised aggregation's shape (pp_agg_spec_kernel)
+    u32 pp_spec_sub = 0;  // its rounds per partition: 2^pp_spec_sub
     u32* pp_spill = nullptr;  // [count, partition ids...] spilled by the record-centric kernel
     u32* pp_cnt = nullptr;
     u64 pp_cnt_cap = 0;
@@ -1229,7 +1232,7 @@ static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 row
 // Levels 2 and 3 (NewTransformPartitionBucket + the final bucket split): every level-1 partition
 // of both record kinds is re-scattered by the next hash bits until the estimated groups of a
 // final partition fit half a workgroup's LDS table.
-static int pp_prepare(dbg_agg_handle* h) {
+static int pp_prepare(dbg_agg_handle* h, bool spec_ok) {
     const Spec& S = h->spec;
     const u64 nr = h->ppk[0].l1_n, nsr = h->ppk[1].l1_n;
     // estimated groups: the probe's, raised to the capacity hint (a hint below what the probe saw
@@ -1267,6 +1270,28 @@ static int pp_prepare(dbg_agg_handle* h) {
             k2 = B - PP_L1_BITS;
             k3 = 0;
             h->pp_rc_sub = std::max<u32>(sub, 1);  // >= 1 round bit: the flag doubles as "record-centric"
+        }
+    }
+    // Compile-time specialised aggregation (result columns, raw records of a supported shape): a
+    // partition is loaded once and aggregated in 2^sub LDS rounds, so partitions hold up to the
+    // kernel's register budget of records and level 2 alone (<= 10 bits) sizes them — no level 3.
+    h->pp_spec = -1;
+    static const bool spec_on = !(getenv("DBG_X_PPSPEC") && getenv("DBG_X_PPSPEC")[0] == '0');
+    u32 scap = 0, smax = 0;
+    const int shape = (spec_on && spec_ok && !h->pp_rc_sub && nsr == 0 && nr > 0) ? pp_spec_shape(S, &scap, &smax) : -1;
+    if (shape >= 0) {
+        const double fill = 0.75 * (double)smax;  // average records per partition (the max stays below smax)
+        u32 b2 = PP_L1_BITS + 1;
+        while ((double)nr / (double)(1ULL << b2) > fill && b2 < PP_L1_BITS + 10) ++b2;
+        const double gp = g / (double)(1ULL << b2);
+        u32 sub = 0;
+        while (gp / (double)(1u << sub) > 0.45 * (double)scap && sub < 5) ++sub;
+        if ((double)nr / (double)(1ULL << b2) <= fill && gp / (double)(1u << sub) <= 0.45 * (double)scap && B >= b2) {
+            B = b2;
+            k2 = B - PP_L1_BITS;
+            k3 = 0;
+            h->pp_spec = shape;
+            h->pp_spec_sub = sub;
         }
     }
     h->pp_bits = B;
@@ -1353,7 +1378,7 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     HIPCHECK(hipMemsetAsync(h->pp_tot, 0, PPT_WORDS * 8, h->stream));
     const u64 N = pp_records(h);
     if (!N) return DBG_OK;
-    RETURN_IF(pp_prepare(h));
+    RETURN_IF(pp_prepare(h, mode == 1 || (od && !od->ser)));
     PPAggOut o;
     memset(&o, 0, sizeof(o));
     o.tot = h->pp_tot;
@@ -1383,7 +1408,16 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     }
     auto& R = h->ppk[0];
     auto& T = h->ppk[1];
-    if (h->pp_rc_sub) {
+    if (h->pp_spec >= 0) {
+        constexpr u32 SPILL_CAP = 4096;
+        if (!h->pp_spill) RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + SPILL_CAP) * 4));
+        HIPCHECK(hipMemsetAsync(h->pp_spill, 0, 4, h->stream));
+        prof::Scope ps("pp_agg", h->stream);
+        launch_pp_agg_spec(h->stream, h->pp_spec, mode, 1u << h->pp_bits, R.part, R.fin, h->pp_spec_sub, o, h->pp_spill, SPILL_CAP);
+        // partitions larger than its register budget (skewed keys): the generic kernel, spilled ids only
+        launch_pp_agg(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.part, nullptr, R.fin, R.alt, nullptr, nullptr,
+                      o, h->pp_spill, SPILL_CAP);
+    } else if (h->pp_rc_sub) {
         constexpr u32 SPILL_CAP = 4096;
         if (!h->pp_spill) RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + SPILL_CAP) * 4));
         HIPCHECK(hipMemsetAsync(h->pp_spill, 0, 4, h->stream));
@@ -1876,8 +1910,15 @@ int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy) {
 
 int dbg_agg_get_strategy(dbg_agg_handle* h, int* partitioned, uint64_t* extra_rounds) {
     if (!h || !partitioned) return fail(DBG_ERR_INVALID, "null argument");
-    *partitioned = h->pp ? 1 : 0;
+    *partitioned = h->pp ? (h->pp_spec >= 0 ? 2 : 1) : 0;
     if (extra_rounds) *extra_rounds = h->pp_stat_rounds;
+    return DBG_OK;
+}
+
+int dbg_agg_set_partition_keys(dbg_agg_handle* h, int n_keys) {
+    if (!h) return fail(DBG_ERR_INVALID, "null handle");
+    if (n_keys < 0 || n_keys > h->spec.n_keys) return fail(DBG_ERR_INVALID, "partition keys: 0..n_group_cols");
+    h->part_keys = n_keys;
     return DBG_OK;
 }
 
@@ -2264,7 +2305,16 @@ int dbg_agg_partition(dbg_agg_handle* h, uint32_t n_parts, int scheme, uint64_t*
     const Spec& S = h->spec;
     u64 nb = h->pp ? pp_grec_blocks(std::max<u64>(h->n_groups, 1)) : finalize_blocks(h->cap);
     const u32* lpart = nullptr;
-    if (scheme == 2 && n_parts > 1) {  // hash2bucket<bits, true> of each group's FastHash
+    const bool prefix = scheme != 2 && h->part_keys > 0 && h->part_keys < S.n_keys;
+    if (prefix && h->pp) return fail(DBG_ERR_UNSUPPORTED, "partition keys: table strategy only");
+    if (prefix && n_parts > 1) {  // buckets of the first part_keys key columns' group hash, per slot
+        RETURN_IF(ensure_buf(&h->d_lpart, &h->lpart_cap, (h->cap + 1) / 2 + 1));
+        prof::Scope ps("prefix_bucket", h->stream);
+        launch_prefix_slot_bucket(h->stream, h->dspec, h->dbatches, table_desc(h), h->part_keys, n_parts, scheme, (u32*)h->d_lpart);
+        lpart = (const u32*)h->d_lpart;
+        scheme = 2;  // count and export read lpart
+    }
+    if (scheme == 2 && n_parts > 1 && !prefix) {  // hash2bucket<bits, true> of each group's FastHash
         const u64 n = h->pp ? h->n_groups : h->cap + 1;
         RETURN_IF(ensure_buf(&h->d_lpart, &h->lpart_cap, n / 2 + 1));
         prof::Scope ps("legacy_bucket", h->stream);

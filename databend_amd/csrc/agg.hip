@@ -50,9 +50,10 @@ __device__ __forceinline__ u64 pack_key(const Spec& S, const DCol* keys, u64 i) 
 }
 
 
-__device__ __forceinline__ u64 hash_packed(const Spec& S, u64 key) {
+__device__ __forceinline__ u64 hash_packed(const Spec& S, u64 key, int nk = -1) {
     u64 h = 0;
-    for (int c = 0; c < S.n_keys; ++c) {
+    if (nk < 0) nk = S.n_keys;
+    for (int c = 0; c < nk; ++c) {
         const dbg_datatype& t = S.key_types[c];
         bool v = t.nullable ? ((key >> (8 * S.voff[c])) & 0xff) != 0 : true;
         u64 b = (key >> (8 * S.koff[c])) & width_mask(type_width(t.type));
@@ -799,6 +800,29 @@ __global__ void __launch_bounds__(BLOCK) legacy_slot_bucket_kernel(const Spec* _
     }
 }
 
+// Bucket (scheme 0 or 1) of every occupied slot by the group hash of its first `nk` key columns: a
+// DISTINCT aggregate's pair table (keys..., x) is bucketed by its group's keys alone, so each of
+// its buckets holds exactly the pairs of the groups the same bucket of the main table holds
+// (AggregateDistinctCombinator's set travels inside its group's state in the reference,
+// FUN/aggregate_combinator_distinct.rs:94-105).
+__global__ void __launch_bounds__(BLOCK) prefix_slot_bucket_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                  TableDesc t, int nk, u32 n_parts, int scheme, u32* __restrict__ out) {
+    const Spec& S = *spec;
+    for (u64 s = blockIdx.x * (u64)BLOCK + threadIdx.x; s <= t.cap; s += (u64)gridDim.x * BLOCK) {
+        const u64 e = t.slots[s * t.stride_words];
+        if (e == SLOT_EMPTY) continue;
+        const u64 h = S.inline_keys ? hash_packed(S, s == t.cap ? SLOT_EMPTY : e, nk) : group_hash(batches[ref_bid(e)].keys, nk, ref_row(e));
+        out[s] = part_of(h, n_parts, scheme, nullptr, s);
+    }
+}
+
+void launch_prefix_slot_bucket(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, int nk, u32 n_parts,
+                               int scheme, u32* out) {
+    u64 blocks = (t.cap + 1 + BLOCK - 1) / BLOCK;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(prefix_slot_bucket_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, batches, t, nk, n_parts, scheme, out);
+}
+
 void launch_legacy_slot_bucket(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const LegacyLayout& L,
                                u32* out) {
     u64 blocks = (t.cap + 1 + BLOCK - 1) / BLOCK;
@@ -1495,7 +1519,9 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
 // ------------------------------------------------------------------------------------------
 #define FAST_UNROLL 4
 #ifndef TAIL_ON
-#define TAIL_ON 1  // dynamic stream tail of fused-chain launches (make TAIL=0: off, for A/B runs)
+// dynamic stream tail of fused-chain launches: measured and not kept (C2 step 45.7 -> 51.3 us,
+// profiles/r04/c2_tail_ab.json); make TAIL=1 builds it for A/B runs
+#define TAIL_ON 0
 #endif
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // Column data reached through a descriptor is a generic pointer to the compiler, which then

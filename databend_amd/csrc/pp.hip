@@ -1245,12 +1245,12 @@ template <int MODE, int W>
 __global__ void __launch_bounds__(PP_AGG_NT) pp_agg_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                           u32 n_parts, const u64* __restrict__ raw_off, const u64* __restrict__ st_off,
                                                           u8* raw, u8* raw_alt, u8* st, u8* st_alt, u32 cap, PPAggOut out,
-                                                          const u32* __restrict__ plist) {
+                                                          const u32* __restrict__ plist, u32 plist_cap) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     const Spec& S = *spec;
     // plist: aggregate only the partitions plist[1 .. plist[0]] (those the record-centric kernel
     // spilled), numbered 0 .. plist[0] - 1 here
-    if (plist) n_parts = min(n_parts, plist[0]);
+    if (plist) n_parts = min(n_parts, min(plist[0], plist_cap));  // (a count past the cap flagged ERR_OVF_LOST)
     auto pid = [&](u32 q) -> u32 { return plist ? plist[1 + q] : q; };
     const u32 sw = S.pp_sw, kw8 = S.pp_kw / 8, rwr = S.pp_rw_raw, rws = S.pp_rw_state;
     l64* slots = (l64*)lds_raw;
@@ -1604,7 +1604,7 @@ void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
     const int W = wpr <= 1 ? 1 : wpr <= 2 ? 2 : wpr <= 4 ? 4 : wpr <= 6 ? 6 : wpr <= 8 ? 8 : 0;
 #define PP_AGG_LAUNCH(M, WW)                                                                                        \
     hipLaunchKernelGGL((pp_agg_kernel<M, WW>), dim3(grid), dim3(PP_AGG_NT), lds, s, dspec, batches, n_parts, raw_off, \
-                       st_off, raw, raw_alt, st, st_alt, cap, out, plist)
+                       st_off, raw, raw_alt, st, st_alt, cap, out, plist, plist_cap)
 #define PP_AGG_W(M)                                  \
     switch (W) {                                     \
         case 1: PP_AGG_LAUNCH(M, 1); break;          \
@@ -1621,6 +1621,407 @@ void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
     }
 #undef PP_AGG_W
 #undef PP_AGG_LAUNCH
+}
+
+// ------------------------------------------------------------------------------------------
+// Compile-time specialised aggregation of raw records (pp_agg_spec_kernel).
+//
+// The generic kernel above interprets the Spec per record: a loop over the aggregates with a
+// switch on kind, argument width and type, a generic row writer, and a slot-table claim that
+// initialises states and then applies the record with LDS atomics.  For the common shape —
+// fixed-width non-nullable keys, COUNT(*) / SUM / AVG over non-nullable integer arguments, the
+// final result written as columns — every one of those decisions is a template parameter here:
+//   * key types and argument types / offsets are compile-time (offsets from the same packing rule
+//     as build_spec, checked against the Spec on the host before launch);
+//   * a slot is [key words][row count][one sum word per SUM / AVG]: AVG's count and COUNT(*) are the
+//     same row count (arguments are non-nullable), so C4's state is 3 words instead of 4;
+//   * a claimer initialises the slot from its own record (count 1, sums = its values) before
+//     publishing the tag: a new group costs no LDS atomics, a repeat costs one add per word;
+//   * probes read a dense u32 tag array (one LDS word per probe step), the key words only on a
+//     tag match;
+//   * claimed slots join the output list with one LDS add per wave (ballot), not one per lane;
+//   * a partition (up to PP_AGG_NT x RPT records) is loaded into registers once and aggregated in
+//     2^sub_bits rounds selected by the hash bits below the partition's, so a partition holds
+//     2^sub_bits LDS tables' worth of groups and the level-3 scatter is gone (AGG/
+//     transform_aggregate_final.rs:71-156 aggregates one bucket per task the same way).
+// A record whose probe window is full stays pending and is inserted into the emptied table in
+// a further mini-round (consistent per key: slots only fill within a mini-round).  Partitions
+// larger than the register budget are listed in `spill` for the generic kernel.
+// ------------------------------------------------------------------------------------------
+enum { PS_COUNT = 1, PS_SUM = 2, PS_AVG = 3 };
+#define PS_AGG(kind, t) (((kind) << 8) | ((t) & 0xff))
+__host__ __device__ constexpr int ps_kind(int a) { return a >> 8; }
+__host__ __device__ constexpr int ps_type(int a) { return a & 0xff; }
+__host__ __device__ constexpr u32 ps_tw(int t) {
+    return (t == DBG_INT8 || t == DBG_UINT8) ? 1u
+           : (t == DBG_INT16 || t == DBG_UINT16) ? 2u
+           : (t == DBG_INT32 || t == DBG_UINT32 || t == DBG_DATE) ? 4u : 8u;
+}
+__host__ __device__ constexpr bool ps_signed(int t) { return !(t == DBG_UINT8 || t == DBG_UINT16 || t == DBG_UINT32 || t == DBG_UINT64); }
+__host__ __device__ constexpr bool ps_has_arg(int a) { return ps_kind(a) == PS_SUM || ps_kind(a) == PS_AVG; }
+// build_spec's raw record packing: key bytes, then each argument aligned to its width
+__host__ __device__ constexpr u32 ps_align(u32 po, int a) { return ps_has_arg(a) ? ((po + ps_tw(ps_type(a)) - 1) & ~(ps_tw(ps_type(a)) - 1)) : po; }
+__host__ __device__ constexpr u32 ps_next(u32 po, int a) { return ps_has_arg(a) ? ps_align(po, a) + ps_tw(ps_type(a)) : po; }
+
+template <int K0, int K1, int A0, int A1, int A2>
+struct PsShape {
+    static constexpr int NK = K1 < 0 ? 1 : 2;
+    static constexpr u32 KB = ps_tw(K0) + (K1 < 0 ? 0u : ps_tw(K1));  // packed key bytes
+    static constexpr u32 KW = (KB + 7) / 8;
+    static constexpr u64 KLAST = (KB & 7) == 0 ? ~0ULL : ((1ULL << (8 * (KB & 7))) - 1);
+    static constexpr u32 OFF0 = ps_align(KB, A0);
+    static constexpr u32 OFF1 = ps_align(ps_next(KB, A0), A1);
+    static constexpr u32 OFF2 = ps_align(ps_next(ps_next(KB, A0), A1), A2);
+    static constexpr u32 END = ps_next(ps_next(ps_next(KB, A0), A1), A2);
+    static constexpr int NSUM = (ps_has_arg(A0) ? 1 : 0) + (ps_has_arg(A1) ? 1 : 0) + (ps_has_arg(A2) ? 1 : 0);
+    static constexpr u32 BW = KW + 1 + NSUM;  // slot body words: key, row count, sums
+    // Spec state words (build_spec: COUNT 1, SUM 1, AVG 2 — sum, count) and the state record bytes
+    static constexpr u32 swords(int a) { return a == 0 ? 0u : (ps_kind(a) == PS_AVG ? 2u : 1u); }
+    static constexpr u32 REC_BYTES = 8 * (KW + swords(A0) + swords(A1) + swords(A2));
+    static constexpr u32 off(int a) { return a == 0 ? OFF0 : (a == 1 ? OFF1 : OFF2); }
+    static constexpr int agg(int a) { return a == 0 ? A0 : (a == 1 ? A1 : A2); }
+    // sum word of aggregate a (after the row count)
+    static constexpr u32 sumw(int a) {
+        return KW + 1 + (a > 0 && ps_has_arg(A0) ? 1 : 0) + (a > 1 && ps_has_arg(A1) ? 1 : 0);
+    }
+};
+
+__device__ __forceinline__ u64 ps_ext(u64 v, int t) {  // argument bits -> the wrapping 64-bit sum addend
+    const u32 w = ps_tw(t);
+    if (w == 8) return v;
+    v &= (1ULL << (8 * w)) - 1;
+    if (ps_signed(t) && ((v >> (8 * w - 1)) & 1)) v |= ~((1ULL << (8 * w)) - 1);
+    return v;
+}
+
+// LDS of one workgroup: [tags u32 cap][body u64 cap x BW][list u16 cap][stage: words u64 PS_STAGE x W,
+// slot hash u32 PS_STAGE, origin u16 PS_STAGE][pending u32 PP_AGG_NT]
+#define PS_STAGE 1024
+__host__ __device__ constexpr size_t ps_lds_bytes(u32 cap, u32 bw, u32 w) {
+    return 8 * (size_t)((cap + 1) / 2) + (size_t)cap * 8 * bw + 2 * (size_t)((cap + 3) & ~3u) + (size_t)PS_STAGE * (8 * w + 4 + 2) +
+           4 * (size_t)PP_AGG_NT;
+}
+
+template <int MODE, int W, int RPT, int K0, int K1, int A0, int A1, int A2>
+__global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
+                                                               u32 sub_bits, u32 cap, PPAggOut out, u32* __restrict__ spill, u32 spill_cap) {
+    typedef PsShape<K0, K1, A0, A1, A2> SH;
+    constexpr u32 KW = SH::KW, BW = SH::BW;
+    static_assert(KW <= (u32)W && SH::END <= 8u * W, "record words");
+    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    l32* tags = (l32*)lds_raw;                                     // [cap] 0 empty, 1 being claimed, else tag
+    l64* body = (l64*)lds_raw + (cap + 1) / 2;                     // [cap][BW]
+    l16* list = (l16*)(body + (size_t)cap * BW);                   // claimed slots of the round
+    l64* sw_ = (l64*)(list + ((cap + 3) & ~3u));                   // staged records [PS_STAGE][W]
+    l32* slo = (l32*)(sw_ + (size_t)PS_STAGE * W);                 // their slot hash bits
+    l16* sorg = (l16*)(slo + PS_STAGE);                            // their origin (thread << 4 | register index)
+    l32* pend = (l32*)(((uintptr_t)(sorg + PS_STAGE) + 3) & ~(uintptr_t)3);  // [PP_AGG_NT] probe-window misses
+    __shared__ u32 nlist, scount;
+    __shared__ u64 gbase;
+    const u32 tid = threadIdx.x, lane = tid & 63;
+    const u32 smask = (1u << sub_bits) - 1;
+    const u32 win = cap < PP_WINDOW ? cap : PP_WINDOW;
+    for (u32 j = tid; j < cap; j += PP_AGG_NT) tags[j] = 0;
+    pend[tid] = 0;
+    if (tid == 0) nlist = scount = 0;
+    __syncthreads();
+    // one staged record into the table; false = no room in its probe window
+    auto insert = [&](u32 k) -> bool {
+        RegRec<W> rk;
+#pragma unroll
+        for (int w = 0; w < W; ++w) rk.r[w] = sw_[(size_t)k * W + w];
+        const u32 lo = slo[k];
+        const u32 tag = (lo & ~3u) | 2u;
+        u32 pos = (u32)(((u64)lo * cap) >> 32);
+        bool claimed = false;
+        int at = -1;
+        for (u32 q = 0; q < win; ++q) {
+            l32* tp = tags + pos;
+            u32 t = __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t == 0) {
+                u32 old = 0;
+                __hip_atomic_compare_exchange_strong(tp, &old, 1u, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == 0) {  // claimed: key words, the record's own contribution, then the tag
+                    l64* e = body + (size_t)pos * BW;
+#pragma unroll
+                    for (u32 w = 0; w < KW; ++w) e[w] = w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w];
+                    e[KW] = 1;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        if (ps_has_arg(SH::agg(a))) e[SH::sumw(a)] = ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a)));
+                    __hip_atomic_store(tp, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    claimed = true;
+                    at = (int)pos;
+                    break;
+                }
+                t = old;
+            }
+            while (t == 1) t = __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t == tag) {
+                l64* e = body + (size_t)pos * BW;
+                bool eq = true;
+#pragma unroll
+                for (u32 w = 0; w < KW; ++w) eq &= e[w] == (w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w]);
+                if (eq) {
+                    at_add<AS_LDS>((wptr<AS_LDS>)(e + KW), 1ULL);
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        if (ps_has_arg(SH::agg(a)))
+                            at_add<AS_LDS>((wptr<AS_LDS>)(e + SH::sumw(a)),
+                                           ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a))));
+                    at = (int)pos;
+                    break;
+                }
+            }
+            pos = pos + 1 == cap ? 0 : pos + 1;
+        }
+        // new groups join the round's list: one LDS add per wave (called with the wave converged)
+        const u64 m = __ballot(claimed);
+        if (m) {
+            const u32 lead = (u32)__ffsll((long long)m) - 1;
+            u32 b = 0;
+            if (lane == lead) b = atomicAdd(&nlist, (u32)__popcll(m));
+            b = __shfl(b, (int)lead);
+            if (claimed) list[b + (u32)__popcll(m & ((1ULL << lane) - 1))] = (u16)at;
+        }
+        return at >= 0;
+    };
+    for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
+        const u64 o0 = raw_off[p], n = raw_off[p + 1] - o0;
+        if (n == 0) continue;
+        if (n > (u64)PP_AGG_NT * RPT) {  // uniform: the generic kernel takes it
+            if (tid == 0) {
+                const u32 k = atomicAdd(spill, 1u);
+                if (k < spill_cap) spill[1 + k] = p;
+                else atomicOr((unsigned long long*)(out.tot + PPT_ERR), (unsigned long long)ERR_OVF_LOST);
+            }
+            continue;
+        }
+        // the partition's slot hash bits -> registers (records loaded with buffer loads: one 32-bit
+        // lane offset, the range check returning zeros past the partition); a record's round is the
+        // low sub_bits of its hash (the partition is the top bits, the slot position the top bits of
+        // the low word).  The records themselves are re-read when staged in their round (L2 / MALL:
+        // the partition was just streamed).
+        u32 lo[RPT];
+        const u8* base = raw + o0 * (8 * W);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * (8 * W)), 0x00020000);
+        typedef u32 v2u32 __attribute__((ext_vector_type(2)));
+        auto load_rec = [&](int u) {
+            RegRec<W> r;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * (8 * W) + 8 * w, u * (PP_AGG_NT * 8 * W), 0);
+                r.r[w] = (u64)v.x | ((u64)v.y << 32);
+            }
+            return r;
+        };
+        u32 valid = 0;
+#pragma unroll
+        for (int u0 = 0; u0 < RPT; u0 += 4) {  // 4 records in flight per lane
+            RegRec<W> rr[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (u0 + k < RPT) rr[k] = load_rec(u0 + k);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int u = u0 + k;
+                if (u >= RPT) break;
+                u64 h = hash_bits(K0, rr[k].le(0, ps_tw(K0)));
+                if (K1 >= 0) h = (h * NULL_HASH_VAL) ^ hash_bits(K1, rr[k].le(ps_tw(K0), ps_tw(K1)));
+                lo[u] = (u32)pp_mix(h);
+                valid |= ((u64)u * PP_AGG_NT + tid < n) ? (1u << u) : 0u;
+            }
+        }
+        for (u32 round = 0; round <= smask; ++round) {
+            u32 act = 0;
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) act |= (lo[u] & smask) == round ? (1u << u) : 0u;
+            act &= valid;
+            while (true) {  // mini-rounds: the round's records, then its probe-window misses
+                while (true) {  // stage <= PS_STAGE of them at a time (compacted: every lane busy)
+#pragma unroll
+                    for (int u = 0; u < RPT; ++u) {
+                        const bool on = (act >> u) & 1;
+                        const u64 m = __ballot(on);
+                        if (!m) continue;
+                        const u32 lead = (u32)__ffsll((long long)m) - 1;
+                        u32 b = 0;
+                        if (lane == lead) b = atomicAdd(&scount, (u32)__popcll(m));
+                        b = __shfl(b, (int)lead);
+                        const u32 k = b + (u32)__popcll(m & ((1ULL << lane) - 1));
+                        if (on && k < PS_STAGE) {
+                            const RegRec<W> r = load_rec(u);
+#pragma unroll
+                            for (int w = 0; w < W; ++w) sw_[(size_t)k * W + w] = r.r[w];
+                            slo[k] = lo[u];
+                            sorg[k] = (u16)((tid << 4) | (u32)u);
+                            act &= ~(1u << u);
+                        }
+                    }
+                    __syncthreads();
+                    const u32 ms = min(scount, (u32)PS_STAGE);
+                    for (u32 k0 = 0; k0 < ms; k0 += PP_AGG_NT) {
+                        const u32 k = k0 + tid;
+                        if (k < ms && !insert(k))
+                            __hip_atomic_fetch_or(pend + (sorg[k] >> 4), 1u << (sorg[k] & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    __syncthreads();
+                    if (tid == 0) scount = 0;
+                    if (!__syncthreads_or(act != 0)) break;
+                }
+                // the round's groups out as result rows, their tags cleared for the next table
+                if (tid == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
+                __syncthreads();
+                const u32 ng = nlist;
+                for (u32 k = tid; k < ng; k += PP_AGG_NT) {
+                    const u32 pos = list[k];
+                    const l64* e = body + (size_t)pos * BW;
+                    const u64 row = gbase + k;
+                    if (MODE == 1) {  // group records in the state-record format: [key words][Spec state words]
+                        if (row < out.grec_cap) {
+                            u64* d = (u64*)(out.grec + row * SH::REC_BYTES);
+#pragma unroll
+                            for (u32 w = 0; w < KW; ++w) d[w] = e[w];
+                            u32 q = KW;
+                            const u64 cnt = e[KW];
+#pragma unroll
+                            for (int a = 0; a < 3; ++a) {
+                                const int A = SH::agg(a);
+                                if (A == 0) continue;
+                                if (ps_kind(A) == PS_COUNT) d[q++] = cnt;
+                                else if (ps_kind(A) == PS_SUM) d[q++] = e[SH::sumw(a)];
+                                else {
+                                    d[q++] = e[SH::sumw(a)];
+                                    d[q++] = cnt;
+                                }
+                            }
+                        }
+                    } else if (row < out.cols.cap_groups) {
+                        RegRec<KW> kr;
+#pragma unroll
+                        for (u32 w = 0; w < KW; ++w) kr.r[w] = e[w];
+                        write_bytes(out.cols.key_data[0], row, ps_tw(K0), kr.le(0, ps_tw(K0)), 0);
+                        if (out.cols.key_valid[0]) out.cols.key_valid[0][row] = 1;
+                        if (K1 >= 0) {
+                            write_bytes(out.cols.key_data[1], row, ps_tw(K1), kr.le(ps_tw(K0), ps_tw(K1)), 0);
+                            if (out.cols.key_valid[1]) out.cols.key_valid[1][row] = 1;
+                        }
+                        const u64 cnt = e[KW];
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) {
+                            const int A = SH::agg(a);
+                            if (A == 0) continue;
+                            u64 v;
+                            if (ps_kind(A) == PS_COUNT) {
+                                v = cnt;
+                            } else if (ps_kind(A) == PS_SUM) {
+                                v = e[SH::sumw(a)];
+                            } else {  // AVG: the sum as i64 (u64 for unsigned arguments) / count, as f64
+                                const u64 sv = e[SH::sumw(a)];
+                                const double sum = ps_signed(ps_type(A)) ? (double)(i64)sv : (double)sv;
+                                v = (u64)__double_as_longlong(sum / (double)cnt);
+                            }
+                            ((u64*)out.cols.agg_data[a])[row] = v;
+                            if (out.cols.agg_valid[a]) out.cols.agg_valid[a][row] = 1;
+                        }
+                    }
+                    tags[pos] = 0;
+                }
+                __syncthreads();
+                if (tid == 0) nlist = 0;
+                act = pend[tid];
+                pend[tid] = 0;
+                if (!__syncthreads_or(act != 0)) break;
+                if (tid == 0) atomicAdd((unsigned long long*)(out.tot + PPT_ROUNDS), 1ULL);
+            }
+        }
+    }
+}
+
+// The instantiated shapes: C4 (ClickBench Q33) and the one-key COUNT / SUM forms.
+#define PS_SHAPES(X)                                                                                          \
+    X(2, DBG_INT64, DBG_INT32, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT16), PS_AGG(PS_AVG, DBG_INT16))       \
+    X(1, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), 0, 0)                                                             \
+    X(2, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT64), 0)                                     \
+    X(2, DBG_INT64, DBG_INT64, PS_AGG(PS_COUNT, 0), 0, 0)
+#define PP_SPEC_RPT 16
+
+static int ps_code(const DAgg& A) {
+    if (A.kind == DBG_AGG_COUNT) return A.arg_type < 0 ? PS_AGG(PS_COUNT, 0) : -1;
+    if (A.arg_type < 0 || A.arg_nullable || A.sumk != SUMK_I64 || A.res_width != 8) return -1;
+    const int t = A.arg_type;
+    const bool ints = t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
+                      t == DBG_UINT32 || t == DBG_UINT64;
+    if (!ints) return -1;
+    if (A.kind == DBG_AGG_SUM) return PS_AGG(PS_SUM, t);
+    if (A.kind == DBG_AGG_AVG && !A.avg_round && A.res_type == DBG_FLOAT64) return PS_AGG(PS_AVG, t);
+    return -1;
+}
+
+template <int K0, int K1, int A0, int A1, int A2>
+static bool ps_match(const Spec& S) {
+    typedef PsShape<K0, K1, A0, A1, A2> SH;
+    const int nk = SH::NK, na = (A0 ? 1 : 0) + (A1 ? 1 : 0) + (A2 ? 1 : 0);
+    if (S.pp_str || S.n_keys != nk || S.n_aggs != na || S.flags_word >= 0) return false;
+    const int kt[2] = {K0, K1};
+    for (int c = 0; c < nk; ++c)
+        if (S.key_types[c].type != kt[c] || S.key_types[c].nullable || S.koff[c] != (c == 0 ? 0u : ps_tw(K0))) return false;
+    const int ac[3] = {A0, A1, A2};
+    for (int a = 0; a < na; ++a) {
+        if (ps_code(S.aggs[a]) != ac[a]) return false;
+        if (ps_has_arg(ac[a]) && S.pp_aoff[a] != SH::off(a)) return false;
+    }
+    return S.pp_rw_raw == ((SH::END + 7) & ~7u) && S.pp_kw == 8 * SH::KW && S.pp_rw_state == SH::REC_BYTES;
+}
+
+#define PS_LDS (78 * 1024)  // two workgroups per CU
+static u32 ps_cap(u32 bw, u32 w) {
+    u32 cap = (u32)((PS_LDS - ps_lds_bytes(0, bw, w) - 64) / (4 + 8 * bw + 2)) & ~3u;
+    while (cap > 64 && ps_lds_bytes(cap, bw, w) + 64 > PS_LDS) cap -= 4;
+    return cap;
+}
+
+int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
+    int id = 0, found = -1;
+    u32 bw = 0, w = 0;
+#define PS_TRY(WW, K0, K1, A0, A1, A2)                        \
+    if (found < 0 && ps_match<K0, K1, A0, A1, A2>(S)) {     \
+        found = id;                                         \
+        bw = PsShape<K0, K1, A0, A1, A2>::BW;               \
+        w = WW;                                             \
+    }                                                       \
+    ++id;
+    PS_SHAPES(PS_TRY)
+#undef PS_TRY
+    if (found >= 0) {
+        *cap = ps_cap(bw, w);
+        *max_records = PP_AGG_NT * PP_SPEC_RPT;
+    }
+    return found;
+}
+
+void launch_pp_agg_spec(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
+                        const PPAggOut& out, u32* spill, u32 spill_cap) {
+    if (!n_parts) return;
+    const u32 grid = n_parts < 8192 ? n_parts : 8192;
+    // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
+    const char* cx = getenv("DBG_X_PPSPEC_CAP");
+    const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
+    int id = 0;
+#define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
+    if (shape == id) {                                                                                                  \
+        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW), cap_x);                          \
+        const size_t lds = ps_lds_bytes(cap, bw, WW) + 16;                                                              \
+        if (mode == 0)                                                                                                  \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_SPEC_RPT, K0, K1, A0, A1, A2>), dim3(grid), dim3(PP_AGG_NT),  \
+                               lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                       \
+        else                                                                                                            \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_SPEC_RPT, K0, K1, A0, A1, A2>), dim3(grid), dim3(PP_AGG_NT),  \
+                               lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                       \
+    }                                                                                                                   \
+    ++id;
+    PS_SHAPES(PS_LAUNCH)
+#undef PS_LAUNCH
 }
 
 // ------------------------------------------------------------------------------------------

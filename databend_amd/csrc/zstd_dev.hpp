@@ -13,8 +13,40 @@
 //
 // Tables live in LDS (one set per page); the literals of the current block go to a per-page
 // scratch of ZS_MAX_BLOCK bytes in global memory.
+//
+// The same source builds on the host (ZS_HOST: one "lane", plain loads) for the decoder's CPU
+// test against libzstd-made frames (tests/test_zstd_host.py); the device build is the product.
 #pragma once
+#ifdef ZS_HOST
+#include <cstdint>
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+#define ZS_FN static inline
+#define ZS_MFN inline
+#define ZS_CONST static const
+#define ZS_LD(p) (*(const u8*)(p))
+#define ZS_LANES 1u
+#define ZS_LANE_ID 0u
+#define ZS_WAVE_SYNC()
+#define ZS_CLZ(v) __builtin_clz(v)
+#else
 #include "device.hpp"
+#define ZS_FN __device__ __forceinline__
+#define ZS_MFN __device__ __forceinline__
+#define ZS_CONST __device__ __constant__ const
+#define ZS_LD(p) gld<u8>(p)
+#define ZS_LANES 64u
+#define ZS_LANE_ID (threadIdx.x & 63)
+#define ZS_WAVE_SYNC()                                   \
+    do {                                                 \
+        __builtin_amdgcn_wave_barrier();                 \
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); \
+        __builtin_amdgcn_wave_barrier();                 \
+    } while (0)
+#define ZS_CLZ(v) __clz(v)
+#endif
 
 #define ZS_MAX_BLOCK (128 * 1024)
 #define ZS_HUF_MAXBITS 11
@@ -36,36 +68,36 @@ struct ZsTables {
 };
 
 // ---- predefined distributions and code tables (RFC 8878 §3.1.1.3.2.2) ----
-__device__ __constant__ const short zs_ll_def[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+ZS_CONST short zs_ll_def[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
                                                     2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
-__device__ __constant__ const short zs_ml_def[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+ZS_CONST short zs_ml_def[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                                     1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
-__device__ __constant__ const short zs_of_def[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
-__device__ __constant__ const u32 zs_ll_base[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,   12,   13,   14,   15,    16,    18,
+ZS_CONST short zs_of_def[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+ZS_CONST u32 zs_ll_base[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,   12,   13,   14,   15,    16,    18,
                                                    20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
-__device__ __constant__ const u8 zs_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+ZS_CONST u8 zs_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
                                                   1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-__device__ __constant__ const u32 zs_ml_base[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12,  13,  14,  15,  16,   17,   18,   19,   20,
+ZS_CONST u32 zs_ml_base[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12,  13,  14,  15,  16,   17,   18,   19,   20,
                                                    21, 22, 23, 24, 25, 26, 27, 28, 29, 30,  31,  32,  33,  34,   35,   37,   39,   41,
                                                    43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
-__device__ __constant__ const u8 zs_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+ZS_CONST u8 zs_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                                   0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 
-__device__ __forceinline__ u32 zs_highbit(u32 v) { return 31 - __clz(v); }
+ZS_FN u32 zs_highbit(u32 v) { return 31 - ZS_CLZ(v); }
 
 // Forward little-endian bit reader over [p, p + n) (FSE table descriptions)
 struct ZsFwd {
     const u8* p;
     u64 n;      // bytes
     u64 bit;    // next bit
-    __device__ __forceinline__ u32 peek(u32 k) const {  // k <= 32; bytes past the end read as 0
+    ZS_MFN u32 peek(u32 k) const {  // k <= 32; bytes past the end read as 0
         u64 v = 0;
         const u64 b0 = bit >> 3;
         for (u32 i = 0; i < 5; ++i)
-            if (b0 + i < n) v |= (u64)gld<u8>(p + b0 + i) << (8 * i);
+            if (b0 + i < n) v |= (u64)ZS_LD(p + b0 + i) << (8 * i);
         return (u32)((v >> (bit & 7)) & ((1ULL << k) - 1));
     }
-    __device__ __forceinline__ void skip(u32 k) { bit += k; }
+    ZS_MFN void skip(u32 k) { bit += k; }
 };
 
 // Backward bit reader (RFC 8878 §4.1): the stream is read from its end; the last byte's highest
@@ -74,22 +106,22 @@ struct ZsBwd {
     const u8* p;
     u64 n;
     long long pos;
-    __device__ __forceinline__ bool init(const u8* s, u64 len) {
+    ZS_MFN bool init(const u8* s, u64 len) {
         p = s;
         n = len;
         if (!len) return false;
-        const u32 last = gld<u8>(s + len - 1);
+        const u32 last = ZS_LD(s + len - 1);
         if (!last) return false;
         pos = (long long)(8 * (len - 1) + zs_highbit(last));
         return true;
     }
-    __device__ __forceinline__ u64 window(long long at) const {  // 64 bits starting at bit `at` (may be < 0)
+    ZS_MFN u64 window(long long at) const {  // 64 bits starting at bit `at` (may be < 0)
         u64 v = 0;
         const long long b0 = at >> 3;  // floor
         for (int i = 0; i < 9; ++i) {
             const long long b = b0 + i;
             if (b >= 0 && (u64)b < n) {
-                const u64 byte = gld<u8>(p + b);
+                const u64 byte = ZS_LD(p + b);
                 const long long sh = (long long)8 * i - (at - 8 * b0);
                 if (sh >= 0 && sh < 64) v |= byte << sh;
                 else if (sh < 0 && sh > -8) v |= byte >> (-sh);
@@ -97,16 +129,16 @@ struct ZsBwd {
         }
         return v;
     }
-    __device__ __forceinline__ u64 read(u32 k) {  // k <= 56
+    ZS_MFN u64 read(u32 k) {  // k <= 56
         if (!k) return 0;
         pos -= k;
         return window(pos) & ((1ULL << k) - 1);
     }
-    __device__ __forceinline__ u32 peek(u32 k) const { return (u32)(window(pos - k) & ((1ULL << k) - 1)); }
+    ZS_MFN u32 peek(u32 k) const { return (u32)(window(pos - k) & ((1ULL << k) - 1)); }
 };
 
 // FSE_readNCount: normalized counts of symbols 0..*max_sym; returns bytes consumed (0 = bad)
-__device__ __forceinline__ u64 zs_read_ncount(const u8* p, u64 n, short* norm, u32* max_sym, u32* log, u32 max_log) {
+ZS_FN u64 zs_read_ncount(const u8* p, u64 n, short* norm, u32* max_sym, u32* log, u32 max_log) {
     ZsFwd r{p, n, 0};
     const u32 al = r.peek(4) + 5;
     r.skip(4);
@@ -158,7 +190,7 @@ __device__ __forceinline__ u64 zs_read_ncount(const u8* p, u64 n, short* norm, u
 }
 
 // FSE_buildDTable
-__device__ __forceinline__ bool zs_build_fse(ZsFse* t, const short* norm, u32 max_sym, u32 log) {
+ZS_FN bool zs_build_fse(ZsFse* t, const short* norm, u32 max_sym, u32 log) {
     const u32 size = 1u << log;
     u32 high = size - 1;
     u16 next[64];
@@ -189,16 +221,16 @@ __device__ __forceinline__ bool zs_build_fse(ZsFse* t, const short* norm, u32 ma
     return true;
 }
 
-__device__ __forceinline__ void zs_rle_fse(ZsFse* t, u32 sym) {
+ZS_FN void zs_rle_fse(ZsFse* t, u32 sym) {
     t[0].sym = (u8)sym;
     t[0].nbits = 0;
     t[0].next = 0;
 }
 
 // Huffman tree description (RFC 8878 §4.2.1) -> decoding table; returns bytes consumed (0 = bad)
-__device__ __forceinline__ u64 zs_read_huffman(const u8* p, u64 n, ZsTables& T) {
+ZS_FN u64 zs_read_huffman(const u8* p, u64 n, ZsTables& T) {
     if (!n) return 0;
-    const u32 hb = gld<u8>(p);
+    const u32 hb = ZS_LD(p);
     u32 nw = 0;
     u64 used;
     if (hb >= 128) {  // direct 4-bit weights
@@ -206,7 +238,7 @@ __device__ __forceinline__ u64 zs_read_huffman(const u8* p, u64 n, ZsTables& T) 
         used = 1 + (nw + 1) / 2;
         if (used > n) return 0;
         for (u32 i = 0; i < nw; ++i) {
-            const u32 b = gld<u8>(p + 1 + i / 2);
+            const u32 b = ZS_LD(p + 1 + i / 2);
             T.weights[i] = (u8)((i & 1) ? (b & 15) : (b >> 4));
         }
     } else {  // FSE-compressed weights, two interleaved states
@@ -274,7 +306,7 @@ __device__ __forceinline__ u64 zs_read_huffman(const u8* p, u64 n, ZsTables& T) 
 }
 
 // one Huffman-coded literal stream of `count` bytes into out (lane 0)
-__device__ __forceinline__ bool zs_huf_stream(const u8* p, u64 n, u64 count, const ZsTables& T, u8* out) {
+ZS_FN bool zs_huf_stream(const u8* p, u64 n, u64 count, const ZsTables& T, u8* out) {
     ZsBwd b;
     if (!b.init(p, n)) return false;
     const u32 mb = T.huf_bits;
@@ -288,31 +320,35 @@ __device__ __forceinline__ bool zs_huf_stream(const u8* p, u64 n, u64 count, con
 
 // Decode one zstd frame sequence occupying src[0, sn) into dst[0, dn) (exact size).  Called by
 // all 64 lanes of the wave (uniform control flow); lane 0 does the entropy decoding.
-__device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& T) {
-    const u32 lane = threadIdx.x & 63;
+ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& T) {
+    const u32 lane = ZS_LANE_ID;
+#ifdef ZS_HOST
+    u64 sh[8];
+#else
     __shared__ u64 sh[8];  // broadcast slots
+#endif
     u64 ip = 0, op = 0;
     bool bad = false;
     u32 rep[3] = {1, 4, 8};
     auto wave_copy = [&](u8* d, const u8* s, u64 len) {
-        for (u64 j = lane; j < len; j += 64) d[j] = gld<u8>(s + j);
-        __builtin_amdgcn_wave_barrier();
+        for (u64 j = lane; j < len; j += ZS_LANES) d[j] = ZS_LD(s + j);
+        ZS_WAVE_SYNC();
     };
     while (!bad && ip < sn) {
         // ---- frame header ----
         if (ip + 4 > sn) { bad = true; break; }
-        const u32 magic = gld<u8>(src + ip) | (gld<u8>(src + ip + 1) << 8) | (gld<u8>(src + ip + 2) << 16) | ((u32)gld<u8>(src + ip + 3) << 24);
+        const u32 magic = ZS_LD(src + ip) | (ZS_LD(src + ip + 1) << 8) | (ZS_LD(src + ip + 2) << 16) | ((u32)ZS_LD(src + ip + 3) << 24);
         ip += 4;
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
             if (ip + 4 > sn) { bad = true; break; }
-            const u32 sz = gld<u8>(src + ip) | (gld<u8>(src + ip + 1) << 8) | (gld<u8>(src + ip + 2) << 16) | ((u32)gld<u8>(src + ip + 3) << 24);
+            const u32 sz = ZS_LD(src + ip) | (ZS_LD(src + ip + 1) << 8) | (ZS_LD(src + ip + 2) << 16) | ((u32)ZS_LD(src + ip + 3) << 24);
             ip += 4;
             if (sz > sn - ip) { bad = true; break; }
             ip += sz;
             continue;
         }
         if (magic != 0xFD2FB528u || ip >= sn) { bad = true; break; }
-        const u32 fhd = gld<u8>(src + ip++);
+        const u32 fhd = ZS_LD(src + ip++);
         const u32 fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did = fhd & 3;
         if (fhd & 8) { bad = true; break; }  // reserved bit
         if (!single) ip += 1;                 // window descriptor
@@ -327,7 +363,7 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
         bool last = false;
         while (!bad && !last) {
             if (ip + 3 > sn) { bad = true; break; }
-            const u32 bh = gld<u8>(src + ip) | (gld<u8>(src + ip + 1) << 8) | (gld<u8>(src + ip + 2) << 16);
+            const u32 bh = ZS_LD(src + ip) | (ZS_LD(src + ip + 1) << 8) | (ZS_LD(src + ip + 2) << 16);
             ip += 3;
             last = bh & 1;
             const u32 btype = (bh >> 1) & 3, bsize = bh >> 3;
@@ -338,9 +374,9 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                 op += bsize;
             } else if (btype == 1) {  // RLE
                 if (ip >= sn || bsize > dn - op) { bad = true; break; }
-                const u8 v = gld<u8>(src + ip);
-                for (u64 j = lane; j < bsize; j += 64) dst[op + j] = v;
-                __builtin_amdgcn_wave_barrier();
+                const u8 v = ZS_LD(src + ip);
+                for (u64 j = lane; j < bsize; j += ZS_LANES) dst[op + j] = v;
+                ZS_WAVE_SYNC();
                 ip += 1;
                 op += bsize;
             } else if (btype == 2) {  // compressed: lane 0 decodes, results broadcast through LDS
@@ -352,19 +388,19 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                     u64 q = 0;
                     bool ok = true;
                     // -- literals section --
-                    const u32 b0 = bn ? gld<u8>(b) : 0;
+                    const u32 b0 = bn ? ZS_LD(b) : 0;
                     const u32 lt = b0 & 3, sf = (b0 >> 2) & 3;
                     u64 regen = 0, csize = 0;
                     u32 streams = 1;
                     if (lt <= 1) {
                         if (sf == 0 || sf == 2) { regen = b0 >> 3; q = 1; }
-                        else if (sf == 1) { regen = (b0 >> 4) + ((u64)gld<u8>(b + 1) << 4); q = 2; }
-                        else { regen = (b0 >> 4) + ((u64)gld<u8>(b + 1) << 4) + ((u64)gld<u8>(b + 2) << 12); q = 3; }
+                        else if (sf == 1) { regen = (b0 >> 4) + ((u64)ZS_LD(b + 1) << 4); q = 2; }
+                        else { regen = (b0 >> 4) + ((u64)ZS_LD(b + 1) << 4) + ((u64)ZS_LD(b + 2) << 12); q = 3; }
                     } else {
                         u64 h = 0;
                         const u32 hl = sf <= 1 ? 3 : (sf == 2 ? 4 : 5);
                         if (hl > bn) ok = false;
-                        for (u32 i = 0; ok && i < hl; ++i) h |= (u64)gld<u8>(b + i) << (8 * i);
+                        for (u32 i = 0; ok && i < hl; ++i) h |= (u64)ZS_LD(b + i) << (8 * i);
                         const u32 fb = sf <= 1 ? 10 : (sf == 2 ? 14 : 18);
                         regen = (h >> 4) & ((1ULL << fb) - 1);
                         csize = (h >> (4 + fb)) & ((1ULL << fb) - 1);
@@ -375,13 +411,13 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                     if (ok && lt == 0) {  // raw literals
                         if (regen > bn - q) ok = false;
                         else {
-                            for (u64 i = 0; i < regen; ++i) lit[i] = gld<u8>(b + q + i);
+                            for (u64 i = 0; i < regen; ++i) lit[i] = ZS_LD(b + q + i);
                             q += regen;
                         }
                     } else if (ok && lt == 1) {  // RLE literals
                         if (q >= bn) ok = false;
                         else {
-                            const u8 v = gld<u8>(b + q);
+                            const u8 v = ZS_LD(b + q);
                             for (u64 i = 0; i < regen; ++i) lit[i] = v;
                             q += 1;
                         }
@@ -402,8 +438,8 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                             } else {
                                 if (sl < 6) ok = false;
                                 else {
-                                    const u64 s1 = gld<u8>(s) | (gld<u8>(s + 1) << 8), s2 = gld<u8>(s + 2) | (gld<u8>(s + 3) << 8),
-                                              s3 = gld<u8>(s + 4) | (gld<u8>(s + 5) << 8);
+                                    const u64 s1 = ZS_LD(s) | (ZS_LD(s + 1) << 8), s2 = ZS_LD(s + 2) | (ZS_LD(s + 3) << 8),
+                                              s3 = ZS_LD(s + 4) | (ZS_LD(s + 5) << 8);
                                     const u64 per = (regen + 3) / 4;
                                     if (6 + s1 + s2 + s3 > sl || 3 * per > regen) ok = false;
                                     else {
@@ -422,14 +458,14 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                     if (ok && q >= bn) ok = false;
                     u64 nseq = 0;
                     if (ok) {
-                        const u32 c0 = gld<u8>(b + q);
+                        const u32 c0 = ZS_LD(b + q);
                         if (c0 < 128) { nseq = c0; q += 1; }
-                        else if (c0 < 255) { if (q + 2 > bn) ok = false; else { nseq = ((c0 - 128) << 8) + gld<u8>(b + q + 1); q += 2; } }
-                        else { if (q + 3 > bn) ok = false; else { nseq = gld<u8>(b + q + 1) + ((u64)gld<u8>(b + q + 2) << 8) + 0x7F00; q += 3; } }
+                        else if (c0 < 255) { if (q + 2 > bn) ok = false; else { nseq = ((c0 - 128) << 8) + ZS_LD(b + q + 1); q += 2; } }
+                        else { if (q + 3 > bn) ok = false; else { nseq = ZS_LD(b + q + 1) + ((u64)ZS_LD(b + q + 2) << 8) + 0x7F00; q += 3; } }
                     }
                     if (ok && nseq) {
                         if (q >= bn) ok = false;
-                        const u32 modes = ok ? gld<u8>(b + q++) : 0;
+                        const u32 modes = ok ? ZS_LD(b + q++) : 0;
                         if (modes & 3) ok = false;
                         // LL, OF, ML tables in that order
                         for (int k = 0; k < 3 && ok; ++k) {
@@ -448,7 +484,7 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                                 *have = 1;
                             } else if (m == 1) {  // RLE
                                 if (q >= bn) { ok = false; break; }
-                                const u32 sym = gld<u8>(b + q++);
+                                const u32 sym = ZS_LD(b + q++);
                                 if (sym > maxsym) { ok = false; break; }
                                 zs_rle_fse(t, sym);
                                 *lg = 0;
@@ -524,11 +560,10 @@ __device__ __forceinline__ bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn
                     sh[0] = op;
                     sh[1] = ok ? 0 : 1;
                 }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                ZS_WAVE_SYNC();
                 op = sh[0];
                 bad = sh[1] != 0;
-                __builtin_amdgcn_wave_barrier();
+                ZS_WAVE_SYNC();
             } else {
                 bad = true;
             }

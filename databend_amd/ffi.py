@@ -19,7 +19,7 @@ _LIB = None
 EXPORTED = [
     "dbg_version", "dbg_last_error", "dbg_device_count", "dbg_agg_result_type", "dbg_agg_create",
     "dbg_agg_destroy", "dbg_agg_set_stream", "dbg_agg_reset", "dbg_agg_add_groups", "dbg_agg_finalize",
-    "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_set_recycle", "dbg_agg_finalize_into_async", "dbg_agg_finalize_wait", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
+    "dbg_agg_result", "dbg_agg_finalize_into", "dbg_agg_set_recycle", "dbg_agg_set_partition_keys", "dbg_agg_finalize_into_async", "dbg_agg_finalize_wait", "dbg_agg_record_width", "dbg_agg_partition", "dbg_agg_export_records",
     "dbg_agg_merge_records", "dbg_agg_export_fixed", "dbg_agg_capacity", "dbg_agg_merge_fixed", "dbg_filter_select", "dbg_take_fixed", "dbg_sort_limit_indices", "dbg_sort_limit_multi", "dbg_agg_compact", "dbg_agg_retained_bytes", "dbg_prof_enable", "dbg_prof_reset",
     "dbg_prof_get", "dbg_prof_marker", "dbg_datagen", "dbg_agg_set_strategy", "dbg_agg_get_strategy",
     "dbg_agg_record_layout", "dbg_agg_set_host_staging",
@@ -76,6 +76,7 @@ def lib():
         L.dbg_agg_result.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), C.c_int]
         L.dbg_agg_finalize_into.argtypes = [VP, P(abi.dbg_out_column), P(abi.dbg_out_column), U64, P(U64), P(U64), P(U64)]
         L.dbg_agg_set_recycle.argtypes = [VP, C.c_int]
+        L.dbg_agg_set_partition_keys.argtypes = [VP, C.c_int]
         L.dbg_agg_set_host_staging.argtypes = [VP, U64]
         L.dbg_comm_get_unique_id.argtypes = [VP]
         L.dbg_comm_create.argtypes = [VP, C.c_int, C.c_int, C.c_int, P(VP)]

@@ -22,7 +22,7 @@ from .device import DeviceColumn, empty
 from .ffi import check, lib
 
 # TableCompression (storages/common/table_meta/src/table/table_compression.rs:25-31) -> codec
-COMPRESSION_CODEC = {"none": abi.PQ_UNCOMPRESSED, "snappy": abi.PQ_SNAPPY, "lz4": abi.PQ_LZ4_RAW}
+COMPRESSION_CODEC = {"none": abi.PQ_UNCOMPRESSED, "snappy": abi.PQ_SNAPPY, "lz4": abi.PQ_LZ4_RAW, "zstd": abi.PQ_ZSTD}
 
 
 @dataclass

@@ -266,6 +266,13 @@ int dbg_agg_finalize_wait(dbg_agg_handle* h, uint64_t* n_groups, uint64_t* strin
  * must therefore stay unchanged until that next call returns — true of DataBlocks, which are
  * immutable once produced (EXP/block.rs).  Launch errors of the insert surface from that call. */
 int dbg_agg_set_recycle(dbg_agg_handle* h, int on);
+/* Bucket groups in dbg_agg_partition schemes 0 / 1 by the group hash of their first `n_keys` key
+ * columns (0 = all, the default).  A DISTINCT aggregate's pair table (keys..., x) set to the
+ * query's key count lands every pair in the bucket of its group (AggregateDistinctCombinator's set
+ * travels inside the group's state, src/query/functions/src/aggregates/
+ * aggregate_combinator_distinct.rs:94-105).  Table strategy only (DBG_ERR_UNSUPPORTED once the
+ * handle is partitioned). */
+int dbg_agg_set_partition_keys(dbg_agg_handle* h, int n_keys);
 
 /* Host-block staging (default off).  The reference hands TransformPartialAggregate blocks of at
  * most max_block_size = 65,536 rows (src/query/settings/src/settings_default.rs:131), one
@@ -295,8 +302,9 @@ int dbg_agg_set_host_staging(dbg_agg_handle* h, uint64_t rows);
  * final partitions; dbg_agg_export_fixed / dbg_agg_merge_fixed return DBG_ERR_UNSUPPORTED. */
 enum { DBG_STRATEGY_AUTO = 0, DBG_STRATEGY_TABLE = 1, DBG_STRATEGY_PARTITIONED = 2 };
 int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy);
-/* *partitioned = the handle's current mode; *extra_rounds (may be NULL) = partitions of the last
- * partitioned finalize whose groups needed more than one LDS round. */
+/* *partitioned = the handle's current mode (0 table, 1 partitioned payload, 2 partitioned payload
+ * whose last finalize ran the compile-time specialised aggregation); *extra_rounds (may be NULL) =
+ * partitions of the last partitioned finalize whose groups needed more than one LDS round. */
 int dbg_agg_get_strategy(dbg_agg_handle* h, int* partitioned, uint64_t* extra_rounds);
 
 /* ---- partial-state records: exchange / partition bucket (EAGG/payload.rs:356-391,

@@ -3,6 +3,8 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r4d
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "filter or fused or pred or fast or partitioned_insert or bench" "tests/test_gpu_fullsize.py::test_c3_full_1b" "tests/test_gpu_fullsize.py::test_c2_full_100m" > gpurun_out/r4d/pytest.log 2>&1 || { tail -30 gpurun_out/r4d/pytest.log; exit 1; }
 tail -2 gpurun_out/r4d/pytest.log
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parquet.py tests/test_gpu_legacy_buckets.py tests/test_legacy_hash.py -m gpu > gpurun_out/r4d/pytest2.log 2>&1 || { tail -30 gpurun_out/r4d/pytest2.log; exit 1; }
+tail -2 gpurun_out/r4d/pytest2.log
 for nt in 512 1024; do
   DBG_X_SLICE_NT=$nt timeout -k 10 180 python -u scripts/step_timing_cfg.py 3 4 > gpurun_out/r4d/steps_c3_$nt.json 2>&1 || { tail -5 gpurun_out/r4d/steps_c3_$nt.json; exit 1; }
   echo "slice $nt $(tail -1 gpurun_out/r4d/steps_c3_$nt.json)"

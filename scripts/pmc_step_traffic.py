@@ -1,7 +1,8 @@
 """HBM traffic per step from two rocprofv3 --pmc passes over scripts/pmc_run.py (FETCH_SIZE and
 WRITE_SIZE in separate runs), corrected as MI355X_MICROARCH.md's HBM section prescribes: the
-counters are in KiB; on gfx950 FETCH_SIZE counts wide coalesced streaming reads at half their
-bytes, so it is doubled; WRITE_SIZE is taken as reported.  Every dispatch between the two
+counters are in KiB; on gfx950 FETCH_SIZE counts every 128-B read request (streaming or a random
+probe's miss) as 64 B, so it is doubled; WRITE_SIZE is taken as reported (calibrated against known
+bytes and the TCC_EA0_RDREQ/WRREQ request counters: profiles/r04/pmc_calibration.json).  Every dispatch between the two
 dbg_marker_kernel dispatches belongs to the timed steps.
 
     python scripts/pmc_step_traffic.py gpurun_out/pmc_c4 STEPS profiles/pmc_traffic_c4.json [algorithmic_bytes]
@@ -67,8 +68,8 @@ def main():
         "algorithmic_bytes": alg,
         "traffic_over_algorithmic": (read_b + write_b) / alg if alg else None,
         "kernels_per_step": kernels,
-        "correction": "FETCH_SIZE x2 (gfx950 counts 16 B/lane streaming reads at half their bytes), KiB -> bytes; "
-                      "WRITE_SIZE as reported (MI355X_MICROARCH.md, HBM section)",
+        "correction": "FETCH_SIZE x2 (gfx950 counts each 128-B read request, streaming or random, as 64 B: "
+                      "profiles/r04/pmc_calibration.json), KiB -> bytes; WRITE_SIZE as reported",
         "source": os.path.relpath(d),
     }
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)

@@ -17,7 +17,7 @@ from databend_amd import column as col
 from databend_amd.scan import ColumnChunk
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CODEC = {"UNCOMPRESSED": abi.PQ_UNCOMPRESSED, "SNAPPY": abi.PQ_SNAPPY, "LZ4": abi.PQ_LZ4_RAW, "LZ4_RAW": abi.PQ_LZ4_RAW}
+CODEC = {"UNCOMPRESSED": abi.PQ_UNCOMPRESSED, "SNAPPY": abi.PQ_SNAPPY, "LZ4": abi.PQ_LZ4_RAW, "LZ4_RAW": abi.PQ_LZ4_RAW, "ZSTD": abi.PQ_ZSTD}
 PTYPE = {"BOOLEAN": abi.PQ_BOOLEAN, "INT32": abi.PQ_INT32, "INT64": abi.PQ_INT64, "INT96": abi.PQ_INT96,
          "FLOAT": abi.PQ_FLOAT, "DOUBLE": abi.PQ_DOUBLE, "BYTE_ARRAY": abi.PQ_BYTE_ARRAY,
          "FIXED_LEN_BYTE_ARRAY": abi.PQ_FIXED_LEN_BYTE_ARRAY}

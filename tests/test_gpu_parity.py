@@ -59,6 +59,7 @@ def gpu_aggregate(keys, aggs, filt=None, on_device=False, capacity_hint=0, batch
         block = ht.merge_result()
         if info is not None:
             info["partitioned"], info["extra_rounds"] = ht.strategy()
+            info["specialised"] = ht.pp_specialised()
     finally:
         ht.close()
     na = len(aggs)

@@ -245,3 +245,42 @@ def test_pp_record_centric(kind):
     w = Column.from_numbers(col.Int16, rng.integers(0, 2560, n))
     g, info = check_pp(keys, [("count", None), ("sum", i16), ("sql_avg", w), ("min", w)], on_device=True)
     assert g > 1_000_000
+
+
+@pytest.mark.parametrize("kind", ["c4_unique", "c4_dup", "c4_skewed", "i64_count", "i64_sum", "i64_i64", "small_table"])
+def test_pp_specialised_kernel(kind, monkeypatch):
+    """The compile-time specialised aggregation (pp.hip pp_agg_spec_kernel) on every instantiated
+    shape: C4 (Int64, Int32 keys; COUNT(*), SUM(Int16), AVG(Int16)) with mostly-unique keys, a few
+    records per key, and a skewed key whose partition exceeds the kernel's register budget (spilled
+    to the generic kernel); one-key COUNT / COUNT+SUM and two-Int64-key COUNT; and a forced small
+    LDS table (probe-window misses re-inserted in pending rounds) — all against the oracle."""
+    rng = np.random.default_rng(len(kind) * 7 + 1)
+    n = 4_000_000
+    i16 = Column.from_numbers(col.Int16, rng.integers(-3, 3, n))
+    w = Column.from_numbers(col.Int16, rng.integers(-2560, 2560, n))
+    aggs = [("count", None), ("sum", i16), ("sql_avg", w)]
+    if kind in ("c4_unique", "small_table"):
+        keys = [Column.from_numbers(col.Int64, rng.permutation(n).astype(np.int64) * 7919 - 3),
+                Column.from_numbers(col.Int32, rng.integers(-2**31, 2**31 - 1, n))]
+    elif kind == "c4_dup":
+        keys = [Column.from_numbers(col.Int64, rng.integers(0, n // 3, n)), Column.from_numbers(col.Int32, rng.integers(0, 2, n))]
+    elif kind == "c4_skewed":
+        k = rng.integers(0, n, n)
+        k[rng.random(n) < 0.2] = 42  # 20 % of the rows in one group: its partition is spilled
+        keys = [Column.from_numbers(col.Int64, k), Column.from_numbers(col.Int32, np.zeros(n, dtype=np.int64))]
+    elif kind == "i64_count":
+        keys = [Column.from_numbers(col.Int64, rng.integers(-2**62, 2**62, n))]
+        aggs = [("count", None)]
+    elif kind == "i64_sum":
+        keys = [Column.from_numbers(col.Int64, rng.integers(0, n // 2, n))]
+        aggs = [("count", None), ("sum", Column.from_numbers(col.Int64, rng.integers(-2**50, 2**50, n)))]
+    else:
+        keys = [Column.from_numbers(col.Int64, rng.integers(0, n, n)), Column.from_numbers(col.Int64, rng.integers(0, 3, n))]
+        aggs = [("count", None)]
+    if kind == "small_table":
+        monkeypatch.setenv("DBG_X_PPSPEC_CAP", "256")
+    g, info = check_pp(keys, aggs, on_device=True, batches=2)
+    assert info["specialised"]
+    assert g > 1_000_000 or kind == "c4_dup"
+    if kind == "small_table":
+        assert info["extra_rounds"] > 0
