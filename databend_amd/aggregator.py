@@ -486,6 +486,10 @@ class AggregateMeta:
     data: Optional[List["AggregateMeta"]] = None
     serialized: Optional[DataBlock] = None
     legacy: bool = False  # a legacy HashMethod partial's bucket (-1 = single-level, else 0..255)
+    # DISTINCT aggregates: per distinct aggregate j, the bucket's distinct (keys..., x_j) pairs —
+    # the AggregateDistinctCombinator sets that travel inside their groups' states in the reference
+    # (FUN/aggregate_combinator_distinct.rs:94-105), bucketed by the group keys alone
+    distinct: Optional[List[Payload]] = None
 
     @staticmethod
     def create_agg_payload(bucket: int, payload: Payload, max_partition_count: int) -> "AggregateMeta":
@@ -559,8 +563,17 @@ class TransformPartialAggregate:
                  staging_rows: int = DEFAULT_STAGING_ROWS, compact_bytes: int = DEFAULT_COMPACT_BYTES):
         self.params = params
         self.config = (config or HashTableConfig()).with_partial(True)
-        self.hashtable = AggregateHashTable(params, self.config, device)
-        if staging_rows:
+        self.distinct = None
+        if any(f.distinct for f in params.aggregate_functions):
+            # a DISTINCT aggregate forces the table to its max radix bits (:146-155); its sets are
+            # pair tables beside the main one (databend_amd/distinct.py)
+            from .distinct import DistinctPartial
+            self.config = self.config.with_initial_radix_bits(self.config.max_radix_bits)
+            self.distinct = DistinctPartial(params, device)
+            self.hashtable = self.distinct.table
+        else:
+            self.hashtable = AggregateHashTable(params, self.config, device)
+        if staging_rows and self.distinct is None:
             self.hashtable.set_host_staging(staging_rows)
         # once the copies of host blocks a referenced-key table keeps exceed this, the table is
         # compacted to its groups (0 = never)
@@ -577,6 +590,9 @@ class TransformPartialAggregate:
         from the block by index; the block's rows are added to the HBM table."""
         groups = [block.columns[i] for i in group_indices]
         args = [None if i is None else block.columns[i] for i in arg_indices]
+        if self.distinct is not None:
+            self.distinct.add_groups(groups, args, block.num_rows(), filter_program)
+            return []
         self.hashtable.add_groups(groups, args, rows=block.num_rows(), filter_program=filter_program)
         # compact on the bytes retained since the last compaction, not on the total: the compacted
         # group records themselves count towards the total, and once they alone pass the limit a
@@ -595,6 +611,8 @@ class TransformPartialAggregate:
         reference converts after the block that reaches it, :330-350; groups only grow, so the
         final count decides the same), then emits the non-empty of 256 buckets
         hash2bucket<8, true>(FastHash(key)) (HT/partitioned_hashtable.rs:77-83)."""
+        if self.distinct is not None:
+            return self.distinct.on_finish(1 << self.config.max_radix_bits)
         n_groups = sum(self.hashtable.partition(1, 1)[0])
         if not self.params.enable_experimental_aggregate_hashtable:
             if not n_groups:
@@ -613,7 +631,10 @@ class TransformPartialAggregate:
         return [AggregateMeta.create_agg_payload(b, p, 1 << bits) for b, p in enumerate(payloads) if len(p)]
 
     def close(self):
-        self.hashtable.close()
+        if self.distinct is not None:
+            self.distinct.close()
+        else:
+            self.hashtable.close()
 
 
 class TransformPartitionBucket:
@@ -635,6 +656,9 @@ class TransformPartitionBucket:
         """partition_payload (:389-429) for AggregatePayload, partition_block (:341-387) for
         Serialized: the rows re-inserted into a scratch table (merge_states / batch_merge), then
         exported as records at the larger radix."""
+        if meta.distinct is not None:
+            from .distinct import repartition_distinct
+            return repartition_distinct(self.params, meta, max_partition_count, self.device)
         scratch = AggregateHashTable(self.params, HashTableConfig(True), self.device)
         try:
             if meta.is_serialized():
@@ -697,6 +721,9 @@ class TransformFinalAggregate:
         """AggregatePayload -> combine_payload (merge_states); Serialized -> add_groups with the
         Binary states (batch_merge), as transform_agg_hashtable does for each variant."""
         items = list(meta.data) if meta.is_partitioned() else [meta]
+        if any(f.distinct for f in self.params.aggregate_functions):
+            from .distinct import final_distinct
+            return final_distinct(self.params, items, self.device)
         items = [m for m in items if (m.is_serialized() and m.serialized.num_rows()) or
                  (m.payload is not None and len(m.payload))]
         if not items:

@@ -1697,13 +1697,13 @@ __device__ __forceinline__ u64 ps_ext(u64 v, int t) {  // argument bits -> the w
 // LDS of one workgroup: [tags u32 cap][body u64 cap x BW][list u16 cap][stage: words u64 PS_STAGE x W,
 // slot hash u32 PS_STAGE, origin u16 PS_STAGE][pending u32 PP_AGG_NT]
 #define PS_STAGE 1024
-__host__ __device__ constexpr size_t ps_lds_bytes(u32 cap, u32 bw, u32 w) {
+__host__ __device__ constexpr size_t ps_lds_bytes(u32 cap, u32 bw, u32 w, u32 nt) {
     return 8 * (size_t)((cap + 1) / 2) + (size_t)cap * 8 * bw + 2 * (size_t)((cap + 3) & ~3u) + (size_t)PS_STAGE * (8 * w + 4 + 2) +
-           4 * (size_t)PP_AGG_NT;
+           4 * (size_t)nt;
 }
 
-template <int MODE, int W, int RPT, int K0, int K1, int A0, int A1, int A2>
-__global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
+template <int MODE, int W, int RPT, int SNT, int K0, int K1, int A0, int A1, int A2>
+__global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
                                                                u32 sub_bits, u32 cap, PPAggOut out, u32* __restrict__ spill, u32 spill_cap) {
     typedef PsShape<K0, K1, A0, A1, A2> SH;
     constexpr u32 KW = SH::KW, BW = SH::BW;
@@ -1715,13 +1715,13 @@ __global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, 
     l64* sw_ = (l64*)(list + ((cap + 3) & ~3u));                   // staged records [PS_STAGE][W]
     l32* slo = (l32*)(sw_ + (size_t)PS_STAGE * W);                 // their slot hash bits
     l16* sorg = (l16*)(slo + PS_STAGE);                            // their origin (thread << 4 | register index)
-    l32* pend = (l32*)(((uintptr_t)(sorg + PS_STAGE) + 3) & ~(uintptr_t)3);  // [PP_AGG_NT] probe-window misses
+    l32* pend = (l32*)(((uintptr_t)(sorg + PS_STAGE) + 3) & ~(uintptr_t)3);  // [SNT] probe-window misses
     __shared__ u32 nlist, scount;
     __shared__ u64 gbase;
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 smask = (1u << sub_bits) - 1;
     const u32 win = cap < PP_WINDOW ? cap : PP_WINDOW;
-    for (u32 j = tid; j < cap; j += PP_AGG_NT) tags[j] = 0;
+    for (u32 j = tid; j < cap; j += SNT) tags[j] = 0;
     pend[tid] = 0;
     if (tid == 0) nlist = scount = 0;
     __syncthreads();
@@ -1786,10 +1786,37 @@ __global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, 
         }
         return at >= 0;
     };
+    // A partition's records live in registers (RPT per lane, loaded with buffer loads: one 32-bit
+    // lane offset, the range check returning zeros past the partition), and the next partition of
+    // this workgroup is loaded into a second register set while the current one is aggregated.
+    typedef u32 v2u32 __attribute__((ext_vector_type(2)));
+    auto load_part = [&](u32 q, RegRec<W>* dst, u64& n_out) {
+        n_out = 0;
+        if (q >= n_parts) return;
+        const u64 o0 = raw_off[q], n = raw_off[q + 1] - o0;
+        n_out = n;
+        if (n == 0 || n > (u64)SNT * RPT) return;
+        const u8* base = raw + o0 * (8 * W);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * (8 * W)), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < RPT; ++u)
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * (8 * W) + 8 * w, u * (SNT * 8 * W), 0);
+                dst[u].r[w] = (u64)v.x | ((u64)v.y << 32);
+            }
+    };
+    RegRec<W> nxt[RPT];
+    u64 n_nxt;
+    load_part(blockIdx.x, nxt, n_nxt);
     for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
-        const u64 o0 = raw_off[p], n = raw_off[p + 1] - o0;
+        RegRec<W> rr[RPT];
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) rr[u] = nxt[u];
+        const u64 n = n_nxt;
+        load_part(p + gridDim.x, nxt, n_nxt);  // in flight during this partition's rounds
         if (n == 0) continue;
-        if (n > (u64)PP_AGG_NT * RPT) {  // uniform: the generic kernel takes it
+        if (n > (u64)SNT * RPT) {  // uniform: the generic kernel takes it
             if (tid == 0) {
                 const u32 k = atomicAdd(spill, 1u);
                 if (k < spill_cap) spill[1 + k] = p;
@@ -1797,45 +1824,26 @@ __global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, 
             }
             continue;
         }
-        // the partition's slot hash bits -> registers (records loaded with buffer loads: one 32-bit
-        // lane offset, the range check returning zeros past the partition); a record's round is the
-        // low sub_bits of its hash (the partition is the top bits, the slot position the top bits of
-        // the low word).  The records themselves are re-read when staged in their round (L2 / MALL:
-        // the partition was just streamed).
-        u32 lo[RPT];
-        const u8* base = raw + o0 * (8 * W);
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * (8 * W)), 0x00020000);
-        typedef u32 v2u32 __attribute__((ext_vector_type(2)));
-        auto load_rec = [&](int u) {
-            RegRec<W> r;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * (8 * W) + 8 * w, u * (PP_AGG_NT * 8 * W), 0);
-                r.r[w] = (u64)v.x | ((u64)v.y << 32);
-            }
-            return r;
+        // slot hash bits; a record's round is the low sub_bits of its hash (the partition is the
+        // top bits, the slot position the top bits of the low word)
+        auto slot_hash = [&](const RegRec<W>& r) -> u32 {
+            u64 h = hash_bits(K0, r.le(0, ps_tw(K0)));
+            if (K1 >= 0) h = (h * NULL_HASH_VAL) ^ hash_bits(K1, r.le(ps_tw(K0), ps_tw(K1)));
+            return (u32)pp_mix(h);
         };
+        u32 rdp[(RPT + 3) / 4];  // rounds, 8 bits each (the hash is recomputed when a record is staged)
         u32 valid = 0;
 #pragma unroll
-        for (int u0 = 0; u0 < RPT; u0 += 4) {  // 4 records in flight per lane
-            RegRec<W> rr[4];
+        for (int q = 0; q < (RPT + 3) / 4; ++q) rdp[q] = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (u0 + k < RPT) rr[k] = load_rec(u0 + k);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int u = u0 + k;
-                if (u >= RPT) break;
-                u64 h = hash_bits(K0, rr[k].le(0, ps_tw(K0)));
-                if (K1 >= 0) h = (h * NULL_HASH_VAL) ^ hash_bits(K1, rr[k].le(ps_tw(K0), ps_tw(K1)));
-                lo[u] = (u32)pp_mix(h);
-                valid |= ((u64)u * PP_AGG_NT + tid < n) ? (1u << u) : 0u;
-            }
+        for (int u = 0; u < RPT; ++u) {
+            rdp[u / 4] |= (slot_hash(rr[u]) & smask) << (8 * (u % 4));
+            valid |= ((u64)u * SNT + tid < n) ? (1u << u) : 0u;
         }
         for (u32 round = 0; round <= smask; ++round) {
             u32 act = 0;
 #pragma unroll
-            for (int u = 0; u < RPT; ++u) act |= (lo[u] & smask) == round ? (1u << u) : 0u;
+            for (int u = 0; u < RPT; ++u) act |= ((rdp[u / 4] >> (8 * (u % 4))) & 0xff) == round ? (1u << u) : 0u;
             act &= valid;
             while (true) {  // mini-rounds: the round's records, then its probe-window misses
                 while (true) {  // stage <= PS_STAGE of them at a time (compacted: every lane busy)
@@ -1850,17 +1858,16 @@ __global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, 
                         b = __shfl(b, (int)lead);
                         const u32 k = b + (u32)__popcll(m & ((1ULL << lane) - 1));
                         if (on && k < PS_STAGE) {
-                            const RegRec<W> r = load_rec(u);
 #pragma unroll
-                            for (int w = 0; w < W; ++w) sw_[(size_t)k * W + w] = r.r[w];
-                            slo[k] = lo[u];
+                            for (int w = 0; w < W; ++w) sw_[(size_t)k * W + w] = rr[u].r[w];
+                            slo[k] = slot_hash(rr[u]);
                             sorg[k] = (u16)((tid << 4) | (u32)u);
                             act &= ~(1u << u);
                         }
                     }
                     __syncthreads();
                     const u32 ms = min(scount, (u32)PS_STAGE);
-                    for (u32 k0 = 0; k0 < ms; k0 += PP_AGG_NT) {
+                    for (u32 k0 = 0; k0 < ms; k0 += SNT) {
                         const u32 k = k0 + tid;
                         if (k < ms && !insert(k))
                             __hip_atomic_fetch_or(pend + (sorg[k] >> 4), 1u << (sorg[k] & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1873,7 +1880,7 @@ __global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, 
                 if (tid == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
                 __syncthreads();
                 const u32 ng = nlist;
-                for (u32 k = tid; k < ng; k += PP_AGG_NT) {
+                for (u32 k = tid; k < ng; k += SNT) {
                     const u32 pos = list[k];
                     const l64* e = body + (size_t)pos * BW;
                     const u64 row = gbase + k;
@@ -1945,6 +1952,7 @@ __global__ void __launch_bounds__(PP_AGG_NT, 4) pp_agg_spec_kernel(u32 n_parts, 
     X(2, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT64), 0)                                     \
     X(2, DBG_INT64, DBG_INT64, PS_AGG(PS_COUNT, 0), 0, 0)
 #define PP_SPEC_RPT 16
+#define PP_SPEC_NT 512
 
 static int ps_code(const DAgg& A) {
     if (A.kind == DBG_AGG_COUNT) return A.arg_type < 0 ? PS_AGG(PS_COUNT, 0) : -1;
@@ -1974,11 +1982,11 @@ static bool ps_match(const Spec& S) {
     return S.pp_rw_raw == ((SH::END + 7) & ~7u) && S.pp_kw == 8 * SH::KW && S.pp_rw_state == SH::REC_BYTES;
 }
 
-#define PS_LDS (78 * 1024)  // two workgroups per CU
+#define PS_LDS (152 * 1024)  // one workgroup per CU: the largest table, the fewest rounds
 static u32 ps_cap(u32 bw, u32 w) {
-    u32 cap = (u32)((PS_LDS - ps_lds_bytes(0, bw, w) - 64) / (4 + 8 * bw + 2)) & ~3u;
-    while (cap > 64 && ps_lds_bytes(cap, bw, w) + 64 > PS_LDS) cap -= 4;
-    return cap;
+    u32 cap = (u32)((PS_LDS - ps_lds_bytes(0, bw, w, PP_SPEC_NT) - 64) / (4 + 8 * bw + 2)) & ~3u;
+    while (cap > 64 && ps_lds_bytes(cap, bw, w, PP_SPEC_NT) + 64 > PS_LDS) cap -= 4;
+    return std::min<u32>(cap, 65532);
 }
 
 int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
@@ -1995,7 +2003,7 @@ int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
 #undef PS_TRY
     if (found >= 0) {
         *cap = ps_cap(bw, w);
-        *max_records = PP_AGG_NT * PP_SPEC_RPT;
+        *max_records = PP_SPEC_NT * PP_SPEC_RPT;
     }
     return found;
 }
@@ -2003,7 +2011,7 @@ int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
 void launch_pp_agg_spec(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
                         const PPAggOut& out, u32* spill, u32 spill_cap) {
     if (!n_parts) return;
-    const u32 grid = n_parts < 8192 ? n_parts : 8192;
+    const u32 grid = n_parts < 256 ? n_parts : 256;  // one persistent workgroup per CU
     // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
     const char* cx = getenv("DBG_X_PPSPEC_CAP");
     const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
@@ -2011,13 +2019,13 @@ void launch_pp_agg_spec(hipStream_t s, int shape, int mode, u32 n_parts, const u
 #define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
     if (shape == id) {                                                                                                  \
         const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW), cap_x);                          \
-        const size_t lds = ps_lds_bytes(cap, bw, WW) + 16;                                                              \
+        const size_t lds = ps_lds_bytes(cap, bw, WW, PP_SPEC_NT) + 16;                                                  \
         if (mode == 0)                                                                                                  \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_SPEC_RPT, K0, K1, A0, A1, A2>), dim3(grid), dim3(PP_AGG_NT),  \
-                               lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                       \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
+                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
         else                                                                                                            \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_SPEC_RPT, K0, K1, A0, A1, A2>), dim3(grid), dim3(PP_AGG_NT),  \
-                               lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                       \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
+                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
     }                                                                                                                   \
     ++id;
     PS_SHAPES(PS_LAUNCH)

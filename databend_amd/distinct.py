@@ -23,6 +23,15 @@ Declaring the plain aggregates' arguments nullable does not change them: every r
 and every result that can be NULL is already Nullable through the OrNull adaptor (count stays
 UInt64, count(*) becomes count of a never-NULL dummy).  Between the phases only group counts reach
 the host; the pairs never leave the device.
+
+Inside the processors (TransformPartialAggregate / TransformPartitionBucket /
+TransformFinalAggregate, aggregator.py) the same split crosses the stages: the partial keeps T and
+one pair table per distinct aggregate (`DistinctPartial`), at the max radix bits the reference
+forces for DISTINCT (AGG/transform_aggregate_partial.rs:146-155); on_finish exports T's buckets
+and each pair table's buckets bucketed by the group keys alone (dbg_agg_set_partition_keys), so a
+bucket's pairs are exactly its groups' value sets — the combinator's state — and travel with it
+(AggregateMeta.distinct).  The final stage (`final_distinct`) merges T's records, dedupes each
+pair set across partials in a final pair table, and feeds the pairs into T as above.
 """
 from __future__ import annotations
 
@@ -33,7 +42,7 @@ import numpy as np
 
 from . import abi
 from .aggregates import AggregateFunction, AggregateFunctionFactory
-from .aggregator import AggregateHashTable, AggregatorParams, HashTableConfig
+from .aggregator import AggregateHashTable, AggregateMeta, AggregatorParams, HashTableConfig, export_buckets
 from .column import Column, DataBlock, DataType
 from .ffi import Unsupported
 
@@ -190,3 +199,155 @@ def count_distinct(group_columns: Sequence[Column], arg: Column, filter_pred=Non
     params = AggregatorParams([k.dtype for k in keys], [F.get("count_distinct", [], [arg.dtype])])
     prog = FilterProgram(filter_pred, [c.to_abi() for c in filter_columns]) if filter_pred is not None else None
     return DistinctAggregator(params).run(keys, [arg], filter_program=prog)
+
+
+# ---- the processor form (aggregator.py): pair sets crossing the partial -> final boundary ----
+
+def _t_params(params: AggregatorParams) -> AggregatorParams:
+    fns = []
+    for f in params.aggregate_functions:
+        if f.arg is None:
+            fns.append(replace(f, arg=_DUMMY, distinct=False))
+        else:
+            fns.append(replace(f, arg=f.arg.wrap_nullable(), distinct=False))
+    return AggregatorParams(list(params.group_data_types), fns)
+
+
+def _pair_params(params: AggregatorParams, j: int) -> AggregatorParams:
+    F = AggregateFunctionFactory.instance()
+    return AggregatorParams(list(params.group_data_types) + [params.aggregate_functions[j].arg], [F.get("count")])
+
+
+def _pair_table(params: AggregatorParams, j: int, partial: bool, device: int) -> AggregateHashTable:
+    t = AggregateHashTable(_pair_params(params, j), HashTableConfig(partial), device)
+    t.set_strategy(abi.STRATEGY_TABLE)  # bucketing by the key prefix is a table-strategy export
+    t.set_partition_keys(len(params.group_data_types))
+    return t
+
+
+class DistinctPartial:
+    """TransformPartialAggregate's state for a query with DISTINCT aggregates: the main table T
+    (plain aggregates; the distinct ones' arguments NULL) and one pair table per distinct
+    aggregate, all fed from the same blocks."""
+
+    def __init__(self, params: AggregatorParams, device: int = -1):
+        _check_supported(params.group_data_types, params.aggregate_functions)
+        self.params = params
+        self.device = device
+        self.t_params = _t_params(params)
+        self.table = AggregateHashTable(self.t_params, HashTableConfig(True), device)
+        self.distinct_idx = [j for j, f in enumerate(params.aggregate_functions) if f.distinct]
+        self.pairs = {j: _pair_table(params, j, True, device) for j in self.distinct_idx}
+        self._keep = []
+
+    def add_groups(self, group_columns, args, rows: int, filter_program=None) -> None:
+        on_device = not isinstance(group_columns[0], Column)
+        fns = self.params.aggregate_functions
+        nulls = _NullSource(rows, on_device)
+        ones = _Ones(rows, on_device)
+        a = []
+        for j, f in enumerate(fns):
+            if f.distinct:
+                a.append(nulls.column(f.arg, rows))
+            elif args[j] is None:
+                a.append(ones.column(rows))
+            else:
+                a.append(args[j].to_abi())
+        self.table.add_groups_abi([c.to_abi() for c in group_columns], a, rows, filter_program, on_device)
+        for j in self.distinct_idx:
+            self.pairs[j].add_groups(list(group_columns) + [args[j]], [None], rows=rows, filter_program=filter_program,
+                                     on_device=on_device)
+        if on_device:  # the device inputs of the staged launches must outlive them
+            self._keep.append((nulls, ones))
+
+    def on_finish(self, n_parts: int) -> List[AggregateMeta]:
+        t_b = export_buckets(self.table, n_parts)
+        p_b = {j: export_buckets(self.pairs[j], n_parts) for j in self.distinct_idx}
+        out = []
+        for b in range(n_parts):
+            d = [p_b[j][b] for j in self.distinct_idx]
+            if len(t_b[b]) or any(len(x) for x in d):
+                out.append(AggregateMeta(b, t_b[b], n_parts, distinct=d))
+        return out
+
+    def close(self):
+        self.table.close()
+        for t in self.pairs.values():
+            t.close()
+        self._keep.clear()
+
+
+def repartition_distinct(params: AggregatorParams, meta: AggregateMeta, n_parts: int, device: int = -1) -> List[AggregateMeta]:
+    """TransformPartitionBucket's alignment of a DISTINCT meta written with fewer buckets: T's
+    payload and every pair payload re-exported at n_parts buckets (pairs by their group keys)."""
+    import torch
+    t_params = _t_params(params)
+    idx = [j for j, f in enumerate(params.aggregate_functions) if f.distinct]
+    scratch = AggregateHashTable(t_params, HashTableConfig(True), device)
+    pts = {j: _pair_table(params, j, True, device) for j in idx}
+    try:
+        p = meta.payload
+        if p is not None and len(p):
+            scratch.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
+        for j, q in zip(idx, meta.distinct):
+            if len(q):
+                pts[j].merge_records(q.records, q.strings, [q.n_records], [q.string_bytes])
+        t_b = export_buckets(scratch, n_parts)
+        p_b = {j: export_buckets(pts[j], n_parts) for j in idx}
+        torch.cuda.current_stream().synchronize()
+    finally:
+        scratch.close()
+        for t in pts.values():
+            t.close()
+    out = []
+    for b in range(n_parts):
+        d = [p_b[j][b] for j in idx]
+        if len(t_b[b]) or any(len(x) for x in d):
+            out.append(AggregateMeta(b, t_b[b], n_parts, distinct=d))
+    return out
+
+
+def final_distinct(params: AggregatorParams, items: Sequence[AggregateMeta], device: int = -1) -> DataBlock:
+    """TransformFinalAggregate for one bucket of a query with DISTINCT aggregates: T merges every
+    partial's states; each distinct aggregate's pairs are deduplicated across partials in a final
+    pair table, then enter T as that aggregate's argument (the other aggregates' arguments NULL)."""
+    if any(m.is_serialized() for m in items):
+        raise Unsupported(abi.DBG_ERR_UNSUPPORTED, "serialized DISTINCT states (borsh sets) stay on the CPU final")
+    t_params = _t_params(params)
+    fns = params.aggregate_functions
+    idx = [j for j, f in enumerate(fns) if f.distinct]
+    if not any((m.payload is not None and len(m.payload)) or any(len(x) for x in (m.distinct or [])) for m in items):
+        return params.empty_result_block()
+    final = AggregateHashTable(t_params, HashTableConfig(False), device)
+    keep = []
+    try:
+        for m in items:
+            p = m.payload
+            if p is not None and len(p):
+                final.merge_records(p.records, p.strings, [p.n_records], [p.string_bytes])
+        for jj, j in enumerate(idx):
+            pt = _pair_table(params, j, False, device)
+            try:
+                for m in items:
+                    q = m.distinct[jj]
+                    if len(q):
+                        pt.merge_records(q.records, q.strings, [q.n_records], [q.string_bytes])
+                pairs = pt.merge_result_device()[1:]  # [keys..., x]
+            finally:
+                pt.close()
+            keep.append(pairs)
+            n = len(pairs[0])
+            if n == 0:
+                continue
+            nulls = _NullSource(n, True)
+            keep.append(nulls)
+            a = []
+            for i, f in enumerate(fns):
+                if i == j:
+                    a.append(pairs[-1].to_abi())
+                else:
+                    a.append(nulls.column(_DUMMY if f.arg is None else f.arg, n))
+            final.add_groups_abi([c.to_abi() for c in pairs[:-1]], a, n, None, True)
+        return final.merge_result()
+    finally:
+        final.close()

@@ -148,3 +148,65 @@ def test_distinct_without_keys_is_unsupported():
     params = AggregatorParams([], [F.get("count_distinct", [], [col.Int64])])
     with pytest.raises(Unsupported):
         DistinctAggregator(params)
+
+
+@pytest.mark.parametrize("mixed_bits", [False, True])
+def test_distinct_through_partial_bucket_final(mixed_bits):
+    """DISTINCT inside the processors (AGG/transform_aggregate_partial.rs:146-155 forces the max
+    radix bits; the combinator's set travels with its group): two partials over host blocks, each
+    with the main table and a pair table per distinct aggregate; TransformPartitionBucket aligns
+    (mixed_bits: one partial written at fewer buckets, re-exported pairs bucketed by the group
+    keys alone); TransformFinalAggregate merges T and dedupes the pairs across partials per bucket.
+    Every bucket holds only its own groups; the union equals the single-node DistinctAggregator
+    and the Python restatement of the combinator."""
+    from databend_amd.aggregator import (DataBlock, HashTableConfig, TransformFinalAggregate, TransformPartialAggregate,
+                                         TransformPartitionBucket)
+    from oracle import oracle
+    from tests.test_gpu_parity import slice_col
+    rng = np.random.default_rng(77)
+    n = 300_000
+    region = Column.from_numbers(col.Int32, rng.integers(0, 500, n))
+    user = Column.from_numbers(col.Int64, rng.integers(0, 30_000, n) * 7919, validity=rng.random(n) > 0.05)
+    adv = Column.from_numbers(col.Int16, np.where(rng.random(n) < 0.9, 0, rng.integers(1, 33, n)))
+    s = Column.from_strings([b"s%d" % v for v in rng.integers(0, 40, n)])
+    aggs = [("sum", adv), ("count", None), ("count_distinct", user), ("count_distinct", s)]
+    fns = [F.get(fn, [], [c.dtype] if c is not None else []) for fn, c in aggs]
+    params = AggregatorParams([region.dtype], fns)
+    cols = [region, adv, user, s]
+    arg_idx = [1, None, 2, 3]
+    cfg_a = HashTableConfig(max_radix_bits=5)
+    cfg_b = HashTableConfig(max_radix_bits=3 if mixed_bits else 5)
+    pa, pb = TransformPartialAggregate(params, cfg_a), TransformPartialAggregate(params, cfg_b)
+    try:
+        half = n // 2
+        for p, lo, hi in ((pa, 0, half), (pb, half, n)):
+            for b in range(lo, hi, 65536):
+                e = min(hi, b + 65536)
+                p.transform(DataBlock([slice_col(c, b, e) for c in cols]), [0], arg_idx)
+        metas = pa.on_finish() + pb.on_finish()
+        assert all(m.distinct is not None and len(m.distinct) == 2 for m in metas)
+        bucket = TransformPartitionBucket(params)
+        bucket.push(metas)
+        parts = bucket.finish()
+        maxp = 32
+        final = TransformFinalAggregate(params)
+        out = {}
+        for part in parts:
+            blk = final.transform(part)
+            ks = blk.columns[4:]
+            if not len(ks[0]):
+                continue
+            h = oracle.group_hash(ks)
+            assert (((h & np.uint64((1 << 48) - 1)) >> np.uint64(48 - 5)) == part.bucket).all()
+            for i, kk in enumerate(ks[0].values()):
+                assert kk not in out
+                out[kk] = tuple(c.values()[i] for c in blk.columns[:4])
+    finally:
+        pa.close()
+        pb.close()
+    ref = DistinctAggregator(params).run([region], [adv, None, user, s])
+    exp = {kk: tuple(c.values()[i] for c in ref.columns[:4]) for i, kk in enumerate(ref.columns[4].values())}
+    assert out == exp
+    cd = _expected_distinct(region, "count", user)
+    assert {k: v[2] for k, v in out.items()} == cd
+    assert maxp == 32
