@@ -163,6 +163,7 @@ struct dbg_agg_handle {
     u64* counters = nullptr;   // device, CNT_WORDS
     u64* hcounters = nullptr;  // pinned
     u64* hcounters_dev = nullptr;  // its device mapping (finalize_small writes it directly)
+    u64* dense = nullptr;          // fused_dense's direct-mapped counts + presence bitmap (zero between launches)
     // overflow lists (deferred)
     u64* ovf_rows = nullptr;
     u64 ovf_rows_cap = 0;
@@ -869,7 +870,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
                     h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->d_lpart, h->vbytes, h->part_sorted, h->part_bounds,
-                    h->part_temp, h->ser_err};
+                    h->part_temp, h->ser_err, h->dense};
     for (void* p : bufs)
         if (p) hipFree(p);
     for (auto& K : h->ppk) {
@@ -1392,6 +1393,8 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
                 hipDeviceSynchronize();
                 hipMemcpy(v, x_pptrace, 64, hipMemcpyDeviceToHost);
                 const double n = v[5] ? (double)v[5] : 1.0;
+                fprintf(stderr, "pptrace raw us/partition [0..4] %.2f %.2f %.2f %.2f %.2f (spec kernel: load+hash, stage, insert, "
+                                "emit, barriers)\n", v[0] * 0.01 / n, v[1] * 0.01 / n, v[2] * 0.01 / n, v[3] * 0.01 / n, v[4] * 0.01 / n);
                 fprintf(stderr, "pptrace partitions %llu groups/partition %.0f  per partition us: insert %.2f sync %.2f "
                                 "atomic %.2f write %.2f tail %.2f\n", (unsigned long long)v[5], v[6] / n, v[0] * 0.01 / n,
                         v[1] * 0.01 / n, v[2] * 0.01 / n, v[3] * 0.01 / n, v[4] * 0.01 / n);
@@ -2039,6 +2042,25 @@ static int fin_launch(dbg_agg_handle* h) {
         ff.on = 1;
         ff.table_empty = h->def_clean ? 1 : 0;
         ff.trace = nullptr;
+        ff.dense = nullptr;
+        ff.dense_n = 0;
+        {  // COUNT(*) over a <= 16-bit key into a recycled table: the direct-mapped hand-off
+            // measured and not kept (C2 step 45.1 -> 138 us: 256 workgroups' device atomics on the
+            // same ~33 addresses serialise at the memory side, profiles/r04/c2_dense_ab.json):
+            // EXPERIMENT, DBG_X_DENSE=1
+            static const bool dense_on = getenv("DBG_X_DENSE") && getenv("DBG_X_DENSE")[0] == '1';
+            const int kt = S.key_types[0].type;
+            const u32 kw = (kt == DBG_INT8 || kt == DBG_UINT8) ? 1 : ((kt == DBG_INT16 || kt == DBG_UINT16) ? 2 : 0);
+            const bool co = S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1;
+            if (dense_on && kw && co && h->def_clean && S.n_keys == 1) {
+                if (!h->dense) {
+                    RETURN_IF(dev_alloc((void**)&h->dense, (65536 + 1024) * 8));
+                    HIPCHECK(hipMemsetAsync(h->dense, 0, (65536 + 1024) * 8, h->stream));
+                }
+                ff.dense = h->dense;
+                ff.dense_n = kw == 1 ? 256u : 65536u;
+            }
+        }
         static u64* x_trace = nullptr;  // EXPERIMENT (DBG_X_TRACE): 8 words per launch, 4096 launches
         static std::vector<u64> x_init;
         if (kPhaseTrace && getenv("DBG_X_TRACE")) {

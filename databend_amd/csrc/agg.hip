@@ -1322,6 +1322,110 @@ __device__ __forceinline__ bool view_find(u64* view, const TableDesc& t, u64 key
     return false;
 }
 
+// The end of a fused COUNT(*) launch over keys of <= 16 bits (ClickBench Q8: Int16 AdvEngineID):
+// a direct-mapped hand-off instead of the parked-row tree.  Every workgroup adds its LDS table's
+// counts into a dense array indexed by the key (device atomics without return, issued as soon as
+// it has streamed its share — overlapping the workgroups still streaming) and sets the key's bit
+// in a presence bitmap, then takes the launch ticket; the last arrival reads the bitmap and the
+// counts of the set bits (zeroing both behind it for the next launch), merges them into an LDS
+// view of the table and runs the count-only finalize.  The critical path after the last workgroup
+// streams is one atomic drain, one ticket and two dependent loads — against the tree's two park /
+// ticket / reload levels — and the merge no longer grows with the grid.
+template <typename T>
+__device__ __forceinline__ void fused_dense(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots,
+                                            u32 sw, u32* lcount, u32 nt, const TableDesc& t, u32 my_claims, u32 my_ovf,
+                                            const FusedFin& ff) {
+    __shared__ u32 role, bad, vcl, wg_ovf;
+    __shared__ u64 hbm_claims, ovf_seen;
+    const u32 dn = ff.dense_n, dmask = dn - 1;
+    u64* dcnt = ff.dense;
+    u64* dbits = ff.dense + dn;
+    if (threadIdx.x == 0) wg_ovf = 0;
+    // 1. the LDS table into the dense array (no return values: the stores drain before the ticket)
+    for (u32 s = threadIdx.x; s < lds_slots; s += nt) {
+        const u64* p = lds + (u64)s * sw;
+        const u64 e = p[0];
+        if (e == SLOT_EMPTY) continue;
+        const u32 idx = (u32)e & dmask;
+        __hip_atomic_fetch_add(dcnt + idx, p[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(dbits + (idx >> 6), 1ULL << (idx & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (my_claims) atomicAdd(&lcount[1], my_claims);
+    if (my_ovf) atomicAdd(&wg_ovf, my_ovf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (lcount[1]) {
+            atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const u64 add = 1 + ((u64)lcount[1] << 16) + ((u64)wg_ovf << 40);
+        const u64 tk = atomicAdd((unsigned long long*)(t.counters + CNT_FIN_TICKET), (unsigned long long)add) + add;
+        role = (tk & 0xFFFF) == gridDim.x ? 1u : 0u;
+        hbm_claims = (tk >> 16) & 0xFFFFFF;
+        ovf_seen = tk >> 40;
+    }
+    __syncthreads();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (!role) return;
+    // 2. the last arrival: view of the table, the dense groups merged into it, finalize
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
+        atomicExch((unsigned long long*)(t.counters + CNT_TAIL), 0ULL);  // every workgroup has left its tail
+        bad = 0;
+        vcl = 0;
+        lcount[2] = 0;
+        if (kPhaseTrace && ff.trace) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
+    }
+    const u64 n = (t.cap + 1) * sw;  // host: <= the launch's dynamic LDS
+    if (ff.table_empty && hbm_claims == 0)
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = S.slot_init[i % sw];
+    else
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = ld_sc1(t.slots + i);
+    __syncthreads();
+    u32 vclaims = 0;
+    for (u32 w = threadIdx.x; w < (dn >> 6); w += nt) {
+        u64 b = ld_sc1(dbits + w);
+        if (!b) continue;
+        st_sc1(dbits + w, 0);
+        while (b) {
+            const u32 j = (u32)__builtin_ctzll(b);
+            b &= b - 1;
+            const u32 idx = (w << 6) | j;
+            const u64 c = ld_sc1(dcnt + idx);
+            st_sc1(dcnt + idx, 0);
+            const u64 key = (u64)idx;  // the inline packed key of a <= 16-bit column: its raw bits
+            u64 slot;
+            if (view_find(lds, t, key, vclaims, slot)) {
+                lds[slot * sw + 1] += c;  // one thread per key
+            } else {  // an overflow record (the host grows the table and finalizes again)
+                const u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), 1ULL);
+                if (k < t.ovf_recs_cap) {
+                    u64* r = t.ovf_recs + k * t.stride_words;
+                    r[0] = key;
+                    r[1] = c;
+                } else {
+                    atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+                }
+                bad = 1;
+            }
+        }
+    }
+    if (vclaims) atomicAdd(&vcl, vclaims);
+    __syncthreads();
+    const bool known = ff.table_empty && ovf_seen == 0 && !bad;
+    if (threadIdx.x == 0 && vcl && !known) {
+        atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)vcl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
+    finalize_count_only<T>(t, lds, ff, known, vcl);
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
+}
+
 // The low-cardinality end of a fused insert + finalize launch (ClickBench Q8: 32 groups in every
 // workgroup's LDS table).  The HBM table is not written on the way: partial tables travel as
 // parked rows up a two-level tree and are merged in LDS, and the last workgroup finalizes from
@@ -1906,6 +2010,12 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         atomicMin((unsigned long long*)ff.trace + 1, (unsigned long long)tm);
         atomicMax((unsigned long long*)ff.trace + 2, (unsigned long long)tm);
     }
+    if constexpr (CO && sizeof(T) <= 2) {
+        if (ff.on && ff.dense && t.scratch != nullptr && gridDim.x > 1 && gridDim.x < 65536) {
+            fused_dense<T>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims, my_ovf, ff);
+            return;
+        }
+    }
     if (ff.on && t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks) {
         fused_chain<T, CO>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims, my_ovf, ff);
         return;
@@ -1941,7 +2051,11 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (lo > hi) { lo = 1; hi = 0; }  // stays empty in T (1 > 0 for every T)
     const int nt = 1024;
     static_assert(FIN_NT == 1024, "the fused finalize runs on the insert's workgroup");
-    const u64 max_blocks = 256;  // one 1024-lane workgroup per CU (512 / 768 / 1024 / 2048 measured: 52 / 55 / 63 / 90 us a C2 step)
+    // one 1024-lane workgroup per CU (parked-row chain: 512 / 768 / 1024 / 2048 measured 52 / 55 / 63
+    // / 90 us a C2 step); EXPERIMENT DBG_X_FAST_GRID for the dense hand-off, whose merge does not
+    // grow with the grid
+    static const u64 x_grid = getenv("DBG_X_FAST_GRID") ? (u64)atoll(getenv("DBG_X_FAST_GRID")) : 0;
+    const u64 max_blocks = (x_grid && fused && fused->dense) ? x_grid : 256;
     size_t shmem = fast_shmem(table_bytes);
     FusedFin ff;
     if (fused) ff = *fused;

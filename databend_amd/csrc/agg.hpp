@@ -277,6 +277,10 @@ struct FusedFin {
     int on;
     int table_empty;  // the HBM table held no group when the launch started (fused chain)
     u64* trace;  // EXPERIMENT (DBG_X_TRACE): phase timestamps of this launch, s_memrealtime ticks
+    // direct-mapped hand-off for COUNT(*) over keys of <= 16 bits (fused_dense): dense_n counts then
+    // dense_n / 64 bitmap words, all zero between launches; nullptr = the parked-row chain
+    u64* dense;
+    u32 dense_n;
 };
 // host side: would launch_insert of this batch take the fast kernel (and so could fuse)?
 bool insert_can_fuse(const Spec& S, const BatchDesc& hb, u64 cap);

@@ -1716,15 +1716,43 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
     l32* slo = (l32*)(sw_ + (size_t)PS_STAGE * W);                 // their slot hash bits
     l16* sorg = (l16*)(slo + PS_STAGE);                            // their origin (thread << 4 | register index)
     l32* pend = (l32*)(((uintptr_t)(sorg + PS_STAGE) + 3) & ~(uintptr_t)3);  // [SNT] probe-window misses
-    __shared__ u32 nlist, scount;
+    __shared__ u32 nlist, scount, anyw[3];
     __shared__ u64 gbase;
     const u32 tid = threadIdx.x, lane = tid & 63;
+    // Barriers order LDS only: the output stores and the next partition's prefetched loads stay in
+    // flight across them (__syncthreads' workgroup fence would wait for every outstanding global
+    // access — the prefetch included).
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // block-wide OR over three rotating LDS words: call c clears the word call c + 1 votes into
+    // before its barrier (that word was last read in call c - 2, before call c - 1's barrier)
+    u32 anyc = 0;
+    auto block_any = [&](bool v) -> bool {
+        const u32 q = anyc % 3;
+        if (tid == 0) anyw[(q + 1) % 3] = 0;
+        if (__ballot(v) && lane == 0) atomicOr(&anyw[q], 1u);
+        lds_barrier();
+        ++anyc;
+        return anyw[q] != 0;
+    };
     const u32 smask = (1u << sub_bits) - 1;
     const u32 win = cap < PP_WINDOW ? cap : PP_WINDOW;
+    // EXPERIMENT (TRACE=1 build, DBG_X_PPTRACE): phase times of sampled workgroups, thread 0
+    const bool tr = kPhaseTrace && out.trace && (blockIdx.x & 15) == 0 && tid == 0;
+    u64 tm0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto tick = [&](int slot) {
+        if (tr) {
+            const u64 tm = __builtin_amdgcn_s_memrealtime();
+            atomicAdd((unsigned long long*)out.trace + slot, tm - tm0);
+            tm0 = tm;
+        }
+    };
     for (u32 j = tid; j < cap; j += SNT) tags[j] = 0;
     pend[tid] = 0;
-    if (tid == 0) nlist = scount = 0;
-    __syncthreads();
+    if (tid == 0) {
+        nlist = scount = 0;
+        anyw[0] = anyw[1] = anyw[2] = 0;
+    }
+    lds_barrier();
     // one staged record into the table; false = no room in its probe window
     auto insert = [&](u32 k) -> bool {
         RegRec<W> rk;
@@ -1824,6 +1852,7 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
             }
             continue;
         }
+        if (tr) atomicAdd((unsigned long long*)out.trace + 5, 1ULL);
         // slot hash bits; a record's round is the low sub_bits of its hash (the partition is the
         // top bits, the slot position the top bits of the low word)
         auto slot_hash = [&](const RegRec<W>& r) -> u32 {
@@ -1831,54 +1860,69 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
             if (K1 >= 0) h = (h * NULL_HASH_VAL) ^ hash_bits(K1, r.le(ps_tw(K0), ps_tw(K1)));
             return (u32)pp_mix(h);
         };
-        u32 rdp[(RPT + 3) / 4];  // rounds, 8 bits each (the hash is recomputed when a record is staged)
+        u32 lo[RPT];  // slot hash bits; the round is the low sub_bits
         u32 valid = 0;
 #pragma unroll
-        for (int q = 0; q < (RPT + 3) / 4; ++q) rdp[q] = 0;
-#pragma unroll
         for (int u = 0; u < RPT; ++u) {
-            rdp[u / 4] |= (slot_hash(rr[u]) & smask) << (8 * (u % 4));
+            lo[u] = slot_hash(rr[u]);
             valid |= ((u64)u * SNT + tid < n) ? (1u << u) : 0u;
         }
+        tick(0);  // the partition's loads landed, hashed
         for (u32 round = 0; round <= smask; ++round) {
             u32 act = 0;
 #pragma unroll
-            for (int u = 0; u < RPT; ++u) act |= ((rdp[u / 4] >> (8 * (u % 4))) & 0xff) == round ? (1u << u) : 0u;
+            for (int u = 0; u < RPT; ++u) act |= (lo[u] & smask) == round ? (1u << u) : 0u;
             act &= valid;
             while (true) {  // mini-rounds: the round's records, then its probe-window misses
                 while (true) {  // stage <= PS_STAGE of them at a time (compacted: every lane busy)
+                    // one LDS add per wave for all RPT slots: the ballots first (no memory ops),
+                    // then the wave's base, then each slot's running offset (wave-uniform)
+                    u64 mb[RPT];
+                    u32 wtot = 0;
 #pragma unroll
                     for (int u = 0; u < RPT; ++u) {
+                        mb[u] = __ballot((act >> u) & 1);
+                        wtot += (u32)__popcll(mb[u]);
+                    }
+                    u32 wbase = 0;
+                    if (wtot) {
+                        if (lane == 0) wbase = atomicAdd(&scount, wtot);
+                        wbase = __builtin_amdgcn_readfirstlane(wbase);
+                    }
+                    u32 run = wbase;
+#pragma unroll
+                    for (int u = 0; u < RPT; ++u) {
+                        const u64 m = mb[u];
                         const bool on = (act >> u) & 1;
-                        const u64 m = __ballot(on);
-                        if (!m) continue;
-                        const u32 lead = (u32)__ffsll((long long)m) - 1;
-                        u32 b = 0;
-                        if (lane == lead) b = atomicAdd(&scount, (u32)__popcll(m));
-                        b = __shfl(b, (int)lead);
-                        const u32 k = b + (u32)__popcll(m & ((1ULL << lane) - 1));
+                        const u32 k = run + (u32)__popcll(m & ((1ULL << lane) - 1));
+                        run += (u32)__popcll(m);
                         if (on && k < PS_STAGE) {
 #pragma unroll
                             for (int w = 0; w < W; ++w) sw_[(size_t)k * W + w] = rr[u].r[w];
-                            slo[k] = slot_hash(rr[u]);
+                            slo[k] = lo[u];
                             sorg[k] = (u16)((tid << 4) | (u32)u);
                             act &= ~(1u << u);
                         }
                     }
-                    __syncthreads();
+                    tick(1);
+                    lds_barrier();
+                    tick(4);
                     const u32 ms = min(scount, (u32)PS_STAGE);
                     for (u32 k0 = 0; k0 < ms; k0 += SNT) {
                         const u32 k = k0 + tid;
                         if (k < ms && !insert(k))
                             __hip_atomic_fetch_or(pend + (sorg[k] >> 4), 1u << (sorg[k] & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    __syncthreads();
+                    tick(2);
+                    lds_barrier();
                     if (tid == 0) scount = 0;
-                    if (!__syncthreads_or(act != 0)) break;
+                    const bool more = block_any(act != 0);
+                    tick(4);
+                    if (!more) break;
                 }
                 // the round's groups out as result rows, their tags cleared for the next table
                 if (tid == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
-                __syncthreads();
+                lds_barrier();
                 const u32 ng = nlist;
                 for (u32 k = tid; k < ng; k += SNT) {
                     const u32 pos = list[k];
@@ -1934,11 +1978,13 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
                     }
                     tags[pos] = 0;
                 }
-                __syncthreads();
+                tick(3);
+                lds_barrier();
+                tick(4);
                 if (tid == 0) nlist = 0;
                 act = pend[tid];
                 pend[tid] = 0;
-                if (!__syncthreads_or(act != 0)) break;
+                if (!block_any(act != 0)) break;
                 if (tid == 0) atomicAdd((unsigned long long*)(out.tot + PPT_ROUNDS), 1ULL);
             }
         }
