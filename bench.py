@@ -505,7 +505,7 @@ def measure_scan(steps: int, rows: int = 1 << 26) -> dict:
     adv = np.where(rng.random(rows) < 0.9937, 0, rng.integers(1, 33, rows)).astype(np.int16)
     res = {"workload": "clickbench AdvEngineID (Int16) column, 2^26 rows (one row group), Fuse parquet shape", "rows": rows}
     dec = ParquetChunkDecoder()
-    for comp in ("NONE", "SNAPPY"):
+    for comp in ("NONE", "SNAPPY", "ZSTD"):
         t = pa.table({"a": pa.array(adv)}, schema=pa.schema([pa.field("a", pa.int16(), nullable=False)]))
         bio = io.BytesIO()
         pq.write_table(t, bio, compression=comp, use_dictionary=False, row_group_size=1 << 30, data_page_size=1 << 20)
@@ -520,7 +520,7 @@ def measure_scan(steps: int, rows: int = 1 << 26) -> dict:
         c.len = len(chunk)
         c.physical_type = abi.PQ_INT32
         c.max_def_level = 0
-        c.codec = abi.PQ_UNCOMPRESSED if comp == "NONE" else abi.PQ_SNAPPY
+        c.codec = {"NONE": abi.PQ_UNCOMPRESSED, "SNAPPY": abi.PQ_SNAPPY, "ZSTD": abi.PQ_ZSTD}[comp]
         out_t = torch.empty(rows * 2, dtype=torch.uint8, device="cuda")
         o = abi.dbg_out_column()
         o.data = out_t.data_ptr()

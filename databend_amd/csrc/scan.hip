@@ -74,19 +74,23 @@ struct ScanArgs {
     u32* nwalk;        // [n_pages] values found by pq_walk
     u64* sptr;         // [rows] String payload source addresses (page buffer or chunk)
     u8* out_data;      // target values (BOOLEAN: value bytes, packed afterwards)
+    int32_t need_vb;   // the definition bytes are read afterwards (nullable target / NULL check)
     u64* out_offs;     // String: lengths, then the scan
     u64* err;
 };
 
 // ---------------------------------------------------------------------------------------------
-// Decompression (one wave per page).  Loads of the compressed stream are wave-uniform.
+// Decompression (one wave per page): the compressed stream is staged into an LDS window with
+// coalesced loads and its tags parsed from there (wave-uniform); literal and match bytes are
+// copied by all 64 lanes.
 // ---------------------------------------------------------------------------------------------
 #define RING 65536
-__device__ __forceinline__ u32 ld_u8(const u8* p) { return *(const volatile u8*)p; }
 
+#define IWIN 16384  // the compressed stream's window in LDS: tags are parsed from LDS, not HBM
 template <int CODEC>
 __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     __shared__ u8 ring[RING];
+    __shared__ u8 inw[IWIN];
     const ScanPage pg = a.pages[blockIdx.x];
     const u32 lane = threadIdx.x;
     // an uncompressed page is decoded where it lies in the chunk (page_base): nothing to copy
@@ -103,6 +107,19 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     const u32 sn = pg.comp - pg.lv, on = pg.uncomp - pg.lv;
     bool bad = false;
     u32 p = 0, w = 0;  // input / output cursors (uniform)
+    // bytes [wb, we) of the stream are staged in inw; rd(q) reads stream byte q (wb <= q < we),
+    // need(k) restages from p when fewer than k bytes (or the end of the stream) remain staged
+    u32 wb = 0, we = 0;
+    auto need = [&](u32 k) {
+        if (p >= wb && (p + k <= we || we == sn)) return;
+        wb = p;
+        we = sn - p < IWIN ? sn : p + IWIN;
+        __builtin_amdgcn_wave_barrier();  // every lane is done reading the old window
+        for (u32 j = lane; j < we - wb; j += 64) inw[j] = s[wb + j];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    auto rd = [&](u32 q) -> u32 { return inw[q - wb]; };
     // bounds are compared without wrapping (p <= sn and w <= on hold throughout): a 4-byte
     // Snappy literal length near 2^32 must fail here, not wrap past the check
     auto copy_lit = [&](u64 len) {
@@ -135,16 +152,18 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     };
     if (CODEC == DBG_PQ_SNAPPY) {
         u32 n = 0, sh = 0;  // preamble: uncompressed length (varint)
+        need(5);
         for (;;) {
             if (p >= sn || sh > 28) { bad = true; break; }
-            const u32 c = ld_u8(s + p++);
+            const u32 c = rd(p++);
             n |= (c & 0x7F) << sh;
             sh += 7;
             if (!(c & 0x80)) break;
         }
         if (n != on) bad = true;
         while (!bad && p < sn) {
-            const u32 tag = ld_u8(s + p++);
+            need(5);  // a tag and its length / offset bytes
+            const u32 tag = rd(p++);
             const u32 kind = tag & 3;
             if (kind == 0) {
                 u32 len = tag >> 2;
@@ -152,7 +171,7 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
                     const u32 nb = len - 59;
                     if (p + nb > sn) { bad = true; break; }
                     len = 0;
-                    for (u32 k = 0; k < nb; ++k) len |= ld_u8(s + p + k) << (8 * k);
+                    for (u32 k = 0; k < nb; ++k) len |= rd(p + k) << (8 * k);
                     p += nb;
                 }
                 copy_lit((u64)len + 1);
@@ -161,17 +180,17 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
                 if (kind == 1) {
                     if (p + 1 > sn) { bad = true; break; }
                     len = ((tag >> 2) & 7) + 4;
-                    off = ((tag >> 5) << 8) | ld_u8(s + p);
+                    off = ((tag >> 5) << 8) | rd(p);
                     p += 1;
                 } else if (kind == 2) {
                     if (p + 2 > sn) { bad = true; break; }
                     len = (tag >> 2) + 1;
-                    off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8);
+                    off = rd(p) | (rd(p + 1) << 8);
                     p += 2;
                 } else {
                     if (p + 4 > sn) { bad = true; break; }
                     len = (tag >> 2) + 1;
-                    off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8) | (ld_u8(s + p + 2) << 16) | (ld_u8(s + p + 3) << 24);
+                    off = rd(p) | (rd(p + 1) << 8) | (rd(p + 2) << 16) | (rd(p + 3) << 24);
                     p += 4;
                 }
                 copy_back(off, len);
@@ -179,12 +198,14 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
         }
     } else {  // LZ4 block: [token][literal length+][literals][offset u16][match length+]
         while (!bad && p < sn) {
-            const u32 tok = ld_u8(s + p++);
+            need(16);
+            const u32 tok = rd(p++);
             u64 lit = tok >> 4;
             if (lit == 15)
                 for (;;) {
                     if (p >= sn) { bad = true; break; }
-                    const u32 c = ld_u8(s + p++);
+                    need(1);
+                    const u32 c = rd(p++);
                     lit += c;
                     if (c != 255) break;
                 }
@@ -192,13 +213,15 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
             copy_lit(lit);
             if (bad || p >= sn) break;  // the last sequence has literals only
             if (p + 2 > sn) { bad = true; break; }
-            const u32 off = ld_u8(s + p) | (ld_u8(s + p + 1) << 8);
+            need(2);
+            const u32 off = rd(p) | (rd(p + 1) << 8);
             p += 2;
             u64 ml = tok & 15;
             if (ml == 15)
                 for (;;) {
                     if (p >= sn) { bad = true; break; }
-                    const u32 c = ld_u8(s + p++);
+                    need(1);
+                    const u32 c = rd(p++);
                     ml += c;
                     if (c != 255) break;
                 }
@@ -470,7 +493,8 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
     // 1. definition levels -> one byte per row
     if (split) {
         const u32 per = (n + gridDim.y - 1) / gridDim.y, lo = blockIdx.y * per, hi = min(n, lo + per);
-        for (u32 k = lo + threadIdx.x; k < hi; k += DEC_NT) vb[k] = 1;
+        if (a.need_vb)
+            for (u32 k = lo + threadIdx.x; k < hi; k += DEC_NT) vb[k] = 1;
     } else if (a.max_def) {
         if (!hybrid_expand(base, d0, d1, 1, n, rt, [&](u32 k, u32 v) { vb[k] = (u8)(v != 0); })) return fail(SERR_MALFORMED);
     } else {
@@ -571,6 +595,59 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
         }
         return bad;
     };
+    if (split && (pw == 4 || pw == 8) && a.ptype != DBG_PQ_FIXED_LEN_BYTE_ARRAY && a.ttype != DBG_DECIMAL128 && a.twidth <= pw &&
+        (u64)vp + (u64)n * pw <= pg.uncomp) {
+        // required PLAIN 4- / 8-byte values into an integer / float target: 4 values per lane from
+        // aligned dword loads (the page's values start at any byte: funnel shifts), narrowed to the
+        // target width and stored as one 4 x width word when the row is aligned
+        const u32 per = (n + gridDim.y - 1) / gridDim.y;
+        const u32 lo = min(n, ((blockIdx.y * per) + 3) & ~3u), hi = min(n, (((blockIdx.y + 1) * per) + 3) & ~3u);
+        const u8* vbase = base + vp;
+        const u32 tw = a.twidth;
+        for (u32 k0 = lo + 4 * threadIdx.x; k0 < hi; k0 += 4 * DEC_NT) {
+            const u32 cnt = min(4u, hi - k0);
+            const u8* p = vbase + (u64)k0 * pw;
+            // byte-aligned values: gfx950 global loads take unaligned addresses (the compiler emits
+            // whole-dword loads for these memcpys), consecutive lanes read consecutive 16 B
+            u64 v[4] = {0, 0, 0, 0};
+            if (cnt == 4 && pw == 4) {
+                u32 w[4];
+                __builtin_memcpy(w, p, 16);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = w[j];
+            } else if (cnt == 4) {
+                __builtin_memcpy(v, p, 32);
+            } else {
+                for (u32 j = 0; j < cnt; ++j) {
+                    if (pw == 4) {
+                        u32 x;
+                        __builtin_memcpy(&x, p + 4 * j, 4);
+                        v[j] = x;
+                    } else {
+                        __builtin_memcpy(&v[j], p + 8 * j, 8);
+                    }
+                }
+            }
+            u8* dst = a.out_data + (pg.row0 + k0) * (u64)tw;
+            if (tw == 2 && cnt == 4 && !((uintptr_t)dst & 7)) {
+                *(u64*)dst = (v[0] & 0xFFFF) | ((v[1] & 0xFFFF) << 16) | ((v[2] & 0xFFFF) << 32) | ((v[3] & 0xFFFF) << 48);
+            } else if (tw == 4 && cnt == 4 && !((uintptr_t)dst & 15)) {
+                typedef u32 v4u32 __attribute__((ext_vector_type(4)));
+                *(v4u32*)dst = v4u32{(u32)v[0], (u32)v[1], (u32)v[2], (u32)v[3]};
+            } else {
+                for (u32 j = 0; j < cnt; ++j) {
+                    u8* dj = dst + (u64)j * tw;
+                    switch (tw) {
+                        case 1: *dj = (u8)v[j]; break;
+                        case 2: *(uint16_t*)dj = (uint16_t)v[j]; break;
+                        case 4: *(u32*)dj = (u32)v[j]; break;
+                        default: *(u64*)dj = v[j]; break;
+                    }
+                }
+            }
+        }
+        return;
+    }
     if (split) {
         const u32 per = (n + gridDim.y - 1) / gridDim.y, lo = blockIdx.y * per, hi = min(n, lo + per);
         bool bad = false;
@@ -950,6 +1027,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     a.nwalk = ctx->nwalk;
     a.sptr = ctx->sptr;
     a.out_data = is_bool ? ctx->bools : (u8*)out->data;
+    a.need_vb = (target.nullable || c.max_def_level) ? 1 : 0;
     a.out_offs = out->offsets;
     a.err = ctx->err;
     if (!pages.empty()) {

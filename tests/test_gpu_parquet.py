@@ -195,3 +195,35 @@ def test_errors_not_faults(dec):
         dec.decode(c2, target_of(a2, nullable=False))
     # the decoder is still usable afterwards
     assert check_file(dec, buf) == 2
+
+
+@pytest.mark.parametrize("comp", ["NONE", "SNAPPY", "ZSTD"])
+def test_required_plain_vectorised(dec, comp):
+    """Required (non-null) PLAIN 4- and 8-byte physical values — the vectorised decode path: four
+    values per lane from aligned dword loads with funnel shifts (page value sections start at any
+    byte), narrowed to the target width — over many small pages, ragged page sizes and every
+    narrowing the targets allow, against pyarrow."""
+    import pyarrow as pa
+    rng = np.random.default_rng(21)
+    n = 300_007
+    cols = {
+        "i8": pa.array(rng.integers(-128, 128, n).astype(np.int8)),
+        "u8": pa.array(rng.integers(0, 256, n).astype(np.uint8)),
+        "i16": pa.array(rng.integers(-32768, 32768, n).astype(np.int16)),
+        "u16": pa.array(rng.integers(0, 65536, n).astype(np.uint16)),
+        "i32": pa.array(rng.integers(-2**31, 2**31, n).astype(np.int32)),
+        "u32": pa.array(rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)),
+        "i64": pa.array(rng.integers(-2**62, 2**62, n)),
+        "f32": pa.array(rng.random(n).astype(np.float32)),
+        "f64": pa.array(rng.random(n)),
+    }
+    schema = pa.schema([pa.field(k, v.type, nullable=False) for k, v in cols.items()])
+    t = pa.table(list(cols.values()), schema=schema)
+    for page in (1000, 4093, 65536):
+        buf = write(t, compression=comp, use_dictionary=False, data_page_size=page, row_group_size=1 << 30)
+        m = 0
+        for name, _, ch, at in file_chunks(buf):
+            got = gpu_values(dec, ch, at, nullable=False)
+            assert got == expected_values(t.column(name), at), (comp, page, name)
+            m += 1
+        assert m == len(cols)
