@@ -109,6 +109,13 @@ def _check_supported(keys: Sequence[DataType], functions: Sequence[AggregateFunc
             raise Unsupported(abi.DBG_ERR_UNSUPPORTED, "DISTINCT over Boolean stays on the CPU path")
     if any(t.type_id == abi.BOOLEAN for t in keys):
         raise Unsupported(abi.DBG_ERR_UNSUPPORTED, "Boolean group keys with DISTINCT stay on the CPU path")
+    for f in functions:
+        # the final table declares every plain aggregate's argument nullable; that keeps the result
+        # type only when the function already returns Nullable (the OrNull adaptor, the factory's
+        # default) or cannot return NULL at all (count)
+        if not f.distinct and not f.or_null and f.arg is not None and f.kind != abi.AGG_COUNT:
+            raise Unsupported(abi.DBG_ERR_UNSUPPORTED, f"{f.display_name}: a non-OrNull {f.name()} beside DISTINCT "
+                              "would change its result type; it stays on the CPU path")
 
 
 class DistinctAggregator:

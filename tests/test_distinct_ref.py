@@ -40,3 +40,25 @@ def test_factory_distinct_suffix():
     assert s.return_type() == col.Int64.wrap_nullable()
     with pytest.raises(Unsupported):
         s.to_abi()  # a distinct aggregate is not one table state: DistinctAggregator runs it
+
+
+def test_non_or_null_plain_aggregate_beside_distinct_is_unsupported():
+    """DistinctAggregator declares every plain aggregate's argument nullable in its final table;
+    a sum/min/max/avg built without the OrNull adaptor would change its result type, so it is
+    refused (UNSUPPORTED: the caller keeps the CPU path) — no device needed to decide."""
+    import pytest
+    from databend_amd import column as col
+    from databend_amd.aggregates import AggregateFunctionFactory
+    from databend_amd.aggregator import AggregatorParams
+    from databend_amd.distinct import DistinctAggregator
+    from databend_amd.ffi import Unsupported
+    F = AggregateFunctionFactory.instance()
+    ok = AggregatorParams([col.Int32], [F.get("count_distinct", [], [col.Int64]), F.get("sum", [], [col.Int64])])
+    DistinctAggregator(ok)
+    bad = AggregatorParams([col.Int32], [F.get("count_distinct", [], [col.Int64]),
+                                         F.get_or_null("sum", [], [col.Int64], False)])
+    with pytest.raises(Unsupported):
+        DistinctAggregator(bad)
+    cnt = AggregatorParams([col.Int32], [F.get("count_distinct", [], [col.Int64]),
+                                         F.get_or_null("count", [], [col.Int64], False)])
+    DistinctAggregator(cnt)  # count never returns NULL: allowed
