@@ -529,17 +529,31 @@ def measure_scan(steps: int, rows: int = 1 << 26) -> dict:
                                                      C.byref(nr), C.byref(sb)))
         call()
         assert nr.value == rows and torch.equal(out_t.view(torch.int16), torch.from_numpy(adv).cuda())
+        from databend_amd import ffi
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
+        ffi.prof_reset()
+        ffi.prof_enable(True)
         ev0.record()
         for _ in range(steps):
             call()
         ev1.record()
         torch.cuda.synchronize()
+        ffi.prof_enable(False)
+        kern = ffi.prof_read()
         ms = ev0.elapsed_time(ev1) / steps
         alg = len(chunk) + rows * 2
-        res[comp.lower()] = {"chunk_bytes": len(chunk), "ms_per_chunk": ms, "rows_per_s": rows / (ms * 1e-3),
+        # device time of the decode kernels alone (HIP events on the decoder's stream): the rest of
+        # ms_per_chunk is the host's page-header parse (one Thrift header per 20 000-row page) and the
+        # call's launches / read-back
+        kms = sum(v[0] for k, v in kern.items() if k in ("pq_decode", "pq_inflate")) / steps
+        npg, nrw = C.c_uint32(), C.c_uint64()
+        check(lib().dbg_parquet_chunk_rows(C.byref(c), C.byref(nrw), C.byref(npg)))
+        res[comp.lower()] = {"chunk_bytes": len(chunk), "pages": npg.value,
+                             "ms_per_chunk": ms, "rows_per_s": rows / (ms * 1e-3),
                              "achieved_gbs": alg / (ms * 1e-3) / 1e9, "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "kernel_ms_per_chunk": kms,
+                             "kernel_frac": (alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS) if kms else None,
                              "algorithmic_bytes": alg, "bit_exact": True}
         del dchunk, out_t
     dec.close()

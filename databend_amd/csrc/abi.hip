@@ -120,6 +120,10 @@ struct Scope {
 };
 }  // namespace prof
 
+// the same HIP-event scopes for the other translation units (scan.hip)
+void* prof_scope_begin(const char* name, hipStream_t s) { return prof::enabled ? new prof::Scope(name, s) : nullptr; }
+void prof_scope_end(void* p) { delete (prof::Scope*)p; }
+
 // ------------------------------------------------------------------------------------------
 // handle
 // ------------------------------------------------------------------------------------------

@@ -34,6 +34,8 @@
 #include "../../include/dbgpu_scan.h"
 
 int abi_fail(int code, const std::string& msg);  // abi.hip: sets dbg_last_error
+void* prof_scope_begin(const char* name, hipStream_t s);  // abi.hip: dbg_prof_* event scopes
+void prof_scope_end(void* p);
 void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits);
 void launch_exclusive_scan(hipStream_t s, u64* data, u64 n, u64* total);
 
@@ -609,6 +611,7 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
             const u8* p = vbase + (u64)k0 * pw;
             // byte-aligned values: gfx950 global loads take unaligned addresses (the compiler emits
             // whole-dword loads for these memcpys), consecutive lanes read consecutive 16 B
+            // (every index below is a constant: the arrays stay in registers, no scratch)
             u64 v[4] = {0, 0, 0, 0};
             if (cnt == 4 && pw == 4) {
                 u32 w[4];
@@ -618,13 +621,17 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
             } else if (cnt == 4) {
                 __builtin_memcpy(v, p, 32);
             } else {
-                for (u32 j = 0; j < cnt; ++j) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if ((u32)j >= cnt) continue;
                     if (pw == 4) {
                         u32 x;
                         __builtin_memcpy(&x, p + 4 * j, 4);
                         v[j] = x;
                     } else {
-                        __builtin_memcpy(&v[j], p + 8 * j, 8);
+                        u64 x;
+                        __builtin_memcpy(&x, p + 8 * j, 8);
+                        v[j] = x;
                     }
                 }
             }
@@ -635,7 +642,9 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
                 typedef u32 v4u32 __attribute__((ext_vector_type(4)));
                 *(v4u32*)dst = v4u32{(u32)v[0], (u32)v[1], (u32)v[2], (u32)v[3]};
             } else {
-                for (u32 j = 0; j < cnt; ++j) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if ((u32)j >= cnt) continue;
                     u8* dj = dst + (u64)j * tw;
                     switch (tw) {
                         case 1: *dj = (u8)v[j]; break;
@@ -776,15 +785,21 @@ int parse_pages(const dbg_parquet_chunk& c, std::vector<HostPage>& out) {
     while (pos < c.len) {
         Compact r{c.host, c.len, pos};
         HostPage pg{-1, -1, -1, 0};
-        auto sub = [&](std::vector<std::pair<i64, i64>>& kv) {
+        // the nested header's integer fields (no heap allocation per page: a chunk of 2^26 rows
+        // holds ~3 400 pages at the writers' 20 000-row page cap)
+        struct KV {
+            i64 f[16], v[16];
+            int n = 0;
+        };
+        auto sub = [&](KV& kv) {
             r.fields([&](i64 fid, int t) {
-                if (t == 5 || t == 6) { kv.push_back({fid, r.zigzag()}); return true; }
-                if (t == 1 || t == 2) { kv.push_back({fid, t == 1 ? 1 : 0}); return true; }
+                if ((t == 5 || t == 6) && kv.n < 16) { kv.f[kv.n] = fid; kv.v[kv.n++] = r.zigzag(); return true; }
+                if ((t == 1 || t == 2) && kv.n < 16) { kv.f[kv.n] = fid; kv.v[kv.n++] = t == 1 ? 1 : 0; return true; }
                 return false;
             });
         };
-        auto get = [](const std::vector<std::pair<i64, i64>>& kv, i64 f, i64 d) {
-            for (auto& x : kv) if (x.first == f) return x.second;
+        auto get = [](const KV& kv, i64 f, i64 d) {
+            for (int i = 0; i < kv.n; ++i) if (kv.f[i] == f) return kv.v[i];
             return d;
         };
         r.fields([&](i64 fid, int t) {
@@ -792,7 +807,7 @@ int parse_pages(const dbg_parquet_chunk& c, std::vector<HostPage>& out) {
             if (fid == 2 && t == 5) { pg.uncomp = r.zigzag(); return true; }
             if (fid == 3 && t == 5) { pg.comp = r.zigzag(); return true; }
             if ((fid == 5 || fid == 7 || fid == 8) && t == 12) {
-                std::vector<std::pair<i64, i64>> kv;
+                KV kv;
                 sub(kv);
                 if (fid == 5) { pg.num_values = get(kv, 1, -1); pg.encoding = get(kv, 2, -1); }
                 if (fid == 7) { pg.num_values = get(kv, 1, -1); pg.encoding = get(kv, 2, -1); }
@@ -844,6 +859,8 @@ struct dbg_scan_ctx {
     u64* herr = nullptr; // pinned
     u8* zlit = nullptr;  // ZSTD literal scratch, ZS_MAX_BLOCK per page
     u64 zlit_cap = 0;
+    ScanPage* hpages = nullptr;  // pinned staging of the page table (an async upload, not a pageable copy)
+    u64 hpages_cap = 0;
 };
 
 namespace {
@@ -908,6 +925,7 @@ int dbg_scan_destroy(dbg_scan_ctx* c) {
     for (void* p : dev)
         if (p) hipFree(p);
     if (c->herr) hipHostFree(c->herr);
+    if (c->hpages) hipHostFree(c->hpages);
     delete c;
     return DBG_OK;
 }
@@ -1004,9 +1022,20 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     if (is_bool) SCAN_RET(ensure(&ctx->bools, &ctx->bools_cap, row + 1));
     if (c.codec == DBG_PQ_ZSTD) SCAN_RET(ensure(&ctx->zlit, &ctx->zlit_cap, (u64)pages.size() * ZS_MAX_BLOCK + 16));
     if (target.nullable && c.max_def_level && !out->validity && row) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null validity buffer");
-    SCAN_HIP(hipMemcpyAsync(ctx->pages, pages.data(), pages.size() * sizeof(ScanPage), hipMemcpyHostToDevice, s));
+    if (ctx->hpages_cap < pages.size() + 1) {
+        // the previous call's upload may still read the old staging buffer
+        SCAN_HIP(hipStreamSynchronize(s));
+        if (ctx->hpages) SCAN_HIP(hipHostFree(ctx->hpages));
+        ctx->hpages = nullptr;
+        ctx->hpages_cap = 0;
+        const u64 cap = pages.size() + pages.size() / 2 + 16;
+        SCAN_HIP(hipHostMalloc((void**)&ctx->hpages, cap * sizeof(ScanPage), hipHostMallocDefault));
+        ctx->hpages_cap = cap;
+    }
+    memcpy(ctx->hpages, pages.data(), pages.size() * sizeof(ScanPage));
+    SCAN_HIP(hipMemcpyAsync(ctx->pages, ctx->hpages, pages.size() * sizeof(ScanPage), hipMemcpyHostToDevice, s));
     SCAN_HIP(hipMemsetAsync(ctx->err, 0, 16, s));
-    SCAN_HIP(hipMemsetAsync(ctx->nwalk, 0, pages.size() * 4, s));
+    if (c.physical_type == DBG_PQ_BYTE_ARRAY) SCAN_HIP(hipMemsetAsync(ctx->nwalk, 0, pages.size() * 4, s));
     ScanArgs a;
     memset(&a, 0, sizeof(a));
     a.chunk = upload ? ctx->chunk : c.device;
@@ -1032,19 +1061,32 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     a.err = ctx->err;
     if (!pages.empty()) {
         const dim3 g((u32)pages.size());
+        void* ps = c.codec != DBG_PQ_UNCOMPRESSED ? prof_scope_begin("pq_inflate", s) : nullptr;
         switch (c.codec) {
             case DBG_PQ_SNAPPY: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_SNAPPY>, g, dim3(64), 0, s, a); break;
             case DBG_PQ_LZ4_RAW: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_LZ4_RAW>, g, dim3(64), 0, s, a); break;
             case DBG_PQ_ZSTD: hipLaunchKernelGGL(pq_zstd_kernel, g, dim3(64), 0, s, a, ctx->zlit); break;
-            default: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_UNCOMPRESSED>, g, dim3(64), 0, s, a); break;
+            default: {  // uncompressed pages are decoded where they lie; only a size mismatch is checked
+                bool mismatch = false;
+                for (const auto& pg : pages) mismatch |= pg.comp != pg.uncomp;
+                if (mismatch) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: uncompressed page sizes differ");
+                break;
+            }
         }
+        prof_scope_end(ps);
         SCAN_HIP(hipGetLastError());
         if (c.physical_type == DBG_PQ_BYTE_ARRAY) {
             hipLaunchKernelGGL(pq_walk_kernel, dim3((u32)((pages.size() + 63) / 64)), dim3(64), 0, s, a);
             SCAN_HIP(hipGetLastError());
         }
-        // required PLAIN pages are split 16 ways (1 MiB pages of 2-byte values: 500 K rows each)
-        hipLaunchKernelGGL(pq_decode_kernel, dim3((u32)pages.size(), c.max_def_level ? 1 : 16), dim3(DEC_NT), 0, s, a);
+        // required PLAIN pages are split over the grid's y dimension into pieces of >= 8192 values
+        // (writers cap pages at 20 000 rows — pyarrow, parquet-rs — or at 1 MiB: up to 16 pieces)
+        u64 maxn = 0;
+        for (const auto& pg : pages) maxn = std::max<u64>(maxn, pg.num_values);
+        const u32 ysplit = c.max_def_level ? 1u : (u32)std::min<u64>(16, std::max<u64>(1, (maxn + 8191) / 8192));
+        ps = prof_scope_begin("pq_decode", s);
+        hipLaunchKernelGGL(pq_decode_kernel, dim3((u32)pages.size(), ysplit), dim3(DEC_NT), 0, s, a);
+        prof_scope_end(ps);
         SCAN_HIP(hipGetLastError());
     }
     if (is_str) {
