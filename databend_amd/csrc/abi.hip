@@ -242,6 +242,7 @@ struct dbg_agg_handle {
     // ---- partitioned payload (pp.hip): high-cardinality mode ----
     bool pp = false;          // batches go to the radix-partitioned payload, not the HBM table
     double pp_ratio = 1.0;    // estimated groups per selected row (cardinality probe)
+    double est_groups = 0;    // the probe's (or the last finalize's) group estimate for this batch
     bool pp_probed = false;   // pp_ratio comes from a probe (not the default upper bound)
     struct Seg {
         u64 base, n;
@@ -1020,6 +1021,7 @@ static void note_observed(dbg_agg_handle* h) {
 // D = G (1 - exp(-s / G)) and Haas's GEE sqrt(N / s) f1 + (D - f1), capped at the selected rows.
 static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     const Spec& S = h->spec;
+    h->est_groups = 0;  // set below only from this batch's probe or observation
     const int mode = h->strategy == DBG_STRATEGY_TABLE ? 0 : (h->strategy == DBG_STRATEGY_PARTITIONED ? 2 : 1);
     if (h->pp || !mode || !S.pp_ok || h->table_rows) return DBG_OK;
     if (mode == 1 && (rows < PP_MIN_ROWS || (!S.has_strings && S.inline_width <= 2))) return DBG_OK;
@@ -1028,6 +1030,7 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
         const double ratio = std::min(1.0, (double)h->obs_groups / (double)h->obs_rows);
         h->pp_ratio = std::max(ratio, 1e-9);
         h->pp_probed = true;
+        h->est_groups = ratio * (double)rows;
         if (ratio * (double)rows > (double)PP_MIN_GROUPS && ratio > 0.5) h->pp = true;
         return DBG_OK;
     }
@@ -1061,6 +1064,7 @@ static int pp_maybe_switch(dbg_agg_handle* h, u32 bid, u64 rows) {
     const double g = std::min(nsel, std::max(1.25 * gu, gee));
     h->pp_ratio = std::min(1.0, std::max(g / nsel, 1e-9));
     h->pp_probed = true;
+    h->est_groups = g;
     // the partitioned payload beats the HBM table when keys are mostly unique (ClickBench Q33:
     // 1e9 groups in 1e9 rows); moderate cardinality stays on the table
     if (mode == 2 || (g > (double)PP_MIN_GROUPS && h->pp_ratio > 0.5)) h->pp = true;
@@ -1533,6 +1537,13 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
     // high cardinality: the radix-partitioned payload instead of the HBM table (pp.hip)
     if (!h->pp) RETURN_IF(pp_maybe_switch(h, bid, rows));
     if (h->pp) return pp_add_batch(h, st, bid, rows, 0);
+    // A first batch the probe puts at many groups gets a table sized for them before its insert:
+    // the partitioned insert needs a large table, and growing by overflow afterwards costs the
+    // whole batch again (C3's first 1e9-row batch into the initial table: 1.5 s + a retry pass)
+    if (h->table_rows == 0 && h->pp_probed && h->est_groups > 65536.0) {
+        const u64 target = pow2_at_least((u64)std::min(2.0 * h->est_groups + 1.0, (double)(1ULL << 31)));
+        if (target > h->cap) RETURN_IF(grow_table(h, target));
+    }
     h->table_rows += rows;
     const bool was_clean = h->clean;
     h->clean = false;
