@@ -558,6 +558,139 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
     block_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
 }
 
+// ------------------------------------------------------------------------------------------
+// agg_insert_short: the generic insert specialised for short String keys and COUNT / SUM / AVG over
+// non-nullable arguments (TPC-H Q1: GROUP BY l_returnflag, l_linestatus — 1-byte strings — with
+// seven Decimal128 SUM / AVG).  The generic kernel's chain per queued row is: predicate -> LDS
+// queue -> key offsets -> key bytes -> hash -> LDS probe -> the representative row's offsets ->
+// its bytes -> the arguments -> LDS atomics, seven dependent global round trips.  Here a row's
+// predicate column, key offsets and argument values are loaded together (no queue: the rows stay
+// on their lanes), each key of <= 7 bytes is packed with its length into one word, and the LDS
+// probe compares the packed words against a side array beside the table — the representative
+// row is read only by the lane that claims a slot (for the group hash the HBM entry needs).  The
+// table itself is the generic one (same entries and state words), so rows with longer keys, a
+// full table and the end-of-block flush all use the generic code unchanged.
+// ------------------------------------------------------------------------------------------
+#define SHORT_MAXA 8
+__global__ void __launch_bounds__(BLOCK) agg_insert_short_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    const u32 sw = S.stride_words;
+    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);  // [0] lds claims, [1] hbm claims
+    u64* pk0 = lds + (u64)lds_slots * sw + 2;          // packed keys of slots claimed here (~0: none)
+    u64* pk1 = pk0 + lds_slots;
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    lds_table_init(S, lds, lds_slots, sw, BLOCK);
+    for (u32 j = threadIdx.x; j < lds_slots; j += BLOCK) pk0[j] = pk1[j] = ~0ULL;
+    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 r0 = (u64)blockIdx.x * rows_per_block;
+    const u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    u32 my_claims = 0;
+    const int nk = S.n_keys;
+    // one row: everything it reads from HBM issued before anything is used
+    auto row = [&](u64 i) {
+        u64 alo[SHORT_MAXA], ahi[SHORT_MAXA];
+#pragma unroll
+        for (int a = 0; a < SHORT_MAXA; ++a) {
+            alo[a] = ahi[a] = 0;
+            if (a < S.n_aggs && S.aggs[a].arg_type >= 0) {
+                alo[a] = dcol_bits(B.args[a], i);
+                if (S.aggs[a].sumk == SUMK_I128 && S.aggs[a].kind != DBG_AGG_COUNT) ahi[a] = dcol_hi(B.args[a], i);
+            }
+        }
+        const StrRef s0 = dcol_str(B.keys[0], i);
+        const StrRef s1 = nk > 1 ? dcol_str(B.keys[1], i) : StrRef{nullptr, 0};
+        const bool pass = B.n_nodes == 0 || eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+        if (!pass) return;
+        if (s0.len > 7 || s1.len > 7) {  // long keys: the generic path
+            insert_one<false, false>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+            return;
+        }
+        const u64 k0 = (s0.len << 56) | (s0.len ? (load_partial(s0.p, s0.len) & width_mask((u32)s0.len)) : 0);
+        const u64 k1 = nk > 1 ? ((s1.len << 56) | (s1.len ? (load_partial(s1.p, s1.len) & width_mask((u32)s1.len)) : 0)) : 0;
+        u32 pos = (u32)slot_mix(k0 ^ slot_mix(k1)) & lmask;
+        int ls = -1;
+        for (int p = 0; p < LDS_PROBE_CAP; ++p) {
+            wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)pos * sw);
+            u64 ev = vld<AS_LDS>(e);
+            if (ev == SLOT_EMPTY) {
+                volatile __attribute__((address_space(3))) u32* lc = (volatile __attribute__((address_space(3))) u32*)lcount;
+                if (*lc >= llimit) break;  // full: the generic path (its probe may still find the key)
+                const u64 h = group_hash(B.keys, nk, i);
+                const u64 key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+                const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
+                if (old == SLOT_EMPTY) {
+                    ((volatile __attribute__((address_space(3))) u64*)pk0)[pos] = k0;
+                    ((volatile __attribute__((address_space(3))) u64*)pk1)[pos] = k1;
+                    __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ls = (int)pos;
+                    break;
+                }
+                ev = old;
+            }
+            // a slot whose packed keys are not written yet (or claimed by the generic path) reads
+            // as ~0 and does not match: at worst the key gets a second slot, merged at the flush
+            if (((volatile __attribute__((address_space(3))) u64*)pk0)[pos] == k0 &&
+                ((volatile __attribute__((address_space(3))) u64*)pk1)[pos] == k1) {
+                ls = (int)pos;
+                break;
+            }
+            pos = (pos + 1) & lmask;
+        }
+        if (ls < 0) {
+            insert_one<false, false>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+            return;
+        }
+        wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
+#pragma unroll
+        for (int a = 0; a < SHORT_MAXA; ++a) {
+            if (a >= S.n_aggs) break;
+            const DAgg& A = S.aggs[a];
+            wptr<AS_LDS> w = st + A.w0;
+            if (A.kind == DBG_AGG_COUNT) {
+                at_add<AS_LDS>(w, 1ULL);
+                continue;
+            }
+            if (A.sumk == SUMK_I64) {
+                u64 v = alo[a];
+                switch (A.arg_type) {
+                    case DBG_INT8: v = (u64)(i64)(int8_t)v; break;
+                    case DBG_INT16: v = (u64)(i64)(int16_t)v; break;
+                    case DBG_INT32: case DBG_DATE: v = (u64)(i64)(int32_t)v; break;
+                    default: break;
+                }
+                at_add<AS_LDS>(w, v);
+            } else if (A.sumk == SUMK_F64) {
+                at_addf<AS_LDS>(w, A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)alo[a]) : __longlong_as_double((long long)alo[a]));
+            } else {
+                add128<AS_LDS>(w, alo[a], ahi[a]);
+            }
+            if (A.kind == DBG_AGG_AVG) at_add<AS_LDS>(w + (A.sumk == SUMK_I128 ? 2 : 1), 1ULL);
+        }
+    };
+    for (u64 i = r0 + threadIdx.x; i < r1; i += BLOCK) row(i);
+    __syncthreads();
+    block_flush<false, false>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
+}
+
+// host: the short-key specialisation applies (hb = host copy of the batch descriptor)
+static bool short_eligible(const Spec& S, const BatchDesc& hb) {
+    if (S.inline_keys || S.n_keys < 1 || S.n_keys > 2 || S.n_aggs > SHORT_MAXA || S.flags_word >= 0 || hb.is_records) return false;
+    for (int c = 0; c < S.n_keys; ++c)
+        if (S.key_types[c].type != DBG_STRING || S.key_types[c].nullable || hb.keys[c].layout != LAYOUT_ARROW) return false;
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        if (A.kind != DBG_AGG_COUNT && A.kind != DBG_AGG_SUM && A.kind != DBG_AGG_AVG) return false;
+        if (A.arg_type >= 0 && A.arg_nullable) return false;
+    }
+    return true;
+}
+
 static u32 lds_slots_for(const Spec& S, u32 budget = LDS_BUDGET_BYTES) {
     u32 bytes_per = (u32)S.stride_words * 8;
     u32 n = 1;
@@ -2119,6 +2252,17 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
         }
     }
     u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
+    static const bool x_noshort = getenv("DBG_X_SHORT") && getenv("DBG_X_SHORT")[0] == '0';
+    if (!records && use_lds && hb && !x_noshort && short_eligible(S, *hb)) {
+        u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
+        if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
+        if (blocks < 1) blocks = 1;
+        u64 rpb = (rows + blocks - 1) / blocks;
+        blocks = (rows + rpb - 1) / rpb;
+        const size_t shmem = (size_t)lslots * S.stride_words * 8 + 16 + (size_t)lslots * 16;
+        hipLaunchKernelGGL(agg_insert_short_kernel, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        return;
+    }
     // enough workgroups to fill 256 CUs several times over, each a contiguous row range
     u64 min_rows_per_block = (u64)BLOCK * 16;
     u64 blocks = (rows + min_rows_per_block - 1) / min_rows_per_block;

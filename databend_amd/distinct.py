@@ -204,7 +204,7 @@ def count_distinct(group_columns: Sequence[Column], arg: Column, filter_pred=Non
     F = AggregateFunctionFactory.instance()
     keys = list(group_columns)
     params = AggregatorParams([k.dtype for k in keys], [F.get("count_distinct", [], [arg.dtype])])
-    prog = FilterProgram(filter_pred, [c.to_abi() for c in filter_columns]) if filter_pred is not None else None
+    prog = FilterProgram(filter_pred, list(filter_columns)) if filter_pred is not None else None
     return DistinctAggregator(params).run(keys, [arg], filter_program=prog)
 
 

@@ -99,11 +99,15 @@ def true_() -> Pred:
 
 
 class FilterProgram:
-    """A predicate bound to its columns, marshalled as `dbg_filter` (kept alive by this object)."""
+    """A predicate bound to its columns, marshalled as `dbg_filter` (kept alive by this object).
+    `cols` holds `dbg_column` structs or column objects (Column / DeviceColumn): objects are kept
+    referenced here, so a device column's HBM outlives kernels still queued on it as long as the
+    program does (add_groups retains the program of an on-device batch until reset/close)."""
 
-    def __init__(self, pred: Pred, cols: Sequence[abi.dbg_column]):
+    def __init__(self, pred: Pred, cols: Sequence):
         self.pred = pred
-        self.cols = list(cols)
+        self._owners = [c for c in cols if hasattr(c, "to_abi")]
+        self.cols = [c.to_abi() if hasattr(c, "to_abi") else c for c in cols]
         post = pred.postfix()
         self._keep = []
         self.nodes = (abi.dbg_pred_node * len(post))()
@@ -160,7 +164,7 @@ class FilterExecutor:
     def select(self, columns, rows: int):
         import torch
         from .ffi import check, lib
-        prog = FilterProgram(self.pred, [columns[i].to_abi() for i in self.predicate_columns])
+        prog = FilterProgram(self.pred, [columns[i] for i in self.predicate_columns])
         sel = torch.empty(max(1, rows), dtype=torch.int32, device=columns[0].data.device)
         n = C.c_uint64()
         check(lib().dbg_filter_select(prog.ptr(), rows, sel.data_ptr(), C.byref(n), None))

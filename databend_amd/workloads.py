@@ -200,7 +200,7 @@ class ConfigRunner:
         for inp in self.inputs:
             if self.shape.predicate:
                 name, op, const = self.shape.predicate
-                self.programs.append(FilterProgram(cmp(0, op, const), [inp[name].to_abi()]))
+                self.programs.append(FilterProgram(cmp(0, op, const), [inp[name]]))
             else:
                 self.programs.append(None)
         self.key_abi = [[inp[k] for k in self.shape.keys] for inp in self.inputs]

@@ -41,7 +41,7 @@ def _run(keys, aggs, filt=None, on_device=False):
         args = [None if c is None else DeviceColumn.from_host(c) for c in args]
         if fcols is not None:
             fcols = [DeviceColumn.from_host(c) for c in fcols]
-    prog = FilterProgram(filt[0], [c.to_abi() for c in fcols]) if filt is not None else None
+    prog = FilterProgram(filt[0], fcols) if filt is not None else None
     blk = DistinctAggregator(params).run(keys, args, filter_program=prog)
     na = len(aggs)
     return blk.columns[na:], blk.columns[:na]

@@ -43,7 +43,7 @@ class FusedRunner:
         a = abi.dbg_column()
         a.dt = abi.dbg_datatype(-1, 0, 0, 0, 0)
         args = abi_array([a])
-        fp = FilterProgram(cmp(0, pred[0], pred[1]), [dk.to_abi()]) if pred else None
+        fp = FilterProgram(cmp(0, pred[0], pred[1]), [dk]) if pred else None
         L = lib()
         check(L.dbg_agg_reset(self.table.h))
         check(L.dbg_agg_add_groups(self.table.h, keys, args, fp.ptr() if fp else None, n, 1))

@@ -54,7 +54,7 @@ def gpu_aggregate(keys, aggs, filt=None, on_device=False, capacity_hint=0, batch
                 if fcols is not None:
                     fcols = [DeviceColumn.from_host(c) for c in fcols]
             if fcols is not None:
-                fp = FilterProgram(filt[0], [c.to_abi() for c in fcols])
+                fp = FilterProgram(filt[0], fcols)  # keeps the (device) columns alive
             ht.add_groups(ks, ars, rows=hi - lo, filter_program=fp, on_device=on_device)
         block = ht.merge_result()
         if info is not None:

@@ -98,7 +98,7 @@ def test_partial_bucket_final_pipeline(case):
             for s in range(lo, hi, BLOCK):
                 e = min(hi, s + BLOCK)
                 blk = _block(keys, aggs, pred_col, s, e)
-                fp = FilterProgram(cmp(0, op, const), [blk.columns[pred_idx].to_abi()])
+                fp = FilterProgram(cmp(0, op, const), [blk.columns[pred_idx]])
                 p.transform(blk, list(range(nk)), arg_idx, filter_program=fp)
         metas_b = part_b.on_finish()  # finishes first: the hint is still small
         metas_a = part_a.on_finish()
