@@ -563,69 +563,278 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
 // non-nullable arguments (TPC-H Q1: GROUP BY l_returnflag, l_linestatus — 1-byte strings — with
 // seven Decimal128 SUM / AVG).  The generic kernel's chain per queued row is: predicate -> LDS
 // queue -> key offsets -> key bytes -> hash -> LDS probe -> the representative row's offsets ->
-// its bytes -> the arguments -> LDS atomics, seven dependent global round trips.  Here a row's
-// predicate column, key offsets and argument values are loaded together (no queue: the rows stay
-// on their lanes), each key of <= 7 bytes is packed with its length into one word, and the LDS
-// probe compares the packed words against a side array beside the table — the representative
-// row is read only by the lane that claims a slot (for the group hash the HBM entry needs).  The
-// table itself is the generic one (same entries and state words), so rows with longer keys, a
-// full table and the end-of-block flush all use the generic code unchanged.
+// its bytes -> the arguments -> LDS atomics, seven dependent global round trips.  Here the rows
+// stay on their lanes (no queue): a row's key offsets and argument values are loaded together,
+// then its key bytes with the predicate's column (fetching a row ahead, SHORT_PIPE=1, costs two
+// waves per SIMD of occupancy and measured slower: C1 insert 0.26 -> 0.32 ms).  Each key of <= 7 bytes is packed with its length into
+// one word, and the LDS probe compares the packed words against a side array beside the table —
+// the representative row is read only by the lane that claims a slot (for the group hash the HBM
+// entry needs).
+//
+// Decimal SUM / AVG arguments of precision p with rows_per_block * 10^p < 2^63 (`narrow`, bit per
+// aggregate) accumulate in the low state word alone, as a signed 64-bit partial (no carry, so a
+// non-returning LDS add instead of add128's returning add + dependent high add); before the flush
+// the high word is set to the partial's sign.  Slots are therefore either "short" (claimed here,
+// packed keys in the side array, narrow representation) or "generic" (claimed by the fallback
+// for longer keys or a full probe, marked PK_GEN, standard representation); each path matches only
+// its own slots, so the two never mix (a key may hold a slot of each: the flush merges them).
+// The end-of-block flush is the generic one.
 // ------------------------------------------------------------------------------------------
 #define SHORT_MAXA 8
-__global__ void __launch_bounds__(BLOCK) agg_insert_short_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                                u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots) {
+#ifndef SHORT_PIPE
+#define SHORT_PIPE 0
+#endif
+#define PK_NONE (~0ULL)
+#define PK_GEN (~0ULL - 1)
+typedef __attribute__((address_space(3))) u64 lds_u64;
+typedef volatile __attribute__((address_space(3))) u64 vlds_u64;
+typedef volatile __attribute__((address_space(3))) u32 vlds_u32;
+struct ShortRow {
+    u64 o[4];               // key offsets [k0 begin, k0 end, k1 begin, k1 end]
+    u64 lo[SHORT_MAXA];     // argument low words (or the whole value)
+    u64 hi[SHORT_MAXA];     // Decimal128 high words of wide sums
+};
+// End of the short-key insert: a merge tree over parked tables, fan-in SHORT_FANIN per level.
+// block_flush parks each workgroup's table and lets the last of every FLUSH_GROUP merge them and
+// flush to HBM, so G / FLUSH_GROUP leaders still add into the same few HBM slots, serialised at
+// the memory side (C1: 366 leaders x 4 groups).  Here a level's leader parks its merged table
+// again, one level up, until one root flushes: the HBM table sees one add per group.  Parked rows
+// carry the slot's packed keys (words n_words+1, n_words+2), so a merge compares them in LDS and
+// never reads a representative row.  Node n of level L parks in the scratch row of workgroup
+// n * FANIN^L (read by its own leader before), its tickets sit at a per-level offset.  Hand-off
+// as in block_flush: sc1 stores, vmcnt drain + barrier before the ticket add, acquire + sc1 loads.
+// A table with a generic slot or more than SCR_ENTRIES short slots flushes directly and parks an
+// empty row.
+#define SHORT_FANIN 4
+__device__ __forceinline__ void short_tree_flush(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots,
+                                                 u32 sw, u32* lcount, u64* pk0, u64* pk1, const TableDesc& t, u32 my_claims) {
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    const u32 nw = (u32)S.n_words;
+    u64* counts = t.scratch;
+    u64* tickets = t.scratch + t.scr_blocks;
+    u64* rows = t.scratch + 2 * (u64)t.scr_blocks;
+    u32 node = blockIdx.x, n_nodes = gridDim.x, shift = 0, toff = 0;
+    for (;;) {
+        // the table in LDS: count slots; [4] generic slots, [5] short slots
+        if (threadIdx.x == 0) lcount[4] = lcount[5] = 0;
+        __syncthreads();
+        for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+            const u64 e = lds[(u64)s * sw];
+            if (e == SLOT_EMPTY) continue;
+            atomicAdd(&lcount[pk0[s] == PK_GEN || pk0[s] == PK_NONE ? 4 : 5], 1u);
+        }
+        __syncthreads();
+        const bool root = n_nodes == 1;
+        const bool direct = root || lcount[4] != 0 || lcount[5] > SCR_ENTRIES;
+        const u64 b = (u64)node << shift;  // this node's scratch row
+        if (direct) {
+            flush_lds_direct<false, false>(S, batches, B, lds, lds_slots, sw, BLOCK, t, my_claims);
+            if (!root && threadIdx.x == 0) st_sc1(counts + b, 0);
+        } else {
+            if (threadIdx.x == 0) lcount[2] = 0;
+            __syncthreads();
+            u64* row = rows + b * SCR_ENTRIES * sw;
+            for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+                const u64* p = lds + (u64)s * sw;
+                if (p[0] == SLOT_EMPTY) continue;
+                const u32 k = atomicAdd(&lcount[2], 1u);
+                u64* d = row + (u64)k * sw;
+                for (u32 w = 0; w <= nw; ++w) st_sc1(d + w, p[w]);
+                st_sc1(d + nw + 1, pk0[s]);
+                st_sc1(d + nw + 2, pk1[s]);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) st_sc1(counts + b, lcount[2]);
+        }
+        if (root) break;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const u32 g = node / SHORT_FANIN;
+        const u32 gsize = min((u32)SHORT_FANIN, n_nodes - g * SHORT_FANIN);
+        if (threadIdx.x == 0) {
+            const u64 tk = atomicAdd((unsigned long long*)(tickets + toff + g), 1ULL);
+            lcount[3] = tk == (u64)gsize - 1 ? 1u : 0u;
+        }
+        __syncthreads();
+        if (!lcount[3]) break;
+        // this workgroup leads node g one level up: merge the members' parked rows
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tickets[toff + g] = 0;  // ready for the next launch (all members have added)
+        }
+        lds_table_init(S, lds, lds_slots, sw, BLOCK);
+        for (u32 j = threadIdx.x; j < lds_slots; j += BLOCK) pk0[j] = pk1[j] = PK_NONE;
+        if (threadIdx.x == 0) lcount[0] = 0;
+        __syncthreads();
+        for (u32 f = threadIdx.x; f < gsize * SCR_ENTRIES; f += BLOCK) {
+            const u64 mb = ((u64)g * SHORT_FANIN + f / SCR_ENTRIES) << shift, k = f % SCR_ENTRIES;
+            const u64* r = rows + (mb * SCR_ENTRIES + k) * sw;
+            const u64 cnt = ld_sc1(counts + mb);
+            const u64 e = ld_sc1(r);
+            if (k >= cnt) continue;
+            const u64 q0 = ld_sc1(r + nw + 1), q1 = ld_sc1(r + nw + 2);
+            u32 pos = (u32)slot_mix(q0 ^ slot_mix(q1)) & lmask;
+            int ls = -1;
+            for (int p = 0; p < LDS_PROBE_CAP; ++p) {
+                wptr<AS_LDS> ep = asp<AS_LDS>(lds + (u64)pos * sw);
+                u64 ev = vld<AS_LDS>(ep);
+                if (ev == SLOT_EMPTY) {
+                    if (*(vlds_u32*)lcount >= llimit) break;
+                    const u64 old = at_cas<AS_LDS>(ep, SLOT_EMPTY, e);
+                    if (old == SLOT_EMPTY) {
+                        ((vlds_u64*)pk0)[pos] = q0;
+                        ((vlds_u64*)pk1)[pos] = q1;
+                        __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                        ls = (int)pos;
+                        break;
+                    }
+                }
+                if (((vlds_u64*)pk0)[pos] == q0 && ((vlds_u64*)pk1)[pos] == q1) {
+                    ls = (int)pos;
+                    break;
+                }
+                pos = (pos + 1) & lmask;
+            }
+            if (ls >= 0) {
+                apply_state<AS_LDS, true>(S, asp<AS_LDS>(lds + (u64)ls * sw), r);
+                continue;
+            }
+            // the merge table is full: this row goes to HBM by itself
+            bool claimed;
+            const u64 h = group_hash(B.keys, S.n_keys, ref_row(e));
+            const u64 gs = g_find<false>(S, batches, B.keys, ref_row(e), e, h, t, t.probe_limit, claimed);
+            if (gs == ~0ULL) {
+                push_ovf_rec<true>(S, t, e, r);
+                continue;
+            }
+            my_claims += claimed ? 1 : 0;
+            apply_state<AS_GLB, true>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), r);
+        }
+        __syncthreads();
+        toff += (n_nodes + SHORT_FANIN - 1) / SHORT_FANIN;
+        node = g;
+        n_nodes = (n_nodes + SHORT_FANIN - 1) / SHORT_FANIN;
+        shift += 2;  // log2(SHORT_FANIN)
+    }
+    if (my_claims) atomicAdd(&lcount[1], my_claims);
+    __syncthreads();
+    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+}
+
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6))) agg_insert_short_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                                u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots,
+                                                                u32 rep_mask, int xmode, u32 narrow, int tree_ok) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
     const u32 sw = S.stride_words;
-    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);  // [0] lds claims, [1] hbm claims
-    u64* pk0 = lds + (u64)lds_slots * sw + 2;          // packed keys of slots claimed here (~0: none)
+    u32* lcount = (u32*)(lds + (u64)lds_slots * sw);  // [0] lds claims, [1] hbm claims, [2..5] flush
+    u64* pk0 = lds + (u64)lds_slots * sw + 4;          // packed keys of short slots (PK_NONE / PK_GEN)
     u64* pk1 = pk0 + lds_slots;
     const u32 lmask = lds_slots - 1;
     const u32 llimit = lds_slots - lds_slots / 4;
     lds_table_init(S, lds, lds_slots, sw, BLOCK);
-    for (u32 j = threadIdx.x; j < lds_slots; j += BLOCK) pk0[j] = pk1[j] = ~0ULL;
-    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
+    for (u32 j = threadIdx.x; j < lds_slots; j += BLOCK) pk0[j] = pk1[j] = PK_NONE;
+    if (threadIdx.x < 8) lcount[threadIdx.x] = 0;
     __syncthreads();
     const u64 r0 = (u64)blockIdx.x * rows_per_block;
     const u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
     u32 my_claims = 0;
     const int nk = S.n_keys;
-    // one row: everything it reads from HBM issued before anything is used
-    auto row = [&](u64 i) {
-        u64 alo[SHORT_MAXA], ahi[SHORT_MAXA];
+    const int na = S.n_aggs;
+    vlds_u32* lc = (vlds_u32*)lcount;
+    auto fetch = [&](u64 i, ShortRow& r) __attribute__((always_inline)) {
+        r.o[0] = gld<u64>(B.keys[0].offsets + i);
+        r.o[1] = gld<u64>(B.keys[0].offsets + i + 1);
+        r.o[2] = r.o[3] = 0;
+        if (nk > 1) {
+            r.o[2] = gld<u64>(B.keys[1].offsets + i);
+            r.o[3] = gld<u64>(B.keys[1].offsets + i + 1);
+        }
 #pragma unroll
         for (int a = 0; a < SHORT_MAXA; ++a) {
-            alo[a] = ahi[a] = 0;
-            if (a < S.n_aggs && S.aggs[a].arg_type >= 0) {
-                alo[a] = dcol_bits(B.args[a], i);
-                if (S.aggs[a].sumk == SUMK_I128 && S.aggs[a].kind != DBG_AGG_COUNT) ahi[a] = dcol_hi(B.args[a], i);
+            r.lo[a] = r.hi[a] = 0;
+            if (a < na && S.aggs[a].arg_type >= 0 && S.aggs[a].kind != DBG_AGG_COUNT) {
+                r.lo[a] = dcol_bits(B.args[a], i);
+                if (S.aggs[a].sumk == SUMK_I128 && !((narrow >> a) & 1)) r.hi[a] = dcol_hi(B.args[a], i);
             }
         }
-        const StrRef s0 = dcol_str(B.keys[0], i);
-        const StrRef s1 = nk > 1 ? dcol_str(B.keys[1], i) : StrRef{nullptr, 0};
-        const bool pass = B.n_nodes == 0 || eval_pred(B.nodes, B.n_nodes, B.fcols, i);
-        if (!pass) return;
-        if (s0.len > 7 || s1.len > 7) {  // long keys: the generic path
-            insert_one<false, false>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+    };
+    // the fallback: a generic slot (PK_GEN) of this workgroup's table, else the HBM table
+    auto generic_row = [&](u64 i) __attribute__((always_inline)) {
+        const u64 h = group_hash(B.keys, nk, i);
+        const u64 key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+        u32 s = (u32)((h >> 16) & lmask);
+        const int cap = *lc >= llimit ? 2 : LDS_PROBE_CAP;
+        int ls = -1;
+        for (int p = 0; p < cap; ++p) {
+            wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)s * sw);
+            u64 ev = vld<AS_LDS>(e);
+            if (ev == SLOT_EMPTY) {
+                if (*lc >= llimit) break;
+                const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
+                if (old == SLOT_EMPTY) {
+                    ((vlds_u64*)pk0)[s] = PK_GEN;
+                    __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ls = (int)s;
+                    break;
+                }
+                ev = old;
+            }
+            // a slot whose marker is not written yet reads as not generic: at worst a second slot
+            if (((vlds_u64*)pk0)[s] == PK_GEN && (ev >> 48) == (key >> 48) && ref_equal(S, batches, B.keys, i, ev)) {
+                ls = (int)s;
+                break;
+            }
+            s = (s + 1) & lmask;
+        }
+        if (ls >= 0) {
+            apply_row<AS_LDS>(S, asp<AS_LDS>(lds + (u64)ls * sw), B, i);
             return;
         }
-        const u64 k0 = (s0.len << 56) | (s0.len ? (load_partial(s0.p, s0.len) & width_mask((u32)s0.len)) : 0);
-        const u64 k1 = nk > 1 ? ((s1.len << 56) | (s1.len ? (load_partial(s1.p, s1.len) & width_mask((u32)s1.len)) : 0)) : 0;
+        bool claimed;
+        const u64 gs = g_find<false>(S, batches, B.keys, i, key, h, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_row(t, bid, i);
+            return;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
+    };
+    auto process = [&](u64 i, const ShortRow& r) __attribute__((always_inline)) {
+        const u64 l0 = r.o[1] - r.o[0], l1 = r.o[3] - r.o[2];
+        const bool shortk = l0 <= 7 && l1 <= 7;
+        // key bytes and the predicate's column: issued together, one wait
+        u64 b0 = 0, b1 = 0;
+        if (shortk && l0) b0 = load_partial(B.keys[0].data + r.o[0], l0);
+        if (shortk && l1) b1 = load_partial(B.keys[1].data + r.o[2], l1);
+        const bool pass = B.n_nodes == 0 || eval_pred(B.nodes, B.n_nodes, B.fcols, i);
+        if (!pass) return;
+        if (!shortk) {
+            generic_row(i);
+            return;
+        }
+        const u64 k0 = (l0 << 56) | (b0 & width_mask((u32)l0));
+        u64 k1 = nk > 1 ? ((l1 << 56) | (b1 & width_mask((u32)l1))) : 0;
+        if (rep_mask && *lc < lds_slots / 8)
+            k1 |= (u64)((threadIdx.x & rep_mask) + 1) << 59;  // a replica of the key's slot: fewer lanes per LDS address
         u32 pos = (u32)slot_mix(k0 ^ slot_mix(k1)) & lmask;
         int ls = -1;
         for (int p = 0; p < LDS_PROBE_CAP; ++p) {
             wptr<AS_LDS> e = asp<AS_LDS>(lds + (u64)pos * sw);
             u64 ev = vld<AS_LDS>(e);
             if (ev == SLOT_EMPTY) {
-                volatile __attribute__((address_space(3))) u32* lc = (volatile __attribute__((address_space(3))) u32*)lcount;
-                if (*lc >= llimit) break;  // full: the generic path (its probe may still find the key)
+                if (*lc >= llimit) break;  // full: the generic path
                 const u64 h = group_hash(B.keys, nk, i);
                 const u64 key = (h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
                 const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
                 if (old == SLOT_EMPTY) {
-                    ((volatile __attribute__((address_space(3))) u64*)pk0)[pos] = k0;
-                    ((volatile __attribute__((address_space(3))) u64*)pk1)[pos] = k1;
+                    ((vlds_u64*)pk0)[pos] = k0;
+                    ((vlds_u64*)pk1)[pos] = k1;
                     __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                     ls = (int)pos;
@@ -633,23 +842,22 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_short_kernel(const Spec* __r
                 }
                 ev = old;
             }
-            // a slot whose packed keys are not written yet (or claimed by the generic path) reads
-            // as ~0 and does not match: at worst the key gets a second slot, merged at the flush
-            if (((volatile __attribute__((address_space(3))) u64*)pk0)[pos] == k0 &&
-                ((volatile __attribute__((address_space(3))) u64*)pk1)[pos] == k1) {
+            // packed keys not written yet (or a generic slot) do not match: at worst a second slot
+            if (((vlds_u64*)pk0)[pos] == k0 && ((vlds_u64*)pk1)[pos] == k1) {
                 ls = (int)pos;
                 break;
             }
             pos = (pos + 1) & lmask;
         }
         if (ls < 0) {
-            insert_one<false, false>(S, batches, B, bid, i, lds, lmask, sw, lcount, llimit, t, my_claims);
+            generic_row(i);
             return;
         }
+        if (xmode == 2 || xmode == 4) return;  // timing ablation only
         wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
 #pragma unroll
         for (int a = 0; a < SHORT_MAXA; ++a) {
-            if (a >= S.n_aggs) break;
+            if (a >= na) break;
             const DAgg& A = S.aggs[a];
             wptr<AS_LDS> w = st + A.w0;
             if (A.kind == DBG_AGG_COUNT) {
@@ -657,7 +865,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_short_kernel(const Spec* __r
                 continue;
             }
             if (A.sumk == SUMK_I64) {
-                u64 v = alo[a];
+                u64 v = r.lo[a];
                 switch (A.arg_type) {
                     case DBG_INT8: v = (u64)(i64)(int8_t)v; break;
                     case DBG_INT16: v = (u64)(i64)(int16_t)v; break;
@@ -666,16 +874,49 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_short_kernel(const Spec* __r
                 }
                 at_add<AS_LDS>(w, v);
             } else if (A.sumk == SUMK_F64) {
-                at_addf<AS_LDS>(w, A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)alo[a]) : __longlong_as_double((long long)alo[a]));
+                at_addf<AS_LDS>(w, A.arg_type == DBG_FLOAT32 ? (double)__uint_as_float((u32)r.lo[a]) : __longlong_as_double((long long)r.lo[a]));
+            } else if ((narrow >> a) & 1) {
+                at_add<AS_LDS>(w, r.lo[a]);  // signed 64-bit partial, widened before the flush
             } else {
-                add128<AS_LDS>(w, alo[a], ahi[a]);
+                add128<AS_LDS>(w, r.lo[a], r.hi[a]);
             }
             if (A.kind == DBG_AGG_AVG) at_add<AS_LDS>(w + (A.sumk == SUMK_I128 ? 2 : 1), 1ULL);
         }
     };
-    for (u64 i = r0 + threadIdx.x; i < r1; i += BLOCK) row(i);
+    static_assert(SHORT_PIPE == 0 || SHORT_PIPE == 1, "");
+    u64 i = r0 + threadIdx.x;
+    if (SHORT_PIPE && i < r1) {  // loads one row ahead (measured slower: occupancy 6 -> 4 waves)
+        ShortRow cur;
+        fetch(i, cur);
+        for (; i < r1; i += BLOCK) {
+            ShortRow nxt;
+            const u64 in = i + BLOCK;
+            if (in < r1) fetch(in, nxt);
+            process(i, cur);
+            cur = nxt;
+        }
+    } else {
+        for (; i < r1; i += BLOCK) {
+            ShortRow cur;
+            fetch(i, cur);
+            process(i, cur);
+        }
+    }
     __syncthreads();
-    block_flush<false, false>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
+    if (xmode >= 3) return;  // timing ablation only (DBG_X_SHORT=3: no flush)
+    if (narrow) {  // short slots: narrow partials -> Decimal128 state (high word = sign)
+        for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+            const u64 pk = pk0[s];
+            if (pk == PK_NONE || pk == PK_GEN) continue;
+            u64* st = lds + (u64)s * sw;
+            for (int a = 0; a < na; ++a)
+                if ((narrow >> a) & 1) st[S.aggs[a].w0 + 1] = (u64)((i64)st[S.aggs[a].w0] >> 63);
+        }
+        __syncthreads();
+    }
+    const bool tree = tree_ok && t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks;  // uniform
+    if (tree) short_tree_flush(S, batches, B, lds, lds_slots, sw, lcount, pk0, pk1, t, my_claims);
+    else block_flush<false, false>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
 }
 
 // host: the short-key specialisation applies (hb = host copy of the batch descriptor)
@@ -1128,7 +1369,7 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
 template <int MAXPER>
 __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDesc* batches, const TableDesc& t, const u64* view,
                                                     const OutDesc& out, u64* totals, u64* host_mirror, int recycle, u64 seq,
-                                                    u64* trace = nullptr, bool writeback = false) {
+                                                    u64* trace = nullptr, bool writeback = false, int xfin = 0) {
     __shared__ u64 wsum[FIN_NT / 64][1 + DBG_MAX_KEYS];
     __shared__ u64 cnts[CNT_WORDS];
     auto mark = [&](int k) { if (kPhaseTrace && trace && threadIdx.x == 0) trace[k] = __builtin_amdgcn_s_memrealtime(); };
@@ -1204,6 +1445,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
     // write pass over the occupied slots only (one write_group instance in the code; the entry
     // is re-read from the cache rather than indexed out of the register array)
     const u32 occ_all = occ;
+    if (xfin & 1) occ = 0;  // timing ablation only
     while (occ && p < out.cap_groups) {
         const u32 k = __builtin_ctz(occ);
         occ &= occ - 1;
@@ -1214,7 +1456,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
     }
     mark(8);
     u64 n = total < out.cap_groups ? total : out.cap_groups;
-    if (has_bits) {
+    if (has_bits && !(xfin & 2)) {
         __syncthreads();  // validity bytes of every row are in global memory
         for (u64 k = threadIdx.x; k < (n + 7) / 8; k += FIN_NT)
             for (int c = 0; c < S.n_keys + S.n_aggs; ++c) {
@@ -1286,14 +1528,16 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
 
 __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                 TableDesc t, OutDesc out, u64* totals, u64* host_mirror,
-                                                                int recycle, u64 seq) {
-    finalize_small_body<FIN_MAXPER>(*spec, batches, t, t.slots, out, totals, host_mirror, recycle, seq);
+                                                                int recycle, u64 seq, int xfin) {
+    if (xfin & 8) return;  // timing ablation only
+    finalize_small_body<FIN_MAXPER>(*spec, batches, t, t.slots, out, totals, host_mirror, recycle, seq, nullptr, false, xfin);
 }
 
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
                            u64* totals, u64* host_mirror, int recycle, u64 seq) {
+    static const int xfin = getenv("DBG_X_FIN") ? atoi(getenv("DBG_X_FIN")) : 0;
     hipLaunchKernelGGL(finalize_small_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, out, totals, host_mirror, recycle,
-                       seq);
+                       seq, xfin);
 }
 
 // The last workgroup of an insert launch finalizes the table (FusedFin).  Hand-off
@@ -2252,15 +2496,30 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
         }
     }
     u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
-    static const bool x_noshort = getenv("DBG_X_SHORT") && getenv("DBG_X_SHORT")[0] == '0';
+    static const int x_short = getenv("DBG_X_SHORT") ? atoi(getenv("DBG_X_SHORT")) : 1;
+    static const u32 x_rep = getenv("DBG_X_SHORT_REP") ? (u32)atoi(getenv("DBG_X_SHORT_REP")) : 0;
+    const bool x_noshort = x_short == 0;
     if (!records && use_lds && hb && !x_noshort && short_eligible(S, *hb)) {
         u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
         if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
         if (blocks < 1) blocks = 1;
         u64 rpb = (rows + blocks - 1) / blocks;
         blocks = (rows + rpb - 1) / rpb;
-        const size_t shmem = (size_t)lslots * S.stride_words * 8 + 16 + (size_t)lslots * 16;
-        hipLaunchKernelGGL(agg_insert_short_kernel, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots);
+        const size_t shmem = (size_t)lslots * S.stride_words * 8 + 32 + (size_t)lslots * 16;
+        // narrow Decimal sums: rows_per_block * 10^p < 2^63 (a workgroup's partial fits in i64)
+        u32 narrow = 0;
+        for (int a = 0; a < S.n_aggs; ++a) {
+            const DAgg& A = S.aggs[a];
+            if (A.sumk != SUMK_I128 || A.kind == DBG_AGG_COUNT || A.arg_type != DBG_DECIMAL128) continue;
+            const int p = hb->args[a].precision;
+            double lim = 1.0;
+            for (int k = 0; k < p; ++k) lim *= 10.0;
+            if (p > 0 && p <= 18 && lim * (double)rpb < 9.0e18) narrow |= 1u << a;
+        }
+        if (getenv("DBG_X_NARROW") && getenv("DBG_X_NARROW")[0] == '0') narrow = 0;
+        static const bool x_tree = getenv("DBG_X_TREE") && getenv("DBG_X_TREE")[0] == '1';
+        hipLaunchKernelGGL(agg_insert_short_kernel, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots,
+                           x_rep ? x_rep - 1 : 0u, x_short, narrow, x_tree && S.stride_words >= S.n_words + 3 ? 1 : 0);
         return;
     }
     // enough workgroups to fill 256 CUs several times over, each a contiguous row range

@@ -189,6 +189,20 @@ __device__ __forceinline__ U128 dec_round_div(u64 lo, u64 hi, int k, u64 d) {
         if (l1 == 0) l2 += 1;
     }
     u64 r;
+    if (d <= 0xFFFFFFFFULL) {  // a count below 2^32 (always, in practice): six 64/32 long-division
+                               // steps instead of 192 shift-subtract iterations
+        const u32 dig[6] = {(u32)(l2 >> 32), (u32)l2, (u32)(l1 >> 32), (u32)l1, (u32)(n0 >> 32), (u32)n0};
+        u32 qd[6];
+        r = 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const u64 cur = (r << 32) | dig[j];
+            qd[j] = (u32)(cur / d);
+            r = cur - (u64)qd[j] * d;
+        }
+        U128 q{((u64)qd[4] << 32) | qd[5], ((u64)qd[2] << 32) | qd[3]};
+        return neg ? u128_neg(q) : q;
+    }
     div128_64(0, l2, d, &r);  // the quotient's top limb is dropped (low 128 bits)
     u64 q1 = div128_64(r, l1, d, &r);
     u64 q0 = div128_64(r, n0, d, &r);
