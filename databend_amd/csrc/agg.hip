@@ -1457,9 +1457,13 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
     mark(8);
     u64 n = total < out.cap_groups ? total : out.cap_groups;
     if (has_bits && !(xfin & 2)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // validity bytes of every row are in global memory
-        for (u64 k = threadIdx.x; k < (n + 7) / 8; k += FIN_NT)
-            for (int c = 0; c < S.n_keys + S.n_aggs; ++c) {
+        const u32 ncols = (u32)(S.n_keys + S.n_aggs);
+        for (u64 f = threadIdx.x; f < (n + 7) / 8 * ncols; f += FIN_NT) {  // one (byte, column) per thread
+            const u64 k = f / ncols;
+            const int c = (int)(f % ncols);
+            {
                 const u8* bytes = c < S.n_keys ? out.key_valid[c] : out.agg_valid[c - S.n_keys];
                 u8* bits = c < S.n_keys ? out.key_bits[c] : out.agg_bits[c - S.n_keys];
                 if (!bytes || !bits) continue;
@@ -1470,6 +1474,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
                 }
                 bits[k] = b;
             }
+        }
     }
     if (threadIdx.x == 0) {
         totals[0] = total;

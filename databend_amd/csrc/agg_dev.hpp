@@ -142,6 +142,13 @@ __device__ __forceinline__ U128 u128_div_u64(U128 a, u64 d) {
     q.hi = a.hi / d;
     u64 r = a.hi % d;
     u64 lo = 0;
+    if (d <= 0xFFFFFFFFULL) {  // two 64/32 long-division steps instead of 64 iterations
+        const u64 c1 = (r << 32) | (a.lo >> 32);
+        const u64 q1 = c1 / d;
+        const u64 c0 = ((c1 - q1 * d) << 32) | (a.lo & 0xFFFFFFFFULL);
+        q.lo = (q1 << 32) | (c0 / d);
+        return q;
+    }
     for (int b = 63; b >= 0; --b) {
         u64 top = r >> 63;
         r = (r << 1) | ((a.lo >> b) & 1);
