@@ -581,6 +581,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
 // The end-of-block flush is the generic one.
 // ------------------------------------------------------------------------------------------
 #define SHORT_MAXA 8
+#define SHORT_MAX_SLOTS 65536  // HBM table slots up to which the short-key insert is taken
 #ifndef SHORT_PIPE
 #define SHORT_PIPE 0
 #endif
@@ -2504,7 +2505,10 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     static const int x_short = getenv("DBG_X_SHORT") ? atoi(getenv("DBG_X_SHORT")) : 1;
     static const u32 x_rep = getenv("DBG_X_SHORT_REP") ? (u32)atoi(getenv("DBG_X_SHORT_REP")) : 0;
     const bool x_noshort = x_short == 0;
-    if (!records && use_lds && hb && !x_noshort && short_eligible(S, *hb)) {
+    // low cardinality only: with a table already sized for many groups (the cardinality probe, or
+    // earlier batches) most rows miss the workgroup's LDS table, and the generic kernel's queued
+    // HBM path serves those far better than this kernel's per-row fallback (C5: 31 vs 95 ms)
+    if (!records && use_lds && hb && !x_noshort && t.cap + 1 <= SHORT_MAX_SLOTS && short_eligible(S, *hb)) {
         u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
         if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
         if (blocks < 1) blocks = 1;
