@@ -189,6 +189,11 @@ struct dbg_agg_handle {
     std::vector<BatchDesc*> pinned_descs;   // pinned staging desc per batch id (pooled)
     std::vector<BatchDesc*> pinned_chunks;  // their allocations
     std::vector<DevBuf> owned;             // device copies of host inputs / filter constants
+    // before_merge exchange receive buffers (records, string blobs) when this is the final table:
+    // kept across resets and grown only, so a step allocates nothing; `xrecv_busy` while the table
+    // may reference them (merged since the last reset) — an exchange then allocates fresh ones
+    DevBuf xrecv[2];
+    bool xrecv_busy = false;
 
     // finalize state
     bool finalized = false;
@@ -232,6 +237,7 @@ struct dbg_agg_handle {
     void* part_temp = nullptr;
     size_t part_temp_cap = 0;
     u64 table_rows = 0;  // rows / records inserted into the HBM table since the last reset
+    u64 remerged = 0;    // of which records dbg_agg_compact merged back (groups, not input rows)
     int strategy = DBG_STRATEGY_AUTO;
     u64 hint_groups = 0;  // dbg_agg_params.capacity_hint
     // cardinality the last table-mode finalize observed (kept across reset): rows / records
@@ -264,7 +270,8 @@ struct dbg_agg_handle {
     u32 pp_rc_sub = 0;  // > 0: record-centric aggregation in 2^pp_rc_sub rounds per partition (pp.hip)
     int pp_spec = -1;   // >= 0: the compile-time specialised aggregation's shape (pp_agg_spec_kernel)
     u32 pp_spec_sub = 0;  // its rounds per partition: 2^pp_spec_sub
-    u32* pp_spill = nullptr;  // [count, partition ids...] spilled by the record-centric kernel
+    u32* pp_spill = nullptr;  // [count, partition ids...] spilled by the specialised / record-centric kernel
+    u64 pp_spill_cap = 0;     // ids it holds: one per final partition, so no spill is ever dropped
     u32* pp_cnt = nullptr;
     u64 pp_cnt_cap = 0;
     u64* pp_off = nullptr;
@@ -872,6 +879,8 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto& b : h->owned) hipFree(b.p);
+    for (auto& b : h->xrecv)
+        if (b.p) hipFree(b.p);
     for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
                     h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->d_lpart, h->vbytes, h->part_sorted, h->part_bounds,
@@ -929,6 +938,8 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     h->pending_rows = h->pending_recs = 0;
     h->finalized = false;
     h->table_rows = 0;
+    h->remerged = 0;
+    h->xrecv_busy = false;  // no group references the exchange's receive buffers any more
     for (auto& K : h->ppk) {  // partitioned payload: records dropped, buffers kept (the mode too)
         K.l1_n = 0;
         K.segs.clear();
@@ -1009,8 +1020,10 @@ extern "C" {
 #define PP_SET_CAP (1ULL << 19)  // 2^18 samples at most: <= 50 % load
 
 static void note_observed(dbg_agg_handle* h) {
-    if (h->pp || !h->table_rows) return;
-    h->obs_rows = h->table_rows;
+    // compaction's re-merged group records are not input rows: leave them out of the ratio
+    const u64 rows = h->table_rows > h->remerged ? h->table_rows - h->remerged : 0;
+    if (h->pp || !rows) return;
+    h->obs_rows = rows;
     h->obs_groups = h->n_groups;
 }
 
@@ -1263,7 +1276,7 @@ static int pp_prepare(dbg_agg_handle* h, bool spec_ok) {
     // LDS round's records — no level 3.
     h->pp_rc_sub = 0;
     // measured slower than the slot-table kernel on C4 (pp_agg 74 vs 58 ms): opt-in (DBG_X_PPRC=1)
-    static const bool rc_on = getenv("DBG_X_PPRC") && getenv("DBG_X_PPRC")[0] == '1';
+    static const bool rc_on = X_ENV("DBG_X_PPRC") && X_ENV("DBG_X_PPRC")[0] == '1';
     if (rc_on && pp_rc_ok(S) && nsr == 0 && nr > 0) {
         const double per_part = (double)PP_RC_PART;
         u32 b2 = PP_L1_BITS + 1;
@@ -1285,7 +1298,7 @@ static int pp_prepare(dbg_agg_handle* h, bool spec_ok) {
     // partition is loaded once and aggregated in 2^sub LDS rounds, so partitions hold up to the
     // kernel's register budget of records and level 2 alone (<= 10 bits) sizes them — no level 3.
     h->pp_spec = -1;
-    static const bool spec_on = !(getenv("DBG_X_PPSPEC") && getenv("DBG_X_PPSPEC")[0] == '0');
+    static const bool spec_on = !(X_ENV("DBG_X_PPSPEC") && X_ENV("DBG_X_PPSPEC")[0] == '0');
     u32 scap = 0, smax = 0;
     const int shape = (spec_on && spec_ok && !h->pp_rc_sub && nsr == 0 && nr > 0) ? pp_spec_shape(S, &scap, &smax) : -1;
     if (shape >= 0) {
@@ -1392,7 +1405,7 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     memset(&o, 0, sizeof(o));
     o.tot = h->pp_tot;
     static u64* x_pptrace = nullptr;  // EXPERIMENT (DBG_X_PPTRACE)
-    if (kPhaseTrace && getenv("DBG_X_PPTRACE")) {
+    if (kPhaseTrace && X_ENV("DBG_X_PPTRACE")) {
         if (!x_pptrace) {
             RETURN_IF(dev_alloc((void**)&x_pptrace, 64));
             HIPCHECK(hipMemset(x_pptrace, 0, 64));
@@ -1420,8 +1433,15 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
     auto& R = h->ppk[0];
     auto& T = h->ppk[1];
     if (h->pp_spec >= 0) {
-        constexpr u32 SPILL_CAP = 4096;
-        if (!h->pp_spill) RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + SPILL_CAP) * 4));
+        // every final partition may spill (skewed keys): room for all their ids (<= 1 MB)
+        const u32 SPILL_CAP = 1u << h->pp_bits;
+        if (h->pp_spill_cap < SPILL_CAP) {
+            if (h->pp_spill) HIPCHECK(hipFree(h->pp_spill));
+            h->pp_spill = nullptr;
+            h->pp_spill_cap = 0;
+            RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + (size_t)SPILL_CAP) * 4));
+            h->pp_spill_cap = SPILL_CAP;
+        }
         HIPCHECK(hipMemsetAsync(h->pp_spill, 0, 4, h->stream));
         prof::Scope ps("pp_agg", h->stream);
         launch_pp_agg_spec(h->stream, h->pp_spec, mode, 1u << h->pp_bits, R.part, R.fin, h->pp_spec_sub, o, h->pp_spill, SPILL_CAP);
@@ -1429,8 +1449,15 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
         launch_pp_agg(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.part, nullptr, R.fin, R.alt, nullptr, nullptr,
                       o, h->pp_spill, SPILL_CAP);
     } else if (h->pp_rc_sub) {
-        constexpr u32 SPILL_CAP = 4096;
-        if (!h->pp_spill) RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + SPILL_CAP) * 4));
+        // every final partition may spill (skewed keys): room for all their ids (<= 1 MB)
+        const u32 SPILL_CAP = 1u << h->pp_bits;
+        if (h->pp_spill_cap < SPILL_CAP) {
+            if (h->pp_spill) HIPCHECK(hipFree(h->pp_spill));
+            h->pp_spill = nullptr;
+            h->pp_spill_cap = 0;
+            RETURN_IF(dev_alloc((void**)&h->pp_spill, (1 + (size_t)SPILL_CAP) * 4));
+            h->pp_spill_cap = SPILL_CAP;
+        }
         HIPCHECK(hipMemsetAsync(h->pp_spill, 0, 4, h->stream));
         prof::Scope ps("pp_agg", h->stream);
         launch_pp_agg_rc(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.part, R.fin, 64 - h->pp_bits - h->pp_rc_sub,
@@ -1540,9 +1567,20 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
     // A first batch the probe puts at many groups gets a table sized for them before its insert:
     // the partitioned insert needs a large table, and growing by overflow afterwards costs the
     // whole batch again (C3's first 1e9-row batch into the initial table: 1.5 s + a retry pass)
+    // (AggregateHashTable::get_capacity_for_count: next_pow2(count * LOAD_FACTOR 1.5),
+    // EAGG/aggregate_hashtable.rs:567-569, mod.rs:49 — 2x, the earlier rule, put C3's 1.34e8 groups
+    // 0.06 % below 2^28 and any estimator overshoot doubled the table, a radix pass and both
+    // finalize scans).  Best-effort: capped at half the free device memory, and a failed
+    // allocation keeps the current table (overflow growth then sizes it by the rows it meets).
     if (h->table_rows == 0 && h->pp_probed && h->est_groups > 65536.0) {
-        const u64 target = pow2_at_least((u64)std::min(2.0 * h->est_groups + 1.0, (double)(1ULL << 31)));
-        if (target > h->cap) RETURN_IF(grow_table(h, target));
+        u64 target = pow2_at_least((u64)std::min(1.5 * h->est_groups + 1.0, (double)(1ULL << 31)));
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            while (target > h->cap && (double)(target + 1) * h->spec.stride_words * 8.0 > 0.5 * (double)free_b) target >>= 1;
+        if (target > h->cap && grow_table(h, target) != DBG_OK) {
+            (void)hipGetLastError();
+            g_last_error.clear();
+        }
     }
     h->table_rows += rows;
     const bool was_clean = h->clean;
@@ -1923,6 +1961,8 @@ int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy) {
         return fail(DBG_ERR_UNSUPPORTED, "dbg_agg_set_strategy: records too wide for the partitioned payload");
     h->strategy = strategy;
     h->pp = strategy == DBG_STRATEGY_PARTITIONED;
+    // a new strategy starts a new query on the handle: forget the cardinality the last finalize saw
+    h->obs_rows = h->obs_groups = 0;
     return DBG_OK;
 }
 
@@ -2063,7 +2103,7 @@ static int fin_launch(dbg_agg_handle* h) {
             // measured and not kept (C2 step 45.1 -> 138 us: 256 workgroups' device atomics on the
             // same ~33 addresses serialise at the memory side, profiles/r04/c2_dense_ab.json):
             // EXPERIMENT, DBG_X_DENSE=1
-            static const bool dense_on = getenv("DBG_X_DENSE") && getenv("DBG_X_DENSE")[0] == '1';
+            static const bool dense_on = X_ENV("DBG_X_DENSE") && X_ENV("DBG_X_DENSE")[0] == '1';
             const int kt = S.key_types[0].type;
             const u32 kw = (kt == DBG_INT8 || kt == DBG_UINT8) ? 1 : ((kt == DBG_INT16 || kt == DBG_UINT16) ? 2 : 0);
             const bool co = S.n_aggs == 1 && S.aggs[0].kind == DBG_AGG_COUNT && S.aggs[0].arg_type < 0 && S.aggs[0].w0 == 1;
@@ -2078,7 +2118,7 @@ static int fin_launch(dbg_agg_handle* h) {
         }
         static u64* x_trace = nullptr;  // EXPERIMENT (DBG_X_TRACE): 8 words per launch, 4096 launches
         static std::vector<u64> x_init;
-        if (kPhaseTrace && getenv("DBG_X_TRACE")) {
+        if (kPhaseTrace && X_ENV("DBG_X_TRACE")) {
             if (!x_trace) {
                 RETURN_IF(dev_alloc((void**)&x_trace, 4096 * 128));
                 x_init.assign(16, 0);
@@ -2573,9 +2613,10 @@ int dbg_agg_compact(dbg_agg_handle* h, int* compacted) {
     // the handle keeps its strategy: the re-merged batch (one record per group) must not be
     // probed again — on an AUTO handle with many groups the probe would see ratio ~1 and switch
     // to the partitioned payload, after which compaction does nothing
-    const u64 rows_before = h->table_rows;
+    const u64 rows_before = h->table_rows, remerged_before = h->remerged;
     if (rc == DBG_OK) rc = dbg_agg_reset(h);  // frees the copies of earlier inputs
     h->table_rows = rows_before ? rows_before : 1;
+    h->remerged = remerged_before + n;  // merge_record_batch below counts the n records as rows
     if (rc != DBG_OK) {
         hipFree(rb.p);
         if (strb.p) hipFree(strb.p);
@@ -3012,6 +3053,7 @@ struct dbg_comm {
     u64 send_recs_cap = 0, send_strs_cap = 0;
     hipEvent_t sent = nullptr;  // the last exchange's sends: the next export into the buffers waits
     bool sent_valid = false;
+    hipEvent_t merged = nullptr;  // the final table's stream after a merge: cached receive buffers are reused behind it
     // before-partial payload exchange: send and receive buffers kept between calls (grown only)
     u8* pay_send = nullptr;
     u8* pay_recv[2] = {nullptr, nullptr};
@@ -3049,9 +3091,10 @@ int dbg_comm_create(const uint8_t* id, int n_ranks, int rank, int device, dbg_co
         delete c;
         return fail(DBG_ERR_DEVICE, std::string("ncclCommInitRank: ") + R.ErrorString(r));
     }
-    const u64 words = 2ull * n_ranks * (n_ranks + 1);
+    const u64 words = (2ull * n_ranks + 1) * (n_ranks + 1);  // own [2n + 1] sizes + ok word, then n rows
     if (dev_alloc((void**)&c->dsizes, words * 8) != DBG_OK || hipHostMalloc((void**)&c->hsizes, words * 8, hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sent, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->sent, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->merged, hipEventDisableTiming) != hipSuccess) {
         dbg_comm_destroy(c);
         return fail(DBG_ERR_OOM, "communicator scratch");
     }
@@ -3074,6 +3117,7 @@ void dbg_comm_destroy(dbg_comm* c) {
     if (c->pay_dbuf) hipFree(c->pay_dbuf);
     if (c->hsizes) hipHostFree(c->hsizes);
     if (c->sent) hipEventDestroy(c->sent);
+    if (c->merged) hipEventDestroy(c->merged);
     delete c;
 }
 
@@ -3346,6 +3390,59 @@ int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats*
     return DBG_OK;
 }
 
+// Byte plan of the before_merge exchange for one rank (host only; Payload::scatter's routing,
+// EAGG/payload.rs:356-391, shipped as AggregateExchangeInjector does per destination,
+// AGG/aggregate_exchange_injector.rs:154-235).  all[s * 2n + 2d + {0, 1}] = the records / string
+// bytes source s sends to rank d.  send_bytes[d] / send_bytes[n + d]: this rank's record / blob
+// bytes for d in export (partition-major) order; recv_bytes[s] / recv_bytes[n + s] and
+// recv_records[s]: what source s sends this rank, in merge (source-major) order.  The offsets are
+// their prefix sums.  Self included.
+static void merge_plan(u32 n, u32 me, u32 w, const u64* all, u64* send_bytes, u64* recv_bytes, u64* recv_records) {
+    for (u32 d = 0; d < n; ++d) {
+        send_bytes[d] = all[(u64)me * 2 * n + 2 * d] * w;
+        send_bytes[n + d] = all[(u64)me * 2 * n + 2 * d + 1];
+        recv_records[d] = all[(u64)d * 2 * n + 2 * me];
+        recv_bytes[d] = recv_records[d] * w;
+        recv_bytes[n + d] = all[(u64)d * 2 * n + 2 * me + 1];
+    }
+}
+
+int dbg_merge_exchange_plan(const dbg_agg_params* params, uint32_t n_ranks, uint32_t rank, const uint64_t* all_sizes,
+                            uint32_t* record_width, uint64_t* send_bytes, uint64_t* recv_bytes, uint64_t* recv_records) {
+    if (!params || !all_sizes || !send_bytes || !recv_bytes || !recv_records || n_ranks == 0 || rank >= n_ranks)
+        return fail(DBG_ERR_INVALID, "dbg_merge_exchange_plan: bad argument");
+    Spec S;
+    std::vector<dbg_datatype> rt;
+    RETURN_IF(build_spec(params, S, rt));
+    if (record_width) *record_width = S.rec_width;
+    merge_plan(n_ranks, rank, S.rec_width, all_sizes, send_bytes, recv_bytes, recv_records);
+    return DBG_OK;
+}
+
+// A receive buffer of the final table: its cached one when no group references it (grown only),
+// otherwise a fresh allocation the table owns until its reset.
+static int xrecv_buffer(dbg_agg_handle* fh, int k, u64 bytes, void** out) {
+    bytes = std::max<u64>(bytes, 16);
+    if (fh->xrecv_busy) {
+        DevBuf b;
+        b.bytes = bytes;
+        RETURN_IF(dev_alloc(&b.p, bytes));
+        fh->owned.push_back(b);
+        *out = b.p;
+        return DBG_OK;
+    }
+    DevBuf& b = fh->xrecv[k];
+    if (b.bytes < bytes) {
+        if (b.p) HIPCHECK(hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+        RETURN_IF(dev_alloc(&b.p, bytes));
+        b.bytes = bytes;
+    }
+    *out = b.p;
+    return DBG_OK;
+}
+
 int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final_h, dbg_exchange_stats* stats) {
     if (!c || !partial || !final_h) return fail(DBG_ERR_INVALID, "null argument");
     if (partial->device != c->device || final_h->device != c->device)
@@ -3356,51 +3453,66 @@ int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final
     RcclApi& R = rccl_api();
     if (!R.ok) return fail(DBG_ERR_UNSUPPORTED, R.err);
     HIPCHECK(hipSetDevice(c->device));
-    const int n = c->n, me = c->rank;
-    std::vector<u64> counts(n), sbytes(n);
-    // Payload::scatter's routing (EAGG/payload.rs:377-383): group -> rank hash % n
-    RETURN_IF(dbg_agg_partition(partial, (uint32_t)n, 0, counts.data(), sbytes.data()));
+    const u32 n = (u32)c->n, me = (u32)c->rank, W = 2 * n + 1;  // per rank: [records, bytes] per destination + ok
+    std::vector<u64> counts(n, 0), sbytes(n, 0);
+    // Payload::scatter's routing (EAGG/payload.rs:377-383): group -> rank hash % n.  A local
+    // failure here still takes part in the sizes all-gather (ok word 0), so no peer is left
+    // waiting in it; every rank then sees the same flags and all return together.
+    int rc = dbg_agg_partition(partial, n, 0, counts.data(), sbytes.data());
     uint32_t w = 0;
-    RETURN_IF(dbg_agg_record_width(partial, &w));
+    if (rc == DBG_OK) rc = dbg_agg_record_width(partial, &w);
+    std::string local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
+    if (rc != DBG_OK) std::fill(counts.begin(), counts.end(), 0), std::fill(sbytes.begin(), sbytes.end(), 0);
     hipStream_t s = partial->stream;
-    // 1. sizes: every rank's [records, string bytes] per destination, one all-gather
+    // 1. sizes: every rank's [records, string bytes] per destination and its ok word, one all-gather
     u64* own = c->hsizes;
-    for (int d = 0; d < n; ++d) {
+    for (u32 d = 0; d < n; ++d) {
         own[2 * d] = counts[d];
         own[2 * d + 1] = sbytes[d];
     }
-    HIPCHECK(hipMemcpyAsync(c->dsizes, own, 16ull * n, hipMemcpyHostToDevice, s));
-    RCCLCHECK(R.AllGather(c->dsizes, c->dsizes + 2 * n, 2 * n, ncclUint64, c->comm, s));
-    HIPCHECK(hipMemcpyAsync(c->hsizes + 2 * n, c->dsizes + 2 * n, 16ull * n * n, hipMemcpyDeviceToHost, s));
-    // 2. records + blobs, partition-major, into the communicator's send buffers; the receive
-    //    buffers.  A local failure from here on is made collective (all_ok) before any rank posts a
-    //    send or receive, so no peer waits for transfers this rank never starts.
-    u64 tot_r = 0, tot_s = 0;
-    for (int d = 0; d < n; ++d) {
+    own[2 * n] = rc == DBG_OK ? 1 : 0;
+    HIPCHECK(hipMemcpyAsync(c->dsizes, own, 8ull * W, hipMemcpyHostToDevice, s));
+    RCCLCHECK(R.AllGather(c->dsizes, c->dsizes + W, W, ncclUint64, c->comm, s));
+    HIPCHECK(hipMemcpyAsync(c->hsizes + W, c->dsizes + W, 8ull * W * n, hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    std::vector<u64> all(2ull * n * n);
+    for (u32 r = 0; r < n; ++r) {
+        const u64* row = c->hsizes + W + (u64)r * W;
+        if (row[2 * n] != 1) {
+            if (rc != DBG_OK) return fail(rc, local_err);
+            return fail(DBG_ERR_DEVICE, "exchange: rank " + std::to_string(r) + " failed before the size exchange");
+        }
+        std::copy(row, row + 2 * n, all.begin() + (u64)r * 2 * n);
+    }
+    // 2. the plan, records + blobs (partition-major) into the communicator's send buffers, the
+    //    final table's receive buffers.  A local failure from here on is made collective (all_ok)
+    //    before any rank posts a send or receive.
+    std::vector<u64> send_b(2 * n), recv_b(2 * n), seg_r(n), seg_s(n);
+    merge_plan(n, me, w, all.data(), send_b.data(), recv_b.data(), seg_r.data());
+    u64 tot_r = 0, tot_s = 0, rr = 0, rs = 0;
+    for (u32 d = 0; d < n; ++d) {
         tot_r += counts[d];
         tot_s += sbytes[d];
+        seg_s[d] = recv_b[n + d];
+        rr += seg_r[d];
+        rs += seg_s[d];
     }
     if (c->sent_valid) HIPCHECK(hipEventSynchronize(c->sent));
     c->sent_valid = false;
-    int rc = grow_dev(&c->send_recs, &c->send_recs_cap, tot_r * w);
+    rc = grow_dev(&c->send_recs, &c->send_recs_cap, tot_r * w);
     if (rc == DBG_OK) rc = grow_dev(&c->send_strs, &c->send_strs_cap, tot_s);
     if (rc == DBG_OK) rc = dbg_agg_export_records(partial, c->send_recs, c->send_strs);
-    if (hipStreamSynchronize(s) != hipSuccess && rc == DBG_OK) rc = fail(DBG_ERR_DEVICE, "exchange: size all-gather");
-    const u64* g = c->hsizes + 2 * n;   // g[src * 2n + 2 * dst + {0, 1}]
-    std::vector<u64> seg_r(n), seg_s(n);
-    u64 rr = 0, rs = 0;
-    for (int src = 0; src < n; ++src) {
-        seg_r[src] = g[(u64)src * 2 * n + 2 * me];
-        seg_s[src] = g[(u64)src * 2 * n + 2 * me + 1];
-        rr += seg_r[src];
-        rs += seg_s[src];
-    }
-    if (rc == DBG_OK && (seg_r[me] != counts[me] || seg_s[me] != sbytes[me])) rc = fail(DBG_ERR_INTERNAL, "exchange sizes disagree");
-    // receive buffers belong to the final table: merge_records retains them until its reset
+    if (rc == DBG_OK && (send_b[me] != counts[me] * w || seg_r[me] != counts[me] || seg_s[me] != sbytes[me]))
+        rc = fail(DBG_ERR_INTERNAL, "exchange sizes disagree");
     void *rrec = nullptr, *rstr = nullptr;
-    if (rc == DBG_OK && (rc = dev_alloc(&rrec, rr * w)) == DBG_OK) final_h->owned.push_back({rrec, (size_t)std::max<u64>(rr * w, 16)});
-    if (rc == DBG_OK && (rc = dev_alloc(&rstr, rs)) == DBG_OK) final_h->owned.push_back({rstr, (size_t)std::max<u64>(rs, 16)});
-    const std::string local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
+    if (rc == DBG_OK) rc = xrecv_buffer(final_h, 0, rr * w, &rrec);
+    if (rc == DBG_OK) rc = xrecv_buffer(final_h, 1, rs, &rstr);
+    // the last merge into the cached buffers has read them before this exchange overwrites them
+    if (rc == DBG_OK && final_h->stream != s) {
+        if (hipEventRecord(c->merged, final_h->stream) != hipSuccess || hipStreamWaitEvent(s, c->merged, 0) != hipSuccess)
+            rc = fail(DBG_ERR_DEVICE, "exchange: stream ordering");
+    }
+    local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
     int bad = -1;
     RETURN_IF(all_ok(c, R, s, rc == DBG_OK, &bad));
     if (bad >= 0) {
@@ -3410,22 +3522,24 @@ int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final
     // 3. grouped point-to-point over xGMI (records and blobs; self included)
     RCCLCHECK(R.GroupStart());
     u64 so_r = 0, so_s = 0, ro_r = 0, ro_s = 0;
-    for (int p = 0; p < n; ++p) {
-        if (counts[p]) RCCLCHECK(R.Send(c->send_recs + so_r * w, counts[p] * w, ncclUint8, p, c->comm, s));
-        if (sbytes[p]) RCCLCHECK(R.Send(c->send_strs + so_s, sbytes[p], ncclUint8, p, c->comm, s));
-        if (seg_r[p]) RCCLCHECK(R.Recv((u8*)rrec + ro_r * w, seg_r[p] * w, ncclUint8, p, c->comm, s));
-        if (seg_s[p]) RCCLCHECK(R.Recv((u8*)rstr + ro_s, seg_s[p], ncclUint8, p, c->comm, s));
-        so_r += counts[p];
-        so_s += sbytes[p];
-        ro_r += seg_r[p];
-        ro_s += seg_s[p];
+    for (u32 p = 0; p < n; ++p) {
+        if (send_b[p]) RCCLCHECK(R.Send(c->send_recs + so_r, send_b[p], ncclUint8, (int)p, c->comm, s));
+        if (send_b[n + p]) RCCLCHECK(R.Send(c->send_strs + so_s, send_b[n + p], ncclUint8, (int)p, c->comm, s));
+        if (recv_b[p]) RCCLCHECK(R.Recv((u8*)rrec + ro_r, recv_b[p], ncclUint8, (int)p, c->comm, s));
+        if (recv_b[n + p]) RCCLCHECK(R.Recv((u8*)rstr + ro_s, recv_b[n + p], ncclUint8, (int)p, c->comm, s));
+        so_r += send_b[p];
+        so_s += send_b[n + p];
+        ro_r += recv_b[p];
+        ro_s += recv_b[n + p];
     }
     RCCLCHECK(R.GroupEnd());
     HIPCHECK(hipEventRecord(c->sent, s));
     c->sent_valid = true;
     if (final_h->stream != s) HIPCHECK(hipStreamWaitEvent(final_h->stream, c->sent, 0));
-    // 4. merge_states of what arrived into this rank's final table
-    RETURN_IF(dbg_agg_merge_records(final_h, rrec, rstr, n, seg_r.data(), seg_s.data()));
+    // 4. merge_states of what arrived into this rank's final table; its entries may point into
+    //    the receive buffers until its next reset
+    final_h->xrecv_busy = true;
+    RETURN_IF(dbg_agg_merge_records(final_h, rrec, rstr, (int32_t)n, seg_r.data(), seg_s.data()));
     if (stats) {
         stats->sent_bytes = tot_r * w + tot_s;
         stats->remote_bytes = stats->sent_bytes - counts[me] * w - sbytes[me];

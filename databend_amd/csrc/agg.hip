@@ -854,7 +854,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
             generic_row(i);
             return;
         }
-        if (xmode == 2 || xmode == 4) return;  // timing ablation only
+        if (kExperiments && (xmode == 2 || xmode == 4)) return;  // timing ablation (EXP=1 builds only)
         wptr<AS_LDS> st = asp<AS_LDS>(lds + (u64)ls * sw);
 #pragma unroll
         for (int a = 0; a < SHORT_MAXA; ++a) {
@@ -904,7 +904,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
         }
     }
     __syncthreads();
-    if (xmode >= 3) return;  // timing ablation only (DBG_X_SHORT=3: no flush)
+    if (kExperiments && xmode >= 3) return;  // timing ablation (EXP=1 builds only: no flush)
     if (narrow) {  // short slots: narrow partials -> Decimal128 state (high word = sign)
         for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
             const u64 pk = pk0[s];
@@ -1446,7 +1446,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
     // write pass over the occupied slots only (one write_group instance in the code; the entry
     // is re-read from the cache rather than indexed out of the register array)
     const u32 occ_all = occ;
-    if (xfin & 1) occ = 0;  // timing ablation only
+    if (kExperiments && (xfin & 1)) occ = 0;  // timing ablation (EXP=1 builds only)
     while (occ && p < out.cap_groups) {
         const u32 k = __builtin_ctz(occ);
         occ &= occ - 1;
@@ -1457,7 +1457,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
     }
     mark(8);
     u64 n = total < out.cap_groups ? total : out.cap_groups;
-    if (has_bits && !(xfin & 2)) {
+    if (has_bits && !(kExperiments && (xfin & 2))) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // validity bytes of every row are in global memory
         const u32 ncols = (u32)(S.n_keys + S.n_aggs);
@@ -1535,13 +1535,13 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
 __global__ void __launch_bounds__(FIN_NT) finalize_small_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                 TableDesc t, OutDesc out, u64* totals, u64* host_mirror,
                                                                 int recycle, u64 seq, int xfin) {
-    if (xfin & 8) return;  // timing ablation only
+    if (kExperiments && (xfin & 8)) return;  // timing ablation (EXP=1 builds only)
     finalize_small_body<FIN_MAXPER>(*spec, batches, t, t.slots, out, totals, host_mirror, recycle, seq, nullptr, false, xfin);
 }
 
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
                            u64* totals, u64* host_mirror, int recycle, u64 seq) {
-    static const int xfin = getenv("DBG_X_FIN") ? atoi(getenv("DBG_X_FIN")) : 0;
+    static const int xfin = X_ENV("DBG_X_FIN") ? atoi(X_ENV("DBG_X_FIN")) : 0;
     hipLaunchKernelGGL(finalize_small_kernel, dim3(1), dim3(FIN_NT), 0, s, dspec, batches, t, out, totals, host_mirror, recycle,
                        seq, xfin);
 }
@@ -2437,7 +2437,7 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     // one 1024-lane workgroup per CU (parked-row chain: 512 / 768 / 1024 / 2048 measured 52 / 55 / 63
     // / 90 us a C2 step); EXPERIMENT DBG_X_FAST_GRID for the dense hand-off, whose merge does not
     // grow with the grid
-    static const u64 x_grid = getenv("DBG_X_FAST_GRID") ? (u64)atoll(getenv("DBG_X_FAST_GRID")) : 0;
+    static const u64 x_grid = X_ENV("DBG_X_FAST_GRID") ? (u64)atoll(X_ENV("DBG_X_FAST_GRID")) : 0;
     const u64 max_blocks = (x_grid && fused && fused->dense) ? x_grid : 256;
     size_t shmem = fast_shmem(table_bytes);
     FusedFin ff;
@@ -2502,8 +2502,8 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
         }
     }
     u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
-    static const int x_short = getenv("DBG_X_SHORT") ? atoi(getenv("DBG_X_SHORT")) : 1;
-    static const u32 x_rep = getenv("DBG_X_SHORT_REP") ? (u32)atoi(getenv("DBG_X_SHORT_REP")) : 0;
+    static const int x_short = X_ENV("DBG_X_SHORT") ? atoi(X_ENV("DBG_X_SHORT")) : 1;
+    static const u32 x_rep = X_ENV("DBG_X_SHORT_REP") ? (u32)atoi(X_ENV("DBG_X_SHORT_REP")) : 0;
     const bool x_noshort = x_short == 0;
     // low cardinality only: with a table already sized for many groups (the cardinality probe, or
     // earlier batches) most rows miss the workgroup's LDS table, and the generic kernel's queued
@@ -2525,8 +2525,9 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
             for (int k = 0; k < p; ++k) lim *= 10.0;
             if (p > 0 && p <= 18 && lim * (double)rpb < 9.0e18) narrow |= 1u << a;
         }
-        if (getenv("DBG_X_NARROW") && getenv("DBG_X_NARROW")[0] == '0') narrow = 0;
-        static const bool x_tree = getenv("DBG_X_TREE") && getenv("DBG_X_TREE")[0] == '1';
+        static const bool x_wide = X_ENV("DBG_X_NARROW") && X_ENV("DBG_X_NARROW")[0] == '0';
+        if (x_wide) narrow = 0;
+        static const bool x_tree = X_ENV("DBG_X_TREE") && X_ENV("DBG_X_TREE")[0] == '1';
         hipLaunchKernelGGL(agg_insert_short_kernel, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots,
                            x_rep ? x_rep - 1 : 0u, x_short, narrow, x_tree && S.stride_words >= S.n_words + 3 ? 1 : 0);
         return;

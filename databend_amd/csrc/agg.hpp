@@ -212,6 +212,18 @@ constexpr bool kPhaseTrace = true;
 constexpr bool kPhaseTrace = false;
 #endif
 
+// Experiment knobs (DBG_X_*: ablations, alternative kernels, tile shapes) are read only by a
+// library built with `make EXP=1` (-DDBG_EXPERIMENTS).  The shipped library never reads them, so
+// a stray environment variable cannot change what it computes; the one test hook it keeps is
+// DBG_X_PPSPEC_CAP (a smaller LDS table for the specialised pp aggregation: same results).
+#ifdef DBG_EXPERIMENTS
+constexpr bool kExperiments = true;
+#define X_ENV(name) getenv(name)
+#else
+constexpr bool kExperiments = false;
+#define X_ENV(name) ((const char*)nullptr)
+#endif
+
 struct FusedFin;
 // ---- launch wrappers (agg.hip) ----
 // part.hip: radix-partitioned COUNT(*) insert for high-cardinality single integer keys

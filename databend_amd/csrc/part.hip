@@ -479,7 +479,7 @@ struct RpShape {
 RpShape rp_shape() {
     static RpShape sh = [] {
         RpShape r{512, 16};
-        if (const char* e = getenv("DBG_X_RP")) {
+        if (const char* e = X_ENV("DBG_X_RP")) {
             int a = 0, b = 0;
             if (sscanf(e, "%d,%d", &a, &b) == 2) r = RpShape{a, b};
         }
@@ -591,7 +591,7 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
                        n_slices, bounds);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_slice";
-    static const int slice_nt = getenv("DBG_X_SLICE_NT") ? atoi(getenv("DBG_X_SLICE_NT")) : PART_NT_DEFAULT;
+    static const int slice_nt = X_ENV("DBG_X_SLICE_NT") ? atoi(X_ENV("DBG_X_SLICE_NT")) : PART_NT_DEFAULT;
     const size_t sh = (size_t)(12ULL << PART_SB);
 #define SLICE_GO(EM, NTT) \
     hipLaunchKernelGGL((part_slice_kernel<PART_SB, EM, NTT>), dim3((u32)n_slices), dim3(NTT), sh, s, sorted, bounds, t)

@@ -62,6 +62,21 @@ def exchange_records(recs, strs, counts: Sequence[int], sbytes: Sequence[int], w
     return _exchange_with_sizes(recs, strs, counts, sbytes, width, device, world)
 
 
+def merge_splits(counts, sbytes, got_pairs, width: int):
+    """Byte plan of the before_merge exchange on one rank (the plan dbg_agg_exchange follows,
+    dbg_merge_exchange_plan): counts[d] / sbytes[d] are this rank's records / blob bytes for rank d,
+    got_pairs[s] = (records, blob bytes) source s sends this rank.  Returns (record send splits,
+    blob send splits, record receive splits, blob receive splits, per-source record counts), in
+    bytes except the last; send order is export (partition-major) order, receive order is source
+    order — the order dbg_agg_merge_records takes its segments in."""
+    send_r = [int(c) * width for c in counts]
+    send_s = [int(b) for b in sbytes]
+    seg_records = [int(c) for c, _ in got_pairs]
+    recv_r = [c * width for c in seg_records]
+    recv_s = [int(b) for _, b in got_pairs]
+    return send_r, send_s, recv_r, recv_s, seg_records
+
+
 def _exchange_with_sizes(recs, strs, counts, sbytes, width, device, world):
     import torch
     dist = _dist()
@@ -71,16 +86,13 @@ def _exchange_with_sizes(recs, strs, counts, sbytes, width, device, world):
     got = torch.empty_like(pairs)
     dist.all_to_all_single(got, pairs)
     got = got.view(world, 2).tolist()
-    seg_records = [int(c) for c, _ in got]
-    seg_strings = [int(s) for _, s in got]
-    rrecv = torch.empty(max(1, sum(seg_records) * width), dtype=torch.uint8, device=device)
+    send_r, send_s, recv_r, seg_strings, seg_records = merge_splits(counts, sbytes, got, width)
+    rrecv = torch.empty(max(1, sum(recv_r)), dtype=torch.uint8, device=device)
     srecv = torch.empty(max(1, sum(seg_strings)), dtype=torch.uint8, device=device)
-    nsend = sum(counts) * width
-    dist.all_to_all_single(rrecv[:sum(seg_records) * width], recs[:nsend],
-                           output_split_sizes=[c * width for c in seg_records],
-                           input_split_sizes=[c * width for c in counts])
-    dist.all_to_all_single(srecv[:sum(seg_strings)], strs[:sum(sbytes)],
-                           output_split_sizes=seg_strings, input_split_sizes=list(sbytes))
+    dist.all_to_all_single(rrecv[:sum(recv_r)], recs[:sum(send_r)],
+                           output_split_sizes=recv_r, input_split_sizes=send_r)
+    dist.all_to_all_single(srecv[:sum(seg_strings)], strs[:sum(send_s)],
+                           output_split_sizes=seg_strings, input_split_sizes=send_s)
     return rrecv[:max(0, sum(seg_records) * width)], srecv[:sum(seg_strings)], seg_records, seg_strings
 
 

@@ -301,6 +301,8 @@ int dbg_agg_set_host_staging(dbg_agg_handle* h, uint64_t rows);
  * In partitioned mode a capacity_hint (dbg_agg_params) is the expected group count that sizes the
  * final partitions; dbg_agg_export_fixed / dbg_agg_merge_fixed return DBG_ERR_UNSUPPORTED. */
 enum { DBG_STRATEGY_AUTO = 0, DBG_STRATEGY_TABLE = 1, DBG_STRATEGY_PARTITIONED = 2 };
+/* Setting a strategy also forgets the cardinality the handle's last finalize observed (which
+ * otherwise decides the next first batch's strategy and table size without a probe). */
 int dbg_agg_set_strategy(dbg_agg_handle* h, int strategy);
 /* *partitioned = the handle's current mode (0 table, 1 partitioned payload, 2 partitioned payload
  * whose last finalize ran the compile-time specialised aggregation); *extra_rounds (may be NULL) =
@@ -389,8 +391,20 @@ int dbg_comm_create(const uint8_t* id, int n_ranks, int rank, int device /* -1 =
 void dbg_comm_destroy(dbg_comm* c);
 /* Collective over the communicator's ranks.  partial and final live on the communicator's device
  * and have the same dbg_agg_params (partial = 1 / 0).  Asynchronous except for the size
- * all-gather; stats may be NULL. */
+ * all-gather; stats may be NULL.  A rank whose partition or export fails still takes part in the
+ * size all-gather and in one ok-flag all-gather before any send or receive, so every rank returns
+ * an error together and none is left blocked.  Send buffers live in the communicator and receive
+ * buffers in the final table (grown only, reused once the table has been reset), so a repeated
+ * step allocates no device memory. */
 int dbg_agg_exchange(dbg_comm* c, dbg_agg_handle* partial, dbg_agg_handle* final_table, dbg_exchange_stats* stats);
+/* The byte plan dbg_agg_exchange follows on rank `rank` (host only, no device work):
+ * all_sizes[s * 2n + 2d + {0, 1}] = the records / string bytes source s sends rank d (as
+ * gathered); record_width receives the params' exchange record bytes (may be NULL);
+ * send_bytes[d] / send_bytes[n + d] = this rank's record / blob bytes for rank d (export order);
+ * recv_bytes[s] / recv_bytes[n + s] and recv_records[s] = what source s sends this rank (merge
+ * order).  Offsets are the prefix sums. */
+int dbg_merge_exchange_plan(const dbg_agg_params* params, uint32_t n_ranks, uint32_t rank, const uint64_t* all_sizes,
+                            uint32_t* record_width, uint64_t* send_bytes, uint64_t* recv_bytes, uint64_t* recv_records);
 
 /* ---- before-partial shuffle of the partitioned payload (mostly-unique keys) ----
  * group_by_shuffle_mode = before_partial (src/query/settings/src/settings_default.rs:469-473;

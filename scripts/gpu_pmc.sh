@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: FETCH_SIZE / WRITE_SIZE passes over marker-delimited steps of C1, C3, C4, C5 (kernels changed
+# FETCH_SIZE / WRITE_SIZE passes over marker-delimited steps of C1, C3, C4, C5 (kernels changed
 # this round) -> profiles/pmc_traffic_c*.json via scripts/pmc_step_traffic.py
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out

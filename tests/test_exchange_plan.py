@@ -55,3 +55,53 @@ def test_payload_plan_rejects_bad_arguments():
     recv = (C.c_uint64 * 4)()
     with pytest.raises(DbgError):
         check(lib().dbg_payload_exchange_plan(C.byref(p), 2, 2, counts.ctypes.data_as(C.POINTER(C.c_uint64)), None, send, recv))
+
+
+def _merge_params():
+    """ClickBench Q13's partial shape (SearchPhrase String key; COUNT(*)) beside Q17's (UserID)."""
+    return [AggregatorParams([col.String], [F.get("count")]),
+            AggregatorParams([col.Int64], [F.get("count")]),
+            AggregatorParams([col.Int64, col.Int32], [F.get("count"), F.get("sum", [], [col.Int16]), F.get("sql_avg", [], [col.Int16])])]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 7, 8])
+def test_merge_plan_matches_python(world):
+    """The before_merge exchange's plan inside the library (dbg_merge_exchange_plan, the function
+    dbg_agg_exchange follows) against databend_amd.exchange.merge_splits (the torch.distributed
+    path's plan), with the library's record widths: every rank's send splits equal what each peer
+    receives from it, in the peer's source order, and the sizes include self."""
+    from databend_amd.exchange import merge_splits
+    rng = np.random.default_rng(100 + world)
+    for params in _merge_params():
+        all_sizes = rng.integers(0, 5000, (world, world, 2)).astype(np.uint64)
+        all_sizes[rng.random((world, world)) < 0.2] = 0  # empty segments, self included
+        p, keep = params.to_abi(True, 0, -1)
+        flat = np.ascontiguousarray(all_sizes.reshape(-1))
+        plans = []
+        for rank in range(world):
+            w = C.c_uint32()
+            send = (C.c_uint64 * (2 * world))()
+            recv = (C.c_uint64 * (2 * world))()
+            recs = (C.c_uint64 * world)()
+            check(lib().dbg_merge_exchange_plan(C.byref(p), world, rank, flat.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                                C.byref(w), send, recv, recs))
+            width = w.value
+            assert width % 8 == 0 and width >= 16
+            counts, sbytes = all_sizes[rank, :, 0], all_sizes[rank, :, 1]
+            got = [(int(all_sizes[s, rank, 0]), int(all_sizes[s, rank, 1])) for s in range(world)]
+            sr, ss, rr, rs, seg = merge_splits(counts, sbytes, got, width)
+            assert list(send[:world]) == sr and list(send[world:]) == ss
+            assert list(recv[:world]) == rr and list(recv[world:]) == rs and list(recs) == seg
+            plans.append((list(send), list(recv)))
+        for a in range(world):  # a's send to b is b's receive from a
+            for b in range(world):
+                assert plans[a][0][b] == plans[b][1][a] and plans[a][0][world + b] == plans[b][1][world + a]
+
+
+def test_merge_plan_rejects_bad_arguments():
+    from databend_amd.ffi import DbgError
+    p, keep = _merge_params()[1].to_abi(True, 0, -1)
+    sizes = np.zeros(2 * 2 * 2, dtype=np.uint64)
+    send, recv, recs = (C.c_uint64 * 4)(), (C.c_uint64 * 4)(), (C.c_uint64 * 2)()
+    with pytest.raises(DbgError):
+        check(lib().dbg_merge_exchange_plan(C.byref(p), 2, 2, sizes.ctypes.data_as(C.POINTER(C.c_uint64)), None, send, recv, recs))

@@ -284,3 +284,20 @@ def test_pp_specialised_kernel(kind, monkeypatch):
     assert g > 1_000_000 or kind == "c4_dup"
     if kind == "small_table":
         assert info["extra_rounds"] > 0
+
+
+def test_pp_specialised_many_spills():
+    """Thousands of heavy keys (> 8192 records each, the specialised kernel's register budget)
+    spread over most final partitions: more than 4096 partitions spill to the generic kernel.  The
+    spill list holds one id per final partition, so none is dropped (a fixed 4096-entry list
+    failed the whole aggregate with DBG_ERR_INTERNAL here).  Checked against numpy's unique counts."""
+    rng = np.random.default_rng(2024)
+    heavy, per, uniq = 6000, 8400, 8_000_000
+    k = np.concatenate([np.repeat(rng.integers(2**40, 2**41, heavy), per), rng.integers(0, 2**39, uniq)])
+    k = k[rng.permutation(len(k))].astype(np.int64)
+    keys = [Column.from_numbers(col.Int64, k)]
+    info = {}
+    gk, ga = gpu_aggregate(keys, [("count", None)], strategy=PP, info=info, on_device=True)
+    assert info["partitioned"] and info["specialised"]
+    uk, uc = np.unique(k, return_counts=True)
+    assert_results_equal(gk, ga, [Column.from_numbers(col.Int64, uk)], [Column.from_numbers(col.UInt64, uc.astype(np.uint64))])
