@@ -456,6 +456,20 @@ static int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype
     while (sw < word && sw < 8) sw <<= 1;
     if (word > 8) sw = (word + 7) & ~7;
     S.stride_words = sw;
+    // one non-null String key: the HBM slot also caches the key (agg_insert_str1_kernel), so a
+    // probe compares in the slot's own line instead of reading the representative row
+    S.tstride = sw;
+    S.kc_word = 0;
+    if (S.n_keys == 1 && S.key_types[0].type == DBG_STRING && !S.key_types[0].nullable) {
+        const int need = word + 1 + KC_KEY_WORDS;  // entry + states (+ flags) + hdr + key words
+        int ts = 1;
+        while (ts < need && ts < 8) ts <<= 1;
+        if (need > 8) ts = (need + 7) & ~7;
+        if (ts <= DBG_MAX_WORDS) {
+            S.tstride = ts;
+            S.kc_word = word;
+        }
+    }
     for (int w = 0; w < DBG_MAX_WORDS; ++w) S.slot_init[w] = w == 0 ? SLOT_EMPTY : 0;
     for (int a = 0; a < S.n_aggs; ++a)
         if (S.aggs[a].kind == DBG_AGG_MIN || S.aggs[a].kind == DBG_AGG_MAX)
@@ -509,7 +523,7 @@ static TableDesc table_desc(dbg_agg_handle* h) {
     TableDesc t;
     t.slots = h->slots;
     t.cap = h->cap;
-    t.stride_words = (u32)h->spec.stride_words;
+    t.stride_words = (u32)h->spec.tstride;
     t.probe_limit = (u32)std::min<u64>(h->cap, 512);
     t.counters = h->counters;
     t.ovf_rows = h->ovf_rows;
@@ -540,7 +554,7 @@ static u64 pow2_at_least(u64 x) {
 }
 
 static int alloc_table(dbg_agg_handle* h, u64 cap, u64** out) {
-    size_t bytes = (size_t)(cap + 1) * h->spec.stride_words * 8;
+    size_t bytes = (size_t)(cap + 1) * h->spec.tstride * 8;
     RETURN_IF(dev_alloc((void**)out, bytes));
     prof::Scope ps("table_init", h->stream);
     launch_table_init(h->stream, h->dspec, h->spec, *out, cap);
@@ -623,7 +637,7 @@ static int ensure_ovf(dbg_agg_handle* h, u64 add_rows, u64 add_recs) {
     if (need_recs > h->ovf_recs_cap) {
         if (h->ovf_recs) HIPCHECK(hipFree(h->ovf_recs));
         h->ovf_recs_cap = std::max<u64>(need_recs, 1024);
-        RETURN_IF(dev_alloc((void**)&h->ovf_recs, h->ovf_recs_cap * h->spec.stride_words * 8));
+        RETURN_IF(dev_alloc((void**)&h->ovf_recs, h->ovf_recs_cap * h->spec.tstride * 8));
     }
     h->pending_rows = need_rows;
     h->pending_recs = need_recs;
@@ -949,7 +963,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     // the counters and the sentinel slot now; the slots when a kernel first touches the table
     // (table_desc), or never if a partitioned insert rewrites every slice first
     prof::Scope ps("table_init", h->stream);
-    launch_table_init(h->stream, h->dspec, h->spec, h->slots + h->cap * (u64)h->spec.stride_words, 0, h->counters);
+    launch_table_init(h->stream, h->dspec, h->spec, h->slots + h->cap * (u64)h->spec.tstride, 0, h->counters);
     h->init_pending = true;
     h->clean = true;
     return DBG_OK;
@@ -1576,7 +1590,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
         u64 target = pow2_at_least((u64)std::min(1.5 * h->est_groups + 1.0, (double)(1ULL << 31)));
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-            while (target > h->cap && (double)(target + 1) * h->spec.stride_words * 8.0 > 0.5 * (double)free_b) target >>= 1;
+            while (target > h->cap && (double)(target + 1) * h->spec.tstride * 8.0 > 0.5 * (double)free_b) target >>= 1;
         if (target > h->cap && grow_table(h, target) != DBG_OK) {
             (void)hipGetLastError();
             g_last_error.clear();

@@ -324,7 +324,7 @@ typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 __global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restrict__ spec, u64* slots, u64 n_slots, u64* counters) {
     const Spec& S = *spec;
     if (counters && blockIdx.x == 0 && threadIdx.x < CNT_WORDS) counters[threadIdx.x] = 0;  // dbg_agg_reset
-    const u32 half = (u32)S.stride_words / 2;
+    const u32 half = (u32)S.tstride / 2;
     const u64 n_chunks = n_slots * half;
     v2u64 __attribute__((address_space(1)))* out = (v2u64 __attribute__((address_space(1)))*)slots;
     if (half == 1) {
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(BLOCK) table_init_kernel(const Spec* __restric
 }
 
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* counters) {
-    u64 n = (cap + 1) * (u64)(hspec.stride_words / 2);
+    u64 n = (cap + 1) * (u64)(hspec.tstride / 2);
     u64 blocks = (n + BLOCK - 1) / BLOCK;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(table_init_kernel, dim3((u32)blocks), dim3(BLOCK), 0, s, dspec, slots, cap + 1, counters);
@@ -556,6 +556,346 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
     }
     __syncthreads();
     block_flush<INLINE, RECORDS>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
+}
+
+// ------------------------------------------------------------------------------------------
+// agg_insert_str1: one non-null Arrow String key (ClickBench Q13: SearchPhrase), filtered by
+// `key <op> ''` or not at all, into a table whose slots cache the key (Spec::kc_word).
+//
+// The generic kernel compares every probe against the representative row in global memory: an
+// LDS hit reads that row's offsets and bytes, an LDS miss reads the HBM slot, then the row's
+// offsets and bytes — three dependent random reads before the atomic (C5: 6x the algorithmic
+// bytes).  Here the key's first 32 bytes and a header (hash bits 16..63, length, ready bit) sit
+// beside the entry in LDS and HBM slots alike, so a probe decides inside the slot: an LDS hit
+// touches no global memory, an HBM miss reads its slot's line and adds.  The stream reads two
+// offsets per lane per 16-B load, keeps the selected rows' (byte offset, row, length) in an LDS
+// queue and inserts them 256 at a time with every lane busy.
+//
+// Exactness: a different header means a different key (hash or length differ).  An equal header
+// with equal cached bytes and a length <= 32 is the same key.  Anything else — a header not yet
+// published (a claim in flight on this or another XCD, whose L2s are not coherent), equal headers
+// with different bytes, a key longer than 32 bytes — compares against the representative row
+// (ref_equal), as the generic kernel always does.  A claimer writes the key words with sc1 stores,
+// drains them, then publishes the header sc1 (MI355X_MICROARCH.md, inter-workgroup visibility);
+// readers load the slot with sc1 loads.  In LDS a slot whose header is not yet published is
+// passed over (the row goes to HBM; the flush merges both states), so no lane ever waits.
+// ------------------------------------------------------------------------------------------
+typedef volatile __attribute__((address_space(3))) u64 vlds_u64;
+typedef volatile __attribute__((address_space(3))) u32 vlds_u32;
+#define STR1_ROUNDS 2  // rounds of 2 x BLOCK rows per stream step
+#define STR1_QCAP ((2 * STR1_ROUNDS + 1) * BLOCK)
+#define STR1_LDS_BUDGET (56 * 1024)  // the key-caching LDS table (1024 slots for COUNT)
+
+struct KcKey {
+    u64 k[KC_KEY_WORDS];  // first 32 bytes, little-endian, zero-padded
+    u64 h;                // group hash (hash_bytes)
+    u64 hdr;              // (h & ~0xFFFF) | (len & 0x7FFF) << 1 | 1
+    u32 len;
+};
+
+__device__ __forceinline__ void kc_key(const u8* p, u32 len, KcKey& q) {
+    q.len = len;
+    const u32 n = len < 8 * KC_KEY_WORDS ? len : 8 * KC_KEY_WORDS;
+    const uintptr_t a = (uintptr_t)p;
+    const u32 sh = (u32)(a & 7);
+    const u64* base = (const u64*)(a - sh);
+    const u32 nw = n ? (sh + n + 7) >> 3 : 0;  // aligned words covering [p, p + n): <= 5
+    u64 w[KC_KEY_WORDS + 1];
+#pragma unroll
+    for (int j = 0; j <= KC_KEY_WORDS; ++j) w[j] = (u32)j < nw ? gld<u64>(base + j) : 0;
+#pragma unroll
+    for (int j = 0; j < KC_KEY_WORDS; ++j) {
+        u64 v = sh ? (w[j] >> (8 * sh)) | (w[j + 1] << (64 - 8 * sh)) : w[j];
+        const int rem = (int)n - 8 * j;
+        q.k[j] = rem >= 8 ? v : (rem <= 0 ? 0 : v & ((1ULL << (8 * rem)) - 1));
+    }
+    if (len <= 8 * KC_KEY_WORDS) {  // hash_bytes over the register words (device.hpp)
+        const u64 M = 0xc6a4a7935bd1e995ULL, R = 47;
+        u64 h = 0xe17a1465ULL ^ ((u64)len * M);
+        const u32 nb = len >> 3, tl = len & 7;
+        u64 tail = 0;
+#pragma unroll
+        for (u32 i = 0; i < KC_KEY_WORDS; ++i) {
+            if (i < nb) {
+                u64 x = q.k[i] * M;
+                x ^= x >> R;
+                x *= M;
+                h ^= x;
+                h *= M;
+            }
+            if (i == nb) tail = q.k[i];
+        }
+        if (tl) h ^= __builtin_bswap64(tail) >> (8 * (8 - tl));
+        h ^= h >> R;
+        h *= M;
+        h ^= h >> R;
+        q.h = h;
+    } else {
+        q.h = hash_bytes(p, len);
+    }
+    q.hdr = (q.h & ~0xFFFFULL) | ((u64)(len < 0x7FFF ? len : 0x7FFF) << 1) | 1;
+}
+
+// LDS probe of the key-caching table; -1 = not staged here (use HBM).
+__device__ __forceinline__ int lds_find_kc(u64* lds, u32 lmask, u32 lsw, u32 kc, u32* lcount, u32 llimit, u64 key, const KcKey& q) {
+    if (q.len > 8 * KC_KEY_WORDS) return -1;
+    vlds_u32* lc = (vlds_u32*)lcount;
+    u32 s = (u32)(q.h >> 16) & lmask;
+    const int cap = *lc >= llimit ? 2 : LDS_PROBE_CAP;
+    for (int p = 0; p < cap; ++p) {
+        vlds_u64* e = (vlds_u64*)(lds + (u64)s * lsw);
+        u64 ev = e[0];
+        if (ev == SLOT_EMPTY) {
+            if (*lc >= llimit) return -1;
+            u64 old = at_cas<AS_LDS>(asp<AS_LDS>(lds + (u64)s * lsw), SLOT_EMPTY, key);
+            if (old == SLOT_EMPTY) {
+                __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)lcount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                for (int j = 0; j < KC_KEY_WORDS; ++j) e[kc + 1 + j] = q.k[j];
+                e[kc] = q.hdr;  // volatile LDS accesses stay in order: the words are visible first
+                return (int)s;
+            }
+            ev = old;
+        }
+        if ((ev >> 48) == (key >> 48)) {
+            const u64 hv = e[kc];
+            if (!(hv & 1)) return -1;  // a claim in flight: not waited for
+            if (hv == q.hdr) {
+                bool eq = true;
+#pragma unroll
+                for (int j = 0; j < KC_KEY_WORDS; ++j) eq &= e[kc + 1 + j] == q.k[j];
+                if (eq) return (int)s;
+            }
+        }
+        s = (s + 1) & lmask;
+    }
+    return -1;
+}
+
+// HBM probe with the slot's key cache; exact (see above).  ~0 = probe limit reached.
+__device__ __forceinline__ u64 g_find_kc(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 key, const KcKey& q,
+                                         const TableDesc& t, u32 probe_limit, bool& claimed) {
+    claimed = false;
+    const u32 kc = (u32)S.kc_word;
+    const u64 mask = t.cap - 1;
+    u64 s = (q.h >> 16) & mask;
+    for (u32 p = 0; p < probe_limit; ++p) {
+        u64* slot = t.slots + s * t.stride_words;
+        u64 ev = ld_sc1(slot);
+        if (ev == SLOT_EMPTY) {
+            u64 old = at_cas<AS_GLB>(asp<AS_GLB>(slot), SLOT_EMPTY, key);
+            if (old == SLOT_EMPTY) {
+                claimed = true;
+#pragma unroll
+                for (int j = 0; j < KC_KEY_WORDS; ++j) st_sc1(slot + kc + 1 + j, q.k[j]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_sc1(slot + kc, q.hdr);
+                return s;
+            }
+            ev = old;
+        }
+        if ((ev >> 48) == (key >> 48)) {
+            const u64 hv = ld_sc1(slot + kc);
+            if ((hv & 1) && hv != q.hdr) {  // published and different: another key
+                s = (s + 1) & mask;
+                continue;
+            }
+            bool eq = (hv & 1) && q.len <= 8 * KC_KEY_WORDS;
+#pragma unroll
+            for (int j = 0; j < KC_KEY_WORDS; ++j) eq = eq && ld_sc1(slot + kc + 1 + j) == q.k[j];
+            if (eq || ref_equal(S, batches, keys, i, ev)) return s;
+        }
+        s = (s + 1) & mask;
+    }
+    return ~0ULL;
+}
+
+// The key-caching LDS table into HBM (end of block, and whenever it fills: maybe_flush's rule).
+__device__ __forceinline__ void flush_kc(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots, u32 lsw,
+                                         u32 kc, const TableDesc& t, u32& my_claims) {
+    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+        u64* p = lds + (u64)s * lsw;
+        const u64 e = p[0];
+        if (e == SLOT_EMPTY) continue;
+        KcKey q;
+        const u64 hv = p[kc];
+        const u64 i = ref_row(e);
+        u64 gs;
+        bool claimed;
+        if (hv & 1) {  // every claim has published its header before the flush's barrier
+            q.hdr = hv;
+            q.len = (u32)((hv >> 1) & 0x7FFF);
+            for (int j = 0; j < KC_KEY_WORDS; ++j) q.k[j] = p[kc + 1 + j];
+            // the slot index uses hash bits 16..: the header holds them; the salt is in the entry
+            q.h = (hv & ~0xFFFFULL);
+            gs = g_find_kc(S, batches, B.keys, i, e, q, t, t.probe_limit, claimed);
+        } else {
+            gs = g_find<false>(S, batches, B.keys, i, e, group_hash(B.keys, S.n_keys, i), t, t.probe_limit, claimed);
+        }
+        if (gs == ~0ULL) {
+            push_ovf_rec<false, AS_LDS>(S, t, e, p);
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_state<AS_GLB, false, AS_LDS>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), p);
+    }
+}
+
+__device__ __forceinline__ void lds_init_kc(const Spec& S, u64* lds, u32 lds_slots, u32 lsw) {
+    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+        u64* p = lds + (u64)s * lsw;
+        p[0] = SLOT_EMPTY;
+        for (u32 w = 1; w < lsw; ++w) p[w] = w < (u32)S.kc_word ? S.slot_init[w] : 0;
+    }
+}
+
+template <bool PRED>
+__global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+                                                               u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    const Spec& S = *spec;
+    const BatchDesc& B = batches[bid];
+    const u32 kc = (u32)S.kc_word, lsw = kc + 1 + KC_KEY_WORDS;
+    u32* lcount = (u32*)(lds + (u64)lds_slots * lsw);  // [0] LDS claims, [1] HBM claims, [2] queue length, [3] flush flag
+    u64* qoff = (u64*)(lcount + 4);                    // queue: byte offset of the key
+    u32* qrow = (u32*)(qoff + STR1_QCAP);              // row - r0
+    u32* qlen = qrow + STR1_QCAP;
+    const u32 lmask = lds_slots - 1, llimit = lds_slots - lds_slots / 4;
+    lds_init_kc(S, lds, lds_slots, lsw);
+    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
+    __syncthreads();
+    const DCol& kcol = B.keys[0];
+    const u64* __restrict__ offs = kcol.offsets;
+    const u8* __restrict__ data = kcol.data;
+    const int pcmp = PRED ? B.nodes[0].cmp : 0;
+    const u64 r0 = (u64)blockIdx.x * rows_per_block;
+    const u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    const u32 lane = __lane_id();
+    u32 my_claims = 0;
+
+    auto insert = [&](u64 off, u32 row, u32 len) {
+        const u64 i = r0 + row;
+        KcKey q;
+        kc_key(data + off, len, q);
+        const u64 key = (q.h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
+        const int ls = lds_find_kc(lds, lmask, lsw, kc, lcount, llimit, key, q);
+        if (ls >= 0) {
+            apply_row<AS_LDS>(S, asp<AS_LDS>(lds + (u64)ls * lsw), B, i);
+            return;
+        }
+        bool claimed;
+        const u64 gs = g_find_kc(S, batches, B.keys, i, key, q, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_ovf_row(t, bid, i);
+            return;
+        }
+        my_claims += claimed ? 1 : 0;
+        apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
+    };
+
+    // the full LDS table goes to HBM and starts over (maybe_flush's rule, same cadence)
+    auto maybe_flush_kc = [&]() {
+        if (threadIdx.x == 0)
+            lcount[3] = lcount[0] >= llimit && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+        __syncthreads();
+        const bool now = lcount[3];
+        __syncthreads();
+        if (now) {
+            flush_kc(S, batches, B, lds, lds_slots, lsw, kc, t, my_claims);
+            __syncthreads();
+            lds_init_kc(S, lds, lds_slots, lsw);
+            if (threadIdx.x == 0) lcount[0] = 0;
+            __syncthreads();
+        }
+    };
+
+    constexpr u64 STEP = (u64)STR1_ROUNDS * 2 * BLOCK;
+    u32 step = 0;
+    for (u64 base = r0; base < r1; base += STEP, ++step) {
+        if (step && (step % (FLUSH_ROUND / (2 * STR1_ROUNDS))) == 0) maybe_flush_kc();
+        // two rows per lane per round: offs[i], offs[i + 1] in one 16-B load (i even, offsets
+        // 16-B aligned: host-checked), offs[i + 2] from the next lane — or loaded, by the wave's
+        // last lane and wherever the next lane's pair runs past the batch's last offset
+        u64 a[STR1_ROUNDS][3];
+#pragma unroll
+        for (int k = 0; k < STR1_ROUNDS; ++k) {
+            const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+            const u64 j = i + 1 <= rows ? i : 0;
+            const v2u64 v = *(const v2u64 __attribute__((address_space(1)))*)(offs + j);
+            a[k][0] = v[0];
+            a[k][1] = v[1];
+            a[k][2] = ((lane == 63 || i + 3 > rows) && i + 2 <= rows) ? gld<u64>(offs + i + 2) : 0;
+        }
+        u64 mk[STR1_ROUNDS][2];
+        u32 cnt = 0;
+#pragma unroll
+        for (int k = 0; k < STR1_ROUNDS; ++k) {
+            const u64 nx = __shfl_down(a[k][0], 1);
+            if (lane != 63 && base + (u64)k * 2 * BLOCK + 2 * threadIdx.x + 3 <= rows) a[k][2] = nx;
+            const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const u64 len = a[k][r + 1] - a[k][r];
+                bool sel = i + r < r1;
+                if (PRED) sel = sel && apply_cmp(pcmp, len != 0 ? 1 : 0);
+                mk[k][r] = __ballot(sel);
+                cnt += (u32)__popcll(mk[k][r]);
+            }
+        }
+        if (cnt) {  // queue the step's selected rows: one LDS add per wave
+            u32 wb = 0;
+            if (lane == 0) wb = atomicAdd(&lcount[2], cnt);
+            wb = __shfl(wb, 0);
+            const u64 lt = (1ULL << lane) - 1;
+#pragma unroll
+            for (int k = 0; k < STR1_ROUNDS; ++k) {
+                const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if ((mk[k][r] >> lane) & 1) {
+                        const u32 q = wb + (u32)__popcll(mk[k][r] & lt);
+                        qoff[q] = a[k][r];
+                        qrow[q] = (u32)(i + r - r0);
+                        qlen[q] = (u32)(a[k][r + 1] - a[k][r]);
+                    }
+                    wb += (u32)__popcll(mk[k][r]);
+                }
+            }
+        }
+        __syncthreads();
+        const u32 n = lcount[2];  // < STR1_QCAP
+        if (n >= BLOCK) {
+            const u32 full = n / BLOCK;
+            for (u32 c = 0; c < full; ++c) {
+                const u32 q = c * BLOCK + threadIdx.x;
+                insert(qoff[q], qrow[q], qlen[q]);
+            }
+            const u32 rem = n - full * BLOCK;  // < BLOCK: moved to the front
+            u64 mo = 0;
+            u32 mr = 0, ml = 0;
+            if (threadIdx.x < rem) {
+                const u32 q = full * BLOCK + threadIdx.x;
+                mo = qoff[q];
+                mr = qrow[q];
+                ml = qlen[q];
+            }
+            __syncthreads();
+            if (threadIdx.x < rem) {
+                qoff[threadIdx.x] = mo;
+                qrow[threadIdx.x] = mr;
+                qlen[threadIdx.x] = ml;
+            }
+            if (threadIdx.x == 0) lcount[2] = rem;
+        }
+        __syncthreads();  // the queue is settled before the next step appends
+    }
+    const u32 n = lcount[2];  // < BLOCK
+    if (threadIdx.x < n) insert(qoff[threadIdx.x], qrow[threadIdx.x], qlen[threadIdx.x]);
+    __syncthreads();
+    flush_kc(S, batches, B, lds, lds_slots, lsw, kc, t, my_claims);
+    if (my_claims) atomicAdd(&lcount[1], my_claims);
+    __syncthreads();
+    if (threadIdx.x == 0 && lcount[1]) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -931,6 +1271,20 @@ static bool short_eligible(const Spec& S, const BatchDesc& hb) {
         if (A.arg_type >= 0 && A.arg_nullable) return false;
     }
     return true;
+}
+
+// agg_insert_str1_kernel: one non-null Arrow String key (the Spec's key cache), no predicate or
+// `key <op> ''` on that same column, offsets 16-B aligned, row offsets below 2^32 per workgroup.
+static bool str1_eligible(const Spec& S, const BatchDesc& hb, u64 rows) {
+    if (!S.kc_word || hb.is_records || S.n_keys != 1) return false;
+    const DCol& k = hb.keys[0];
+    if (k.type != DBG_STRING || k.nullable || k.layout != LAYOUT_ARROW || ((uintptr_t)k.offsets & 15)) return false;
+    if (hb.n_nodes == 0) return true;
+    if (hb.n_nodes != 1) return false;
+    const DNode& n = hb.nodes[0];
+    const DCol& c = hb.fcols[n.col];
+    return n.op == DBG_PRED_CMP_CONST && n.str_len == 0 && c.type == DBG_STRING && !c.nullable && c.layout == LAYOUT_ARROW &&
+           c.offsets == k.offsets && c.data == k.data;
 }
 
 static u32 lds_slots_for(const Spec& S, u32 budget = LDS_BUDGET_BYTES) {
@@ -2500,6 +2854,21 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
             case DBG_INT64: case DBG_TIMESTAMP: launch_fast_t<int64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
             case DBG_UINT64: launch_fast_t<uint64_t>(s, dspec, batches, bid, rows, t, lslots, shmem, pred, op, c, count_only, fused); return;
         }
+    }
+    // one non-null String key into a large key-caching table, filtered by `key <op> ''` or not
+    if (!records && use_lds && hb && S.kc_word && t.cap + 1 > SHORT_MAX_SLOTS && str1_eligible(S, *hb, rows)) {
+        const u32 lsw = (u32)S.kc_word + 1 + KC_KEY_WORDS;
+        u32 ls = 1;
+        while ((ls * 2) * lsw * 8 <= STR1_LDS_BUDGET) ls *= 2;
+        const size_t shmem = (size_t)ls * lsw * 8 + 16 + (size_t)STR1_QCAP * 16;
+        u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
+        if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
+        if (blocks < 1) blocks = 1;
+        u64 rpb = ((rows + blocks - 1) / blocks + 1) & ~1ULL;  // even: 16-B offset loads
+        blocks = (rows + rpb - 1) / rpb;
+        if (hb->n_nodes) hipLaunchKernelGGL(agg_insert_str1_kernel<true>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls);
+        else hipLaunchKernelGGL(agg_insert_str1_kernel<false>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls);
+        return;
     }
     u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
     static const int x_short = X_ENV("DBG_X_SHORT") ? atoi(X_ENV("DBG_X_SHORT")) : 1;

@@ -10,6 +10,7 @@
 //     entry = salt16 | batch16 | row32 — the reference's Entry (salt | pointer,
 //     EAGG/aggregate_hashtable.rs:591-636) with the pointer aimed at the immutable input row
 #define SLOT_EMPTY 0xFFFFFFFFFFFFFFFFULL
+#define KC_KEY_WORDS 4  // key bytes cached per slot (32) for one non-null String key (Spec::kc_word)
 
 struct Spec {
     int32_t n_keys;
@@ -17,7 +18,10 @@ struct Spec {
     int32_t inline_width;     // bytes
     int32_t n_aggs;
     int32_t n_words;          // state words (without the entry word)
-    int32_t stride_words;     // entry + states, rounded
+    int32_t stride_words;     // entry + states, rounded (LDS tables, parked rows, records)
+    int32_t tstride;          // HBM table slot words: stride_words, or more with a key cache
+    int32_t kc_word;          // 0, or the slot word of the key cache (single non-null String key):
+                              // [hdr = hash bits 16..63 | len << 1 | ready][first 32 key bytes]
     int32_t flags_word;       // -1 or word index (1-based, slot word)
     int32_t has_strings;
     uint8_t voff[DBG_MAX_KEYS];  // inline: byte offset of the validity byte
@@ -70,7 +74,7 @@ struct BatchDesc {
 struct TableDesc {
     u64* slots;
     u64 cap;  // power of two
-    u32 stride_words;
+    u32 stride_words;  // Spec::tstride
     u32 probe_limit;
     u64* counters;  // [0] claims (groups created), [1] overflow rows, [2] overflow records, [3] error bits
     u64* ovf_rows;  // (bid << 32) | row
