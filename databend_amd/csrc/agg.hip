@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
 // ------------------------------------------------------------------------------------------
 typedef volatile __attribute__((address_space(3))) u64 vlds_u64;
 typedef volatile __attribute__((address_space(3))) u32 vlds_u32;
-#define STR1_ROUNDS 2  // rounds of 2 x BLOCK rows per stream step
+#define STR1_ROUNDS 4  // rounds of 2 x BLOCK rows per stream step
 #define STR1_QCAP ((2 * STR1_ROUNDS + 1) * BLOCK)
 #define STR1_LDS_BUDGET (56 * 1024)  // the key-caching LDS table (1024 slots for COUNT)
 
@@ -672,16 +672,24 @@ __device__ __forceinline__ int lds_find_kc(u64* lds, u32 lmask, u32 lsw, u32 kc,
     return -1;
 }
 
-// HBM probe with the slot's key cache; exact (see above).  ~0 = probe limit reached.
+// HBM probe with the slot's key cache; exact (see above).  ~0 = probe limit reached.  The slot's
+// entry and its cache words are loaded together (16-B loads of one 64-B slot); a stale copy (this
+// CU's L1 or this XCD's L2 holding the line from before a claim) can only show EMPTY — the CAS
+// then returns the real entry — or an unpublished header, which takes the representative row.
 __device__ __forceinline__ u64 g_find_kc(const Spec& S, const BatchDesc* batches, const DCol* keys, u64 i, u64 key, const KcKey& q,
                                          const TableDesc& t, u32 probe_limit, bool& claimed) {
     claimed = false;
-    const u32 kc = (u32)S.kc_word;
+    const u32 kc = (u32)S.kc_word, kp = kc >> 1;
+    const bool odd = kc & 1;
     const u64 mask = t.cap - 1;
     u64 s = (q.h >> 16) & mask;
     for (u32 p = 0; p < probe_limit; ++p) {
         u64* slot = t.slots + s * t.stride_words;
-        u64 ev = ld_sc1(slot);
+        const v2u64 __attribute__((address_space(1)))* sp = (const v2u64 __attribute__((address_space(1)))*)slot;
+        const v2u64 p0 = sp[0], pa = sp[kp], pb = sp[kp + 1], pc = sp[kp + 2];
+        u64 ev = p0[0];
+        u64 hv = odd ? pa[1] : pa[0];
+        u64 w[KC_KEY_WORDS] = {odd ? pb[0] : pa[1], odd ? pb[1] : pb[0], odd ? pc[0] : pb[1], odd ? pc[1] : pc[0]};
         if (ev == SLOT_EMPTY) {
             u64 old = at_cas<AS_GLB>(asp<AS_GLB>(slot), SLOT_EMPTY, key);
             if (old == SLOT_EMPTY) {
@@ -693,16 +701,18 @@ __device__ __forceinline__ u64 g_find_kc(const Spec& S, const BatchDesc* batches
                 return s;
             }
             ev = old;
+            hv = ld_sc1(slot + kc);  // the line was read before the claim: the cache again
+#pragma unroll
+            for (int j = 0; j < KC_KEY_WORDS; ++j) w[j] = ld_sc1(slot + kc + 1 + j);
         }
         if ((ev >> 48) == (key >> 48)) {
-            const u64 hv = ld_sc1(slot + kc);
             if ((hv & 1) && hv != q.hdr) {  // published and different: another key
                 s = (s + 1) & mask;
                 continue;
             }
             bool eq = (hv & 1) && q.len <= 8 * KC_KEY_WORDS;
 #pragma unroll
-            for (int j = 0; j < KC_KEY_WORDS; ++j) eq = eq && ld_sc1(slot + kc + 1 + j) == q.k[j];
+            for (int j = 0; j < KC_KEY_WORDS; ++j) eq = eq && w[j] == q.k[j];
             if (eq || ref_equal(S, batches, keys, i, ev)) return s;
         }
         s = (s + 1) & mask;
@@ -751,18 +761,19 @@ __device__ __forceinline__ void lds_init_kc(const Spec& S, u64* lds, u32 lds_slo
 
 template <bool PRED>
 __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
-                                                               u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots) {
+                                                               u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots,
+                                                               u32 fper, u32 xmode) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
     const u32 kc = (u32)S.kc_word, lsw = kc + 1 + KC_KEY_WORDS;
-    u32* lcount = (u32*)(lds + (u64)lds_slots * lsw);  // [0] LDS claims, [1] HBM claims, [2] queue length, [3] flush flag
-    u64* qoff = (u64*)(lcount + 4);                    // queue: byte offset of the key
-    u32* qrow = (u32*)(qoff + STR1_QCAP);              // row - r0
-    u32* qlen = qrow + STR1_QCAP;
+    // [0] LDS claims, [1] HBM claims, [2] queue length, [3] flush flag, [4] LDS hits, [5] misses
+    u32* lcount = (u32*)(lds + (u64)lds_slots * lsw);
+    u32* qoff = lcount + 8;       // queue: key byte offset - offs[r0]
+    u32* qrl = qoff + STR1_QCAP;  // (row - r0) << 6 | min(len, 63)
     const u32 lmask = lds_slots - 1, llimit = lds_slots - lds_slots / 4;
     lds_init_kc(S, lds, lds_slots, lsw);
-    if (threadIdx.x < 4) lcount[threadIdx.x] = 0;
+    if (threadIdx.x < 8) lcount[threadIdx.x] = 0;
     __syncthreads();
     const DCol& kcol = B.keys[0];
     const u64* __restrict__ offs = kcol.offsets;
@@ -771,18 +782,42 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
     const u64 r0 = (u64)blockIdx.x * rows_per_block;
     const u64 r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
     const u32 lane = __lane_id();
+    const u64 lt = (1ULL << lane) - 1;
+    const u64 off0 = r0 < rows ? gld<u64>(offs + r0) : 0;
     u32 my_claims = 0;
 
-    auto insert = [&](u64 off, u32 row, u32 len) {
-        const u64 i = r0 + row;
+    auto insert = [&](u32 offr, u32 rl) {
+        const u64 i = r0 + (rl >> 6);
+        u64 off = off0 + offr;
+        u32 len = rl & 63;
+        if (len == 63 || offr == ~0u) {  // long key or far offset: read the row's offsets again
+            off = gld<u64>(offs + i);
+            len = (u32)(gld<u64>(offs + i + 1) - off);
+        }
+        // timing ablations (EXP=1 builds only, DBG_X_STR1): 1 stream + queue only, 2 + key loads
+        // and hash, 4 misses dropped, 8 no LDS table
+        if (kExperiments && (xmode & 1)) {
+            if (off == ~0ULL) atomicAdd(&lcount[1], 1u);
+            return;
+        }
         KcKey q;
         kc_key(data + off, len, q);
+        if (kExperiments && (xmode & 2)) {
+            if (q.h == 0x1234567ULL) atomicAdd(&lcount[1], 1u);
+            return;
+        }
         const u64 key = (q.h & 0xFFFF000000000000ULL) | ((u64)bid << 32) | i;
-        const int ls = lds_find_kc(lds, lmask, lsw, kc, lcount, llimit, key, q);
+        const int ls = (kExperiments && (xmode & 8)) ? -1 : lds_find_kc(lds, lmask, lsw, kc, lcount, llimit, key, q);
+        const u64 hm = __ballot(ls >= 0), mm = __ballot(ls < 0);
+        if (lane == 0) {  // the flush rule's hit rate: one LDS add per wave
+            atomicAdd(&lcount[4], (u32)__popcll(hm));
+            atomicAdd(&lcount[5], (u32)__popcll(mm));
+        }
         if (ls >= 0) {
             apply_row<AS_LDS>(S, asp<AS_LDS>(lds + (u64)ls * lsw), B, i);
             return;
         }
+        if (kExperiments && (xmode & 4)) return;
         bool claimed;
         const u64 gs = g_find_kc(S, batches, B.keys, i, key, q, t, t.probe_limit, claimed);
         if (gs == ~0ULL) {
@@ -793,10 +828,17 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
         apply_row<AS_GLB>(S, asp<AS_GLB>(t.slots + gs * t.stride_words), B, i);
     };
 
-    // the full LDS table goes to HBM and starts over (maybe_flush's rule, same cadence)
+    // A full LDS table is flushed to HBM and started over only while it serves few rows (hit rate
+    // below 1/4 since the last check): with Zipf keys (ClickBench Q13) the first keys a workgroup
+    // meets are the hot ones and flushing them every few rounds cost more than it saved (C5 insert
+    // 15.3 -> 13.0 ms without periodic flushes), while clustered input (a key's rows together)
+    // would otherwise send a hot key's rows to one HBM slot for good.
     auto maybe_flush_kc = [&]() {
-        if (threadIdx.x == 0)
-            lcount[3] = lcount[0] >= llimit && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 && ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+        if (threadIdx.x == 0) {
+            lcount[3] = lcount[0] >= llimit && 3 * lcount[4] < lcount[5] && ld_sc1(t.counters + CNT_OVF_ROWS) == 0 &&
+                        ld_sc1(t.counters + CNT_OVF_RECS) == 0;
+            lcount[4] = lcount[5] = 0;
+        }
         __syncthreads();
         const bool now = lcount[3];
         __syncthreads();
@@ -809,30 +851,39 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
         }
     };
 
+    // the stream: two rows per lane per round, offs[i], offs[i + 1] in one 16-B load (i even,
+    // offsets 16-B aligned: host-checked), offs[i + 2] from the next lane — or loaded, by the
+    // wave's last lane and wherever the next lane's pair runs past the batch's last offset.  The
+    // next step's loads are issued before this step's rows are queued and inserted.
     constexpr u64 STEP = (u64)STR1_ROUNDS * 2 * BLOCK;
-    u32 step = 0;
-    for (u64 base = r0; base < r1; base += STEP, ++step) {
-        if (step && (step % (FLUSH_ROUND / (2 * STR1_ROUNDS))) == 0) maybe_flush_kc();
-        // two rows per lane per round: offs[i], offs[i + 1] in one 16-B load (i even, offsets
-        // 16-B aligned: host-checked), offs[i + 2] from the next lane — or loaded, by the wave's
-        // last lane and wherever the next lane's pair runs past the batch's last offset
-        u64 a[STR1_ROUNDS][3];
+    u64 nv[STR1_ROUNDS][3];
+    auto load_step = [&](u64 base) {
 #pragma unroll
         for (int k = 0; k < STR1_ROUNDS; ++k) {
             const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
             const u64 j = i + 1 <= rows ? i : 0;
             const v2u64 v = *(const v2u64 __attribute__((address_space(1)))*)(offs + j);
-            a[k][0] = v[0];
-            a[k][1] = v[1];
-            a[k][2] = ((lane == 63 || i + 3 > rows) && i + 2 <= rows) ? gld<u64>(offs + i + 2) : 0;
+            nv[k][0] = v[0];
+            nv[k][1] = v[1];
+            nv[k][2] = ((lane == 63 || i + 3 > rows) && i + 2 <= rows) ? gld<u64>(offs + i + 2) : 0;
         }
+    };
+    if (r0 < r1) load_step(r0);
+    u32 step = 0;
+    for (u64 base = r0; base < r1; base += STEP, ++step) {
+        if (fper && step && (step % fper) == 0) maybe_flush_kc();
+        u64 a[STR1_ROUNDS][3];
+#pragma unroll
+        for (int k = 0; k < STR1_ROUNDS; ++k)
+            for (int r = 0; r < 3; ++r) a[k][r] = nv[k][r];
+        if (base + STEP < r1) load_step(base + STEP);
         u64 mk[STR1_ROUNDS][2];
         u32 cnt = 0;
 #pragma unroll
         for (int k = 0; k < STR1_ROUNDS; ++k) {
-            const u64 nx = __shfl_down(a[k][0], 1);
-            if (lane != 63 && base + (u64)k * 2 * BLOCK + 2 * threadIdx.x + 3 <= rows) a[k][2] = nx;
             const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+            const u64 nx = __shfl_down(a[k][0], 1);
+            if (lane != 63 && i + 3 <= rows) a[k][2] = nx;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const u64 len = a[k][r + 1] - a[k][r];
@@ -846,7 +897,6 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
             u32 wb = 0;
             if (lane == 0) wb = atomicAdd(&lcount[2], cnt);
             wb = __shfl(wb, 0);
-            const u64 lt = (1ULL << lane) - 1;
 #pragma unroll
             for (int k = 0; k < STR1_ROUNDS; ++k) {
                 const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
@@ -854,9 +904,9 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
                 for (int r = 0; r < 2; ++r) {
                     if ((mk[k][r] >> lane) & 1) {
                         const u32 q = wb + (u32)__popcll(mk[k][r] & lt);
-                        qoff[q] = a[k][r];
-                        qrow[q] = (u32)(i + r - r0);
-                        qlen[q] = (u32)(a[k][r + 1] - a[k][r]);
+                        const u64 d = a[k][r] - off0, len = a[k][r + 1] - a[k][r];
+                        qoff[q] = d < 0xFFFFFFFFULL ? (u32)d : ~0u;
+                        qrl[q] = (u32)(i + r - r0) << 6 | (u32)(len < 63 ? len : 63);
                     }
                     wb += (u32)__popcll(mk[k][r]);
                 }
@@ -866,31 +916,24 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
         const u32 n = lcount[2];  // < STR1_QCAP
         if (n >= BLOCK) {
             const u32 full = n / BLOCK;
-            for (u32 c = 0; c < full; ++c) {
-                const u32 q = c * BLOCK + threadIdx.x;
-                insert(qoff[q], qrow[q], qlen[q]);
-            }
+            for (u32 c = 0; c < full; ++c) insert(qoff[c * BLOCK + threadIdx.x], qrl[c * BLOCK + threadIdx.x]);
             const u32 rem = n - full * BLOCK;  // < BLOCK: moved to the front
-            u64 mo = 0;
-            u32 mr = 0, ml = 0;
+            u32 mo = 0, mr = 0;
             if (threadIdx.x < rem) {
-                const u32 q = full * BLOCK + threadIdx.x;
-                mo = qoff[q];
-                mr = qrow[q];
-                ml = qlen[q];
+                mo = qoff[full * BLOCK + threadIdx.x];
+                mr = qrl[full * BLOCK + threadIdx.x];
             }
             __syncthreads();
             if (threadIdx.x < rem) {
                 qoff[threadIdx.x] = mo;
-                qrow[threadIdx.x] = mr;
-                qlen[threadIdx.x] = ml;
+                qrl[threadIdx.x] = mr;
             }
             if (threadIdx.x == 0) lcount[2] = rem;
         }
         __syncthreads();  // the queue is settled before the next step appends
     }
     const u32 n = lcount[2];  // < BLOCK
-    if (threadIdx.x < n) insert(qoff[threadIdx.x], qrow[threadIdx.x], qlen[threadIdx.x]);
+    if (threadIdx.x < n) insert(qoff[threadIdx.x], qrl[threadIdx.x]);
     __syncthreads();
     flush_kc(S, batches, B, lds, lds_slots, lsw, kc, t, my_claims);
     if (my_claims) atomicAdd(&lcount[1], my_claims);
@@ -1279,6 +1322,7 @@ static bool str1_eligible(const Spec& S, const BatchDesc& hb, u64 rows) {
     if (!S.kc_word || hb.is_records || S.n_keys != 1) return false;
     const DCol& k = hb.keys[0];
     if (k.type != DBG_STRING || k.nullable || k.layout != LAYOUT_ARROW || ((uintptr_t)k.offsets & 15)) return false;
+    if (rows >= (1ULL << 32)) return false;  // queue entries hold (row - r0) << 6 in 32 bits: < 2^26 per workgroup
     if (hb.n_nodes == 0) return true;
     if (hb.n_nodes != 1) return false;
     const DNode& n = hb.nodes[0];
@@ -1410,6 +1454,15 @@ __device__ __forceinline__ u64 key_str_len(const Spec& S, const BatchDesc* batch
     StrRef r = dcol_str(batches[ref_bid(e)].keys[c], ref_row(e));
     return r.len;
 }
+// The same from slot s's key cache when it holds the key (published header, length <= 32): no
+// read of the representative row.
+__device__ __forceinline__ u64 slot_str_len(const Spec& S, const BatchDesc* batches, const TableDesc& t, u64 s, u64 e, int c) {
+    if (S.kc_word && s < t.cap) {
+        const u64 hv = t.slots[s * t.stride_words + S.kc_word];
+        if ((hv & 1) && ((hv >> 1) & 0x7FFF) <= 8 * KC_KEY_WORDS) return (hv >> 1) & 0x7FFF;
+    }
+    return key_str_len(S, batches, e, c);
+}
 
 #define MAX_PARTS_LDS 256
 
@@ -1439,7 +1492,7 @@ __global__ void __launch_bounds__(BLOCK) count_groups_kernel(const Spec* __restr
         }
         if (S.has_strings && !S.inline_keys)
             for (int c = 0; c < S.n_keys; ++c)
-                if (S.key_types[c].type == DBG_STRING) atomicAdd(&ls[c][p], (unsigned long long)key_str_len(S, batches, e, c));
+                if (S.key_types[c].type == DBG_STRING) atomicAdd(&ls[c][p], (unsigned long long)slot_str_len(S, batches, t, s, e, c));
     }
     if (n_parts == 1) {
         for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, 64);
@@ -1606,6 +1659,21 @@ __device__ __forceinline__ void write_group(const Spec& S, const BatchDesc* batc
             write_bytes(out.key_data[c], p, w, b, 0);
             if (out.key_valid[c]) out.key_valid[c][p] = v ? 1 : 0;
         }
+    } else if (S.kc_word && s < t.cap && (st[S.kc_word] & 1) && ((st[S.kc_word] >> 1) & 0x7FFF) <= 8 * KC_KEY_WORDS) {
+        // one String key held by the slot's key cache: no read of the representative row
+        const u32 len = (u32)((st[S.kc_word] >> 1) & 0x7FFF);
+        u64 w[KC_KEY_WORDS];
+#pragma unroll
+        for (int j = 0; j < KC_KEY_WORDS; ++j) w[j] = st[S.kc_word + 1 + j];
+        out.key_offsets[0][p] = sp[0];
+        if (out.key_valid[0]) out.key_valid[0][p] = 1;
+        if (sp[0] + len <= out.cap_str[0]) {
+            u8* d = (u8*)out.key_data[0] + sp[0];
+#pragma unroll
+            for (u32 j = 0; j < 8 * KC_KEY_WORDS; ++j)
+                if (j < len) d[j] = (u8)(w[j >> 3] >> (8 * (j & 7)));
+        }
+        sp[0] += len;
     } else {
         const BatchDesc& RB = batches[ref_bid(e)];
         u64 row = ref_row(e);
@@ -1677,7 +1745,7 @@ __global__ void __launch_bounds__(BLOCK) write_results_kernel(const Spec* __rest
         if (lane == 63) wsum[wave][0] = ic;
         if (ref_strings)
             for (int c = 0; c < S.n_keys; ++c) {
-                sb[c] = (cnt && S.key_types[c].type == DBG_STRING) ? key_str_len(S, batches, e, c) : 0;
+                sb[c] = (cnt && S.key_types[c].type == DBG_STRING) ? slot_str_len(S, batches, t, s, e, c) : 0;
                 u64 is = wave_incl(sb[c]);
                 if (lane == 63) wsum[wave][1 + c] = is;
                 sb[c] = is - sb[c];  // exclusive within the wave
@@ -2858,16 +2926,19 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     // one non-null String key into a large key-caching table, filtered by `key <op> ''` or not
     if (!records && use_lds && hb && S.kc_word && t.cap + 1 > SHORT_MAX_SLOTS && str1_eligible(S, *hb, rows)) {
         const u32 lsw = (u32)S.kc_word + 1 + KC_KEY_WORDS;
+        static const u32 x_mode = X_ENV("DBG_X_STR1") ? (u32)atoi(X_ENV("DBG_X_STR1")) : 0;
+        static const u32 x_lds = X_ENV("DBG_X_STR1_LDS") ? (u32)atoi(X_ENV("DBG_X_STR1_LDS")) * 1024 : STR1_LDS_BUDGET;
+        static const u32 fper = X_ENV("DBG_X_STR1_FLUSH") ? (u32)atoi(X_ENV("DBG_X_STR1_FLUSH")) : 4;
         u32 ls = 1;
-        while ((ls * 2) * lsw * 8 <= STR1_LDS_BUDGET) ls *= 2;
-        const size_t shmem = (size_t)ls * lsw * 8 + 16 + (size_t)STR1_QCAP * 16;
+        while ((ls * 2) * lsw * 8 <= x_lds) ls *= 2;
+        const size_t shmem = (size_t)ls * lsw * 8 + 32 + (size_t)STR1_QCAP * 8;
         u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
         if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
         if (blocks < 1) blocks = 1;
         u64 rpb = ((rows + blocks - 1) / blocks + 1) & ~1ULL;  // even: 16-B offset loads
         blocks = (rows + rpb - 1) / rpb;
-        if (hb->n_nodes) hipLaunchKernelGGL(agg_insert_str1_kernel<true>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls);
-        else hipLaunchKernelGGL(agg_insert_str1_kernel<false>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls);
+        if (hb->n_nodes) hipLaunchKernelGGL(agg_insert_str1_kernel<true>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls, fper, x_mode);
+        else hipLaunchKernelGGL(agg_insert_str1_kernel<false>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls, fper, x_mode);
         return;
     }
     u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
