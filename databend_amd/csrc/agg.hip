@@ -582,8 +582,14 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_kernel(const Spec* __restric
 // ------------------------------------------------------------------------------------------
 typedef volatile __attribute__((address_space(3))) u64 vlds_u64;
 typedef volatile __attribute__((address_space(3))) u32 vlds_u32;
-#define STR1_ROUNDS 4  // rounds of 2 x BLOCK rows per stream step
-#define STR1_QCAP ((2 * STR1_ROUNDS + 1) * BLOCK)
+// STR1_NT threads per workgroup, STR1_ROUNDS rounds of 2 x STR1_NT rows per stream step
+#ifndef STR1_NT
+#define STR1_NT 512
+#endif
+#ifndef STR1_ROUNDS
+#define STR1_ROUNDS 2
+#endif
+#define STR1_QCAP ((2 * STR1_ROUNDS + 1) * STR1_NT)
 #define STR1_LDS_BUDGET (56 * 1024)  // the key-caching LDS table (1024 slots for COUNT)
 
 struct KcKey {
@@ -723,7 +729,7 @@ __device__ __forceinline__ u64 g_find_kc(const Spec& S, const BatchDesc* batches
 // The key-caching LDS table into HBM (end of block, and whenever it fills: maybe_flush's rule).
 __device__ __forceinline__ void flush_kc(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots, u32 lsw,
                                          u32 kc, const TableDesc& t, u32& my_claims) {
-    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+    for (u32 s = threadIdx.x; s < lds_slots; s += STR1_NT) {
         u64* p = lds + (u64)s * lsw;
         const u64 e = p[0];
         if (e == SLOT_EMPTY) continue;
@@ -752,7 +758,7 @@ __device__ __forceinline__ void flush_kc(const Spec& S, const BatchDesc* batches
 }
 
 __device__ __forceinline__ void lds_init_kc(const Spec& S, u64* lds, u32 lds_slots, u32 lsw) {
-    for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
+    for (u32 s = threadIdx.x; s < lds_slots; s += STR1_NT) {
         u64* p = lds + (u64)s * lsw;
         p[0] = SLOT_EMPTY;
         for (u32 w = 1; w < lsw; ++w) p[w] = w < (u32)S.kc_word ? S.slot_init[w] : 0;
@@ -760,7 +766,7 @@ __device__ __forceinline__ void lds_init_kc(const Spec& S, u64* lds, u32 lds_slo
 }
 
 template <bool PRED>
-__global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
+__global__ void __launch_bounds__(STR1_NT) agg_insert_str1_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots,
                                                                u32 fper, u32 xmode) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
@@ -855,12 +861,12 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
     // offsets 16-B aligned: host-checked), offs[i + 2] from the next lane — or loaded, by the
     // wave's last lane and wherever the next lane's pair runs past the batch's last offset.  The
     // next step's loads are issued before this step's rows are queued and inserted.
-    constexpr u64 STEP = (u64)STR1_ROUNDS * 2 * BLOCK;
+    constexpr u64 STEP = (u64)STR1_ROUNDS * 2 * STR1_NT;
     u64 nv[STR1_ROUNDS][3];
     auto load_step = [&](u64 base) {
 #pragma unroll
         for (int k = 0; k < STR1_ROUNDS; ++k) {
-            const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+            const u64 i = base + (u64)k * 2 * STR1_NT + 2 * threadIdx.x;
             const u64 j = i + 1 <= rows ? i : 0;
             const v2u64 v = *(const v2u64 __attribute__((address_space(1)))*)(offs + j);
             nv[k][0] = v[0];
@@ -881,7 +887,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
         u32 cnt = 0;
 #pragma unroll
         for (int k = 0; k < STR1_ROUNDS; ++k) {
-            const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+            const u64 i = base + (u64)k * 2 * STR1_NT + 2 * threadIdx.x;
             const u64 nx = __shfl_down(a[k][0], 1);
             if (lane != 63 && i + 3 <= rows) a[k][2] = nx;
 #pragma unroll
@@ -899,7 +905,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
             wb = __shfl(wb, 0);
 #pragma unroll
             for (int k = 0; k < STR1_ROUNDS; ++k) {
-                const u64 i = base + (u64)k * 2 * BLOCK + 2 * threadIdx.x;
+                const u64 i = base + (u64)k * 2 * STR1_NT + 2 * threadIdx.x;
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
                     if ((mk[k][r] >> lane) & 1) {
@@ -914,14 +920,14 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
         }
         __syncthreads();
         const u32 n = lcount[2];  // < STR1_QCAP
-        if (n >= BLOCK) {
-            const u32 full = n / BLOCK;
-            for (u32 c = 0; c < full; ++c) insert(qoff[c * BLOCK + threadIdx.x], qrl[c * BLOCK + threadIdx.x]);
-            const u32 rem = n - full * BLOCK;  // < BLOCK: moved to the front
+        if (n >= STR1_NT) {
+            const u32 full = n / STR1_NT;
+            for (u32 c = 0; c < full; ++c) insert(qoff[c * STR1_NT + threadIdx.x], qrl[c * STR1_NT + threadIdx.x]);
+            const u32 rem = n - full * STR1_NT;  // < STR1_NT: moved to the front
             u32 mo = 0, mr = 0;
             if (threadIdx.x < rem) {
-                mo = qoff[full * BLOCK + threadIdx.x];
-                mr = qrl[full * BLOCK + threadIdx.x];
+                mo = qoff[full * STR1_NT + threadIdx.x];
+                mr = qrl[full * STR1_NT + threadIdx.x];
             }
             __syncthreads();
             if (threadIdx.x < rem) {
@@ -932,7 +938,7 @@ __global__ void __launch_bounds__(BLOCK) agg_insert_str1_kernel(const Spec* __re
         }
         __syncthreads();  // the queue is settled before the next step appends
     }
-    const u32 n = lcount[2];  // < BLOCK
+    const u32 n = lcount[2];  // < STR1_NT
     if (threadIdx.x < n) insert(qoff[threadIdx.x], qrl[threadIdx.x]);
     __syncthreads();
     flush_kc(S, batches, B, lds, lds_slots, lsw, kc, t, my_claims);
@@ -2932,13 +2938,13 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
         u32 ls = 1;
         while ((ls * 2) * lsw * 8 <= x_lds) ls *= 2;
         const size_t shmem = (size_t)ls * lsw * 8 + 32 + (size_t)STR1_QCAP * 8;
-        u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
+        u64 blocks = (rows + (u64)STR1_NT * 16 - 1) / ((u64)STR1_NT * 16);
         if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
         if (blocks < 1) blocks = 1;
         u64 rpb = ((rows + blocks - 1) / blocks + 1) & ~1ULL;  // even: 16-B offset loads
         blocks = (rows + rpb - 1) / rpb;
-        if (hb->n_nodes) hipLaunchKernelGGL(agg_insert_str1_kernel<true>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls, fper, x_mode);
-        else hipLaunchKernelGGL(agg_insert_str1_kernel<false>, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, ls, fper, x_mode);
+        if (hb->n_nodes) hipLaunchKernelGGL(agg_insert_str1_kernel<true>, dim3((u32)blocks), dim3(STR1_NT), shmem, s, dspec, batches, bid, rows, rpb, t, ls, fper, x_mode);
+        else hipLaunchKernelGGL(agg_insert_str1_kernel<false>, dim3((u32)blocks), dim3(STR1_NT), shmem, s, dspec, batches, bid, rows, rpb, t, ls, fper, x_mode);
         return;
     }
     u32 lslots = use_lds ? lds_slots_for(S, LDS_BUDGET_BYTES) : 1;
