@@ -1458,7 +1458,7 @@ static int pp_agg(dbg_agg_handle* h, int mode, const OutDesc* od) {
         }
         HIPCHECK(hipMemsetAsync(h->pp_spill, 0, 4, h->stream));
         prof::Scope ps("pp_agg", h->stream);
-        launch_pp_agg_spec(h->stream, h->pp_spec, mode, 1u << h->pp_bits, R.part, R.fin, h->pp_spec_sub, o, h->pp_spill, SPILL_CAP);
+        launch_pp_agg_spec(h->stream, S, h->pp_spec, mode, 1u << h->pp_bits, R.part, R.fin, h->pp_spec_sub, o, h->pp_spill, SPILL_CAP);
         // partitions larger than its register budget (skewed keys): the generic kernel, spilled ids only
         launch_pp_agg(h->stream, h->dspec, S, h->dbatches, mode, 1u << h->pp_bits, R.part, nullptr, R.fin, R.alt, nullptr, nullptr,
                       o, h->pp_spill, SPILL_CAP);

@@ -397,11 +397,12 @@ void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
 // ids...], spill_cap ids at most) for launch_pp_agg.
 #define PP_RC_W 4
 #define PP_RC_PART 4096  // records per partition the level sizes aim at (PP_RC_MAXN = 8192 at most)
-// compile-time specialised aggregation (pp.hip pp_agg_spec_kernel): the shape id of a Spec, -1
-// if none fits; cap = its LDS table slots, max_records = records of one partition it holds
+// specialised aggregation (pp.hip pp_agg_spec_kernel): the shape id of a Spec (its raw record
+// words), -1 if the Spec is outside the kernel's class; cap = its LDS table slots, max_records =
+// records of one partition it holds
 int pp_spec_shape(const Spec& hspec, u32* cap, u32* max_records);
-void launch_pp_agg_spec(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
-                        const PPAggOut& out, u32* spill, u32 spill_cap);
+void launch_pp_agg_spec(hipStream_t s, const Spec& hspec, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw,
+                        u32 sub_bits, const PPAggOut& out, u32* spill, u32 spill_cap);
 u32 pp_rc_records(const Spec& hspec);  // records one LDS round holds
 bool pp_rc_ok(const Spec& hspec);
 void launch_pp_agg_rc(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, int mode, u32 n_parts,

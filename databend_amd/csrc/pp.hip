@@ -17,6 +17,7 @@
 // histograms, one workgroup scans them in (source partition, bucket, unit) order, and the scatter
 // pass stages records in LDS, sorts each tile by bucket and writes whole runs.  No device-scope
 // atomics touch the data: HBM traffic is record streams only.
+#include <cstring>
 #include "legacy.hpp"
 #include "agg.hpp"
 #include "agg_dev.hpp"
@@ -1624,23 +1625,25 @@ void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
 }
 
 // ------------------------------------------------------------------------------------------
-// Compile-time specialised aggregation of raw records (pp_agg_spec_kernel).
+// Specialised aggregation of raw records (pp_agg_spec_kernel).
 //
 // The generic kernel above interprets the Spec per record: a loop over the aggregates with a
 // switch on kind, argument width and type, a generic row writer, and a slot-table claim that
-// initialises states and then applies the record with LDS atomics.  For the common shape —
-// fixed-width non-nullable keys, COUNT(*) / SUM / AVG over non-nullable integer arguments, the
-// final result written as columns — every one of those decisions is a template parameter here:
-//   * key types and argument types / offsets are compile-time (offsets from the same packing rule
-//     as build_spec, checked against the Spec on the host before launch);
-//   * a slot is [key words][row count][one sum word per SUM / AVG]: AVG's count and COUNT(*) are the
-//     same row count (arguments are non-nullable), so C4's state is 3 words instead of 4;
-//   * a claimer initialises the slot from its own record (count 1, sums = its values) before
-//     publishing the tag: a new group costs no LDS atomics, a repeat costs one add per word;
+// initialises states and then applies the record with LDS atomics.  This kernel covers the class
+// of mostly-unique GROUP BYs the partitioned payload exists for — one or two fixed-width
+// non-nullable integer keys (<= 16 key bytes), up to PS_MAXA COUNT / SUM / AVG / MIN / MAX over
+// non-nullable integer arguments — with the record's word count W a template parameter (the
+// registers that hold a partition) and the rest a uniform descriptor (PsDesc: key types and
+// widths, per aggregate its kind, argument type, offset and slot word), built on the host from the
+// Spec and checked against the raw-record packing of build_spec:
+//   * a slot is [key words][row count][one value word per SUM / AVG / MIN / MAX]: AVG's count and
+//     COUNT are the same row count (arguments are non-nullable), so an AVG costs one word;
+//   * a claimer initialises the slot from its own record (count 1, values = its arguments) before
+//     publishing the tag: a new group costs no LDS atomics, a repeat one add / min / max per word;
 //   * probes read a dense u32 tag array (one LDS word per probe step), the key words only on a
 //     tag match;
 //   * claimed slots join the output list with one LDS add per wave (ballot), not one per lane;
-//   * a partition (up to PP_AGG_NT x RPT records) is loaded into registers once and aggregated in
+//   * a partition (up to PP_SPEC_NT x RPT records) is loaded into registers once and aggregated in
 //     2^sub_bits rounds selected by the hash bits below the partition's, so a partition holds
 //     2^sub_bits LDS tables' worth of groups and the level-3 scatter is gone (AGG/
 //     transform_aggregate_final.rs:71-156 aggregates one bucket per task the same way).
@@ -1648,45 +1651,32 @@ void launch_pp_agg(hipStream_t s, const Spec* dspec, const Spec& hspec, const Ba
 // a further mini-round (consistent per key: slots only fill within a mini-round).  Partitions
 // larger than the register budget are listed in `spill` for the generic kernel.
 // ------------------------------------------------------------------------------------------
-enum { PS_COUNT = 1, PS_SUM = 2, PS_AVG = 3 };
-#define PS_AGG(kind, t) (((kind) << 8) | ((t) & 0xff))
-__host__ __device__ constexpr int ps_kind(int a) { return a >> 8; }
-__host__ __device__ constexpr int ps_type(int a) { return a & 0xff; }
+enum { PS_COUNT = 1, PS_SUM = 2, PS_AVG = 3, PS_MIN = 4, PS_MAX = 5 };
+#define PS_MAXA 4
+struct PsDesc {
+    u32 nk;                 // keys (1 or 2), packed at bytes [0, kb0) and [kb0, kb0 + kb1)
+    int32_t kt[2];          // their types (the group hash's per-type mixer)
+    u32 kb0, kb1;           // their widths
+    u32 kw;                 // key words (1 or 2)
+    u64 klast;              // key bytes of the last key word
+    u32 na;                 // aggregates
+    u32 bw;                 // slot body words: key words, row count, one word per valued aggregate
+    u32 rec_bytes;          // state record bytes (MODE 1): key words + the Spec's state words
+    int32_t kind[PS_MAXA];  // PS_COUNT .. PS_MAX
+    int32_t at[PS_MAXA];    // argument type (valued aggregates)
+    u32 aoff[PS_MAXA];      // argument byte offset in the raw record
+    u32 aw[PS_MAXA];        // argument width
+    u32 vw[PS_MAXA];        // slot word of the aggregate's value
+    u32 rw[PS_MAXA];        // result column width
+};
 __host__ __device__ constexpr u32 ps_tw(int t) {
     return (t == DBG_INT8 || t == DBG_UINT8) ? 1u
            : (t == DBG_INT16 || t == DBG_UINT16) ? 2u
            : (t == DBG_INT32 || t == DBG_UINT32 || t == DBG_DATE) ? 4u : 8u;
 }
 __host__ __device__ constexpr bool ps_signed(int t) { return !(t == DBG_UINT8 || t == DBG_UINT16 || t == DBG_UINT32 || t == DBG_UINT64); }
-__host__ __device__ constexpr bool ps_has_arg(int a) { return ps_kind(a) == PS_SUM || ps_kind(a) == PS_AVG; }
-// build_spec's raw record packing: key bytes, then each argument aligned to its width
-__host__ __device__ constexpr u32 ps_align(u32 po, int a) { return ps_has_arg(a) ? ((po + ps_tw(ps_type(a)) - 1) & ~(ps_tw(ps_type(a)) - 1)) : po; }
-__host__ __device__ constexpr u32 ps_next(u32 po, int a) { return ps_has_arg(a) ? ps_align(po, a) + ps_tw(ps_type(a)) : po; }
 
-template <int K0, int K1, int A0, int A1, int A2>
-struct PsShape {
-    static constexpr int NK = K1 < 0 ? 1 : 2;
-    static constexpr u32 KB = ps_tw(K0) + (K1 < 0 ? 0u : ps_tw(K1));  // packed key bytes
-    static constexpr u32 KW = (KB + 7) / 8;
-    static constexpr u64 KLAST = (KB & 7) == 0 ? ~0ULL : ((1ULL << (8 * (KB & 7))) - 1);
-    static constexpr u32 OFF0 = ps_align(KB, A0);
-    static constexpr u32 OFF1 = ps_align(ps_next(KB, A0), A1);
-    static constexpr u32 OFF2 = ps_align(ps_next(ps_next(KB, A0), A1), A2);
-    static constexpr u32 END = ps_next(ps_next(ps_next(KB, A0), A1), A2);
-    static constexpr int NSUM = (ps_has_arg(A0) ? 1 : 0) + (ps_has_arg(A1) ? 1 : 0) + (ps_has_arg(A2) ? 1 : 0);
-    static constexpr u32 BW = KW + 1 + NSUM;  // slot body words: key, row count, sums
-    // Spec state words (build_spec: COUNT 1, SUM 1, AVG 2 — sum, count) and the state record bytes
-    static constexpr u32 swords(int a) { return a == 0 ? 0u : (ps_kind(a) == PS_AVG ? 2u : 1u); }
-    static constexpr u32 REC_BYTES = 8 * (KW + swords(A0) + swords(A1) + swords(A2));
-    static constexpr u32 off(int a) { return a == 0 ? OFF0 : (a == 1 ? OFF1 : OFF2); }
-    static constexpr int agg(int a) { return a == 0 ? A0 : (a == 1 ? A1 : A2); }
-    // sum word of aggregate a (after the row count)
-    static constexpr u32 sumw(int a) {
-        return KW + 1 + (a > 0 && ps_has_arg(A0) ? 1 : 0) + (a > 1 && ps_has_arg(A1) ? 1 : 0);
-    }
-};
-
-__device__ __forceinline__ u64 ps_ext(u64 v, int t) {  // argument bits -> the wrapping 64-bit sum addend
+__device__ __forceinline__ u64 ps_ext(u64 v, int t) {  // argument bits -> the 64-bit addend / min-max operand
     const u32 w = ps_tw(t);
     if (w == 8) return v;
     v &= (1ULL << (8 * w)) - 1;
@@ -1702,13 +1692,12 @@ __host__ __device__ constexpr size_t ps_lds_bytes(u32 cap, u32 bw, u32 w, u32 nt
            4 * (size_t)nt;
 }
 
-template <int MODE, int W, int RPT, int SNT, int K0, int K1, int A0, int A1, int A2>
-__global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
-                                                               u32 sub_bits, u32 cap, PPAggOut out, u32* __restrict__ spill, u32 spill_cap) {
-    typedef PsShape<K0, K1, A0, A1, A2> SH;
-    constexpr u32 KW = SH::KW, BW = SH::BW;
-    static_assert(KW <= (u32)W && SH::END <= 8u * W, "record words");
+template <int MODE, int W, int RPT, int SNT>
+__global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32 n_parts, const u64* __restrict__ raw_off,
+                                                               const u8* __restrict__ raw, u32 sub_bits, u32 cap, PPAggOut out,
+                                                               u32* __restrict__ spill, u32 spill_cap) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    const u32 KW = D.kw, BW = D.bw;
     l32* tags = (l32*)lds_raw;                                     // [cap] 0 empty, 1 being claimed, else tag
     l64* body = (l64*)lds_raw + (cap + 1) / 2;                     // [cap][BW]
     l16* list = (l16*)(body + (size_t)cap * BW);                   // claimed slots of the round
@@ -1734,6 +1723,8 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
         ++anyc;
         return anyw[q] != 0;
     };
+    // key word w of a record, masked to the key bytes
+    auto kword = [&](const RegRec<W>& r, u32 w) -> u64 { return w + 1 == KW ? (r.r[w] & D.klast) : r.r[w]; };
     const u32 smask = (1u << sub_bits) - 1;
     const u32 win = cap < PP_WINDOW ? cap : PP_WINDOW;
     // EXPERIMENT (TRACE=1 build, DBG_X_PPTRACE): phase times of sampled workgroups, thread 0
@@ -1772,11 +1763,12 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
                 if (old == 0) {  // claimed: key words, the record's own contribution, then the tag
                     l64* e = body + (size_t)pos * BW;
 #pragma unroll
-                    for (u32 w = 0; w < KW; ++w) e[w] = w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w];
+                    for (u32 w = 0; w < 2; ++w)
+                        if (w < KW) e[w] = kword(rk, w);
                     e[KW] = 1;
 #pragma unroll
-                    for (int a = 0; a < 3; ++a)
-                        if (ps_has_arg(SH::agg(a))) e[SH::sumw(a)] = ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a)));
+                    for (u32 a = 0; a < PS_MAXA; ++a)
+                        if (a < D.na && D.kind[a] != PS_COUNT) e[D.vw[a]] = ps_ext(rk.le(D.aoff[a], D.aw[a]), D.at[a]);
                     __hip_atomic_store(tp, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     claimed = true;
                     at = (int)pos;
@@ -1789,14 +1781,18 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
                 l64* e = body + (size_t)pos * BW;
                 bool eq = true;
 #pragma unroll
-                for (u32 w = 0; w < KW; ++w) eq &= e[w] == (w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w]);
+                for (u32 w = 0; w < 2; ++w)
+                    if (w < KW) eq &= e[w] == kword(rk, w);
                 if (eq) {
                     at_add<AS_LDS>((wptr<AS_LDS>)(e + KW), 1ULL);
 #pragma unroll
-                    for (int a = 0; a < 3; ++a)
-                        if (ps_has_arg(SH::agg(a)))
-                            at_add<AS_LDS>((wptr<AS_LDS>)(e + SH::sumw(a)),
-                                           ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a))));
+                    for (u32 a = 0; a < PS_MAXA; ++a) {
+                        if (a >= D.na || D.kind[a] == PS_COUNT) continue;
+                        const u64 v = ps_ext(rk.le(D.aoff[a], D.aw[a]), D.at[a]);
+                        wptr<AS_LDS> vp = (wptr<AS_LDS>)(e + D.vw[a]);
+                        if (D.kind[a] == PS_SUM || D.kind[a] == PS_AVG) at_add<AS_LDS>(vp, v);
+                        else at_minmax<AS_LDS>(vp, v, D.kind[a] == PS_MIN, ps_signed(D.at[a]));
+                    }
                     at = (int)pos;
                     break;
                 }
@@ -1856,8 +1852,8 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
         // slot hash bits; a record's round is the low sub_bits of its hash (the partition is the
         // top bits, the slot position the top bits of the low word)
         auto slot_hash = [&](const RegRec<W>& r) -> u32 {
-            u64 h = hash_bits(K0, r.le(0, ps_tw(K0)));
-            if (K1 >= 0) h = (h * NULL_HASH_VAL) ^ hash_bits(K1, r.le(ps_tw(K0), ps_tw(K1)));
+            u64 h = hash_bits(D.kt[0], r.le(0, D.kb0));
+            if (D.nk == 2) h = (h * NULL_HASH_VAL) ^ hash_bits(D.kt[1], r.le(D.kb0, D.kb1));
             return (u32)pp_mix(h);
         };
         u32 lo[RPT];  // slot hash bits; the round is the low sub_bits
@@ -1928,51 +1924,53 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
                     const u32 pos = list[k];
                     const l64* e = body + (size_t)pos * BW;
                     const u64 row = gbase + k;
+                    const u64 cnt = e[KW];
                     if (MODE == 1) {  // group records in the state-record format: [key words][Spec state words]
                         if (row < out.grec_cap) {
-                            u64* d = (u64*)(out.grec + row * SH::REC_BYTES);
+                            u64* d = (u64*)(out.grec + row * D.rec_bytes);
+                            u32 q = 0;
 #pragma unroll
-                            for (u32 w = 0; w < KW; ++w) d[w] = e[w];
-                            u32 q = KW;
-                            const u64 cnt = e[KW];
+                            for (u32 w = 0; w < 2; ++w)
+                                if (w < KW) d[q++] = e[w];
 #pragma unroll
-                            for (int a = 0; a < 3; ++a) {
-                                const int A = SH::agg(a);
-                                if (A == 0) continue;
-                                if (ps_kind(A) == PS_COUNT) d[q++] = cnt;
-                                else if (ps_kind(A) == PS_SUM) d[q++] = e[SH::sumw(a)];
-                                else {
-                                    d[q++] = e[SH::sumw(a)];
+                            for (u32 a = 0; a < PS_MAXA; ++a) {
+                                if (a >= D.na) continue;
+                                const int kd = D.kind[a];
+                                if (kd == PS_COUNT) {
                                     d[q++] = cnt;
+                                } else if (kd == PS_AVG) {  // the Spec's AVG state: sum, count
+                                    d[q++] = e[D.vw[a]];
+                                    d[q++] = cnt;
+                                } else {
+                                    d[q++] = e[D.vw[a]];
                                 }
                             }
                         }
                     } else if (row < out.cols.cap_groups) {
-                        RegRec<KW> kr;
-#pragma unroll
-                        for (u32 w = 0; w < KW; ++w) kr.r[w] = e[w];
-                        write_bytes(out.cols.key_data[0], row, ps_tw(K0), kr.le(0, ps_tw(K0)), 0);
+                        RegRec<2> kr;
+                        kr.r[0] = e[0];
+                        kr.r[1] = KW > 1 ? e[1] : 0;
+                        write_bytes(out.cols.key_data[0], row, D.kb0, kr.le(0, D.kb0), 0);
                         if (out.cols.key_valid[0]) out.cols.key_valid[0][row] = 1;
-                        if (K1 >= 0) {
-                            write_bytes(out.cols.key_data[1], row, ps_tw(K1), kr.le(ps_tw(K0), ps_tw(K1)), 0);
+                        if (D.nk == 2) {
+                            write_bytes(out.cols.key_data[1], row, D.kb1, kr.le(D.kb0, D.kb1), 0);
                             if (out.cols.key_valid[1]) out.cols.key_valid[1][row] = 1;
                         }
-                        const u64 cnt = e[KW];
 #pragma unroll
-                        for (int a = 0; a < 3; ++a) {
-                            const int A = SH::agg(a);
-                            if (A == 0) continue;
+                        for (u32 a = 0; a < PS_MAXA; ++a) {
+                            if (a >= D.na) continue;
+                            const int kd = D.kind[a];
                             u64 v;
-                            if (ps_kind(A) == PS_COUNT) {
+                            if (kd == PS_COUNT) {
                                 v = cnt;
-                            } else if (ps_kind(A) == PS_SUM) {
-                                v = e[SH::sumw(a)];
-                            } else {  // AVG: the sum as i64 (u64 for unsigned arguments) / count, as f64
-                                const u64 sv = e[SH::sumw(a)];
-                                const double sum = ps_signed(ps_type(A)) ? (double)(i64)sv : (double)sv;
+                            } else if (kd == PS_AVG) {  // the sum as i64 (u64 for unsigned arguments) / count, as f64
+                                const u64 sv = e[D.vw[a]];
+                                const double sum = ps_signed(D.at[a]) ? (double)(i64)sv : (double)sv;
                                 v = (u64)__double_as_longlong(sum / (double)cnt);
+                            } else {
+                                v = e[D.vw[a]];
                             }
-                            ((u64*)out.cols.agg_data[a])[row] = v;
+                            write_bytes(out.cols.agg_data[a], row, D.rw[a], v, 0);
                             if (out.cols.agg_valid[a]) out.cols.agg_valid[a][row] = 1;
                         }
                     }
@@ -1991,41 +1989,82 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const 
     }
 }
 
-// The instantiated shapes: C4 (ClickBench Q33) and the one-key COUNT / SUM forms.
-#define PS_SHAPES(X)                                                                                          \
-    X(2, DBG_INT64, DBG_INT32, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT16), PS_AGG(PS_AVG, DBG_INT16))       \
-    X(1, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), 0, 0)                                                             \
-    X(2, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT64), 0)                                     \
-    X(2, DBG_INT64, DBG_INT64, PS_AGG(PS_COUNT, 0), 0, 0)
-#define PP_SPEC_RPT 16
 #define PP_SPEC_NT 512
+#define PS_MAXW 6  // raw record words: 16 key bytes + 4 x 8 argument bytes
+// records per lane: the two register sets (the partition and the next one's prefetch) stay at
+// <= 128 VGPRs
+__host__ __device__ constexpr int ps_rpt(int w) { return w <= 2 ? 16 : (w <= 4 ? 8 : 4); }
 
-static int ps_code(const DAgg& A) {
-    if (A.kind == DBG_AGG_COUNT) return A.arg_type < 0 ? PS_AGG(PS_COUNT, 0) : -1;
-    if (A.arg_type < 0 || A.arg_nullable || A.sumk != SUMK_I64 || A.res_width != 8) return -1;
-    const int t = A.arg_type;
-    const bool ints = t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
-                      t == DBG_UINT32 || t == DBG_UINT64;
-    if (!ints) return -1;
-    if (A.kind == DBG_AGG_SUM) return PS_AGG(PS_SUM, t);
-    if (A.kind == DBG_AGG_AVG && !A.avg_round && A.res_type == DBG_FLOAT64) return PS_AGG(PS_AVG, t);
-    return -1;
+static bool ps_int_type(int t) {
+    return t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
+           t == DBG_UINT32 || t == DBG_UINT64;
 }
 
-template <int K0, int K1, int A0, int A1, int A2>
-static bool ps_match(const Spec& S) {
-    typedef PsShape<K0, K1, A0, A1, A2> SH;
-    const int nk = SH::NK, na = (A0 ? 1 : 0) + (A1 ? 1 : 0) + (A2 ? 1 : 0);
-    if (S.pp_str || S.n_keys != nk || S.n_aggs != na || S.flags_word >= 0) return false;
-    const int kt[2] = {K0, K1};
-    for (int c = 0; c < nk; ++c)
-        if (S.key_types[c].type != kt[c] || S.key_types[c].nullable || S.koff[c] != (c == 0 ? 0u : ps_tw(K0))) return false;
-    const int ac[3] = {A0, A1, A2};
-    for (int a = 0; a < na; ++a) {
-        if (ps_code(S.aggs[a]) != ac[a]) return false;
-        if (ps_has_arg(ac[a]) && S.pp_aoff[a] != SH::off(a)) return false;
+// The descriptor of a Spec the kernel covers, or false.  Checks the raw-record packing of
+// build_spec (keys contiguous from byte 0, each argument aligned to its width after them) and
+// the state record format against what the kernel reads and writes.
+static bool ps_desc(const Spec& S, PsDesc& D, u32& W) {
+    memset(&D, 0, sizeof(D));
+    if (S.pp_str || S.n_keys < 1 || S.n_keys > 2 || S.n_aggs < 1 || S.n_aggs > PS_MAXA || S.flags_word >= 0) return false;
+    D.nk = (u32)S.n_keys;
+    u32 kb = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const int t = S.key_types[c].type;
+        const bool ok = ps_int_type(t) || t == DBG_DATE || t == DBG_TIMESTAMP;
+        if (!ok || S.key_types[c].nullable || S.koff[c] != kb) return false;
+        D.kt[c] = t;
+        const u32 w = t == DBG_TIMESTAMP ? 8u : ps_tw(t);
+        if (c == 0) D.kb0 = w;
+        else D.kb1 = w;
+        kb += w;
     }
-    return S.pp_rw_raw == ((SH::END + 7) & ~7u) && S.pp_kw == 8 * SH::KW && S.pp_rw_state == SH::REC_BYTES;
+    D.kw = (kb + 7) / 8;
+    D.klast = (kb & 7) == 0 ? ~0ULL : ((1ULL << (8 * (kb & 7))) - 1);
+    if (S.pp_kw != 8 * D.kw) return false;
+    D.na = (u32)S.n_aggs;
+    u32 po = kb, vw = D.kw + 1, rec_words = D.kw;
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        int kd;
+        if (A.kind == DBG_AGG_COUNT) {
+            if (A.arg_type >= 0 && A.arg_nullable) return false;
+            kd = PS_COUNT;  // COUNT(*) or COUNT(non-nullable x): the row count
+        } else {
+            if (A.arg_type < 0 || A.arg_nullable || !ps_int_type(A.arg_type)) return false;
+            if (A.kind == DBG_AGG_SUM && A.sumk == SUMK_I64 && A.res_width == 8) kd = PS_SUM;
+            else if (A.kind == DBG_AGG_AVG && A.sumk == SUMK_I64 && !A.avg_round && A.res_type == DBG_FLOAT64) kd = PS_AVG;
+            else if ((A.kind == DBG_AGG_MIN || A.kind == DBG_AGG_MAX) && (A.mmk == MMK_I64 || A.mmk == MMK_U64) &&
+                     (u32)A.res_width == ps_tw(A.arg_type))
+                kd = A.kind == DBG_AGG_MIN ? PS_MIN : PS_MAX;
+            else
+                return false;
+        }
+        D.kind[a] = kd;
+        D.rw[a] = kd == PS_MIN || kd == PS_MAX ? ps_tw(A.arg_type) : 8u;
+        const u32 nwords = kd == PS_AVG ? 2u : 1u;  // the Spec's state words
+        if (A.nwords != (int)nwords || A.w0 != (int)(rec_words - D.kw + 1)) return false;
+        rec_words += nwords;
+        if (A.arg_type >= 0 && kd != PS_COUNT) {
+            const u32 w = ps_tw(A.arg_type);
+            po = (po + w - 1) & ~(w - 1);
+            D.at[a] = A.arg_type;
+            D.aoff[a] = po;
+            D.aw[a] = w;
+            if (S.pp_aoff[a] != po) return false;
+            po += w;
+            D.vw[a] = vw++;
+        } else if (A.arg_type >= 0) {
+            // COUNT(x): build_spec still packs x into the raw record
+            const u32 w = ps_tw(A.arg_type);
+            po = (po + w - 1) & ~(w - 1);
+            if (S.pp_aoff[a] != po) return false;
+            po += w;
+        }
+    }
+    D.bw = vw;
+    D.rec_bytes = 8 * rec_words;
+    W = (S.pp_rw_raw + 7) / 8;
+    return S.pp_rw_raw == ((po + 7) & ~7u) && W >= 1 && W <= PS_MAXW && S.pp_rw_state == D.rec_bytes;
 }
 
 #define PS_LDS (152 * 1024)  // one workgroup per CU: the largest table, the fewest rounds
@@ -2036,45 +2075,43 @@ static u32 ps_cap(u32 bw, u32 w) {
 }
 
 int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
-    int id = 0, found = -1;
-    u32 bw = 0, w = 0;
-#define PS_TRY(WW, K0, K1, A0, A1, A2)                        \
-    if (found < 0 && ps_match<K0, K1, A0, A1, A2>(S)) {     \
-        found = id;                                         \
-        bw = PsShape<K0, K1, A0, A1, A2>::BW;               \
-        w = WW;                                             \
-    }                                                       \
-    ++id;
-    PS_SHAPES(PS_TRY)
-#undef PS_TRY
-    if (found >= 0) {
-        *cap = ps_cap(bw, w);
-        *max_records = PP_SPEC_NT * PP_SPEC_RPT;
-    }
-    return found;
+    PsDesc D;
+    u32 W = 0;
+    if (!ps_desc(S, D, W)) return -1;
+    *cap = ps_cap(D.bw, W);
+    *max_records = PP_SPEC_NT * ps_rpt((int)W);
+    return (int)W;
 }
 
-void launch_pp_agg_spec(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
-                        const PPAggOut& out, u32* spill, u32 spill_cap) {
+void launch_pp_agg_spec(hipStream_t s, const Spec& S, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw,
+                        u32 sub_bits, const PPAggOut& out, u32* spill, u32 spill_cap) {
     if (!n_parts) return;
+    PsDesc D;
+    u32 W = 0;
+    if (!ps_desc(S, D, W) || (int)W != shape) return;  // the host planned with pp_spec_shape: never taken
     const u32 grid = n_parts < 256 ? n_parts : 256;  // one persistent workgroup per CU
     // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
     const char* cx = getenv("DBG_X_PPSPEC_CAP");
     const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
-    int id = 0;
-#define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
-    if (shape == id) {                                                                                                  \
-        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW), cap_x);                          \
-        const size_t lds = ps_lds_bytes(cap, bw, WW, PP_SPEC_NT) + 16;                                                  \
-        if (mode == 0)                                                                                                  \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
-                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
-        else                                                                                                            \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
-                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
-    }                                                                                                                   \
-    ++id;
-    PS_SHAPES(PS_LAUNCH)
+    const u32 cap = std::min(ps_cap(D.bw, W), cap_x);
+    const size_t lds = ps_lds_bytes(cap, D.bw, W, PP_SPEC_NT) + 16;
+#define PS_LAUNCH(WW)                                                                                                            \
+    case WW:                                                                                                                     \
+        if (mode == 0)                                                                                                           \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, ps_rpt(WW), PP_SPEC_NT>), dim3(grid), dim3(PP_SPEC_NT), lds, s, D,     \
+                               n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                                     \
+        else                                                                                                                     \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, ps_rpt(WW), PP_SPEC_NT>), dim3(grid), dim3(PP_SPEC_NT), lds, s, D,     \
+                               n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                                     \
+        break;
+    switch (W) {
+        PS_LAUNCH(1)
+        PS_LAUNCH(2)
+        PS_LAUNCH(3)
+        PS_LAUNCH(4)
+        PS_LAUNCH(5)
+        PS_LAUNCH(6)
+    }
 #undef PS_LAUNCH
 }
 

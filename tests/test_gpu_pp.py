@@ -247,7 +247,8 @@ def test_pp_record_centric(kind):
     assert g > 1_000_000
 
 
-@pytest.mark.parametrize("kind", ["c4_unique", "c4_dup", "c4_skewed", "i64_count", "i64_sum", "i64_i64", "small_table"])
+@pytest.mark.parametrize("kind", ["c4_unique", "c4_dup", "c4_skewed", "i64_count", "i64_sum", "i64_i64", "small_table",
+                                  "i32_minmax", "date_ts_4aggs", "u64_sum_avg", "u16_u8_count"])
 def test_pp_specialised_kernel(kind, monkeypatch):
     """The compile-time specialised aggregation (pp.hip pp_agg_spec_kernel) on every instantiated
     shape: C4 (Int64, Int32 keys; COUNT(*), SUM(Int16), AVG(Int16)) with mostly-unique keys, a few
@@ -274,6 +275,23 @@ def test_pp_specialised_kernel(kind, monkeypatch):
     elif kind == "i64_sum":
         keys = [Column.from_numbers(col.Int64, rng.integers(0, n // 2, n))]
         aggs = [("count", None), ("sum", Column.from_numbers(col.Int64, rng.integers(-2**50, 2**50, n)))]
+    elif kind == "i32_minmax":  # shapes outside the benchmark: the kernel's class, not a list of queries
+        keys = [Column.from_numbers(col.Int32, rng.integers(-2**31, 2**31 - 1, n))]
+        aggs = [("count", None), ("min", Column.from_numbers(col.Int32, rng.integers(-2**31, 2**31 - 1, n))),
+                ("max", Column.from_numbers(col.UInt16, rng.integers(0, 2**16, n))), ("sum", Column.from_numbers(col.Int8, rng.integers(-128, 128, n)))]
+    elif kind == "date_ts_4aggs":
+        keys = [Column.from_numbers(col.Date, rng.integers(0, 20000, n).astype(np.int32)),
+                Column.from_numbers(col.Timestamp, rng.integers(0, n, n) * 1_000_000)]
+        aggs = [("sum", Column.from_numbers(col.Int64, rng.integers(-2**40, 2**40, n))),
+                ("avg", Column.from_numbers(col.UInt32, rng.integers(0, 2**32 - 1, n, dtype=np.uint64).astype(np.uint32))),
+                ("max", Column.from_numbers(col.Int64, rng.integers(-2**62, 2**62, n))), ("count", None)]
+    elif kind == "u64_sum_avg":
+        keys = [Column.from_numbers(col.UInt64, rng.integers(0, 2**63, n, dtype=np.uint64))]
+        aggs = [("sum", Column.from_numbers(col.UInt64, rng.integers(0, 2**40, n, dtype=np.uint64))),
+                ("sql_avg", Column.from_numbers(col.Int32, rng.integers(-2**31, 2**31 - 1, n)))]
+    elif kind == "u16_u8_count":
+        keys = [Column.from_numbers(col.UInt16, rng.integers(0, 2**16, n)), Column.from_numbers(col.UInt8, rng.integers(0, 256, n))]
+        aggs = [("count", None), ("min", Column.from_numbers(col.Int16, rng.integers(-2**15, 2**15, n)))]
     else:
         keys = [Column.from_numbers(col.Int64, rng.integers(0, n, n)), Column.from_numbers(col.Int64, rng.integers(0, 3, n))]
         aggs = [("count", None)]
@@ -281,7 +299,7 @@ def test_pp_specialised_kernel(kind, monkeypatch):
         monkeypatch.setenv("DBG_X_PPSPEC_CAP", "256")
     g, info = check_pp(keys, aggs, on_device=True, batches=2)
     assert info["specialised"]
-    assert g > 1_000_000 or kind == "c4_dup"
+    assert g > 1_000_000 or kind in ("c4_dup", "u16_u8_count")
     if kind == "small_table":
         assert info["extra_rounds"] > 0
 
