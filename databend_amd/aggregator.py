@@ -590,16 +590,18 @@ class TransformPartialAggregate:
         from the block by index; the block's rows are added to the HBM table."""
         groups = [block.columns[i] for i in group_indices]
         args = [None if i is None else block.columns[i] for i in arg_indices]
+        # the tables' inputs are compacted away on the bytes retained since the last compaction,
+        # not on the total: the compacted group records themselves count towards the total, and
+        # once they alone pass the limit a total-based trigger would compact again after every
+        # block.  A DISTINCT partial compacts its main table and its pair tables together.
+        owner = self.distinct if self.distinct is not None else self.hashtable
         if self.distinct is not None:
             self.distinct.add_groups(groups, args, block.num_rows(), filter_program)
-            return []
-        self.hashtable.add_groups(groups, args, rows=block.num_rows(), filter_program=filter_program)
-        # compact on the bytes retained since the last compaction, not on the total: the compacted
-        # group records themselves count towards the total, and once they alone pass the limit a
-        # total-based trigger would compact again after every block
-        if self.compact_bytes and self.hashtable.retained_bytes() - self._compacted_bytes > self.compact_bytes:
-            self.hashtable.compact()
-            self._compacted_bytes = self.hashtable.retained_bytes()
+        else:
+            self.hashtable.add_groups(groups, args, rows=block.num_rows(), filter_program=filter_program)
+        if self.compact_bytes and owner.retained_bytes() - self._compacted_bytes > self.compact_bytes:
+            owner.compact()
+            self._compacted_bytes = owner.retained_bytes()
         return []
 
     def on_finish(self) -> List[AggregateMeta]:

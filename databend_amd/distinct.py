@@ -267,6 +267,21 @@ class DistinctPartial:
         if on_device:  # the device inputs of the staged launches must outlive them
             self._keep.append((nulls, ones))
 
+    def retained_bytes(self) -> int:
+        """Device bytes the main table and the pair tables keep for the inputs they reference."""
+        return self.table.retained_bytes() + sum(t.retained_bytes() for t in self.pairs.values())
+
+    def compact(self) -> None:
+        """dbg_agg_compact of the main table and every pair table: each then references one record
+        batch of its own groups (or pairs), so the copies of earlier host blocks are released and
+        the partial's memory follows its groups and value sets, not the rows it saw.  Compaction
+        synchronises the table's stream, so the device columns kept for staged launches are free
+        to go too."""
+        self.table.compact()
+        for t in self.pairs.values():
+            t.compact()
+        self._keep.clear()
+
     def on_finish(self, n_parts: int) -> List[AggregateMeta]:
         t_b = export_buckets(self.table, n_parts)
         p_b = {j: export_buckets(self.pairs[j], n_parts) for j in self.distinct_idx}

@@ -210,3 +210,43 @@ def test_distinct_through_partial_bucket_final(mixed_bits):
     cd = _expected_distinct(region, "count", user)
     assert {k: v[2] for k, v in out.items()} == cd
     assert maxp == 32
+
+
+def test_distinct_partial_compacts_its_tables():
+    """A DISTINCT partial over many host blocks of String keys and String values keeps copies of
+    the blocks its main table and pair tables reference; with a small compact_bytes it compacts
+    them together, so the retained bytes follow the groups and value sets (bounded), and the
+    result still equals the single-node DistinctAggregator."""
+    from databend_amd.aggregator import DataBlock, TransformFinalAggregate, TransformPartialAggregate, TransformPartitionBucket
+    from tests.test_gpu_parity import slice_col
+    rng = np.random.default_rng(91)
+    n = 400_000
+    k = Column.from_strings([b"key-%05d" % v for v in rng.integers(0, 2000, n)])
+    x = Column.from_strings([b"val-%03d" % v for v in rng.integers(0, 40, n)])
+    i64 = Column.from_numbers(col.Int64, rng.integers(-1000, 1000, n))
+    aggs = [("sum", i64), ("count_distinct", x)]
+    fns = [F.get(fn, [], [c.dtype]) for fn, c in aggs]
+    params = AggregatorParams([k.dtype], fns)
+    limit = 4 << 20
+    p = TransformPartialAggregate(params, compact_bytes=limit)
+    peak = 0
+    try:
+        for b in range(0, n, 16384):
+            e = min(n, b + 16384)
+            p.transform(DataBlock([slice_col(c, b, e) for c in (k, i64, x)]), [0], [1, 2])
+            peak = max(peak, p.distinct.retained_bytes())
+        assert peak < 3 * limit, peak  # without compaction: every block's copy (> 20 MB)
+        metas = p.on_finish()
+    finally:
+        p.close()
+    bucket = TransformPartitionBucket(params)
+    bucket.push(metas)
+    final = TransformFinalAggregate(params)
+    out = {}
+    for part in bucket.finish():
+        blk = final.transform(part)
+        for i, kk in enumerate(blk.columns[2].values()):
+            out[kk] = (blk.columns[0].values()[i], blk.columns[1].values()[i])
+    ref = DistinctAggregator(params).run([k], [i64, x])
+    exp = {kk: (ref.columns[0].values()[i], ref.columns[1].values()[i]) for i, kk in enumerate(ref.columns[2].values())}
+    assert out == exp
