@@ -218,8 +218,9 @@ constexpr bool kPhaseTrace = false;
 
 // Experiment knobs (DBG_X_*: ablations, alternative kernels, tile shapes) are read only by a
 // library built with `make EXP=1` (-DDBG_EXPERIMENTS).  The shipped library never reads them, so
-// a stray environment variable cannot change what it computes; the one test hook it keeps is
-// DBG_X_PPSPEC_CAP (a smaller LDS table for the specialised pp aggregation: same results).
+// a stray environment variable cannot change what it computes; the test hooks it keeps are
+// DBG_X_PPSPEC_CAP and DBG_X_PPSPEC_DESC (a smaller LDS table / the descriptor kernel for the
+// specialised pp aggregation: same results).
 #ifdef DBG_EXPERIMENTS
 constexpr bool kExperiments = true;
 #define X_ENV(name) getenv(name)

@@ -313,10 +313,15 @@ template <int W>
 struct RegRec {
     u64 r[W];
     __device__ __forceinline__ u64 word(u32 w) const {
+        // a select chain over register values: the opaque copy keeps the optimizer from folding it
+        // into one load at a dynamic index, which puts the whole record array in scratch (W >= 3)
         u64 v = r[0];
 #pragma unroll
-        for (int k = 1; k < W; ++k)
-            if (w == (u32)k) v = r[k];
+        for (int k = 1; k < W; ++k) {
+            u64 c = r[k];
+            asm volatile("" : "+v"(c));
+            v = w == (u32)k ? c : v;
+        }
         return v;
     }
     __device__ __forceinline__ u64 le(u32 off, u32 nb) const {
@@ -1657,6 +1662,9 @@ struct PsDesc {
     u32 nk;                 // keys (1 or 2), packed at bytes [0, kb0) and [kb0, kb0 + kb1)
     int32_t kt[2];          // their types (the group hash's per-type mixer)
     u32 kb0, kb1;           // their widths
+    u32 k1w, k1s;           // key 1 as a shift pair: record word and bit offset (it may straddle into the next word)
+    u64 km0, km1;           // value masks of key 0 and key 1
+    u32 hc;                 // hash mixer classes of the keys (ps_hclass): hc0 * 5 + hc1, hc1 = 4 for one key
     u32 kw;                 // key words (1 or 2)
     u64 klast;              // key bytes of the last key word
     u32 na;                 // aggregates
@@ -1666,6 +1674,10 @@ struct PsDesc {
     int32_t at[PS_MAXA];    // argument type (valued aggregates)
     u32 aoff[PS_MAXA];      // argument byte offset in the raw record
     u32 aw[PS_MAXA];        // argument width
+    u32 xw[PS_MAXA];        // the argument as a shift pair: record word, bit offset in it (arguments
+    u32 xs[PS_MAXA];        // are aligned to their width, so never straddle a word), and the
+    u32 xe[PS_MAXA];        // shift that extends it (64 - 8 x width) — sign- or zero- per xsg
+    u32 xsg[PS_MAXA];
     u32 vw[PS_MAXA];        // slot word of the aggregate's value
     u32 rw[PS_MAXA];        // result column width
 };
@@ -1692,8 +1704,73 @@ __host__ __device__ constexpr size_t ps_lds_bytes(u32 cap, u32 bw, u32 w, u32 nt
            4 * (size_t)nt;
 }
 
+// one result cell: stores through an address-space-1 view (a generic pointer compiles to flat
+// stores, which count against lgkmcnt: every LDS wait of the emit loop would then drain them)
+__device__ __forceinline__ void ps_store(void* dst, u64 row, u32 w, u64 v) {
+    typedef __attribute__((address_space(1))) u8 g8;
+    g8* p = (g8*)dst + row * w;
+    if (w == 8) *(__attribute__((address_space(1))) u64*)p = v;
+    else if (w == 4) *(__attribute__((address_space(1))) u32*)p = (u32)v;
+    else if (w == 2) *(__attribute__((address_space(1))) uint16_t*)p = (uint16_t)v;
+    else *p = (u8)v;
+}
+
+// The group hash's per-type mixer (hash_bits) in four classes: sign-extended 8 / 16 / 32-bit
+// values, and the raw 64-bit pattern (64-bit and unsigned types).  The slot hashes of a
+// partition's records are computed under ONE uniform dispatch on the key classes (a per-record
+// switch on the runtime key type made the hash phase a chain of branches: 2.6 -> 8.7 us a partition).
+__host__ __device__ constexpr int ps_hclass(int t) {
+    return t == DBG_INT8 ? 0 : (t == DBG_INT16 ? 1 : ((t == DBG_INT32 || t == DBG_DATE) ? 2 : 3));
+}
+template <int C>
+__device__ __forceinline__ u64 ps_hmix(u64 b) {
+    if (C == 0) return hash_prim((u64)(i64)(int8_t)b);
+    if (C == 1) return hash_prim((u64)(i64)(int16_t)b);
+    if (C == 2) return hash_prim((u64)(i64)(int32_t)b);
+    return hash_prim(b);
+}
+template <int W, int RPT, int C0, int C1>
+__device__ __forceinline__ void ps_hash_all(const PsDesc& D, const RegRec<W>* rr, u32* lo) {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        u64 h = ps_hmix<C0>(rr[u].r[0] & D.km0);
+        if (C1 < 4) {
+            u64 k1 = rr[u].word(D.k1w) >> D.k1s;
+            if (D.k1s && W > 1) k1 |= rr[u].word(D.k1w + 1) << (64 - D.k1s);
+            h = (h * NULL_HASH_VAL) ^ ps_hmix<C1 < 4 ? C1 : 3>(k1 & D.km1);
+        }
+        lo[u] = (u32)pp_mix(h);
+    }
+}
+template <int W, int RPT, int C0>
+__device__ __forceinline__ void ps_hash_c1(const PsDesc& D, const RegRec<W>* rr, u32* lo) {
+    switch (D.hc % 5) {
+        case 0: ps_hash_all<W, RPT, C0, 0>(D, rr, lo); break;
+        case 1: ps_hash_all<W, RPT, C0, 1>(D, rr, lo); break;
+        case 2: ps_hash_all<W, RPT, C0, 2>(D, rr, lo); break;
+        case 3: ps_hash_all<W, RPT, C0, 3>(D, rr, lo); break;
+        default: ps_hash_all<W, RPT, C0, 4>(D, rr, lo); break;
+    }
+}
+template <int W, int RPT>
+__device__ __forceinline__ void ps_hash(const PsDesc& D, const RegRec<W>* rr, u32* lo) {
+    switch (D.hc / 5) {
+        case 0: ps_hash_c1<W, RPT, 0>(D, rr, lo); break;
+        case 1: ps_hash_c1<W, RPT, 1>(D, rr, lo); break;
+        case 2: ps_hash_c1<W, RPT, 2>(D, rr, lo); break;
+        default: ps_hash_c1<W, RPT, 3>(D, rr, lo); break;
+    }
+}
+
+// argument a of a register record, extended to 64 bits (the sum addend / min-max operand)
+template <int W>
+__device__ __forceinline__ u64 ps_arg(const PsDesc& D, const RegRec<W>& r, u32 a) {
+    const u64 x = r.word(D.xw[a]) >> D.xs[a];
+    return D.xsg[a] ? (u64)((i64)(x << D.xe[a]) >> D.xe[a]) : ((x << D.xe[a]) >> D.xe[a]);
+}
+
 template <int MODE, int W, int RPT, int SNT>
-__global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32 n_parts, const u64* __restrict__ raw_off,
+__global__ void __launch_bounds__(SNT, 1) pp_agg_desc_kernel(const PsDesc D, u32 n_parts, const u64* __restrict__ raw_off,
                                                                const u8* __restrict__ raw, u32 sub_bits, u32 cap, PPAggOut out,
                                                                u32* __restrict__ spill, u32 spill_cap) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
@@ -1768,7 +1845,7 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32
                     e[KW] = 1;
 #pragma unroll
                     for (u32 a = 0; a < PS_MAXA; ++a)
-                        if (a < D.na && D.kind[a] != PS_COUNT) e[D.vw[a]] = ps_ext(rk.le(D.aoff[a], D.aw[a]), D.at[a]);
+                        if (a < D.na && D.kind[a] != PS_COUNT) e[D.vw[a]] = ps_arg<W>(D, rk, a);
                     __hip_atomic_store(tp, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     claimed = true;
                     at = (int)pos;
@@ -1788,7 +1865,7 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32
 #pragma unroll
                     for (u32 a = 0; a < PS_MAXA; ++a) {
                         if (a >= D.na || D.kind[a] == PS_COUNT) continue;
-                        const u64 v = ps_ext(rk.le(D.aoff[a], D.aw[a]), D.at[a]);
+                        const u64 v = ps_arg<W>(D, rk, a);
                         wptr<AS_LDS> vp = (wptr<AS_LDS>)(e + D.vw[a]);
                         if (D.kind[a] == PS_SUM || D.kind[a] == PS_AVG) at_add<AS_LDS>(vp, v);
                         else at_minmax<AS_LDS>(vp, v, D.kind[a] == PS_MIN, ps_signed(D.at[a]));
@@ -1851,9 +1928,508 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32
         if (tr) atomicAdd((unsigned long long*)out.trace + 5, 1ULL);
         // slot hash bits; a record's round is the low sub_bits of its hash (the partition is the
         // top bits, the slot position the top bits of the low word)
+        u32 lo[RPT];  // slot hash bits; the round is the low sub_bits
+        ps_hash<W, RPT>(D, rr, lo);
+        u32 valid = 0;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) valid |= ((u64)u * SNT + tid < n) ? (1u << u) : 0u;
+        tick(0);  // the partition's loads landed, hashed
+        for (u32 round = 0; round <= smask; ++round) {
+            u32 act = 0;
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) act |= (lo[u] & smask) == round ? (1u << u) : 0u;
+            act &= valid;
+            while (true) {  // mini-rounds: the round's records, then its probe-window misses
+                while (true) {  // stage <= PS_STAGE of them at a time (compacted: every lane busy)
+                    // one LDS add per wave for all RPT slots: the ballots first (no memory ops),
+                    // then the wave's base, then each slot's running offset (wave-uniform)
+                    u64 mb[RPT];
+                    u32 wtot = 0;
+#pragma unroll
+                    for (int u = 0; u < RPT; ++u) {
+                        mb[u] = __ballot((act >> u) & 1);
+                        wtot += (u32)__popcll(mb[u]);
+                    }
+                    u32 wbase = 0;
+                    if (wtot) {
+                        if (lane == 0) wbase = atomicAdd(&scount, wtot);
+                        wbase = __builtin_amdgcn_readfirstlane(wbase);
+                    }
+                    u32 run = wbase;
+#pragma unroll
+                    for (int u = 0; u < RPT; ++u) {
+                        const u64 m = mb[u];
+                        const bool on = (act >> u) & 1;
+                        const u32 k = run + (u32)__popcll(m & ((1ULL << lane) - 1));
+                        run += (u32)__popcll(m);
+                        if (on && k < PS_STAGE) {
+#pragma unroll
+                            for (int w = 0; w < W; ++w) sw_[(size_t)k * W + w] = rr[u].r[w];
+                            slo[k] = lo[u];
+                            sorg[k] = (u16)((tid << 4) | (u32)u);
+                            act &= ~(1u << u);
+                        }
+                    }
+                    tick(1);
+                    lds_barrier();
+                    tick(4);
+                    const u32 ms = min(scount, (u32)PS_STAGE);
+                    for (u32 k0 = 0; k0 < ms; k0 += SNT) {
+                        const u32 k = k0 + tid;
+                        if (k < ms && !insert(k))
+                            __hip_atomic_fetch_or(pend + (sorg[k] >> 4), 1u << (sorg[k] & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    tick(2);
+                    lds_barrier();
+                    if (tid == 0) scount = 0;
+                    const bool more = block_any(act != 0);
+                    tick(4);
+                    if (!more) break;
+                }
+                // the round's groups out as result rows, their tags cleared for the next table
+                if (tid == 0) gbase = nlist ? atomicAdd((unsigned long long*)(out.tot + PPT_GROUPS), (unsigned long long)nlist) : 0;
+                lds_barrier();
+                const u32 ng = nlist;
+                if (MODE == 1) {
+                    for (u32 k = tid; k < ng; k += SNT) {  // group records in the state-record format
+                        const l64* e = body + (size_t)list[k] * BW;
+                        const u64 row = gbase + k;
+                        const u64 cnt = e[KW];
+                        if (row >= out.grec_cap) continue;
+                        __attribute__((address_space(1))) u64* d = (__attribute__((address_space(1))) u64*)(out.grec + row * D.rec_bytes);
+                        u32 q = 0;
+#pragma unroll
+                        for (u32 w = 0; w < 2; ++w)
+                            if (w < KW) d[q++] = e[w];
+#pragma unroll
+                        for (u32 a = 0; a < PS_MAXA; ++a) {
+                            if (a >= D.na) continue;
+                            const int kd = D.kind[a];
+                            if (kd == PS_COUNT) {
+                                d[q++] = cnt;
+                            } else if (kd == PS_AVG) {  // the Spec's AVG state: sum, count
+                                d[q++] = e[D.vw[a]];
+                                d[q++] = cnt;
+                            } else {
+                                d[q++] = e[D.vw[a]];
+                            }
+                        }
+                    }
+                } else {
+                    // result columns, one column at a time: the column's kind and width are
+                    // decided once (uniform), so each loop is a plain LDS read -> global store
+                    // (a per-group switch over kinds and widths tripled this phase)
+                    const u64 cap_g = out.cols.cap_groups;
+                    auto col_loop = [&](auto value_of, void* dst, u32 w) {
+                        typedef __attribute__((address_space(1))) u8 g8;
+                        g8* base = (g8*)dst;
+                        for (u32 k = tid; k < ng; k += SNT) {
+                            const u64 row = gbase + k;
+                            if (row >= cap_g) continue;
+                            const u64 v = value_of(body + (size_t)list[k] * BW);
+                            if (w == 8) ((__attribute__((address_space(1))) u64*)base)[row] = v;
+                            else if (w == 4) ((__attribute__((address_space(1))) u32*)base)[row] = (u32)v;
+                            else if (w == 2) ((__attribute__((address_space(1))) uint16_t*)base)[row] = (uint16_t)v;
+                            else base[row] = (u8)v;
+                        }
+                    };
+                    auto ones = [&](u8* dst) {
+                        if (dst) col_loop([](const l64*) -> u64 { return 1; }, dst, 1);
+                    };
+                    col_loop([&](const l64* e) -> u64 { return e[0] & D.km0; }, out.cols.key_data[0], D.kb0);
+                    ones(out.cols.key_valid[0]);
+                    if (D.nk == 2) {
+                        if (D.k1w) col_loop([&](const l64* e) -> u64 { return (e[1] >> D.k1s) & D.km1; }, out.cols.key_data[1], D.kb1);
+                        else col_loop([&](const l64* e) -> u64 { return ((e[0] >> D.k1s) | (KW > 1 ? e[1] << (64 - D.k1s) : 0)) & D.km1; },
+                                      out.cols.key_data[1], D.kb1);
+                        ones(out.cols.key_valid[1]);
+                    }
+                    for (u32 a = 0; a < D.na; ++a) {
+                        const int kd = D.kind[a];
+                        const u32 vw = D.vw[a];
+                        if (kd == PS_COUNT) {
+                            col_loop([&](const l64* e) -> u64 { return e[KW]; }, out.cols.agg_data[a], 8);
+                        } else if (kd == PS_AVG) {  // the sum as i64 (u64 for unsigned arguments) / count, as f64
+                            if (ps_signed(D.at[a]))
+                                col_loop([&](const l64* e) -> u64 { return (u64)__double_as_longlong((double)(i64)e[vw] / (double)e[KW]); },
+                                         out.cols.agg_data[a], 8);
+                            else
+                                col_loop([&](const l64* e) -> u64 { return (u64)__double_as_longlong((double)e[vw] / (double)e[KW]); },
+                                         out.cols.agg_data[a], 8);
+                        } else {
+                            col_loop([&](const l64* e) -> u64 { return e[vw]; }, out.cols.agg_data[a], D.rw[a]);
+                        }
+                        ones(out.cols.agg_valid[a]);
+                    }
+                }
+                for (u32 k = tid; k < ng; k += SNT) tags[list[k]] = 0;
+                tick(3);
+                lds_barrier();
+                tick(4);
+                if (tid == 0) nlist = 0;
+                act = pend[tid];
+                pend[tid] = 0;
+                if (!block_any(act != 0)) break;
+                if (tid == 0) atomicAdd((unsigned long long*)(out.tot + PPT_ROUNDS), 1ULL);
+            }
+        }
+    }
+}
+
+#define PP_SPEC_NT 512
+#define PS_MAXW 6  // raw record words: 16 key bytes + 4 x 8 argument bytes
+// records per lane: the two register sets (the partition and the next one's prefetch) stay at
+// <= 128 VGPRs
+#ifndef PS_RPT2
+#define PS_RPT2 16
+#endif
+__host__ __device__ constexpr int ps_rpt(int w) { return w <= 1 ? 16 : (w <= 2 ? PS_RPT2 : (w <= 4 ? 8 : 4)); }
+
+static bool ps_int_type(int t) {
+    return t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
+           t == DBG_UINT32 || t == DBG_UINT64;
+}
+
+// The descriptor of a Spec the kernel covers, or false.  Checks the raw-record packing of
+// build_spec (keys contiguous from byte 0, each argument aligned to its width after them) and
+// the state record format against what the kernel reads and writes.
+static bool ps_desc(const Spec& S, PsDesc& D, u32& W) {
+    memset(&D, 0, sizeof(D));
+    if (S.pp_str || S.n_keys < 1 || S.n_keys > 2 || S.n_aggs < 1 || S.n_aggs > PS_MAXA || S.flags_word >= 0) return false;
+    D.nk = (u32)S.n_keys;
+    u32 kb = 0;
+    for (int c = 0; c < S.n_keys; ++c) {
+        const int t = S.key_types[c].type;
+        const bool ok = ps_int_type(t) || t == DBG_DATE || t == DBG_TIMESTAMP;
+        if (!ok || S.key_types[c].nullable || S.koff[c] != kb) return false;
+        D.kt[c] = t;
+        const u32 w = t == DBG_TIMESTAMP ? 8u : ps_tw(t);
+        const u64 m = w == 8 ? ~0ULL : ((1ULL << (8 * w)) - 1);
+        if (c == 0) {
+            D.kb0 = w;
+            D.km0 = m;
+        } else {
+            D.kb1 = w;
+            D.km1 = m;
+            D.k1w = kb / 8;
+            D.k1s = 8 * (kb % 8);
+        }
+        kb += w;
+    }
+    D.hc = (u32)(ps_hclass(D.kt[0]) * 5 + (D.nk == 2 ? ps_hclass(D.kt[1]) : 4));
+    D.kw = (kb + 7) / 8;
+    D.klast = (kb & 7) == 0 ? ~0ULL : ((1ULL << (8 * (kb & 7))) - 1);
+    if (S.pp_kw != 8 * D.kw) return false;
+    D.na = (u32)S.n_aggs;
+    u32 po = kb, vw = D.kw + 1, rec_words = D.kw;
+    for (int a = 0; a < S.n_aggs; ++a) {
+        const DAgg& A = S.aggs[a];
+        int kd;
+        if (A.kind == DBG_AGG_COUNT) {
+            if (A.arg_type >= 0 && A.arg_nullable) return false;
+            kd = PS_COUNT;  // COUNT(*) or COUNT(non-nullable x): the row count
+        } else {
+            if (A.arg_type < 0 || A.arg_nullable || !ps_int_type(A.arg_type)) return false;
+            if (A.kind == DBG_AGG_SUM && A.sumk == SUMK_I64 && A.res_width == 8) kd = PS_SUM;
+            else if (A.kind == DBG_AGG_AVG && A.sumk == SUMK_I64 && !A.avg_round && A.res_type == DBG_FLOAT64) kd = PS_AVG;
+            else if ((A.kind == DBG_AGG_MIN || A.kind == DBG_AGG_MAX) && (A.mmk == MMK_I64 || A.mmk == MMK_U64) &&
+                     (u32)A.res_width == ps_tw(A.arg_type))
+                kd = A.kind == DBG_AGG_MIN ? PS_MIN : PS_MAX;
+            else
+                return false;
+        }
+        D.kind[a] = kd;
+        D.rw[a] = kd == PS_MIN || kd == PS_MAX ? ps_tw(A.arg_type) : 8u;
+        const u32 nwords = kd == PS_AVG ? 2u : 1u;  // the Spec's state words
+        if (A.nwords != (int)nwords || A.w0 != (int)(rec_words - D.kw + 1)) return false;
+        rec_words += nwords;
+        if (A.arg_type >= 0 && kd != PS_COUNT) {
+            const u32 w = ps_tw(A.arg_type);
+            po = (po + w - 1) & ~(w - 1);
+            D.at[a] = A.arg_type;
+            D.aoff[a] = po;
+            D.aw[a] = w;
+            D.xw[a] = po / 8;
+            D.xs[a] = 8 * (po % 8);
+            D.xe[a] = 64 - 8 * w;
+            D.xsg[a] = ps_signed(A.arg_type) ? 1u : 0u;
+            if (S.pp_aoff[a] != po) return false;
+            po += w;
+            D.vw[a] = vw++;
+        } else if (A.arg_type >= 0) {
+            // COUNT(x): build_spec still packs x into the raw record
+            const u32 w = ps_tw(A.arg_type);
+            po = (po + w - 1) & ~(w - 1);
+            if (S.pp_aoff[a] != po) return false;
+            po += w;
+        }
+    }
+    D.bw = vw;
+    D.rec_bytes = 8 * rec_words;
+    W = (S.pp_rw_raw + 7) / 8;
+    return S.pp_rw_raw == ((po + 7) & ~7u) && W >= 1 && W <= PS_MAXW && S.pp_rw_state == D.rec_bytes;
+}
+
+#define PS_LDS (152 * 1024)  // one workgroup per CU: the largest table, the fewest rounds
+static u32 ps_cap(u32 bw, u32 w) {
+    u32 cap = (u32)((PS_LDS - ps_lds_bytes(0, bw, w, PP_SPEC_NT) - 64) / (4 + 8 * bw + 2)) & ~3u;
+    while (cap > 64 && ps_lds_bytes(cap, bw, w, PP_SPEC_NT) + 64 > PS_LDS) cap -= 4;
+    return std::min<u32>(cap, 65532);
+}
+
+static int ps_desc_shape(const Spec& S, u32* cap, u32* max_records) {
+    PsDesc D;
+    u32 W = 0;
+    if (!ps_desc(S, D, W)) return -1;
+    *cap = ps_cap(D.bw, W);
+    *max_records = PP_SPEC_NT * ps_rpt((int)W);
+    return (int)W;
+}
+
+static void launch_ps_desc(hipStream_t s, const Spec& S, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw,
+                           u32 sub_bits, const PPAggOut& out, u32* spill, u32 spill_cap) {
+    if (!n_parts) return;
+    PsDesc D;
+    u32 W = 0;
+    if (!ps_desc(S, D, W) || (int)W != shape) return;  // the host planned with pp_spec_shape: never taken
+    const u32 grid = n_parts < 256 ? n_parts : 256;  // one persistent workgroup per CU
+    // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
+    const char* cx = getenv("DBG_X_PPSPEC_CAP");
+    const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
+    const u32 cap = std::min(ps_cap(D.bw, W), cap_x);
+    const size_t lds = ps_lds_bytes(cap, D.bw, W, PP_SPEC_NT) + 16;
+#define PS_LAUNCH(WW)                                                                                                            \
+    case WW:                                                                                                                     \
+        if (mode == 0)                                                                                                           \
+            hipLaunchKernelGGL((pp_agg_desc_kernel<0, WW, ps_rpt(WW), PP_SPEC_NT>), dim3(grid), dim3(PP_SPEC_NT), lds, s, D,     \
+                               n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                                     \
+        else                                                                                                                     \
+            hipLaunchKernelGGL((pp_agg_desc_kernel<1, WW, ps_rpt(WW), PP_SPEC_NT>), dim3(grid), dim3(PP_SPEC_NT), lds, s, D,     \
+                               n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                                     \
+        break;
+    switch (W) {
+        PS_LAUNCH(1)
+        PS_LAUNCH(2)
+        PS_LAUNCH(3)
+        PS_LAUNCH(4)
+        PS_LAUNCH(5)
+        PS_LAUNCH(6)
+    }
+#undef PS_LAUNCH
+}
+
+// ------------------------------------------------------------------------------------------
+// Compile-time specialised aggregation of raw records (pp_agg_spec_kernel).
+//
+// The generic kernel above interprets the Spec per record: a loop over the aggregates with a
+// switch on kind, argument width and type, a generic row writer, and a slot-table claim that
+// initialises states and then applies the record with LDS atomics.  For the common shape —
+// fixed-width non-nullable keys, COUNT(*) / SUM / AVG over non-nullable integer arguments, the
+// final result written as columns — every one of those decisions is a template parameter here:
+//   * key types and argument types / offsets are compile-time (offsets from the same packing rule
+//     as build_spec, checked against the Spec on the host before launch);
+//   * a slot is [key words][row count][one sum word per SUM / AVG]: AVG's count and COUNT(*) are the
+//     same row count (arguments are non-nullable), so C4's state is 3 words instead of 4;
+//   * a claimer initialises the slot from its own record (count 1, sums = its values) before
+//     publishing the tag: a new group costs no LDS atomics, a repeat costs one add per word;
+//   * probes read a dense u32 tag array (one LDS word per probe step), the key words only on a
+//     tag match;
+//   * claimed slots join the output list with one LDS add per wave (ballot), not one per lane;
+//   * a partition (up to PP_AGG_NT x RPT records) is loaded into registers once and aggregated in
+//     2^sub_bits rounds selected by the hash bits below the partition's, so a partition holds
+//     2^sub_bits LDS tables' worth of groups and the level-3 scatter is gone (AGG/
+//     transform_aggregate_final.rs:71-156 aggregates one bucket per task the same way).
+// A record whose probe window is full stays pending and is inserted into the emptied table in
+// a further mini-round (consistent per key: slots only fill within a mini-round).  Partitions
+// larger than the register budget are listed in `spill` for the generic kernel.
+// ------------------------------------------------------------------------------------------
+#define PS_AGG(kind, t) (((kind) << 8) | ((t) & 0xff))
+__host__ __device__ constexpr int ps_kind(int a) { return a >> 8; }
+__host__ __device__ constexpr int ps_type(int a) { return a & 0xff; }
+__host__ __device__ constexpr bool ps_has_arg(int a) { return ps_kind(a) == PS_SUM || ps_kind(a) == PS_AVG; }
+// build_spec's raw record packing: key bytes, then each argument aligned to its width
+__host__ __device__ constexpr u32 ps_align(u32 po, int a) { return ps_has_arg(a) ? ((po + ps_tw(ps_type(a)) - 1) & ~(ps_tw(ps_type(a)) - 1)) : po; }
+__host__ __device__ constexpr u32 ps_next(u32 po, int a) { return ps_has_arg(a) ? ps_align(po, a) + ps_tw(ps_type(a)) : po; }
+
+template <int K0, int K1, int A0, int A1, int A2>
+struct PsShape {
+    static constexpr int NK = K1 < 0 ? 1 : 2;
+    static constexpr u32 KB = ps_tw(K0) + (K1 < 0 ? 0u : ps_tw(K1));  // packed key bytes
+    static constexpr u32 KW = (KB + 7) / 8;
+    static constexpr u64 KLAST = (KB & 7) == 0 ? ~0ULL : ((1ULL << (8 * (KB & 7))) - 1);
+    static constexpr u32 OFF0 = ps_align(KB, A0);
+    static constexpr u32 OFF1 = ps_align(ps_next(KB, A0), A1);
+    static constexpr u32 OFF2 = ps_align(ps_next(ps_next(KB, A0), A1), A2);
+    static constexpr u32 END = ps_next(ps_next(ps_next(KB, A0), A1), A2);
+    static constexpr int NSUM = (ps_has_arg(A0) ? 1 : 0) + (ps_has_arg(A1) ? 1 : 0) + (ps_has_arg(A2) ? 1 : 0);
+    static constexpr u32 BW = KW + 1 + NSUM;  // slot body words: key, row count, sums
+    // Spec state words (build_spec: COUNT 1, SUM 1, AVG 2 — sum, count) and the state record bytes
+    static constexpr u32 swords(int a) { return a == 0 ? 0u : (ps_kind(a) == PS_AVG ? 2u : 1u); }
+    static constexpr u32 REC_BYTES = 8 * (KW + swords(A0) + swords(A1) + swords(A2));
+    static constexpr u32 off(int a) { return a == 0 ? OFF0 : (a == 1 ? OFF1 : OFF2); }
+    static constexpr int agg(int a) { return a == 0 ? A0 : (a == 1 ? A1 : A2); }
+    // sum word of aggregate a (after the row count)
+    static constexpr u32 sumw(int a) {
+        return KW + 1 + (a > 0 && ps_has_arg(A0) ? 1 : 0) + (a > 1 && ps_has_arg(A1) ? 1 : 0);
+    }
+};
+
+template <int MODE, int W, int RPT, int SNT, int K0, int K1, int A0, int A1, int A2>
+__global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
+                                                               u32 sub_bits, u32 cap, PPAggOut out, u32* __restrict__ spill, u32 spill_cap) {
+    typedef PsShape<K0, K1, A0, A1, A2> SH;
+    constexpr u32 KW = SH::KW, BW = SH::BW;
+    static_assert(KW <= (u32)W && SH::END <= 8u * W, "record words");
+    extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
+    l32* tags = (l32*)lds_raw;                                     // [cap] 0 empty, 1 being claimed, else tag
+    l64* body = (l64*)lds_raw + (cap + 1) / 2;                     // [cap][BW]
+    l16* list = (l16*)(body + (size_t)cap * BW);                   // claimed slots of the round
+    l64* sw_ = (l64*)(list + ((cap + 3) & ~3u));                   // staged records [PS_STAGE][W]
+    l32* slo = (l32*)(sw_ + (size_t)PS_STAGE * W);                 // their slot hash bits
+    l16* sorg = (l16*)(slo + PS_STAGE);                            // their origin (thread << 4 | register index)
+    l32* pend = (l32*)(((uintptr_t)(sorg + PS_STAGE) + 3) & ~(uintptr_t)3);  // [SNT] probe-window misses
+    __shared__ u32 nlist, scount, anyw[3];
+    __shared__ u64 gbase;
+    const u32 tid = threadIdx.x, lane = tid & 63;
+    // Barriers order LDS only: the output stores and the next partition's prefetched loads stay in
+    // flight across them (__syncthreads' workgroup fence would wait for every outstanding global
+    // access — the prefetch included).
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // block-wide OR over three rotating LDS words: call c clears the word call c + 1 votes into
+    // before its barrier (that word was last read in call c - 2, before call c - 1's barrier)
+    u32 anyc = 0;
+    auto block_any = [&](bool v) -> bool {
+        const u32 q = anyc % 3;
+        if (tid == 0) anyw[(q + 1) % 3] = 0;
+        if (__ballot(v) && lane == 0) atomicOr(&anyw[q], 1u);
+        lds_barrier();
+        ++anyc;
+        return anyw[q] != 0;
+    };
+    const u32 smask = (1u << sub_bits) - 1;
+    const u32 win = cap < PP_WINDOW ? cap : PP_WINDOW;
+    // EXPERIMENT (TRACE=1 build, DBG_X_PPTRACE): phase times of sampled workgroups, thread 0
+    const bool tr = kPhaseTrace && out.trace && (blockIdx.x & 15) == 0 && tid == 0;
+    u64 tm0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto tick = [&](int slot) {
+        if (tr) {
+            const u64 tm = __builtin_amdgcn_s_memrealtime();
+            atomicAdd((unsigned long long*)out.trace + slot, tm - tm0);
+            tm0 = tm;
+        }
+    };
+    for (u32 j = tid; j < cap; j += SNT) tags[j] = 0;
+    pend[tid] = 0;
+    if (tid == 0) {
+        nlist = scount = 0;
+        anyw[0] = anyw[1] = anyw[2] = 0;
+    }
+    lds_barrier();
+    // one staged record into the table; false = no room in its probe window
+    auto insert = [&](u32 k) -> bool {
+        RegRec<W> rk;
+#pragma unroll
+        for (int w = 0; w < W; ++w) rk.r[w] = sw_[(size_t)k * W + w];
+        const u32 lo = slo[k];
+        const u32 tag = (lo & ~3u) | 2u;
+        u32 pos = (u32)(((u64)lo * cap) >> 32);
+        bool claimed = false;
+        int at = -1;
+        for (u32 q = 0; q < win; ++q) {
+            l32* tp = tags + pos;
+            u32 t = __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t == 0) {
+                u32 old = 0;
+                __hip_atomic_compare_exchange_strong(tp, &old, 1u, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == 0) {  // claimed: key words, the record's own contribution, then the tag
+                    l64* e = body + (size_t)pos * BW;
+#pragma unroll
+                    for (u32 w = 0; w < KW; ++w) e[w] = w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w];
+                    e[KW] = 1;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        if (ps_has_arg(SH::agg(a))) e[SH::sumw(a)] = ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a)));
+                    __hip_atomic_store(tp, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    claimed = true;
+                    at = (int)pos;
+                    break;
+                }
+                t = old;
+            }
+            while (t == 1) t = __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t == tag) {
+                l64* e = body + (size_t)pos * BW;
+                bool eq = true;
+#pragma unroll
+                for (u32 w = 0; w < KW; ++w) eq &= e[w] == (w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w]);
+                if (eq) {
+                    at_add<AS_LDS>((wptr<AS_LDS>)(e + KW), 1ULL);
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        if (ps_has_arg(SH::agg(a)))
+                            at_add<AS_LDS>((wptr<AS_LDS>)(e + SH::sumw(a)),
+                                           ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a))));
+                    at = (int)pos;
+                    break;
+                }
+            }
+            pos = pos + 1 == cap ? 0 : pos + 1;
+        }
+        // new groups join the round's list: one LDS add per wave (called with the wave converged)
+        const u64 m = __ballot(claimed);
+        if (m) {
+            const u32 lead = (u32)__ffsll((long long)m) - 1;
+            u32 b = 0;
+            if (lane == lead) b = atomicAdd(&nlist, (u32)__popcll(m));
+            b = __shfl(b, (int)lead);
+            if (claimed) list[b + (u32)__popcll(m & ((1ULL << lane) - 1))] = (u16)at;
+        }
+        return at >= 0;
+    };
+    // A partition's records live in registers (RPT per lane, loaded with buffer loads: one 32-bit
+    // lane offset, the range check returning zeros past the partition), and the next partition of
+    // this workgroup is loaded into a second register set while the current one is aggregated.
+    typedef u32 v2u32 __attribute__((ext_vector_type(2)));
+    auto load_part = [&](u32 q, RegRec<W>* dst, u64& n_out) {
+        n_out = 0;
+        if (q >= n_parts) return;
+        const u64 o0 = raw_off[q], n = raw_off[q + 1] - o0;
+        n_out = n;
+        if (n == 0 || n > (u64)SNT * RPT) return;
+        const u8* base = raw + o0 * (8 * W);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * (8 * W)), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < RPT; ++u)
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * (8 * W) + 8 * w, u * (SNT * 8 * W), 0);
+                dst[u].r[w] = (u64)v.x | ((u64)v.y << 32);
+            }
+    };
+    RegRec<W> nxt[RPT];
+    u64 n_nxt;
+    load_part(blockIdx.x, nxt, n_nxt);
+    for (u32 p = blockIdx.x; p < n_parts; p += gridDim.x) {
+        RegRec<W> rr[RPT];
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) rr[u] = nxt[u];
+        const u64 n = n_nxt;
+        load_part(p + gridDim.x, nxt, n_nxt);  // in flight during this partition's rounds
+        if (n == 0) continue;
+        if (n > (u64)SNT * RPT) {  // uniform: the generic kernel takes it
+            if (tid == 0) {
+                const u32 k = atomicAdd(spill, 1u);
+                if (k < spill_cap) spill[1 + k] = p;
+                else atomicOr((unsigned long long*)(out.tot + PPT_ERR), (unsigned long long)ERR_OVF_LOST);
+            }
+            continue;
+        }
+        if (tr) atomicAdd((unsigned long long*)out.trace + 5, 1ULL);
+        // slot hash bits; a record's round is the low sub_bits of its hash (the partition is the
+        // top bits, the slot position the top bits of the low word)
         auto slot_hash = [&](const RegRec<W>& r) -> u32 {
-            u64 h = hash_bits(D.kt[0], r.le(0, D.kb0));
-            if (D.nk == 2) h = (h * NULL_HASH_VAL) ^ hash_bits(D.kt[1], r.le(D.kb0, D.kb1));
+            u64 h = hash_bits(K0, r.le(0, ps_tw(K0)));
+            if (K1 >= 0) h = (h * NULL_HASH_VAL) ^ hash_bits(K1, r.le(ps_tw(K0), ps_tw(K1)));
             return (u32)pp_mix(h);
         };
         u32 lo[RPT];  // slot hash bits; the round is the low sub_bits
@@ -1924,53 +2500,51 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32
                     const u32 pos = list[k];
                     const l64* e = body + (size_t)pos * BW;
                     const u64 row = gbase + k;
-                    const u64 cnt = e[KW];
                     if (MODE == 1) {  // group records in the state-record format: [key words][Spec state words]
                         if (row < out.grec_cap) {
-                            u64* d = (u64*)(out.grec + row * D.rec_bytes);
-                            u32 q = 0;
+                            u64* d = (u64*)(out.grec + row * SH::REC_BYTES);
 #pragma unroll
-                            for (u32 w = 0; w < 2; ++w)
-                                if (w < KW) d[q++] = e[w];
+                            for (u32 w = 0; w < KW; ++w) d[w] = e[w];
+                            u32 q = KW;
+                            const u64 cnt = e[KW];
 #pragma unroll
-                            for (u32 a = 0; a < PS_MAXA; ++a) {
-                                if (a >= D.na) continue;
-                                const int kd = D.kind[a];
-                                if (kd == PS_COUNT) {
+                            for (int a = 0; a < 3; ++a) {
+                                const int A = SH::agg(a);
+                                if (A == 0) continue;
+                                if (ps_kind(A) == PS_COUNT) d[q++] = cnt;
+                                else if (ps_kind(A) == PS_SUM) d[q++] = e[SH::sumw(a)];
+                                else {
+                                    d[q++] = e[SH::sumw(a)];
                                     d[q++] = cnt;
-                                } else if (kd == PS_AVG) {  // the Spec's AVG state: sum, count
-                                    d[q++] = e[D.vw[a]];
-                                    d[q++] = cnt;
-                                } else {
-                                    d[q++] = e[D.vw[a]];
                                 }
                             }
                         }
                     } else if (row < out.cols.cap_groups) {
-                        RegRec<2> kr;
-                        kr.r[0] = e[0];
-                        kr.r[1] = KW > 1 ? e[1] : 0;
-                        write_bytes(out.cols.key_data[0], row, D.kb0, kr.le(0, D.kb0), 0);
+                        RegRec<KW> kr;
+#pragma unroll
+                        for (u32 w = 0; w < KW; ++w) kr.r[w] = e[w];
+                        write_bytes(out.cols.key_data[0], row, ps_tw(K0), kr.le(0, ps_tw(K0)), 0);
                         if (out.cols.key_valid[0]) out.cols.key_valid[0][row] = 1;
-                        if (D.nk == 2) {
-                            write_bytes(out.cols.key_data[1], row, D.kb1, kr.le(D.kb0, D.kb1), 0);
+                        if (K1 >= 0) {
+                            write_bytes(out.cols.key_data[1], row, ps_tw(K1), kr.le(ps_tw(K0), ps_tw(K1)), 0);
                             if (out.cols.key_valid[1]) out.cols.key_valid[1][row] = 1;
                         }
+                        const u64 cnt = e[KW];
 #pragma unroll
-                        for (u32 a = 0; a < PS_MAXA; ++a) {
-                            if (a >= D.na) continue;
-                            const int kd = D.kind[a];
+                        for (int a = 0; a < 3; ++a) {
+                            const int A = SH::agg(a);
+                            if (A == 0) continue;
                             u64 v;
-                            if (kd == PS_COUNT) {
+                            if (ps_kind(A) == PS_COUNT) {
                                 v = cnt;
-                            } else if (kd == PS_AVG) {  // the sum as i64 (u64 for unsigned arguments) / count, as f64
-                                const u64 sv = e[D.vw[a]];
-                                const double sum = ps_signed(D.at[a]) ? (double)(i64)sv : (double)sv;
+                            } else if (ps_kind(A) == PS_SUM) {
+                                v = e[SH::sumw(a)];
+                            } else {  // AVG: the sum as i64 (u64 for unsigned arguments) / count, as f64
+                                const u64 sv = e[SH::sumw(a)];
+                                const double sum = ps_signed(ps_type(A)) ? (double)(i64)sv : (double)sv;
                                 v = (u64)__double_as_longlong(sum / (double)cnt);
-                            } else {
-                                v = e[D.vw[a]];
                             }
-                            write_bytes(out.cols.agg_data[a], row, D.rw[a], v, 0);
+                            ((u64*)out.cols.agg_data[a])[row] = v;
                             if (out.cols.agg_valid[a]) out.cols.agg_valid[a][row] = 1;
                         }
                     }
@@ -1989,130 +2563,105 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(const PsDesc D, u32
     }
 }
 
-#define PP_SPEC_NT 512
-#define PS_MAXW 6  // raw record words: 16 key bytes + 4 x 8 argument bytes
-// records per lane: the two register sets (the partition and the next one's prefetch) stay at
-// <= 128 VGPRs
-__host__ __device__ constexpr int ps_rpt(int w) { return w <= 2 ? 16 : (w <= 4 ? 8 : 4); }
+// The instantiated shapes: C4 (ClickBench Q33) and the one-key COUNT / SUM forms.
+#define PS_SHAPES(X)                                                                                          \
+    X(2, DBG_INT64, DBG_INT32, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT16), PS_AGG(PS_AVG, DBG_INT16))       \
+    X(1, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), 0, 0)                                                             \
+    X(2, DBG_INT64, -1, PS_AGG(PS_COUNT, 0), PS_AGG(PS_SUM, DBG_INT64), 0)                                     \
+    X(2, DBG_INT64, DBG_INT64, PS_AGG(PS_COUNT, 0), 0, 0)
+#define PP_SPEC_RPT 16
 
-static bool ps_int_type(int t) {
-    return t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
-           t == DBG_UINT32 || t == DBG_UINT64;
+static int ps_code(const DAgg& A) {
+    if (A.kind == DBG_AGG_COUNT) return A.arg_type < 0 ? PS_AGG(PS_COUNT, 0) : -1;
+    if (A.arg_type < 0 || A.arg_nullable || A.sumk != SUMK_I64 || A.res_width != 8) return -1;
+    const int t = A.arg_type;
+    const bool ints = t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
+                      t == DBG_UINT32 || t == DBG_UINT64;
+    if (!ints) return -1;
+    if (A.kind == DBG_AGG_SUM) return PS_AGG(PS_SUM, t);
+    if (A.kind == DBG_AGG_AVG && !A.avg_round && A.res_type == DBG_FLOAT64) return PS_AGG(PS_AVG, t);
+    return -1;
 }
 
-// The descriptor of a Spec the kernel covers, or false.  Checks the raw-record packing of
-// build_spec (keys contiguous from byte 0, each argument aligned to its width after them) and
-// the state record format against what the kernel reads and writes.
-static bool ps_desc(const Spec& S, PsDesc& D, u32& W) {
-    memset(&D, 0, sizeof(D));
-    if (S.pp_str || S.n_keys < 1 || S.n_keys > 2 || S.n_aggs < 1 || S.n_aggs > PS_MAXA || S.flags_word >= 0) return false;
-    D.nk = (u32)S.n_keys;
-    u32 kb = 0;
-    for (int c = 0; c < S.n_keys; ++c) {
-        const int t = S.key_types[c].type;
-        const bool ok = ps_int_type(t) || t == DBG_DATE || t == DBG_TIMESTAMP;
-        if (!ok || S.key_types[c].nullable || S.koff[c] != kb) return false;
-        D.kt[c] = t;
-        const u32 w = t == DBG_TIMESTAMP ? 8u : ps_tw(t);
-        if (c == 0) D.kb0 = w;
-        else D.kb1 = w;
-        kb += w;
+template <int K0, int K1, int A0, int A1, int A2>
+static bool ps_match(const Spec& S) {
+    typedef PsShape<K0, K1, A0, A1, A2> SH;
+    const int nk = SH::NK, na = (A0 ? 1 : 0) + (A1 ? 1 : 0) + (A2 ? 1 : 0);
+    if (S.pp_str || S.n_keys != nk || S.n_aggs != na || S.flags_word >= 0) return false;
+    const int kt[2] = {K0, K1};
+    for (int c = 0; c < nk; ++c)
+        if (S.key_types[c].type != kt[c] || S.key_types[c].nullable || S.koff[c] != (c == 0 ? 0u : ps_tw(K0))) return false;
+    const int ac[3] = {A0, A1, A2};
+    for (int a = 0; a < na; ++a) {
+        if (ps_code(S.aggs[a]) != ac[a]) return false;
+        if (ps_has_arg(ac[a]) && S.pp_aoff[a] != SH::off(a)) return false;
     }
-    D.kw = (kb + 7) / 8;
-    D.klast = (kb & 7) == 0 ? ~0ULL : ((1ULL << (8 * (kb & 7))) - 1);
-    if (S.pp_kw != 8 * D.kw) return false;
-    D.na = (u32)S.n_aggs;
-    u32 po = kb, vw = D.kw + 1, rec_words = D.kw;
-    for (int a = 0; a < S.n_aggs; ++a) {
-        const DAgg& A = S.aggs[a];
-        int kd;
-        if (A.kind == DBG_AGG_COUNT) {
-            if (A.arg_type >= 0 && A.arg_nullable) return false;
-            kd = PS_COUNT;  // COUNT(*) or COUNT(non-nullable x): the row count
-        } else {
-            if (A.arg_type < 0 || A.arg_nullable || !ps_int_type(A.arg_type)) return false;
-            if (A.kind == DBG_AGG_SUM && A.sumk == SUMK_I64 && A.res_width == 8) kd = PS_SUM;
-            else if (A.kind == DBG_AGG_AVG && A.sumk == SUMK_I64 && !A.avg_round && A.res_type == DBG_FLOAT64) kd = PS_AVG;
-            else if ((A.kind == DBG_AGG_MIN || A.kind == DBG_AGG_MAX) && (A.mmk == MMK_I64 || A.mmk == MMK_U64) &&
-                     (u32)A.res_width == ps_tw(A.arg_type))
-                kd = A.kind == DBG_AGG_MIN ? PS_MIN : PS_MAX;
-            else
-                return false;
-        }
-        D.kind[a] = kd;
-        D.rw[a] = kd == PS_MIN || kd == PS_MAX ? ps_tw(A.arg_type) : 8u;
-        const u32 nwords = kd == PS_AVG ? 2u : 1u;  // the Spec's state words
-        if (A.nwords != (int)nwords || A.w0 != (int)(rec_words - D.kw + 1)) return false;
-        rec_words += nwords;
-        if (A.arg_type >= 0 && kd != PS_COUNT) {
-            const u32 w = ps_tw(A.arg_type);
-            po = (po + w - 1) & ~(w - 1);
-            D.at[a] = A.arg_type;
-            D.aoff[a] = po;
-            D.aw[a] = w;
-            if (S.pp_aoff[a] != po) return false;
-            po += w;
-            D.vw[a] = vw++;
-        } else if (A.arg_type >= 0) {
-            // COUNT(x): build_spec still packs x into the raw record
-            const u32 w = ps_tw(A.arg_type);
-            po = (po + w - 1) & ~(w - 1);
-            if (S.pp_aoff[a] != po) return false;
-            po += w;
-        }
+    return S.pp_rw_raw == ((SH::END + 7) & ~7u) && S.pp_kw == 8 * SH::KW && S.pp_rw_state == SH::REC_BYTES;
+}
+
+static int ps_literal_shape(const Spec& S, u32* cap, u32* max_records) {
+    int id = 0, found = -1;
+    u32 bw = 0, w = 0;
+#define PS_TRY(WW, K0, K1, A0, A1, A2)                        \
+    if (found < 0 && ps_match<K0, K1, A0, A1, A2>(S)) {     \
+        found = id;                                         \
+        bw = PsShape<K0, K1, A0, A1, A2>::BW;               \
+        w = WW;                                             \
+    }                                                       \
+    ++id;
+    PS_SHAPES(PS_TRY)
+#undef PS_TRY
+    if (found >= 0) {
+        *cap = ps_cap(bw, w);
+        *max_records = PP_SPEC_NT * PP_SPEC_RPT;
     }
-    D.bw = vw;
-    D.rec_bytes = 8 * rec_words;
-    W = (S.pp_rw_raw + 7) / 8;
-    return S.pp_rw_raw == ((po + 7) & ~7u) && W >= 1 && W <= PS_MAXW && S.pp_rw_state == D.rec_bytes;
+    return found;
 }
 
-#define PS_LDS (152 * 1024)  // one workgroup per CU: the largest table, the fewest rounds
-static u32 ps_cap(u32 bw, u32 w) {
-    u32 cap = (u32)((PS_LDS - ps_lds_bytes(0, bw, w, PP_SPEC_NT) - 64) / (4 + 8 * bw + 2)) & ~3u;
-    while (cap > 64 && ps_lds_bytes(cap, bw, w, PP_SPEC_NT) + 64 > PS_LDS) cap -= 4;
-    return std::min<u32>(cap, 65532);
-}
-
-int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
-    PsDesc D;
-    u32 W = 0;
-    if (!ps_desc(S, D, W)) return -1;
-    *cap = ps_cap(D.bw, W);
-    *max_records = PP_SPEC_NT * ps_rpt((int)W);
-    return (int)W;
-}
-
-void launch_pp_agg_spec(hipStream_t s, const Spec& S, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw,
-                        u32 sub_bits, const PPAggOut& out, u32* spill, u32 spill_cap) {
+static void launch_ps_literal(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
+                              const PPAggOut& out, u32* spill, u32 spill_cap) {
     if (!n_parts) return;
-    PsDesc D;
-    u32 W = 0;
-    if (!ps_desc(S, D, W) || (int)W != shape) return;  // the host planned with pp_spec_shape: never taken
     const u32 grid = n_parts < 256 ? n_parts : 256;  // one persistent workgroup per CU
     // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
     const char* cx = getenv("DBG_X_PPSPEC_CAP");
     const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
-    const u32 cap = std::min(ps_cap(D.bw, W), cap_x);
-    const size_t lds = ps_lds_bytes(cap, D.bw, W, PP_SPEC_NT) + 16;
-#define PS_LAUNCH(WW)                                                                                                            \
-    case WW:                                                                                                                     \
-        if (mode == 0)                                                                                                           \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, ps_rpt(WW), PP_SPEC_NT>), dim3(grid), dim3(PP_SPEC_NT), lds, s, D,     \
-                               n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                                     \
-        else                                                                                                                     \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, ps_rpt(WW), PP_SPEC_NT>), dim3(grid), dim3(PP_SPEC_NT), lds, s, D,     \
-                               n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);                                     \
-        break;
-    switch (W) {
-        PS_LAUNCH(1)
-        PS_LAUNCH(2)
-        PS_LAUNCH(3)
-        PS_LAUNCH(4)
-        PS_LAUNCH(5)
-        PS_LAUNCH(6)
-    }
+    int id = 0;
+#define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
+    if (shape == id) {                                                                                                  \
+        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW), cap_x);                          \
+        const size_t lds = ps_lds_bytes(cap, bw, WW, PP_SPEC_NT) + 16;                                                  \
+        if (mode == 0)                                                                                                  \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
+                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
+        else                                                                                                            \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
+                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
+    }                                                                                                                   \
+    ++id;
+    PS_SHAPES(PS_LAUNCH)
 #undef PS_LAUNCH
+}
+
+// The class above runs on the descriptor kernel; its most common shapes — C4's (Int64, Int32;
+// COUNT, SUM(Int16), AVG(Int16)), one Int64 key with COUNT or COUNT + SUM(Int64), two Int64 keys
+// with COUNT — also have fully compile-time instances (pp_agg_spec_kernel, PS_SHAPES), which the
+// descriptor kernel cannot match yet (C4 pp_agg 36 ms compile-time, 48-53 ms from the descriptor:
+// the emit and insert phases pay for the runtime kinds and widths).  Shape ids: 0.. the literal
+// shapes, PS_DESC_ID + W the descriptor kernel.
+#define PS_DESC_ID 64
+int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
+    // test hook: the descriptor kernel for a literal shape too (same results)
+    const char* fd = getenv("DBG_X_PPSPEC_DESC");
+    const int lit = (fd && fd[0] == '1') ? -1 : ps_literal_shape(S, cap, max_records);
+    if (lit >= 0) return lit;
+    const int w = ps_desc_shape(S, cap, max_records);
+    return w >= 0 ? PS_DESC_ID + w : -1;
+}
+
+void launch_pp_agg_spec(hipStream_t s, const Spec& S, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw,
+                        u32 sub_bits, const PPAggOut& out, u32* spill, u32 spill_cap) {
+    if (shape >= PS_DESC_ID) launch_ps_desc(s, S, shape - PS_DESC_ID, mode, n_parts, raw_off, raw, sub_bits, out, spill, spill_cap);
+    else launch_ps_literal(s, shape, mode, n_parts, raw_off, raw, sub_bits, out, spill, spill_cap);
 }
 
 // ------------------------------------------------------------------------------------------

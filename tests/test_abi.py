@@ -108,11 +108,12 @@ def test_rccl_unique_id_without_device():
 def test_shipped_library_reads_no_experiment_knobs():
     """The shipped library reads no DBG_X_* experiment knob (ablations that skip work, alternative
     kernels, tile shapes): those are compiled in only by `make EXP=1` (agg.hpp X_ENV), so a stray
-    environment variable cannot change a result.  The one knob left is the test hook
-    DBG_X_PPSPEC_CAP (a smaller LDS table for the specialised pp aggregation; same results)."""
+    environment variable cannot change a result.  The knobs left are test hooks of the specialised
+    pp aggregation with the same results: DBG_X_PPSPEC_CAP (a smaller LDS table) and
+    DBG_X_PPSPEC_DESC (the descriptor kernel for a shape that also has a compile-time instance)."""
     import re
     from databend_amd.ffi import LIB_PATH
     with open(LIB_PATH, "rb") as f:
         blob = f.read()
     names = set(m.decode() for m in re.findall(rb"DBG_X_[A-Z0-9_]+", blob))
-    assert names <= {"DBG_X_PPSPEC_CAP"}, names
+    assert names <= {"DBG_X_PPSPEC_CAP", "DBG_X_PPSPEC_DESC"}, names

@@ -248,7 +248,7 @@ def test_pp_record_centric(kind):
 
 
 @pytest.mark.parametrize("kind", ["c4_unique", "c4_dup", "c4_skewed", "i64_count", "i64_sum", "i64_i64", "small_table",
-                                  "i32_minmax", "date_ts_4aggs", "u64_sum_avg", "u16_u8_count"])
+                                  "i32_minmax", "date_ts_4aggs", "u64_sum_avg", "u16_u8_count", "c4_unique_desc", "c4_skewed_desc"])
 def test_pp_specialised_kernel(kind, monkeypatch):
     """The compile-time specialised aggregation (pp.hip pp_agg_spec_kernel) on every instantiated
     shape: C4 (Int64, Int32 keys; COUNT(*), SUM(Int16), AVG(Int16)) with mostly-unique keys, a few
@@ -260,6 +260,9 @@ def test_pp_specialised_kernel(kind, monkeypatch):
     i16 = Column.from_numbers(col.Int16, rng.integers(-3, 3, n))
     w = Column.from_numbers(col.Int16, rng.integers(-2560, 2560, n))
     aggs = [("count", None), ("sum", i16), ("sql_avg", w)]
+    if kind.endswith("_desc"):  # the descriptor kernel on C4's shape (it also has a compile-time instance)
+        monkeypatch.setenv("DBG_X_PPSPEC_DESC", "1")
+        kind = kind[:-5]
     if kind in ("c4_unique", "small_table"):
         keys = [Column.from_numbers(col.Int64, rng.permutation(n).astype(np.int64) * 7919 - 3),
                 Column.from_numbers(col.Int32, rng.integers(-2**31, 2**31 - 1, n))]
