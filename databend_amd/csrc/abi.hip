@@ -597,9 +597,15 @@ static int resolve_overflow(dbg_agg_handle* h) {
             const u64 fit = std::max<u64>(pow2_at_least((u64)(claims * 2.0) + 1), 1024);
             if ((double)claims * 1.5 > (double)h->cap) RETURN_IF(grow_table(h, fit));
             // overflow growth sizes by overflowed ROWS (an upper bound on the groups they hold):
-            // once the groups are known, give back a table more than 4x what they need, so scans
-            // (finalize, table_init) and partitioned inserts touch 2x the groups, not 30x
-            else if (grew && h->cap >= 4 * fit && fit >= h->init_cap) RETURN_IF(grow_table(h, fit));
+            // once the groups are known, give back a table twice or more what they need at the
+            // reference's load factor (get_capacity_for_count: next_pow2(1.5 x count),
+            // EAGG/aggregate_hashtable.rs:567-569), so table_init, the finalize scans and
+            // partitioned inserts touch what the groups need (C5: a first-step overflow left a
+            // 2^25-slot, 2 GB table for 7e6 groups in every later step)
+            else if (grew) {
+                const u64 fit15 = std::max<u64>(pow2_at_least((u64)(claims * 1.5) + 1), 1024);
+                if (h->cap >= 2 * fit15 && fit15 >= h->init_cap) RETURN_IF(grow_table(h, fit15));
+            }
             return DBG_OK;
         }
         u64 need = pow2_at_least(2 * (claims + orows + orecs) + 1);
