@@ -84,6 +84,11 @@ class dbg_parquet_chunk(C.Structure):  # include/dbgpu_scan.h
                 ("type_length", C.c_int32), ("max_def_level", C.c_int32), ("codec", C.c_int32)]
 
 
+class dbg_native_column(C.Structure):  # include/dbgpu_scan.h
+    _fields_ = [("host", C.c_void_p), ("device", C.c_void_p), ("len", C.c_uint64), ("page_lengths", C.POINTER(C.c_uint64)),
+                ("page_rows", C.POINTER(C.c_uint64)), ("n_pages", C.c_uint32), ("nullable", C.c_int32)]
+
+
 # parquet physical types / codecs (dbgpu_scan.h)
 PQ_BOOLEAN, PQ_INT32, PQ_INT64, PQ_INT96, PQ_FLOAT, PQ_DOUBLE, PQ_BYTE_ARRAY, PQ_FIXED_LEN_BYTE_ARRAY = range(8)
 PQ_UNCOMPRESSED, PQ_SNAPPY, PQ_ZSTD, PQ_LZ4_RAW = 0, 1, 6, 7
@@ -93,5 +98,5 @@ DBG_COMM_ID_BYTES = 128
 EXPECTED_SIZES = {
     "dbg_datatype": 8, "dbg_column": 56, "dbg_out_column": 32, "dbg_agg_spec": 16,
     "dbg_pred_node": 64, "dbg_filter": 24, "dbg_agg_params": 48, "dbg_record_layout": 328, "dbg_exchange_stats": 32,
-    "dbg_parquet_chunk": 40,
+    "dbg_parquet_chunk": 40, "dbg_native_column": 48,
 }

@@ -861,6 +861,12 @@ struct dbg_scan_ctx {
     u64 zlit_cap = 0;
     ScanPage* hpages = nullptr;  // pinned staging of the page table (an async upload, not a pageable copy)
     u64 hpages_cap = 0;
+    // native (strawboat) pages: page descriptors and the host-built tables (Bitpacking blocks,
+    // String dictionary entries)
+    u8* npg = nullptr;
+    u64 npg_cap = 0;
+    u64* ntab = nullptr;
+    u64 ntab_cap = 0;
 };
 
 namespace {
@@ -921,7 +927,7 @@ int dbg_scan_create(dbg_scan_ctx** out, void* stream) {
 
 int dbg_scan_destroy(dbg_scan_ctx* c) {
     if (!c) return DBG_OK;
-    void* dev[] = {c->chunk, c->buf, c->pages, c->vbytes, c->idx, c->vstart, c->nwalk, c->sptr, c->bools, c->err};
+    void* dev[] = {c->chunk, c->buf, c->pages, c->vbytes, c->idx, c->vstart, c->nwalk, c->sptr, c->bools, c->err, c->npg, c->ntab};
     for (void* p : dev)
         if (p) hipFree(p);
     if (c->herr) hipHostFree(c->herr);
@@ -1117,6 +1123,551 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
             return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: String payload needs " + std::to_string(ctx->herr[1]) + " bytes");
     }
     if (e & SERR_NULL_IN_REQUIRED) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: NULL in a non-nullable column");
+    return DBG_OK;
+}
+
+}  // extern "C"
+
+// =============================================================================================
+// Fuse native (strawboat) pages -> HBM columns (dbg_native_decode; include/dbgpu_scan.h).
+//
+// The reader this replaces: NativeReader / column_iter_to_arrays (src/common/arrow/src/native/
+// read/*, compression/*), called by BlockReader::deserialize_native_chunks
+// (FUSE/io/read/block/block_reader_native_deserialize.rs).  The host walks each page's structure
+// — validity header, codec headers, a Dict's nested index block and entry list, Bitpacking block
+// headers — bounds-checking everything against the page; basic-codec sections (Lz4 / Zstd /
+// Snappy) are inflated by the Parquet path's kernels; one workgroup per page then decodes the
+// values (or a Dict's indices) and the validity, and a second pass resolves dictionaries.
+// Addresses in the page descriptors are tagged: bits 62-63 select the chunk, the inflate staging
+// buffer or the host-built table, the rest is the byte offset in it.
+// =============================================================================================
+namespace {
+
+enum { NC_NONE = 0, NC_LZ4 = 1, NC_ZSTD = 2, NC_SNAPPY = 3, NC_RLE = 10, NC_DICT = 11, NC_ONE = 12, NC_FREQ = 13, NC_BP = 14,
+       NC_DBP = 15, NC_PATAS = 16 };
+constexpr u64 NT_CHUNK = 0, NT_STAGE = 1ULL << 62, NT_TAB = 2ULL << 62, NT_MASK = (1ULL << 62) - 1;
+
+struct NatBlock {  // one integer block: the values, or a Dict's u32 indices
+    u64 src;       // tagged: raw little-endian values (None, or inflated), OneValue's value, Rle runs, Bitpacking data
+    u64 tab;       // tagged: Bitpacking / DeltaBitpacking block table, u64 per block: data offset from src | bits << 56
+    u32 nrec;      // Rle runs / Bitpacking blocks
+    u32 codec;     // NC_NONE (raw), NC_RLE, NC_ONE, NC_BP, NC_DBP
+};
+struct NatPage {
+    u64 row0;
+    u32 n;
+    u32 kind;      // 0 integer, 1 String
+    u32 tw;        // integer width (Dict indices: 4)
+    u32 dict;      // values through a dictionary: `blk` holds the indices
+    NatBlock blk;
+    u64 valid;     // tagged bitmap (LSB first), or ~0 (no validity: all valid)
+    u64 dsrc;      // Dict: integer values (tw each) / String entries in the table (tagged address, length)
+    u32 dn;        // Dict entries
+    u32 smode;     // String: 0 basic (offsets + bytes), 1 one value, 2 dict
+    u64 soffs;     // String basic: (n + 1) zero-based u64 offsets
+    u64 sdata;     // String basic: the bytes; one value: its bytes
+    u64 stotal;    // String basic: the bytes' length; one value: its length
+};
+// SERR_* bits the inflate kernels also set: SERR_MALFORMED, SERR_COUNT (a section's size)
+enum { NERR_MALFORMED = SERR_MALFORMED, NERR_NULL = SERR_NULL_IN_REQUIRED, NERR_RANGE = SERR_DICT_RANGE };
+
+struct NatBases {
+    const u8* b[3];
+    __device__ __forceinline__ const u8* at(u64 x) const { return b[x >> 62] + (x & NT_MASK); }
+};
+
+__device__ __forceinline__ u64 nat_ld(const u8* p, u32 w) {  // little-endian, unaligned
+    u64 v = 0;
+    for (u32 k = 0; k < w; ++k) v |= (u64)p[k] << (8 * k);
+    return v;
+}
+__device__ __forceinline__ u32 nat_ld32(const u8* p) { return (u32)nat_ld(p, 4); }
+
+#define NAT_NT 256
+// block-wide inclusive scan of u64 (NAT_NT threads); `tot` receives the block total
+__device__ __forceinline__ u64 nat_scan(u64 v, u64* wsum, u64& tot) {
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int d = 1; d < 64; d <<= 1) {
+        const u64 y = __shfl_up(v, d);
+        if ((int)lane >= d) v += y;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    u64 pre = 0;
+    tot = 0;
+    for (u32 w = 0; w < NAT_NT / 64; ++w) {
+        if (w < wave) pre += wsum[w];
+        tot += wsum[w];
+    }
+    return v + pre;
+}
+
+// Decode integer block b (n values of width tw) with every thread of the workgroup; put(i, v).
+template <typename PUT>
+__device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 tw, const NatBases& B, u64* err, PUT put) {
+    __shared__ u64 wsum[NAT_NT / 64];
+    __shared__ u64 rstart[NAT_NT + 1];
+    __shared__ u64 rval[NAT_NT];
+    const u8* src = B.at(b.src);
+    if (b.codec == NC_NONE) {
+        for (u32 i = threadIdx.x; i < n; i += NAT_NT) put(i, nat_ld(src + (u64)i * tw, tw));
+    } else if (b.codec == NC_ONE) {
+        const u64 v = nat_ld(src, tw);
+        for (u32 i = threadIdx.x; i < n; i += NAT_NT) put(i, v);
+    } else if (b.codec == NC_RLE) {  // runs [u32 count][value]: fixed-size records, NAT_NT runs per round
+        const u32 rs = 4 + tw;
+        u64 row = 0;
+        for (u32 r0 = 0; r0 < b.nrec && row < n; r0 += NAT_NT) {
+            const u32 r = r0 + threadIdx.x;
+            const u64 cnt = r < b.nrec ? nat_ld32(src + (u64)r * rs) : 0;
+            u64 tot;
+            const u64 incl = nat_scan(cnt, wsum, tot);
+            rstart[threadIdx.x] = row + incl - cnt;
+            rval[threadIdx.x] = r < b.nrec ? nat_ld(src + (u64)r * rs + 4, tw) : 0;
+            if (threadIdx.x == 0) rstart[NAT_NT] = row + tot;
+            __syncthreads();
+            const u64 end = row + tot < n ? row + tot : n;
+            for (u64 j = row + threadIdx.x; j < end; j += NAT_NT) {
+                u32 lo = 0, hi = NAT_NT - 1;  // the last run starting at or before j
+                while (lo < hi) {
+                    const u32 mid = (lo + hi + 1) >> 1;
+                    if (rstart[mid] <= j) lo = mid;
+                    else hi = mid - 1;
+                }
+                put((u32)j, rval[lo]);
+            }
+            row += tot;
+            __syncthreads();
+        }
+        if (row < n && threadIdx.x == 0) atomicOr((unsigned long long*)err, (unsigned long long)NERR_MALFORMED);
+    } else {  // Bitpacking / DeltaBitpacking: BitPacker4x blocks of 128 (simdcomp 4-lane layout)
+        const u64* tab = (const u64*)B.at(b.tab);
+        auto unpack = [&](u32 i) -> u64 {
+            const u32 blk = i >> 7;
+            if (blk >= b.nrec) return 0;
+            const u64 e = tab[blk];
+            const u32 bits = (u32)(e >> 56);
+            if (!bits) return 0;
+            const u8* d = src + (e & ((1ULL << 56) - 1));
+            const u32 j = i & 127, lane = j & 3, bp = (j >> 2) * bits, w = bp >> 5, sh = bp & 31;
+            u64 v = nat_ld32(d + 4 * (4 * w + lane)) >> sh;
+            if (sh + bits > 32) v |= (u64)nat_ld32(d + 4 * (4 * (w + 1) + lane)) << (32 - sh);
+            return v & (bits >= 32 ? 0xFFFFFFFFULL : ((1ULL << bits) - 1));
+        };
+        if (b.codec == NC_BP) {
+            for (u32 i = threadIdx.x; i < n; i += NAT_NT) put(i, unpack(i));
+        } else {  // deltas in value order, the page's first from 0: a page-wide wrapping prefix sum
+            u64 carry = 0;
+            for (u32 i0 = 0; i0 < n; i0 += NAT_NT) {
+                const u32 i = i0 + threadIdx.x;
+                const u64 dv = i < n ? unpack(i) : 0;
+                u64 tot;
+                const u64 incl = nat_scan(dv, wsum, tot);
+                if (i < n) put(i, (carry + incl) & 0xFFFFFFFFULL);
+                carry += tot;
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// pass 1: validity, integer values (or a Dict's indices), String sources and lengths
+__global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __restrict__ pages, NatBases B, u8* __restrict__ out,
+                                                            u8* __restrict__ vbytes, u32* __restrict__ idx, u64* __restrict__ sptr,
+                                                            u64* __restrict__ lens, u64* err) {
+    const NatPage pg = pages[blockIdx.x];
+    if (vbytes) {
+        const u8* vb = pg.valid == ~0ULL ? nullptr : B.at(pg.valid);
+        for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) vbytes[pg.row0 + i] = vb ? (vb[i >> 3] >> (i & 7)) & 1 : 1;
+    }
+    if (pg.dict) {
+        nat_block(pg.blk, pg.n, 4, B, err, [&](u32 i, u64 v) { idx[pg.row0 + i] = (u32)v; });
+        return;
+    }
+    if (pg.kind == 0) {
+        const u32 tw = pg.tw;
+        u8* o = out + pg.row0 * tw;
+        nat_block(pg.blk, pg.n, tw, B, err, [&](u32 i, u64 v) {
+            u8* d = o + (u64)i * tw;
+            if (tw == 8) *(u64*)d = v;
+            else if (tw == 4) *(u32*)d = (u32)v;
+            else if (tw == 2) *(uint16_t*)d = (uint16_t)v;
+            else *d = (u8)v;
+        });
+        return;
+    }
+    if (pg.smode == 1) {
+        const u64 a = (u64)B.at(pg.sdata);
+        for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) {
+            sptr[pg.row0 + i] = a;
+            lens[pg.row0 + i] = pg.stotal;
+        }
+        return;
+    }
+    const u8* offs = B.at(pg.soffs);
+    const u64 a = (u64)B.at(pg.sdata);
+    for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) {
+        const u64 s0 = nat_ld(offs + 8ULL * i, 8), s1 = nat_ld(offs + 8ULL * (i + 1), 8);
+        if (s1 < s0 || s1 > pg.stotal) {
+            atomicOr((unsigned long long*)err, (unsigned long long)NERR_MALFORMED);
+            sptr[pg.row0 + i] = a;
+            lens[pg.row0 + i] = 0;
+            continue;
+        }
+        sptr[pg.row0 + i] = a + s0;
+        lens[pg.row0 + i] = s1 - s0;
+    }
+}
+
+// pass 2: dictionaries (indices from pass 1, range-checked)
+__global__ void __launch_bounds__(NAT_NT) nat_dict_kernel(const NatPage* __restrict__ pages, NatBases B, u8* __restrict__ out,
+                                                          const u32* __restrict__ idx, u64* __restrict__ sptr, u64* __restrict__ lens,
+                                                          u64* err) {
+    const NatPage pg = pages[blockIdx.x];
+    if (!pg.dict) return;
+    const u8* d = B.at(pg.dsrc);
+    for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) {
+        u32 k = idx[pg.row0 + i];
+        if (k >= pg.dn) {
+            atomicOr((unsigned long long*)err, (unsigned long long)NERR_RANGE);
+            k = 0;
+        }
+        if (pg.kind == 0) {
+            const u32 tw = pg.tw;
+            u8* o = out + (pg.row0 + i) * tw;
+            const u64 v = pg.dn ? nat_ld(d + (u64)k * tw, tw) : 0;
+            for (u32 j = 0; j < tw; ++j) o[j] = (u8)(v >> (8 * j));
+        } else {
+            const u64* e = (const u64*)d + 2 * (u64)k;
+            sptr[pg.row0 + i] = pg.dn ? (u64)B.at(e[0]) : 0;
+            lens[pg.row0 + i] = pg.dn ? e[1] : 0;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) nat_null_check_kernel(const u8* __restrict__ vb, u64 n, u64* err) {
+    for (u64 i = blockIdx.x * 256ULL + threadIdx.x; i < n; i += (u64)gridDim.x * 256)
+        if (!vb[i]) {
+            atomicOr((unsigned long long*)err, (unsigned long long)NERR_NULL);
+            return;
+        }
+}
+
+// ---- host: page structure ----
+struct NatParse {
+    const u8* h;  // column bytes (host)
+    std::vector<ScanPage> jobs[4];  // inflate jobs per basic codec (1 Lz4, 2 Zstd, 3 Snappy)
+    u64 stage = 0;                  // staging bytes
+    std::vector<u64> tab;           // host-built table (u64 words)
+    std::string err;
+    u32 rd32(u64 p) const { u32 v; memcpy(&v, h + p, 4); return v; }
+    u64 rd64(u64 p) const { u64 v; memcpy(&v, h + p, 8); return v; }
+    bool fail(const std::string& m) {
+        if (err.empty()) err = m;
+        return false;
+    }
+    // a basic-codec section [payload, payload + comp) of `uncomp` bytes -> tagged address of its bytes
+    bool basic(u32 codec, u64 payload, u32 comp, u32 uncomp, u64& addr) {
+        if (codec == NC_NONE) {
+            if (comp != uncomp) return fail("None section: compressed and uncompressed sizes differ");
+            addr = NT_CHUNK | payload;
+            return true;
+        }
+        ScanPage j;
+        memset(&j, 0, sizeof(j));
+        j.src = payload;
+        j.dst = stage;
+        j.comp = comp;
+        j.uncomp = uncomp;
+        j.compressed = 1;
+        jobs[codec].push_back(j);
+        addr = NT_STAGE | stage;
+        stage += ((u64)uncomp + 15) & ~15ULL;
+        return true;
+    }
+    // one integer block at p (inside [p, end)) of n values of width tw -> b; q = its end
+    bool int_block(u64 p, u64 end, u32 n, u32 tw, bool allow_dict, NatBlock& b, NatPage* pg, u64& q) {
+        if (p + 9 > end) return fail("integer block header past the page");
+        const u32 codec = h[p], comp = rd32(p + 1), uncomp = rd32(p + 5);
+        const u64 pl = p + 9;
+        if (pl + comp > end) return fail("integer block past the page");
+        q = pl + comp;
+        memset(&b, 0, sizeof(b));
+        switch (codec) {
+            case NC_NONE: case NC_LZ4: case NC_ZSTD: case NC_SNAPPY:
+                if ((u64)uncomp != (u64)n * tw) return fail("integer block: uncompressed size != rows x width");
+                b.codec = NC_NONE;
+                return basic(codec, pl, comp, uncomp, b.src);
+            case NC_ONE:
+                if (comp < tw && n) return fail("OneValue block too short");
+                b.codec = NC_ONE;
+                b.src = NT_CHUNK | pl;
+                return true;
+            case NC_RLE: {
+                const u32 rs = 4 + tw;
+                if (comp % rs) return fail("Rle block: not whole runs");
+                b.codec = NC_RLE;
+                b.src = NT_CHUNK | pl;
+                b.nrec = comp / rs;
+                u64 tot = 0;
+                for (u32 r = 0; r < b.nrec; ++r) tot += rd32(pl + (u64)r * rs);
+                if (tot < n) return fail("Rle runs cover fewer rows than the page");
+                return true;
+            }
+            case NC_BP: case NC_DBP: {
+                if (tw != 4) return fail("Bitpacking of a non-4-byte type");
+                b.codec = codec;
+                b.src = NT_CHUNK | pl;
+                b.nrec = (n + 127) / 128;
+                b.tab = NT_TAB | (8 * (u64)tab.size());
+                u64 x = pl;
+                for (u32 k = 0; k < b.nrec; ++k) {
+                    if (x + 1 > q) return fail("Bitpacking block header past the block");
+                    const u32 bits = h[x];
+                    if (bits > 32 || x + 1 + 16ULL * bits > q) return fail("Bitpacking block past the block");
+                    tab.push_back(((x + 1) - pl) | ((u64)bits << 56));
+                    x += 1 + 16ULL * bits;
+                }
+                return true;
+            }
+            case NC_DICT: {
+                if (!allow_dict || !pg) return fail("Dict inside Dict");
+                u64 r;
+                NatBlock ib;
+                if (!int_block(pl, q, n, 4, false, ib, nullptr, r)) return false;
+                if (r + 4 > q) return fail("Dict entry count past the block");
+                const u32 cnt = rd32(r);
+                if (r + 4 + (u64)cnt * tw > q) return fail("Dict values past the block");
+                pg->dict = 1;
+                pg->dsrc = NT_CHUNK | (r + 4);
+                pg->dn = cnt;
+                b = ib;
+                return true;
+            }
+            case NC_FREQ: err = "unsupported: Freq (roaring exceptions) is decoded on the CPU"; return false;
+            default: err = "unsupported: native codec " + std::to_string(codec) + " is decoded on the CPU"; return false;
+        }
+    }
+    bool str_block(u64 p, u64 end, u32 n, NatPage& pg, u64& q) {
+        if (p + 9 > end) return fail("String block header past the page");
+        const u32 codec = h[p], comp = rd32(p + 1), uncomp = rd32(p + 5);
+        const u64 pl = p + 9;
+        if (pl + comp > end) return fail("String block past the page");
+        q = pl + comp;
+        switch (codec) {
+            case NC_NONE: case NC_LZ4: case NC_ZSTD: case NC_SNAPPY: {  // offsets block, then bytes block
+                if ((u64)uncomp != 8ULL * (n + 1)) return fail("String offsets block: size != (rows + 1) x 8");
+                pg.smode = 0;
+                if (!basic(codec, pl, comp, uncomp, pg.soffs)) return false;
+                const u64 p2 = q;
+                if (p2 + 9 > end) return fail("String bytes header past the page");
+                const u32 c2 = h[p2], comp2 = rd32(p2 + 1), uncomp2 = rd32(p2 + 5);
+                if (c2 > NC_SNAPPY) return fail("String bytes block: not a basic codec");
+                if (p2 + 9 + comp2 > end) return fail("String bytes block past the page");
+                q = p2 + 9 + comp2;
+                pg.stotal = uncomp2;
+                return basic(c2, p2 + 9, comp2, uncomp2, pg.sdata);
+            }
+            case NC_ONE: {
+                if (comp < 4) return fail("OneValue block too short");
+                const u32 len = rd32(pl);
+                if (4ULL + len > comp) return fail("OneValue value past the block");
+                pg.smode = 1;
+                pg.sdata = NT_CHUNK | (pl + 4);
+                pg.stotal = len;
+                return true;
+            }
+            case NC_DICT: {
+                u64 r;
+                NatBlock ib;
+                if (!int_block(pl, q, n, 4, false, ib, nullptr, r)) return false;
+                if (r + 4 > q) return fail("Dict entry count past the block");
+                const u32 cnt = rd32(r);
+                r += 4;
+                pg.smode = 2;
+                pg.dict = 1;
+                pg.blk = ib;
+                pg.dsrc = NT_TAB | (8 * (u64)tab.size());
+                pg.dn = cnt;
+                for (u32 k = 0; k < cnt; ++k) {
+                    if (r + 8 > q) return fail("Dict entry past the block");
+                    const u64 len = rd64(r);
+                    if (len > q - r - 8) return fail("Dict entry bytes past the block");
+                    tab.push_back(NT_CHUNK | (r + 8));
+                    tab.push_back(len);
+                    r += 8 + len;
+                }
+                return true;
+            }
+            case NC_FREQ: err = "unsupported: Freq (roaring exceptions) is decoded on the CPU"; return false;
+            default: err = "unsupported: native String codec " + std::to_string(codec) + " is decoded on the CPU"; return false;
+        }
+    }
+};
+
+bool nat_int_target(int t, u32& w) {
+    switch (t) {
+        case DBG_INT8: case DBG_UINT8: w = 1; return true;
+        case DBG_INT16: case DBG_UINT16: w = 2; return true;
+        case DBG_INT32: case DBG_UINT32: case DBG_DATE: w = 4; return true;
+        case DBG_INT64: case DBG_UINT64: case DBG_TIMESTAMP: w = 8; return true;
+        default: return false;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datatype target, dbg_out_column* out, uint64_t max_rows,
+                      uint64_t max_string_bytes, uint64_t* rows_out, uint64_t* string_bytes) {
+    if (!ctx || !col || !col->host || !out || !rows_out || (col->n_pages && (!col->page_lengths || !col->page_rows)))
+        return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: null argument");
+    *rows_out = 0;
+    if (string_bytes) *string_bytes = 0;
+    const bool is_str = target.type == DBG_STRING;
+    u32 tw = 0;
+    if (!is_str && !nat_int_target(target.type, tw))
+        return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_native: target type " + std::to_string(target.type) + " is decoded on the CPU");
+    NatParse P;
+    P.h = col->host;
+    std::vector<NatPage> pages(col->n_pages);
+    u64 pos = 0, row = 0;
+    for (u32 k = 0; k < col->n_pages; ++k) {
+        NatPage& pg = pages[k];
+        memset(&pg, 0, sizeof(pg));
+        const u64 len = col->page_lengths[k], n = col->page_rows[k];
+        if (pos + len > col->len || n > 0xFFFFFFFFULL) return abi_fail(DBG_ERR_INVALID, "dbg_native: page " + std::to_string(k) + " past the column");
+        const u64 end = pos + len;
+        pg.row0 = row;
+        pg.n = (u32)n;
+        pg.kind = is_str ? 1 : 0;
+        pg.tw = tw;
+        pg.valid = ~0ULL;
+        u64 p = pos;
+        if (col->nullable) {  // write_validity: u32 length + one bit-packed hybrid run
+            if (p + 4 > end) return abi_fail(DBG_ERR_INVALID, "dbg_native: validity header past the page");
+            const u32 vl = P.rd32(p);
+            p += 4;
+            if (vl) {
+                if (p + vl > end) return abi_fail(DBG_ERR_INVALID, "dbg_native: validity past the page");
+                u64 hdr = 0, q = p;
+                for (u32 sh = 0;; sh += 7) {
+                    if (q >= p + vl || sh > 35) return abi_fail(DBG_ERR_INVALID, "dbg_native: validity header");
+                    const u32 c = col->host[q++];
+                    hdr |= (u64)(c & 0x7F) << sh;
+                    if (!(c & 0x80)) break;
+                }
+                if (!(hdr & 1)) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_native: RLE validity run (read_validity reads bit-packed runs only)");
+                if ((hdr >> 1) * 8 < n || q + (n + 7) / 8 > p + vl) return abi_fail(DBG_ERR_INVALID, "dbg_native: validity shorter than the page");
+                pg.valid = NT_CHUNK | q;
+                p += vl;
+            }
+        }
+        u64 q = 0;
+        const bool ok = is_str ? P.str_block(p, end, (u32)n, pg, q) : P.int_block(p, end, (u32)n, tw, true, pg.blk, &pg, q);
+        if (!ok) {
+            const bool unsup = P.err.rfind("unsupported", 0) == 0;
+            return abi_fail(unsup ? DBG_ERR_UNSUPPORTED : DBG_ERR_INVALID, "dbg_native: page " + std::to_string(k) + ": " + P.err);
+        }
+        row += n;
+        pos = end;
+    }
+    *rows_out = row;
+    if (row > max_rows) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: " + std::to_string(row) + " rows exceed max_rows");
+    if (!is_str && !out->data && row) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: null data buffer");
+    if (is_str && !out->offsets) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: String output needs offsets");
+    if (target.nullable && col->nullable && !out->validity && row) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: null validity buffer");
+    hipStream_t s = ctx->stream;
+    const bool upload = col->device == nullptr;
+    if (upload) {
+        SCAN_RET(ensure(&ctx->chunk, &ctx->chunk_cap, col->len + 16));
+        SCAN_HIP(hipMemcpyAsync(ctx->chunk, col->host, col->len, hipMemcpyHostToDevice, s));
+    }
+    SCAN_RET(ensure(&ctx->buf, &ctx->buf_cap, P.stage + 16));
+    SCAN_RET(ensure(&ctx->ntab, &ctx->ntab_cap, P.tab.size() + 1));
+    SCAN_RET(ensure(&ctx->npg, &ctx->npg_cap, pages.size() * sizeof(NatPage) + 16));
+    SCAN_RET(ensure(&ctx->vbytes, &ctx->vbytes_cap, row + 1));
+    SCAN_RET(ensure(&ctx->idx, &ctx->idx_cap, row + 1));
+    u64 njobs = 0;
+    for (int c = 1; c <= 3; ++c) njobs += P.jobs[c].size();
+    SCAN_RET(ensure(&ctx->pages, &ctx->pages_cap, njobs + 1));
+    if (is_str) SCAN_RET(ensure(&ctx->sptr, &ctx->sptr_cap, row + 1));
+    if (!P.jobs[NC_ZSTD].empty()) SCAN_RET(ensure(&ctx->zlit, &ctx->zlit_cap, (u64)P.jobs[NC_ZSTD].size() * ZS_MAX_BLOCK + 16));
+    // the small tables are copied synchronously from pageable memory (staged by the runtime)
+    if (!pages.empty()) SCAN_HIP(hipMemcpyAsync(ctx->npg, pages.data(), pages.size() * sizeof(NatPage), hipMemcpyHostToDevice, s));
+    if (!P.tab.empty()) SCAN_HIP(hipMemcpyAsync(ctx->ntab, P.tab.data(), P.tab.size() * 8, hipMemcpyHostToDevice, s));
+    SCAN_HIP(hipMemsetAsync(ctx->err, 0, 16, s));
+    const u8* chunk = upload ? ctx->chunk : col->device;
+    // basic-codec sections: the Parquet path's inflate kernels over a job list per codec
+    {
+        u64 off = 0;
+        std::vector<ScanPage> all;
+        for (int c = 1; c <= 3; ++c) all.insert(all.end(), P.jobs[c].begin(), P.jobs[c].end());
+        if (!all.empty()) SCAN_HIP(hipMemcpyAsync(ctx->pages, all.data(), all.size() * sizeof(ScanPage), hipMemcpyHostToDevice, s));
+        for (int c = 1; c <= 3; ++c) {
+            const u64 nj = P.jobs[c].size();
+            if (!nj) continue;
+            ScanArgs a;
+            memset(&a, 0, sizeof(a));
+            a.chunk = chunk;
+            a.buf = ctx->buf;
+            a.pages = ctx->pages + off;
+            a.n_pages = (u32)nj;
+            a.err = ctx->err;
+            void* ps = prof_scope_begin("nat_inflate", s);
+            if (c == NC_LZ4) hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_LZ4_RAW>, dim3((u32)nj), dim3(64), 0, s, a);
+            else if (c == NC_SNAPPY) hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_SNAPPY>, dim3((u32)nj), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL(pq_zstd_kernel, dim3((u32)nj), dim3(64), 0, s, a, ctx->zlit);
+            prof_scope_end(ps);
+            SCAN_HIP(hipGetLastError());
+            off += nj;
+        }
+    }
+    NatBases B;
+    B.b[0] = chunk;
+    B.b[1] = ctx->buf;
+    B.b[2] = (const u8*)ctx->ntab;
+    const bool want_vb = col->nullable != 0;
+    if (!pages.empty()) {
+        void* ps = prof_scope_begin("nat_decode", s);
+        hipLaunchKernelGGL(nat_decode_kernel, dim3((u32)pages.size()), dim3(NAT_NT), 0, s, (const NatPage*)ctx->npg, B, (u8*)out->data,
+                           want_vb ? ctx->vbytes : nullptr, ctx->idx, ctx->sptr, out->offsets, ctx->err);
+        hipLaunchKernelGGL(nat_dict_kernel, dim3((u32)pages.size()), dim3(NAT_NT), 0, s, (const NatPage*)ctx->npg, B, (u8*)out->data,
+                           ctx->idx, ctx->sptr, out->offsets, ctx->err);
+        prof_scope_end(ps);
+        SCAN_HIP(hipGetLastError());
+    }
+    if (is_str) {  // lengths -> offsets, then the payload (the Parquet path's gather)
+        if (row) launch_exclusive_scan(s, out->offsets, row, out->offsets + row);
+        else SCAN_HIP(hipMemsetAsync(out->offsets, 0, 8, s));
+        SCAN_HIP(hipMemcpyAsync(ctx->err + 1, out->offsets + row, 8, hipMemcpyDeviceToDevice, s));
+        if (row && out->data)
+            hipLaunchKernelGGL(pq_strings_kernel, dim3((u32)((row + 255) / 256)), dim3(256), 0, s, ctx->sptr, out->offsets, row,
+                               (u8*)out->data, max_string_bytes);
+        SCAN_HIP(hipGetLastError());
+    }
+    if (target.nullable && row && out->validity) {
+        if (want_vb) launch_pack_bits(s, ctx->vbytes, row, out->validity);
+        else SCAN_HIP(hipMemsetAsync(out->validity, 0xFF, (row + 7) / 8, s));
+    }
+    if (!target.nullable && want_vb && row) {
+        hipLaunchKernelGGL(nat_null_check_kernel, dim3((u32)std::min<u64>(1024, (row + 255) / 256)), dim3(256), 0, s, ctx->vbytes, row,
+                           ctx->err);
+        SCAN_HIP(hipGetLastError());
+    }
+    SCAN_HIP(hipMemcpyAsync(ctx->herr, ctx->err, 16, hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipStreamSynchronize(s));
+    const u64 e = ctx->herr[0];
+    if (e & (NERR_MALFORMED | SERR_COUNT)) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: malformed page data");
+    if (e & NERR_RANGE) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: dictionary index out of range");
+    if (is_str) {
+        if (string_bytes) *string_bytes = ctx->herr[1];
+        if (ctx->herr[1] > max_string_bytes)
+            return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: String payload needs " + std::to_string(ctx->herr[1]) + " bytes");
+    }
+    if (e & NERR_NULL) return abi_fail(DBG_ERR_INVALID, "dbg_native_decode: NULL in a non-nullable column");
     return DBG_OK;
 }
 

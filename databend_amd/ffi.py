@@ -27,6 +27,7 @@ EXPORTED = [
     "dbg_agg_payload_counts", "dbg_agg_payload_export", "dbg_agg_payload_import", "dbg_agg_exchange_payload",
     "dbg_payload_exchange_plan", "dbg_merge_exchange_plan",
     "dbg_scan_create", "dbg_scan_destroy", "dbg_parquet_chunk_rows", "dbg_parquet_decode",
+    "dbg_native_decode",
 ]
 
 
@@ -123,6 +124,8 @@ def lib():
         L.dbg_parquet_chunk_rows.argtypes = [P(abi.dbg_parquet_chunk), P(U64), P(C.c_uint32)]
         L.dbg_parquet_decode.argtypes = [VP, P(abi.dbg_parquet_chunk), abi.dbg_datatype, P(abi.dbg_out_column), U64, U64, P(U64),
                                          P(U64)]
+        L.dbg_native_decode.argtypes = [VP, P(abi.dbg_native_column), abi.dbg_datatype, P(abi.dbg_out_column), U64, U64, P(U64),
+                                        P(U64)]
         L.dbg_datagen.argtypes = [C.c_int, U64, U64, U64, P(VP), C.c_int, VP, VP]
         _LIB = L
     return _LIB

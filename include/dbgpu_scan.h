@@ -68,6 +68,30 @@ int dbg_parquet_chunk_rows(const dbg_parquet_chunk* chunk, uint64_t* rows, uint3
 int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_datatype target, dbg_out_column* out,
                        uint64_t max_rows, uint64_t max_string_bytes, uint64_t* rows, uint64_t* string_bytes);
 
+/* ---- Fuse native (strawboat) column pages -> HBM columns ----
+ * Replaces, for one leaf column of a block of a `storage_format = 'native'` table,
+ * BlockReader::deserialize_native_chunks -> NativeReader / column_iter_to_arrays
+ * (FUSE/io/read/block/block_reader_native_deserialize.rs:23-26, 53-...; the pages' format:
+ * src/common/arrow/src/native/{write,read,compression}).  The column's pages are the bytes
+ * [ColumnMeta::offset, + total_len) with PageMeta {length, num_values} per page (mod.rs:27-72).
+ * Page structure (validity, codec headers, Dict / Bitpacking tables) is parsed on the host from
+ * `host`; values are decoded on the device.  Codecs: None / Lz4 / Zstd / Snappy, Rle, Dict,
+ * OneValue, Bitpacking, DeltaBitpacking for integers (Int8..UInt64, Date, Timestamp); None / Lz4 /
+ * Zstd / Snappy, OneValue, Dict for String.  Freq (roaring exceptions), Patas, floats, Booleans,
+ * Decimals and nested columns return DBG_ERR_UNSUPPORTED (the CPU reader).  Outputs as
+ * dbg_parquet_decode. */
+typedef struct dbg_native_column {
+    const uint8_t* host;          /* the column's pages in host memory */
+    const uint8_t* device;        /* the same bytes resident in HBM, or NULL: the call uploads them */
+    uint64_t len;
+    const uint64_t* page_lengths; /* PageMeta.length, n_pages entries */
+    const uint64_t* page_rows;    /* PageMeta.num_values */
+    uint32_t n_pages;
+    int32_t nullable;             /* the field is Optional: every page starts with its validity */
+} dbg_native_column;
+int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datatype target, dbg_out_column* out,
+                      uint64_t max_rows, uint64_t max_string_bytes, uint64_t* rows, uint64_t* string_bytes);
+
 #ifdef __cplusplus
 }
 #endif
