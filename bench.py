@@ -556,7 +556,102 @@ def measure_scan(steps: int, rows: int = 1 << 26) -> dict:
                              "kernel_frac": (alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS) if kms else None,
                              "algorithmic_bytes": alg, "bit_exact": True}
         del dchunk, out_t
+    res.update(measure_native(dec, adv, steps))
     dec.close()
+    return res
+
+
+def native_pages(v, codec: str, page_rows: int = 131072):
+    """The same column as Fuse's native format writes it (NativeWriter, 131072-row pages,
+    non-nullable): 'dict_rle' is what choose_compressor picks for this column (Dict, its u32
+    indices Rle-encoded: integer/dict.rs, rle.rs), 'lz4' / 'none' the basic codecs.  Synthetic
+    bytes built with numpy here (bench input, not the oracle)."""
+    import struct
+    import numpy as np
+    import pyarrow as pa
+    out, lens, rows = bytearray(), [], []
+    w = v.dtype.itemsize
+    for s0 in range(0, len(v), page_rows):
+        pv = v[s0:s0 + page_rows]
+        n = len(pv)
+        if codec == "dict_rle":
+            u, first, inv = np.unique(pv, return_index=True, return_inverse=True)
+            order = np.argsort(first, kind="stable")
+            rank = np.empty(len(u), np.uint32)
+            rank[order] = np.arange(len(u), dtype=np.uint32)
+            idx = rank[inv.reshape(-1)]
+            starts = np.concatenate([[0], np.flatnonzero(np.diff(idx)) + 1])
+            runs = np.empty(len(starts), dtype=[("c", "<u4"), ("v", "<u4")])
+            runs["c"] = np.diff(np.concatenate([starts, [n]]))
+            runs["v"] = idx[starts]
+            rb = runs.tobytes()
+            inner = struct.pack("<BII", 10, len(rb), 4 * n) + rb
+            payload = inner + struct.pack("<I", len(u)) + u[order].astype(v.dtype.newbyteorder("<")).tobytes()
+            page = struct.pack("<BII", 11, len(payload), w * n) + payload
+        else:
+            raw = pv.astype(v.dtype.newbyteorder("<")).tobytes()
+            body = pa.Codec("lz4_raw").compress(raw, asbytes=True) if codec == "lz4" else raw
+            page = struct.pack("<BII", 1 if codec == "lz4" else 0, len(body), len(raw)) + body
+        out += page
+        lens.append(len(page))
+        rows.append(n)
+    return bytes(out), lens, rows
+
+
+def measure_native(dec, adv, steps: int) -> dict:
+    """Native (strawboat) pages of the same column -> HBM: dbg_native_decode per column, bytes
+    resident in HBM, timed like the Parquet legs (host page walk + device decode + read-back)."""
+    import numpy as np
+    import torch
+    import ctypes as C
+    from databend_amd import abi
+    from databend_amd import column as col
+    from databend_amd import ffi
+    from databend_amd.ffi import check, lib
+    rows = len(adv)
+    res = {}
+    for codec in ("dict_rle", "lz4", "none"):
+        buf, lens, prow = native_pages(adv, codec)
+        dbuf = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8).copy()).cuda()
+        hbuf = C.create_string_buffer(buf, len(buf))
+        hl = (C.c_uint64 * len(lens))(*lens)
+        hr = (C.c_uint64 * len(prow))(*prow)
+        c = abi.dbg_native_column()
+        c.host = C.cast(hbuf, C.c_void_p)
+        c.device = dbuf.data_ptr()
+        c.len = len(buf)
+        c.page_lengths = hl
+        c.page_rows = hr
+        c.n_pages = len(lens)
+        c.nullable = 0
+        out_t = torch.empty(rows * 2, dtype=torch.uint8, device="cuda")
+        o = abi.dbg_out_column()
+        o.data = out_t.data_ptr()
+        nr, sb = C.c_uint64(), C.c_uint64()
+        call = lambda: check(lib().dbg_native_decode(dec.h, C.byref(c), col.Int16.to_abi(), C.byref(o), rows, 0, C.byref(nr),
+                                                    C.byref(sb)))
+        call()
+        assert nr.value == rows and torch.equal(out_t.view(torch.int16), torch.from_numpy(adv).cuda())
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ffi.prof_reset()
+        ffi.prof_enable(True)
+        ev0.record()
+        for _ in range(steps):
+            call()
+        ev1.record()
+        torch.cuda.synchronize()
+        ffi.prof_enable(False)
+        kern = ffi.prof_read()
+        ms = ev0.elapsed_time(ev1) / steps
+        kms = sum(v[0] for k, v in kern.items() if k in ("nat_decode", "nat_inflate")) / steps
+        alg = len(buf) + rows * 2
+        res["native_" + codec] = {"column_bytes": len(buf), "pages": len(lens), "ms_per_column": ms,
+                                  "rows_per_s": rows / (ms * 1e-3), "achieved_gbs": alg / (ms * 1e-3) / 1e9,
+                                  "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel_ms_per_column": kms,
+                                  "kernel_frac": (alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS) if kms else None,
+                                  "algorithmic_bytes": alg, "bit_exact": True}
+        del dbuf, out_t
     return res
 
 

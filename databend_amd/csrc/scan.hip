@@ -1176,14 +1176,34 @@ struct NatBases {
     __device__ __forceinline__ const u8* at(u64 x) const { return b[x >> 62] + (x & NT_MASK); }
 };
 
-__device__ __forceinline__ u64 nat_ld(const u8* p, u32 w) {  // little-endian, unaligned
-    u64 v = 0;
-    for (u32 k = 0; k < w; ++k) v |= (u64)p[k] << (8 * k);
-    return v;
+__device__ __forceinline__ u64 nat_ld(const u8* p, u32 w) {  // little-endian; gfx950 global loads take byte addresses
+    if (w == 8) {
+        u64 x;
+        __builtin_memcpy(&x, p, 8);
+        return x;
+    }
+    if (w == 4) {
+        u32 x;
+        __builtin_memcpy(&x, p, 4);
+        return x;
+    }
+    if (w == 2) {
+        uint16_t x;
+        __builtin_memcpy(&x, p, 2);
+        return x;
+    }
+    return *p;
 }
 __device__ __forceinline__ u32 nat_ld32(const u8* p) { return (u32)nat_ld(p, 4); }
+__device__ __forceinline__ void nat_st(u8* d, u64 v, u32 tw) {  // d is tw-aligned (row * tw in a torch buffer)
+    if (tw == 8) *(u64*)d = v;
+    else if (tw == 4) *(u32*)d = (u32)v;
+    else if (tw == 2) *(uint16_t*)d = (uint16_t)v;
+    else *d = (u8)v;
+}
 
 #define NAT_NT 256
+#define NAT_LDS_DICT 2048  // dictionary entries staged in LDS (16 KB); larger ones are read through the caches
 // block-wide inclusive scan of u64 (NAT_NT threads); `tot` receives the block total
 __device__ __forceinline__ u64 nat_scan(u64 v, u64* wsum, u64& tot) {
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1203,44 +1223,83 @@ __device__ __forceinline__ u64 nat_scan(u64 v, u64* wsum, u64& tot) {
     return v + pre;
 }
 
-// Decode integer block b (n values of width tw) with every thread of the workgroup; put(i, v).
-template <typename PUT>
-__device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 tw, const NatBases& B, u64* err, PUT put) {
+// Decode rows [lo, hi) of integer block b (n values of width tw) with every thread of the
+// workgroup, 8 consecutive rows per lane: put8(i0, cnt, v) receives rows i0 .. i0 + cnt - 1
+// (cnt = 8 and i0 a multiple of 8 except at a slice's or an Rle round's edges).  lo is a multiple
+// of 8.  Rle walks all runs (few) and expands only the slice; DeltaBitpacking needs the page's
+// prefix sum, so its page is one slice (lo = 0, hi = n) and puts one row at a time.
+template <typename PUT8>
+__device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 hi, u32 tw, const NatBases& B, u64* err, PUT8 put8) {
     __shared__ u64 wsum[NAT_NT / 64];
-    __shared__ u64 rstart[NAT_NT + 1];
+    __shared__ u64 rstart[NAT_NT];
     __shared__ u64 rval[NAT_NT];
     const u8* src = B.at(b.src);
     if (b.codec == NC_NONE) {
-        for (u32 i = threadIdx.x; i < n; i += NAT_NT) put(i, nat_ld(src + (u64)i * tw, tw));
+        for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) {
+            const u32 cnt = min(8u, hi - i0);
+            const u8* p = src + (u64)i0 * tw;
+            u64 v[8];
+            if (cnt == 8 && tw == 1) {
+                u64 x;
+                __builtin_memcpy(&x, p, 8);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = (x >> (8 * k)) & 0xFF;
+            } else if (cnt == 8 && tw == 2) {
+                uint16_t x[8];
+                __builtin_memcpy(x, p, 16);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = x[k];
+            } else if (cnt == 8 && tw == 4) {
+                u32 x[8];
+                __builtin_memcpy(x, p, 32);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = x[k];
+            } else if (cnt == 8) {
+                __builtin_memcpy(v, p, 64);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = (u32)k < cnt ? nat_ld(p + (u64)k * tw, tw) : 0;
+            }
+            put8(i0, cnt, v);
+        }
     } else if (b.codec == NC_ONE) {
-        const u64 v = nat_ld(src, tw);
-        for (u32 i = threadIdx.x; i < n; i += NAT_NT) put(i, v);
+        const u64 x = nat_ld(src, tw);
+        u64 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = x;
+        for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) put8(i0, min(8u, hi - i0), v);
     } else if (b.codec == NC_RLE) {  // runs [u32 count][value]: fixed-size records, NAT_NT runs per round
         const u32 rs = 4 + tw;
         u64 row = 0;
-        for (u32 r0 = 0; r0 < b.nrec && row < n; r0 += NAT_NT) {
+        for (u32 r0 = 0; r0 < b.nrec && row < hi; r0 += NAT_NT) {
             const u32 r = r0 + threadIdx.x;
             const u64 cnt = r < b.nrec ? nat_ld32(src + (u64)r * rs) : 0;
             u64 tot;
             const u64 incl = nat_scan(cnt, wsum, tot);
             rstart[threadIdx.x] = row + incl - cnt;
             rval[threadIdx.x] = r < b.nrec ? nat_ld(src + (u64)r * rs + 4, tw) : 0;
-            if (threadIdx.x == 0) rstart[NAT_NT] = row + tot;
             __syncthreads();
-            const u64 end = row + tot < n ? row + tot : n;
-            for (u64 j = row + threadIdx.x; j < end; j += NAT_NT) {
-                u32 lo = 0, hi = NAT_NT - 1;  // the last run starting at or before j
-                while (lo < hi) {
-                    const u32 mid = (lo + hi + 1) >> 1;
-                    if (rstart[mid] <= j) lo = mid;
-                    else hi = mid - 1;
+            const u64 a = row > lo ? row : lo, e = row + tot < hi ? row + tot : hi;
+            for (u64 g = (a & ~7ULL) + 8 * threadIdx.x; g < e; g += 8 * NAT_NT) {
+                const u64 j0 = g > a ? g : a, j1 = g + 8 < e ? g + 8 : e;
+                u32 l = 0, h = NAT_NT - 1;  // the last run starting at or before j0
+                while (l < h) {
+                    const u32 mid = (l + h + 1) >> 1;
+                    if (rstart[mid] <= j0) l = mid;
+                    else h = mid - 1;
                 }
-                put((u32)j, rval[lo]);
+                u64 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    while (l + 1 < NAT_NT && rstart[l + 1] <= j0 + k) ++l;
+                    v[k] = rval[l];
+                }
+                put8((u32)j0, (u32)(j1 - j0), v);
             }
             row += tot;
             __syncthreads();
         }
-        if (row < n && threadIdx.x == 0) atomicOr((unsigned long long*)err, (unsigned long long)NERR_MALFORMED);
+        if (row < hi && threadIdx.x == 0) atomicOr((unsigned long long*)err, (unsigned long long)NERR_MALFORMED);
     } else {  // Bitpacking / DeltaBitpacking: BitPacker4x blocks of 128 (simdcomp 4-lane layout)
         const u64* tab = (const u64*)B.at(b.tab);
         auto unpack = [&](u32 i) -> u64 {
@@ -1256,7 +1315,12 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 tw, cons
             return v & (bits >= 32 ? 0xFFFFFFFFULL : ((1ULL << bits) - 1));
         };
         if (b.codec == NC_BP) {
-            for (u32 i = threadIdx.x; i < n; i += NAT_NT) put(i, unpack(i));
+            for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) {
+                u64 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = unpack(i0 + k);
+                put8(i0, min(8u, hi - i0), v);
+            }
         } else {  // deltas in value order, the page's first from 0: a page-wide wrapping prefix sum
             u64 carry = 0;
             for (u32 i0 = 0; i0 < n; i0 += NAT_NT) {
@@ -1264,7 +1328,10 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 tw, cons
                 const u64 dv = i < n ? unpack(i) : 0;
                 u64 tot;
                 const u64 incl = nat_scan(dv, wsum, tot);
-                if (i < n) put(i, (carry + incl) & 0xFFFFFFFFULL);
+                u64 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = (carry + incl) & 0xFFFFFFFFULL;
+                if (i < n) put8(i, 1, v);
                 carry += tot;
                 __syncthreads();
             }
@@ -1272,34 +1339,120 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 tw, cons
     }
 }
 
-// pass 1: validity, integer values (or a Dict's indices), String sources and lengths
-__global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __restrict__ pages, NatBases B, u8* __restrict__ out,
-                                                            u8* __restrict__ vbytes, u32* __restrict__ idx, u64* __restrict__ sptr,
-                                                            u64* __restrict__ lens, u64* err) {
-    const NatPage pg = pages[blockIdx.x];
-    if (vbytes) {
-        const u8* vb = pg.valid == ~0ULL ? nullptr : B.at(pg.valid);
-        for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) vbytes[pg.row0 + i] = vb ? (vb[i >> 3] >> (i & 7)) & 1 : 1;
+// rows i0 .. i0 + cnt - 1 of v[] into a tw-wide column at o (8-byte stores when whole and aligned)
+__device__ __forceinline__ void nat_store8(u8* o, u32 i0, u32 cnt, const u64 (&v)[8], u32 tw) {
+    u8* d = o + (u64)i0 * tw;
+    if (cnt == 8 && !((uintptr_t)d & 7)) {
+        if (tw == 1) {
+            u64 x = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x |= (v[k] & 0xFF) << (8 * k);
+            *(u64*)d = x;
+        } else if (tw == 2) {
+            u64 x0 = 0, x1 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x0 |= (v[k] & 0xFFFF) << (16 * k);
+                x1 |= (v[k + 4] & 0xFFFF) << (16 * k);
+            }
+            ((u64*)d)[0] = x0;
+            ((u64*)d)[1] = x1;
+        } else if (tw == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ((u64*)d)[k] = (v[2 * k] & 0xFFFFFFFFULL) | (v[2 * k + 1] << 32);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ((u64*)d)[k] = v[k];
+        }
+        return;
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if ((u32)k < cnt) nat_st(d + (u64)k * tw, v[k], tw);
+}
+
+// One workgroup per (page, slice): validity bytes, then the values — integers stored in the
+// target width, a dictionary's indices resolved on the spot (the dictionary staged in LDS when
+// it fits), Strings as (source address, length) for the offsets scan and the gather
+__global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __restrict__ pages, NatBases B, u8* __restrict__ out,
+                                                            u8* __restrict__ vbytes, u64* __restrict__ sptr, u64* __restrict__ lens,
+                                                            u64* err) {
+    __shared__ u64 sdict[NAT_LDS_DICT];
+    const NatPage pg = pages[blockIdx.x];
+    const bool whole = pg.blk.codec == NC_DBP;
+    if (whole && blockIdx.y) return;
+    const u32 per = whole ? pg.n : (((pg.n + gridDim.y - 1) / gridDim.y) + 127) & ~127u;
+    const u32 lo = min(pg.n, blockIdx.y * per), hi = min(pg.n, lo + per);
+    if (lo >= hi) return;
+    if (vbytes) {  // 8 rows per lane: one bitmap byte -> 8 flag bytes
+        const u8* vb = pg.valid == ~0ULL ? nullptr : B.at(pg.valid);
+        for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) {
+            const u32 cnt = min(8u, hi - i0);
+            const u32 bits = vb ? vb[i0 >> 3] : 0xFF;
+            u8* d = vbytes + pg.row0 + i0;
+            if (cnt == 8 && !((uintptr_t)d & 7)) {
+                u64 x = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x |= (u64)((bits >> k) & 1) << (8 * k);
+                *(u64*)d = x;
+            } else {
+                for (u32 k = 0; k < cnt; ++k) d[k] = (bits >> k) & 1;
+            }
+        }
+    }
+    const u32 tw = pg.tw;
     if (pg.dict) {
-        nat_block(pg.blk, pg.n, 4, B, err, [&](u32 i, u64 v) { idx[pg.row0 + i] = (u32)v; });
+        const u8* d = B.at(pg.dsrc);
+        const u32 dn = pg.dn;
+        u32 bad = 0;
+        if (pg.kind == 0) {
+            const bool lds = dn <= NAT_LDS_DICT;
+            if (lds) {
+                for (u32 k = threadIdx.x; k < dn; k += NAT_NT) sdict[k] = nat_ld(d + (u64)k * tw, tw);
+                __syncthreads();
+            }
+            u8* o = out + pg.row0 * tw;
+            nat_block(pg.blk, pg.n, lo, hi, 4, B, err, [&](u32 i0, u32 cnt, const u64 (&ix)[8]) {
+                u64 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const u64 x = ix[k];
+                    const bool in = x < dn;
+                    bad |= (u32)k < cnt && !in;
+                    v[k] = !in ? 0 : (lds ? sdict[x] : nat_ld(d + x * tw, tw));
+                }
+                nat_store8(o, i0, cnt, v, tw);
+            });
+        } else {
+            const u64* e = (const u64*)d;
+            nat_block(pg.blk, pg.n, lo, hi, 4, B, err, [&](u32 i0, u32 cnt, const u64 (&ix)[8]) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if ((u32)k >= cnt) continue;
+                    const u64 x = ix[k];
+                    u64 a = (u64)B.at(0), l = 0;
+                    if (x < dn) {
+                        a = (u64)B.at(e[2 * x]);
+                        l = e[2 * x + 1];
+                    } else {
+                        bad = 1;
+                    }
+                    sptr[pg.row0 + i0 + k] = a;
+                    lens[pg.row0 + i0 + k] = l;
+                }
+            });
+        }
+        if (bad) atomicOr((unsigned long long*)err, (unsigned long long)NERR_RANGE);
         return;
     }
     if (pg.kind == 0) {
-        const u32 tw = pg.tw;
         u8* o = out + pg.row0 * tw;
-        nat_block(pg.blk, pg.n, tw, B, err, [&](u32 i, u64 v) {
-            u8* d = o + (u64)i * tw;
-            if (tw == 8) *(u64*)d = v;
-            else if (tw == 4) *(u32*)d = (u32)v;
-            else if (tw == 2) *(uint16_t*)d = (uint16_t)v;
-            else *d = (u8)v;
-        });
+        nat_block(pg.blk, pg.n, lo, hi, tw, B, err, [&](u32 i0, u32 cnt, const u64 (&v)[8]) { nat_store8(o, i0, cnt, v, tw); });
         return;
     }
     if (pg.smode == 1) {
         const u64 a = (u64)B.at(pg.sdata);
-        for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) {
+        for (u32 i = lo + threadIdx.x; i < hi; i += NAT_NT) {
             sptr[pg.row0 + i] = a;
             lens[pg.row0 + i] = pg.stotal;
         }
@@ -1307,43 +1460,15 @@ __global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __res
     }
     const u8* offs = B.at(pg.soffs);
     const u64 a = (u64)B.at(pg.sdata);
-    for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) {
+    u32 bad = 0;
+    for (u32 i = lo + threadIdx.x; i < hi; i += NAT_NT) {
         const u64 s0 = nat_ld(offs + 8ULL * i, 8), s1 = nat_ld(offs + 8ULL * (i + 1), 8);
-        if (s1 < s0 || s1 > pg.stotal) {
-            atomicOr((unsigned long long*)err, (unsigned long long)NERR_MALFORMED);
-            sptr[pg.row0 + i] = a;
-            lens[pg.row0 + i] = 0;
-            continue;
-        }
-        sptr[pg.row0 + i] = a + s0;
-        lens[pg.row0 + i] = s1 - s0;
+        const bool ok = s0 <= s1 && s1 <= pg.stotal;
+        bad |= !ok;
+        sptr[pg.row0 + i] = ok ? a + s0 : a;
+        lens[pg.row0 + i] = ok ? s1 - s0 : 0;
     }
-}
-
-// pass 2: dictionaries (indices from pass 1, range-checked)
-__global__ void __launch_bounds__(NAT_NT) nat_dict_kernel(const NatPage* __restrict__ pages, NatBases B, u8* __restrict__ out,
-                                                          const u32* __restrict__ idx, u64* __restrict__ sptr, u64* __restrict__ lens,
-                                                          u64* err) {
-    const NatPage pg = pages[blockIdx.x];
-    if (!pg.dict) return;
-    const u8* d = B.at(pg.dsrc);
-    for (u32 i = threadIdx.x; i < pg.n; i += NAT_NT) {
-        u32 k = idx[pg.row0 + i];
-        if (k >= pg.dn) {
-            atomicOr((unsigned long long*)err, (unsigned long long)NERR_RANGE);
-            k = 0;
-        }
-        if (pg.kind == 0) {
-            const u32 tw = pg.tw;
-            u8* o = out + (pg.row0 + i) * tw;
-            const u64 v = pg.dn ? nat_ld(d + (u64)k * tw, tw) : 0;
-            for (u32 j = 0; j < tw; ++j) o[j] = (u8)(v >> (8 * j));
-        } else {
-            const u64* e = (const u64*)d + 2 * (u64)k;
-            sptr[pg.row0 + i] = pg.dn ? (u64)B.at(e[0]) : 0;
-            lens[pg.row0 + i] = pg.dn ? e[1] : 0;
-        }
-    }
+    if (bad) atomicOr((unsigned long long*)err, (unsigned long long)NERR_MALFORMED);
 }
 
 __global__ void __launch_bounds__(256) nat_null_check_kernel(const u8* __restrict__ vb, u64 n, u64* err) {
@@ -1589,7 +1714,6 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
     SCAN_RET(ensure(&ctx->ntab, &ctx->ntab_cap, P.tab.size() + 1));
     SCAN_RET(ensure(&ctx->npg, &ctx->npg_cap, pages.size() * sizeof(NatPage) + 16));
     SCAN_RET(ensure(&ctx->vbytes, &ctx->vbytes_cap, row + 1));
-    SCAN_RET(ensure(&ctx->idx, &ctx->idx_cap, row + 1));
     u64 njobs = 0;
     for (int c = 1; c <= 3; ++c) njobs += P.jobs[c].size();
     SCAN_RET(ensure(&ctx->pages, &ctx->pages_cap, njobs + 1));
@@ -1631,11 +1755,13 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
     B.b[2] = (const u8*)ctx->ntab;
     const bool want_vb = col->nullable != 0;
     if (!pages.empty()) {
+        // slices per page: ≫ 256 workgroups over the chip, ≥ 1024 rows per slice
+        u64 maxn = 0;
+        for (const NatPage& pg : pages) maxn = std::max<u64>(maxn, pg.n);
+        u32 split = (u32)std::max<u64>(1, std::min<u64>({16, (4096 + pages.size() - 1) / pages.size(), (maxn + 1023) / 1024}));
         void* ps = prof_scope_begin("nat_decode", s);
-        hipLaunchKernelGGL(nat_decode_kernel, dim3((u32)pages.size()), dim3(NAT_NT), 0, s, (const NatPage*)ctx->npg, B, (u8*)out->data,
-                           want_vb ? ctx->vbytes : nullptr, ctx->idx, ctx->sptr, out->offsets, ctx->err);
-        hipLaunchKernelGGL(nat_dict_kernel, dim3((u32)pages.size()), dim3(NAT_NT), 0, s, (const NatPage*)ctx->npg, B, (u8*)out->data,
-                           ctx->idx, ctx->sptr, out->offsets, ctx->err);
+        hipLaunchKernelGGL(nat_decode_kernel, dim3((u32)pages.size(), split), dim3(NAT_NT), 0, s, (const NatPage*)ctx->npg, B,
+                           (u8*)out->data, want_vb ? ctx->vbytes : nullptr, ctx->sptr, out->offsets, ctx->err);
         prof_scope_end(ps);
         SCAN_HIP(hipGetLastError());
     }
