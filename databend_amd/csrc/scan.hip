@@ -238,6 +238,7 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
 // zstd_dev.hpp.  lit: ZS_MAX_BLOCK bytes of literal scratch per page.
 __global__ void __launch_bounds__(64) pq_zstd_kernel(ScanArgs a, u8* lit) {
     __shared__ ZsTables T;
+    __shared__ ZsWork W;
     const ScanPage pg = a.pages[blockIdx.x];
     const u32 lane = threadIdx.x;
     if (!pg.compressed) {
@@ -249,7 +250,7 @@ __global__ void __launch_bounds__(64) pq_zstd_kernel(ScanArgs a, u8* lit) {
     for (u32 j = lane; j < pg.lv; j += 64) dst[j] = src[j];  // v2 levels (uncompressed) first
     __builtin_amdgcn_wave_barrier();
     const bool ok = pg.comp >= pg.lv && pg.uncomp >= pg.lv &&
-                    zs_decode(src + pg.lv, pg.comp - pg.lv, dst + pg.lv, pg.uncomp - pg.lv, lit + (u64)blockIdx.x * ZS_MAX_BLOCK, T);
+                    zs_decode(src + pg.lv, pg.comp - pg.lv, dst + pg.lv, pg.uncomp - pg.lv, lit + (u64)blockIdx.x * ZS_MAX_BLOCK, T, W);
     if (!ok && lane == 0) atomicOr((unsigned long long*)a.err, (unsigned long long)SERR_MALFORMED);
 }
 

@@ -3,16 +3,19 @@
 // Fuse writes its blocks with TableCompression::Zstd by default
 // (src/query/storages/common/table_meta/src/table/table_compression.rs:24-31), which the parquet
 // writer maps to the ZSTD page codec; the reference decodes it through the `zstd` crate (libzstd).
-// This is an independent restatement of the published format, written for one wave per page:
-// the wave copies raw and RLE blocks; lane 0 parses the frame, entropy-decodes compressed blocks
-// (Huffman literals, FSE sequences — inherently serial bitstreams) and executes their sequences
-// (literal runs and matches, byte by byte so an overlapping match reads bytes it has just
-// written).  Correctness first: a page is a serial stream on one lane, pages run in parallel.
-// Every read is bounds-checked against the compressed page and every write against the page's
-// uncompressed size: a malformed page sets `bad`, never faults.
+// This is an independent restatement of the published format, written for one wave per page.
+// Lane 0 parses the frame and entropy-decodes (Huffman tree, FSE tables, the sequence bitstream —
+// inherently serial); the four Huffman literal streams decode on lanes 0-3 at once; sequences are
+// decoded by lane 0 in batches of ZS_SEQ into LDS and executed by the whole wave: literal runs
+// and matches are copied 64 bytes per step, a match's source bytes read from an LDS ring of the
+// last ZS_RING output bytes (the global output only for longer offsets, after a fence) — an
+// overlapping match is the periodic extension of the `off` bytes before it, so no byte of a match
+// is read after the match writes it.  Every read is bounds-checked against the compressed page
+// and every write against the page's uncompressed size: a malformed page sets `bad`, never
+// faults.
 //
-// Tables live in LDS (one set per page); the literals of the current block go to a per-page
-// scratch of ZS_MAX_BLOCK bytes in global memory.
+// Tables, the ring and the sequence batch live in LDS (one set per page); the literals of the
+// current block go to a per-page scratch of ZS_MAX_BLOCK bytes in global memory.
 //
 // The same source builds on the host (ZS_HOST: one "lane", plain loads) for the decoder's CPU
 // test against libzstd-made frames (tests/test_zstd_host.py); the device build is the product.
@@ -31,6 +34,13 @@ typedef uint64_t u64;
 #define ZS_LANE_ID 0u
 #define ZS_WAVE_SYNC()
 #define ZS_CLZ(v) __builtin_clz(v)
+#define ZS_LDS_SYNC()
+#include <cstring>
+static inline uint64_t zs_ld64(const u8* p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
 #else
 #include "device.hpp"
 #define ZS_FN __device__ __forceinline__
@@ -46,6 +56,17 @@ typedef uint64_t u64;
         __builtin_amdgcn_wave_barrier();                 \
     } while (0)
 #define ZS_CLZ(v) __clz(v)
+// LDS written by some lanes, then read by others of the same wave
+#define ZS_LDS_SYNC()                                      \
+    do {                                                   \
+        __builtin_amdgcn_wave_barrier();                   \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        __builtin_amdgcn_wave_barrier();                   \
+    } while (0)
+typedef u64 zs_u64u __attribute__((aligned(1)));
+__device__ __forceinline__ u64 zs_ld64(const u8* p) {  // gfx950 global loads take byte addresses
+    return *(const zs_u64u __attribute__((address_space(1)))*)p;
+}
 #endif
 
 #define ZS_MAX_BLOCK (128 * 1024)
@@ -53,6 +74,8 @@ typedef uint64_t u64;
 #define ZS_LL_MAXLOG 9
 #define ZS_ML_MAXLOG 9
 #define ZS_OF_MAXLOG 8
+#define ZS_RING 16384  // LDS history of the output (power of two)
+#define ZS_SEQ 256     // sequences decoded per batch
 
 struct ZsFse {  // one FSE decoding table entry
     u8 sym, nbits;
@@ -84,6 +107,12 @@ ZS_CONST u8 zs_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                                   0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 
 ZS_FN u32 zs_highbit(u32 v) { return 31 - ZS_CLZ(v); }
+
+struct ZsWork {  // per-page LDS beside the tables
+    u8 ring[ZS_RING];
+    u32 ll[ZS_SEQ], ml[ZS_SEQ], off[ZS_SEQ];
+    u64 sh[16];  // lane 0 -> wave broadcast slots
+};
 
 // Forward little-endian bit reader over [p, p + n) (FSE table descriptions)
 struct ZsFwd {
@@ -118,6 +147,12 @@ struct ZsBwd {
     ZS_MFN u64 window(long long at) const {  // 64 bits starting at bit `at` (may be < 0)
         u64 v = 0;
         const long long b0 = at >> 3;  // floor
+        if (b0 >= 0 && (u64)b0 + 9 <= n) {  // inside the stream: one 8-byte load and one byte
+            const u32 s = (u32)(at & 7);
+            v = zs_ld64(p + b0) >> s;
+            if (s) v |= (u64)ZS_LD(p + b0 + 8) << (64 - s);
+            return v;
+        }
         for (int i = 0; i < 9; ++i) {
             const long long b = b0 + i;
             if (b >= 0 && (u64)b < n) {
@@ -319,20 +354,21 @@ ZS_FN bool zs_huf_stream(const u8* p, u64 n, u64 count, const ZsTables& T, u8* o
 }
 
 // Decode one zstd frame sequence occupying src[0, sn) into dst[0, dn) (exact size).  Called by
-// all 64 lanes of the wave (uniform control flow); lane 0 does the entropy decoding.
-ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& T) {
+// all lanes of the wave (uniform control flow).
+ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& T, ZsWork& W) {
     const u32 lane = ZS_LANE_ID;
-#ifdef ZS_HOST
-    u64 sh[8];
-#else
-    __shared__ u64 sh[8];  // broadcast slots
-#endif
     u64 ip = 0, op = 0;
     bool bad = false;
+    // sequence state: meaningful in lane 0 only
     u32 rep[3] = {1, 4, 8};
+    ZsBwd bs;
+    u32 sll = 0, sof = 0, sml = 0;
     auto wave_copy = [&](u8* d, const u8* s, u64 len) {
-        for (u64 j = lane; j < len; j += ZS_LANES) d[j] = ZS_LD(s + j);
-        ZS_WAVE_SYNC();
+        for (u64 j = lane; j < len; j += ZS_LANES) {
+            const u8 c = ZS_LD(s + j);
+            d[j] = c;
+            W.ring[(op + j) & (ZS_RING - 1)] = c;
+        }
     };
     while (!bad && ip < sn) {
         // ---- frame header ----
@@ -370,32 +406,39 @@ ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& 
             if (btype == 0) {  // raw
                 if (bsize > sn - ip || bsize > dn - op) { bad = true; break; }
                 wave_copy(dst + op, src + ip, bsize);
+                ZS_LDS_SYNC();
                 ip += bsize;
                 op += bsize;
             } else if (btype == 1) {  // RLE
                 if (ip >= sn || bsize > dn - op) { bad = true; break; }
                 const u8 v = ZS_LD(src + ip);
-                for (u64 j = lane; j < bsize; j += ZS_LANES) dst[op + j] = v;
-                ZS_WAVE_SYNC();
+                for (u64 j = lane; j < bsize; j += ZS_LANES) {
+                    dst[op + j] = v;
+                    W.ring[(op + j) & (ZS_RING - 1)] = v;
+                }
+                ZS_LDS_SYNC();
                 ip += 1;
                 op += bsize;
-            } else if (btype == 2) {  // compressed: lane 0 decodes, results broadcast through LDS
+            } else if (btype == 2) {  // compressed
                 if (bsize > sn - ip || bsize > ZS_MAX_BLOCK) { bad = true; break; }
                 const u8* b = src + ip;
                 const u64 bn = bsize;
                 ip += bsize;
+                // (A) lane 0: literals header, Huffman tree, sequences header and FSE tables
+                // sh: 0 ok, 1 lit mode (0 raw, 1 rle, 2 huffman), 2 regen, 3 raw offset / rle byte,
+                //     4 streams, 5-8 stream offsets, 9-12 stream sizes, 13 nseq
                 if (lane == 0) {
                     u64 q = 0;
                     bool ok = true;
-                    // -- literals section --
                     const u32 b0 = bn ? ZS_LD(b) : 0;
                     const u32 lt = b0 & 3, sf = (b0 >> 2) & 3;
                     u64 regen = 0, csize = 0;
                     u32 streams = 1;
                     if (lt <= 1) {
                         if (sf == 0 || sf == 2) { regen = b0 >> 3; q = 1; }
-                        else if (sf == 1) { regen = (b0 >> 4) + ((u64)ZS_LD(b + 1) << 4); q = 2; }
-                        else { regen = (b0 >> 4) + ((u64)ZS_LD(b + 1) << 4) + ((u64)ZS_LD(b + 2) << 12); q = 3; }
+                        else if (sf == 1) { regen = bn >= 2 ? (b0 >> 4) + ((u64)ZS_LD(b + 1) << 4) : 0; q = 2; }
+                        else { regen = bn >= 3 ? (b0 >> 4) + ((u64)ZS_LD(b + 1) << 4) + ((u64)ZS_LD(b + 2) << 12) : 0; q = 3; }
+                        if (q > bn) ok = false;
                     } else {
                         u64 h = 0;
                         const u32 hl = sf <= 1 ? 3 : (sf == 2 ? 4 : 5);
@@ -408,19 +451,17 @@ ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& 
                         q = hl;
                     }
                     if (regen > ZS_MAX_BLOCK) ok = false;
-                    if (ok && lt == 0) {  // raw literals
+                    W.sh[1] = lt == 0 ? 0 : (lt == 1 ? 1 : 2);
+                    W.sh[2] = regen;
+                    W.sh[4] = 0;
+                    if (ok && lt == 0) {  // raw literals: read in place
                         if (regen > bn - q) ok = false;
-                        else {
-                            for (u64 i = 0; i < regen; ++i) lit[i] = ZS_LD(b + q + i);
-                            q += regen;
-                        }
+                        W.sh[3] = q;
+                        q += regen;
                     } else if (ok && lt == 1) {  // RLE literals
                         if (q >= bn) ok = false;
-                        else {
-                            const u8 v = ZS_LD(b + q);
-                            for (u64 i = 0; i < regen; ++i) lit[i] = v;
-                            q += 1;
-                        }
+                        else W.sh[3] = ZS_LD(b + q);
+                        q += 1;
                     } else if (ok) {  // Huffman, with its tree (2) or the previous block's (3)
                         if (csize > bn - q) ok = false;
                         u64 tq = 0;
@@ -431,30 +472,34 @@ ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& 
                             ok = false;
                         }
                         if (ok) {
-                            const u8* s = b + q + tq;
-                            const u64 sl = csize - tq;
+                            const u64 s0 = q + tq, sl = csize - tq;
                             if (streams == 1) {
-                                ok = zs_huf_stream(s, sl, regen, T, lit);
+                                W.sh[4] = 1;
+                                W.sh[5] = s0;
+                                W.sh[9] = sl;
+                            } else if (sl < 6) {
+                                ok = false;
                             } else {
-                                if (sl < 6) ok = false;
+                                const u64 z1 = ZS_LD(b + s0) | (ZS_LD(b + s0 + 1) << 8), z2 = ZS_LD(b + s0 + 2) | (ZS_LD(b + s0 + 3) << 8),
+                                          z3 = ZS_LD(b + s0 + 4) | (ZS_LD(b + s0 + 5) << 8);
+                                const u64 per = (regen + 3) / 4;
+                                if (6 + z1 + z2 + z3 > sl || 3 * per > regen) ok = false;
                                 else {
-                                    const u64 s1 = ZS_LD(s) | (ZS_LD(s + 1) << 8), s2 = ZS_LD(s + 2) | (ZS_LD(s + 3) << 8),
-                                              s3 = ZS_LD(s + 4) | (ZS_LD(s + 5) << 8);
-                                    const u64 per = (regen + 3) / 4;
-                                    if (6 + s1 + s2 + s3 > sl || 3 * per > regen) ok = false;
-                                    else {
-                                        const u64 s4 = sl - 6 - s1 - s2 - s3;
-                                        ok = zs_huf_stream(s + 6, s1, per, T, lit) && zs_huf_stream(s + 6 + s1, s2, per, T, lit + per) &&
-                                             zs_huf_stream(s + 6 + s1 + s2, s3, per, T, lit + 2 * per) &&
-                                             zs_huf_stream(s + 6 + s1 + s2 + s3, s4, regen - 3 * per, T, lit + 3 * per);
-                                    }
+                                    W.sh[4] = 4;
+                                    W.sh[5] = s0 + 6;
+                                    W.sh[6] = s0 + 6 + z1;
+                                    W.sh[7] = s0 + 6 + z1 + z2;
+                                    W.sh[8] = s0 + 6 + z1 + z2 + z3;
+                                    W.sh[9] = z1;
+                                    W.sh[10] = z2;
+                                    W.sh[11] = z3;
+                                    W.sh[12] = sl - 6 - z1 - z2 - z3;
                                 }
                             }
                             q += csize;
                         }
                     }
-                    // -- sequences section: decoded and executed here (matches read dst) --
-                    u64 lp = 0;  // literals consumed
+                    // sequences header and tables
                     if (ok && q >= bn) ok = false;
                     u64 nseq = 0;
                     if (ok) {
@@ -501,69 +546,147 @@ ZS_FN bool zs_decode(const u8* src, u64 sn, u8* dst, u64 dn, u8* lit, ZsTables& 
                                 ok = false;
                             }
                         }
-                        ZsBwd bs;
                         if (ok && !bs.init(b + q, bn - q)) ok = false;
                         if (ok) {
-                            u32 sll = (u32)bs.read(T.ll_log), sof = (u32)bs.read(T.of_log), sml = (u32)bs.read(T.ml_log);
-                            for (u64 i = 0; i < nseq && ok; ++i) {
-                                const u32 llc = T.ll[sll].sym, ofc = T.of[sof].sym, mlc = T.ml[sml].sym;
-                                if (llc > 35 || mlc > 52 || ofc > 31) { ok = false; break; }
-                                // values: offset, match length, literal length (RFC order)
-                                u64 ofv = (1ULL << ofc) + bs.read(ofc);
-                                const u64 ml = zs_ml_base[mlc] + bs.read(zs_ml_bits[mlc]);
-                                const u64 ll = zs_ll_base[llc] + bs.read(zs_ll_bits[llc]);
-                                // repeat offsets
-                                u64 off;
-                                if (ofv > 3) {
-                                    off = ofv - 3;
-                                    rep[2] = rep[1];
-                                    rep[1] = rep[0];
-                                    rep[0] = (u32)off;
-                                } else {
-                                    const u64 idx = ofv + (ll == 0 ? 1 : 0);
-                                    if (idx == 1) off = rep[0];
-                                    else if (idx == 2) { off = rep[1]; rep[1] = rep[0]; rep[0] = (u32)off; }
-                                    else if (idx == 3) { off = rep[2]; rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = (u32)off; }
-                                    else {
-                                        off = rep[0] - 1;
-                                        off += off == 0 ? 1 : 0;  // as libzstd: 0 is forced to 1
-                                        rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = (u32)off;
-                                    }
-                                }
-                                // state updates (not after the last sequence): LL, ML, OF
-                                if (i + 1 < nseq) {
-                                    sll = T.ll[sll].next + (u32)bs.read(T.ll[sll].nbits);
-                                    sml = T.ml[sml].next + (u32)bs.read(T.ml[sml].nbits);
-                                    sof = T.of[sof].next + (u32)bs.read(T.of[sof].nbits);
-                                }
-                                // execute: literals, then the match
-                                if (ll > regen - lp || ll > dn - op) { ok = false; break; }
-                                for (u64 j = 0; j < ll; ++j) dst[op + j] = lit[lp + j];
-                                op += ll;
-                                lp += ll;
-                                if (off == 0 || off > op || ml > dn - op) { ok = false; break; }
-                                for (u64 j = 0; j < ml; ++j) dst[op + j] = dst[op - off + j];
-                                op += ml;
-                            }
-                            if (ok && bs.pos != 0) ok = false;
+                            sll = (u32)bs.read(T.ll_log);
+                            sof = (u32)bs.read(T.of_log);
+                            sml = (u32)bs.read(T.ml_log);
                         }
                     }
-                    // the remaining literals
-                    if (ok) {
-                        const u64 rest = regen - lp;
-                        if (rest > dn - op) ok = false;
-                        else {
-                            for (u64 j = 0; j < rest; ++j) dst[op + j] = lit[lp + j];
-                            op += rest;
-                        }
-                    }
-                    sh[0] = op;
-                    sh[1] = ok ? 0 : 1;
+                    W.sh[13] = nseq;
+                    W.sh[0] = ok ? 1 : 0;
                 }
-                ZS_WAVE_SYNC();
-                op = sh[0];
-                bad = sh[1] != 0;
-                ZS_WAVE_SYNC();
+                ZS_LDS_SYNC();
+                if (!W.sh[0]) { bad = true; break; }
+                const u32 lmode = (u32)W.sh[1];
+                const u64 regen = W.sh[2], nseq = W.sh[13];
+                const u8* litp = lmode == 0 ? b + W.sh[3] : lit;
+                const u8 lrle = (u8)W.sh[3];
+                // (B) Huffman streams: one lane each
+                if (lmode == 2) {
+                    const u32 ns = (u32)W.sh[4];
+                    const u64 per = ns == 1 ? regen : (regen + 3) / 4;
+                    bool hok = true;
+                    for (u32 k = lane; k < ns; k += ZS_LANES) {
+                        const u64 cnt = ns == 1 ? regen : (k < 3 ? per : regen - 3 * per);
+                        hok = zs_huf_stream(b + W.sh[5 + k], W.sh[9 + k], cnt, T, lit + k * per) && hok;
+                    }
+#ifdef ZS_HOST
+                    const bool all = hok;
+#else
+                    const bool all = __ballot(!hok) == 0;
+#endif
+                    ZS_WAVE_SYNC();  // the literals (global scratch) are visible to every lane
+                    if (!all) { bad = true; break; }
+                }
+                auto lit_at = [&](u64 i) -> u8 { return lmode == 1 ? lrle : ZS_LD(litp + i); };
+                // (C) sequences: lane 0 decodes a batch into LDS, the wave executes it
+                u64 lp = 0;  // literals consumed
+                for (u64 s0 = 0; s0 < nseq && !bad; s0 += ZS_SEQ) {
+                    const u32 nb = (u32)(nseq - s0 < ZS_SEQ ? nseq - s0 : ZS_SEQ);
+                    if (lane == 0) {
+                        bool ok = true;
+                        for (u32 i = 0; i < nb; ++i) {
+                            const u32 llc = T.ll[sll].sym, ofc = T.of[sof].sym, mlc = T.ml[sml].sym;
+                            if (llc > 35 || mlc > 52 || ofc > 31) { ok = false; break; }
+                            // values: offset, match length, literal length (RFC order)
+                            const u64 ofv = (1ULL << ofc) + bs.read(ofc);
+                            const u64 ml = zs_ml_base[mlc] + bs.read(zs_ml_bits[mlc]);
+                            const u64 ll = zs_ll_base[llc] + bs.read(zs_ll_bits[llc]);
+                            u64 off;
+                            if (ofv > 3) {
+                                off = ofv - 3;
+                                rep[2] = rep[1];
+                                rep[1] = rep[0];
+                                rep[0] = (u32)off;
+                            } else {
+                                const u64 idx = ofv + (ll == 0 ? 1 : 0);
+                                if (idx == 1) off = rep[0];
+                                else if (idx == 2) { off = rep[1]; rep[1] = rep[0]; rep[0] = (u32)off; }
+                                else if (idx == 3) { off = rep[2]; rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = (u32)off; }
+                                else {
+                                    off = rep[0] - 1;
+                                    off += off == 0 ? 1 : 0;  // as libzstd: 0 is forced to 1
+                                    rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = (u32)off;
+                                }
+                            }
+                            // state updates (not after the last sequence): LL, ML, OF
+                            if (s0 + i + 1 < nseq) {
+                                sll = T.ll[sll].next + (u32)bs.read(T.ll[sll].nbits);
+                                sml = T.ml[sml].next + (u32)bs.read(T.ml[sml].nbits);
+                                sof = T.of[sof].next + (u32)bs.read(T.of[sof].nbits);
+                            }
+                            if (off > 0xFFFFFFFFull) { ok = false; break; }
+                            W.ll[i] = (u32)ll;
+                            W.ml[i] = (u32)ml;
+                            W.off[i] = (u32)off;
+                        }
+                        if (ok && s0 + nb == nseq && bs.pos != 0) ok = false;
+                        W.sh[0] = ok ? 1 : 0;
+                    }
+                    ZS_LDS_SYNC();
+                    if (!W.sh[0]) { bad = true; break; }
+                    for (u32 i = 0; i < nb; ++i) {
+                        const u64 ll = W.ll[i], ml = W.ml[i], off = W.off[i];
+                        // literals
+                        if (ll > regen - lp || ll > dn - op) { bad = true; break; }
+                        for (u64 j = lane; j < ll; j += ZS_LANES) {
+                            const u8 c = lit_at(lp + j);
+                            dst[op + j] = c;
+                            W.ring[(op + j) & (ZS_RING - 1)] = c;
+                        }
+                        op += ll;
+                        lp += ll;
+                        if (off == 0 || off > op || ml > dn - op) { bad = true; break; }
+                        ZS_LDS_SYNC();
+                        // out[op + j] = out[op - off + j % off]; j % off advanced incrementally
+                        // (r: this lane's j % off, step: ZS_LANES % off)
+                        const u32 o32 = (u32)off, step = ZS_LANES % o32;
+                        if (off <= ZS_RING / 2) {
+                            // from the ring; a segment of at most ZS_RING - off bytes overwrites no
+                            // slot it still reads
+                            u64 done = 0;
+                            while (done < ml) {
+                                const u64 seg = ml - done < ZS_RING - off ? ml - done : ZS_RING - off;
+                                const u64 w = op + done;
+                                u32 r = lane % o32;
+                                for (u64 j = lane; j < seg; j += ZS_LANES) {
+                                    const u8 c = W.ring[(w - off + r) & (ZS_RING - 1)];
+                                    dst[w + j] = c;
+                                    W.ring[(w + j) & (ZS_RING - 1)] = c;
+                                    r += step;
+                                    if (r >= o32) r -= o32;
+                                }
+                                ZS_LDS_SYNC();
+                                done += seg;
+                            }
+                        } else {  // a long offset: its source bytes from the output, made visible first
+                            ZS_WAVE_SYNC();
+                            const u64 w = op;
+                            u32 r = lane % o32;
+                            for (u64 j = lane; j < ml; j += ZS_LANES) {
+                                const u8 c = ZS_LD(dst + w - off + r);
+                                dst[w + j] = c;
+                                W.ring[(w + j) & (ZS_RING - 1)] = c;
+                                r += step;
+                                if (r >= o32) r -= o32;
+                            }
+                            ZS_LDS_SYNC();
+                        }
+                        op += ml;
+                    }
+                }
+                if (bad) break;
+                // (D) the remaining literals
+                const u64 rest = regen - lp;
+                if (rest > dn - op) { bad = true; break; }
+                for (u64 j = lane; j < rest; j += ZS_LANES) {
+                    const u8 c = lit_at(lp + j);
+                    dst[op + j] = c;
+                    W.ring[(op + j) & (ZS_RING - 1)] = c;
+                }
+                ZS_LDS_SYNC();
+                op += rest;
             } else {
                 bad = true;
             }
