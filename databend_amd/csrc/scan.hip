@@ -136,21 +136,33 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
         w += (u32)len;
     };
     auto copy_back = [&](u32 off, u64 len) {
-        if (off == 0 || off > w || off > RING || len > (u64)(on - w)) { bad = true; return; }
-        // byte j repeats the last `off` bytes: out[w + j] = out[w - off + j % off]; chunks of at
-        // most `off` bytes so that every source byte is in the ring before it is read
-        for (u32 c0 = 0; c0 < len; c0 += 64) {
-            const u32 j = c0 + lane;
-            u8 b = 0;
-            if (j < len) b = ring[(w - off + (j % off)) & (RING - 1)];
-            __builtin_amdgcn_wave_barrier();
-            if (j < len) {
-                o[w + j] = b;
-                ring[(w + j) & (RING - 1)] = b;
+        if (off == 0 || off > w || off >= RING || len > (u64)(on - w)) { bad = true; return; }
+        // byte j repeats the last `off` bytes: out[w + j] = out[w - off + j % off], read from the
+        // ring in segments of at most RING - off bytes (a longer one would overwrite ring slots it
+        // still reads when off > RING / 2), 64 bytes per step, each step's reads before its writes
+        auto run = [&](u32 seg) {
+            for (u32 c0 = 0; c0 < seg; c0 += 64) {
+                const u32 j = c0 + lane;
+                u8 b = 0;
+                if (j < seg) b = ring[(w - off + (j % off)) & (RING - 1)];
+                __builtin_amdgcn_wave_barrier();
+                if (j < seg) {
+                    o[w + j] = b;
+                    ring[(w + j) & (RING - 1)] = b;
+                }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
+            w += seg;
+        };
+        if (len <= (u64)(RING - off)) {  // every Snappy copy (<= 64 bytes), most LZ4 matches
+            run((u32)len);
+            return;
         }
-        w += len;
+        while (len) {
+            const u32 seg = (u32)(len < (u64)(RING - off) ? len : (u64)(RING - off));
+            run(seg);
+            len -= seg;
+        }
     };
     if (CODEC == DBG_PQ_SNAPPY) {
         u32 n = 0, sh = 0;  // preamble: uncompressed length (varint)

@@ -211,6 +211,16 @@ def test_string_dict_nested(dec, nested):
     check_str(dec, v, page_rows=2048, codecs=[nat.DICT], nested=nested)
 
 
+@pytest.mark.parametrize("codec", [nat.LZ4, nat.SNAPPY, nat.ZSTD])
+def test_long_back_references(dec, codec):
+    """a 40000-byte value repeated: the compressors emit one match of ~120 KB at offset 40000 —
+    longer than the offset, which is more than half the inflate's 64 KB history ring (LZ4 / Snappy)
+    and more than the Zstd ring (read from the output)."""
+    rng = np.random.default_rng(8)
+    x = bytes(rng.integers(0, 256, 40000, dtype=np.uint8))
+    check_str(dec, [x, x, x, x, b"tail"], codecs=[codec])
+
+
 def test_string_dict_expands_payload(dec):
     """a dictionary whose rows reference a long entry many times: the payload is far larger
     than the page bytes, so the first call reports the size and the wrapper repeats it."""
