@@ -257,6 +257,8 @@ struct dbg_agg_handle {
     struct Kind {  // 0: raw records (add_groups), 1: state records (merge_records)
         u8* l1 = nullptr;
         u64 l1_cap = 0, l1_n = 0;  // records
+        u16* dig = nullptr;        // level-2 digits of records [0, dig_n) (fixed-shape raw level 1)
+        u64 dig_cap = 0, dig_n = 0;
         std::vector<Seg> segs;
         u8* a = nullptr;  // finalize levels: ping-pong buffers, l1_n records each
         u8* b = nullptr;
@@ -908,7 +910,7 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     for (void* p : bufs)
         if (p) hipFree(p);
     for (auto& K : h->ppk) {
-        void* kb[] = {K.l1, K.a, K.b, K.part};
+        void* kb[] = {K.l1, K.a, K.b, K.part, K.dig};
         for (void* q : kb)
             if (q) hipFree(q);
     }
@@ -962,6 +964,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     h->xrecv_busy = false;  // no group references the exchange's receive buffers any more
     for (auto& K : h->ppk) {  // partitioned payload: records dropped, buffers kept (the mode too)
         K.l1_n = 0;
+        K.dig_n = 0;
         K.segs.clear();
     }
     h->pp_grec_ready = false;
@@ -1195,7 +1198,7 @@ static PPFast pp_fast_desc(const Spec& S, const BatchDesc& B, u32 bid, int kind)
 
 static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const u8* recs, const std::vector<PPChunk>& ch,
                          const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out, const PPFast* F = nullptr,
-                         bool counted = false) {
+                         bool counted = false, const u16* dig = nullptr) {
     const u64 K = 1ULL << kbits;
     RETURN_IF(pp_upload_chunks(h, ch, c0));
     if (counted && h->pp_cnt_cap < ch.size() * K) return fail(DBG_ERR_INTERNAL, "fused counts: buffer too small");
@@ -1205,6 +1208,8 @@ static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const 
         prof::Scope ps(PP_COUNT_NAME[level], h->stream);
         if (F && F->kind)
             launch_pp_l1_fast(h->stream, *F, 1, h->pp_dchunks, (u32)ch.size(), h->pp_cnt, nullptr, nullptr, nullptr);
+        else if (dig)
+            launch_pp_count_dig(h->stream, h->pp_dchunks, (u32)ch.size(), dig, kbits, h->pp_cnt);
         else
             launch_pp_count(h->stream, h->dspec, h->dbatches, src, kind, recs, h->pp_dchunks, (u32)ch.size(), shift, kbits, h->pp_cnt,
                             (kind ? h->spec.pp_rw_state : h->spec.pp_rw_raw) / 8);
@@ -1240,7 +1245,8 @@ static int pp_scatter(dbg_agg_handle* h, int level, int src, int kind, const u8*
 static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, int kind) {
     const Spec& S = h->spec;
     auto& K = h->ppk[kind];
-    const PPFast F = pp_fast_desc(S, *st, bid, kind);
+    PPFast F = pp_fast_desc(S, *st, bid, kind);
+    F.dig = nullptr;
     const u32 rw = kind ? S.pp_rw_state : S.pp_rw_raw;
     std::vector<PPChunk> ch;
     for (u64 s = 0; s < rows; s += PP_CHUNK) ch.push_back(PPChunk{s, std::min<u64>(PP_CHUNK, rows - s), bid, 0});
@@ -1264,11 +1270,33 @@ static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 row
         K.l1 = nb;
         K.l1_cap = ncap;
     }
+    // the level-2 digits ride along while every record so far has them (fixed-shape raw batches)
+    const bool with_dig = F.kind == 1 && kind == 0 && K.dig_n == K.l1_n;
+    if (with_dig && K.l1_n + total > K.dig_cap) {
+        const u64 ncap = std::max<u64>(K.l1_n + total, K.dig_n ? 2 * K.dig_cap : 0);
+        u16* nd = nullptr;
+        RETURN_IF(dev_alloc((void**)&nd, ncap * 2 + 64));
+        if (K.dig) {
+            if (K.dig_n) HIPCHECK(hipMemcpyAsync(nd, K.dig, K.dig_n * 2, hipMemcpyDeviceToDevice, h->stream));
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipFree(K.dig));
+        }
+        K.dig = nd;
+        K.dig_cap = ncap;
+    }
+    if (with_dig) F.dig = K.dig + K.l1_n;
     RETURN_IF(pp_scatter(h, 1, 0, kind, nullptr, (u32)ch.size(), 64 - PP_L1_BITS, PP_L1_BITS, K.l1 + K.l1_n * rw, &F));
+    if (with_dig) K.dig_n = K.l1_n + total;
     K.segs.push_back(dbg_agg_handle::Seg{K.l1_n, total, std::vector<u64>(h->pp_hpart, h->pp_hpart + 257)});
     K.l1_n += total;
     h->pp_grec_ready = false;
     return DBG_OK;
+}
+
+// EXPERIMENT (DBG_X_PPDIG=0): level 2 counts from the records instead of the digit array
+static bool kX_no_dig() {
+    static const bool off = X_ENV("DBG_X_PPDIG") && X_ENV("DBG_X_PPDIG")[0] == '0';
+    return off;
 }
 
 // Levels 2 and 3 (NewTransformPartitionBucket + the final bucket split): every level-1 partition
@@ -1369,7 +1397,9 @@ static int pp_prepare(dbg_agg_handle* h, bool spec_ok) {
             RETURN_IF(ensure_dev(&h->pp_mid, &h->pp_mid_cap, (256ULL << k2) + 1));
             p2 = h->pp_mid;
         }
-        RETURN_IF(pp_count_scan(h, 2, 1, kind, K.l1, ch, c0, sh2, k2, p2));
+        // the level-2 count reads the digit array (2 bytes per record) when level 1 wrote one
+        const bool use_dig = K.dig && K.dig_n == K.l1_n && k2 <= 16 && !kX_no_dig();
+        RETURN_IF(pp_count_scan(h, 2, 1, kind, K.l1, ch, c0, sh2, k2, p2, nullptr, false, use_dig ? K.dig : nullptr));
         const u64 G2 = 256ULL << k2;
         const u32 sh3 = sh2 - k3;
         // Level 3's counts ride on the level-2 scatter when every level-2 partition is one level-3
@@ -3250,6 +3280,7 @@ int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, c
         }
         if (total) HIPCHECK(hipMemcpyAsync(K.l1, src, total * rw, hipMemcpyDeviceToDevice, h->stream));
         K.l1_n = total;
+        K.dig_n = 0;  // imported records carry no digits
         K.segs = std::move(segs);
     }
     HIPCHECK(hipStreamSynchronize(h->stream));  // the caller may release the received buffers

@@ -367,7 +367,11 @@ struct PPFast {
     const u8* sdata;
     const u8* pstr;
     u64 pstr_len;
+    uint16_t* dig;  // kind 1 scatter: the next 16 hash bits below the level-1 digit of each record, at
+                    // the record's index (level 2 counts these instead of re-reading the records)
 };
+// level-2 histograms from the level-1 digit array: bucket = dig >> (16 - kbits)
+void launch_pp_count_dig(hipStream_t s, const PPChunk* chunks, u32 n_chunks, const uint16_t* dig, u32 kbits, u32* cnt);
 int launch_pp_l1_fast(hipStream_t s, const PPFast& F, int count, const PPChunk* chunks, u32 n_chunks, u32* cnt, const u64* off,
                       const u64* part_off, u8* dst);
 // aggregation of the final partitions in LDS; mode 0: result columns (fixed-width keys), mode 1:

@@ -413,6 +413,36 @@ void launch_pp_count(hipStream_t s, const Spec* dspec, const BatchDesc* batches,
         hipLaunchKernelGGL((pp_count_kernel<1>), dim3(n_chunks), dim3(PP_NT), 0, s, dspec, batches, kind, src_recs, chunks, shift, kbits, cnt);
 }
 
+// Level-2 histograms from the digit array the level-1 scatter wrote (2 bytes per record instead
+// of the record): bucket = dig >> (16 - kbits)
+__global__ void __launch_bounds__(PP_NT) pp_count_dig_kernel(const PPChunk* __restrict__ chunks, const uint16_t* __restrict__ dig,
+                                                            u32 kbits, u32* __restrict__ cnt) {
+    __shared__ u32 hist[PP_MAXK];
+    const u32 K = 1u << kbits, dsh = 16 - kbits;
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) hist[b] = 0;
+    __syncthreads();
+    const PPChunk ch = chunks[blockIdx.x];
+    const u64 end = ch.start + ch.n;
+    for (u64 i0 = ch.start + threadIdx.x; i0 < end; i0 += (u64)PP_NT * PP_CU) {
+        u32 d[PP_CU];
+#pragma unroll
+        for (int u = 0; u < PP_CU; ++u) {
+            const u64 i = i0 + (u64)u * PP_NT;
+            d[u] = i < end ? (u32)gld<uint16_t>(dig + i) : ~0u;
+        }
+#pragma unroll
+        for (int u = 0; u < PP_CU; ++u)
+            if (d[u] != ~0u) atomicAdd(&hist[d[u] >> dsh], 1u);
+    }
+    __syncthreads();
+    for (u32 b = threadIdx.x; b < K; b += PP_NT) cnt[(u64)blockIdx.x * K + b] = hist[b];
+}
+
+void launch_pp_count_dig(hipStream_t s, const PPChunk* chunks, u32 n_chunks, const uint16_t* dig, u32 kbits, u32* cnt) {
+    if (!n_chunks) return;
+    hipLaunchKernelGGL(pp_count_dig_kernel, dim3(n_chunks), dim3(PP_NT), 0, s, chunks, dig, kbits, cnt);
+}
+
 // ------------------------------------------------------------------------------------------
 // scan: destinations of every (unit, bucket) run, all parallel.
 //   within:  one thread per (group g, bucket b): exclusive prefix over the group's units
@@ -811,8 +841,9 @@ __device__ __forceinline__ bool pp_fast_pred(const PPFast& F, u64 v) {
 // per wave instead of 64 scattered records per store instruction.  LDS (dynamic): staged words
 // [NT * U * W] u64 | bucket of each staged record [NT * U] u16 | tile offsets [K] u32.
 __host__ __device__ constexpr int pp_l1_u(int W) { return W <= 2 ? 4 : (W <= 4 ? 2 : 1); }
-__host__ __device__ constexpr size_t pp_l1_sorted_lds(int W) {
-    return (size_t)PP_NT * pp_l1_u(W) * W * 8 + (size_t)PP_NT * pp_l1_u(W) * 2 + 4 * (1u << PP_L1_BITS);
+__host__ __device__ constexpr size_t pp_l1_sorted_lds(int W) {  // + the staged level-2 digits (u16 each)
+    return (size_t)PP_NT * pp_l1_u(W) * W * 8 + (size_t)PP_NT * pp_l1_u(W) * 2 + 4 * (1u << PP_L1_BITS) +
+           (size_t)PP_NT * pp_l1_u(W) * 2;
 }
 
 template <int COUNT, int W, int NC>
@@ -828,11 +859,13 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
     l64* stage = (l64*)l1_dyn;
     l16* sbk = (l16*)(stage + (size_t)PP_NT * U * W);
     l32* toff = (l32*)(sbk + (size_t)PP_NT * U);
+    l16* sdg = (l16*)(toff + K);
     const PPChunk ch = chunks[blockIdx.x];
     for (u32 b = threadIdx.x; b < K; b += PP_NT) {
         hist[b] = 0;
         if (!COUNT) run[b] = part_off[(u64)ch.group * K + b] + off[(u64)blockIdx.x * K + b];
     }
+    uint16_t __attribute__((address_space(1)))* dig = (uint16_t __attribute__((address_space(1)))*)F.dig;
     __syncthreads();
     const u64 end = ch.start + ch.n;
     const u64 step = (u64)PP_NT * U;
@@ -849,7 +882,7 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
             pv[u] = F.has_pred ? pp_ld_width(F.pptr, F.pwidth, ii) : 0;
         }
     };
-    u32 bk[U], rk[U], m = 0;
+    u32 bk[U], rk[U], dg[U], m = 0;
     RegRec<W> rec[U];
     // selection mask, bucket and (scatter) record of the tile at base from v / pv
     auto assemble = [&](u64 base) {
@@ -880,7 +913,9 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
                     }
                 }
             }
-            bk[u] = (u32)(pp_mix(h) >> shift) & (K - 1);
+            const u64 mh = pp_mix(h);
+            bk[u] = (u32)(mh >> shift) & (K - 1);
+            dg[u] = (u32)(mh >> (shift - 16)) & 0xFFFF;
         }
     };
     if (COUNT) {
@@ -937,6 +972,7 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
 #pragma unroll
                     for (int k = 0; k < W; ++k) stage[(size_t)pos * W + k] = rec[u].r[k];
                     sbk[pos] = (u16)bk[u];
+                    sdg[pos] = (u16)dg[u];
                 }
                 __syncthreads();
                 // word q of the tile's staged records -> consecutive threads, consecutive words
@@ -944,9 +980,10 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
                 for (u32 q = threadIdx.x; q < nw; q += PP_NT) {
                     const u32 j = q / F.wpr, k = q - j * F.wpr;
                     const u32 b = sbk[j];
-                    u64 __attribute__((address_space(1)))* o =
-                        (u64 __attribute__((address_space(1)))*)(dst + (run[b] + (j - toff[b])) * (8 * F.wpr));
+                    const u64 di = run[b] + (j - toff[b]);
+                    u64 __attribute__((address_space(1)))* o = (u64 __attribute__((address_space(1)))*)(dst + di * (8 * F.wpr));
                     o[k] = stage[(size_t)j * W + k];
+                    if (dig && k == 0) dig[di] = sdg[j];  // the digit beside its record
                 }
             } else {
 #pragma unroll
@@ -956,6 +993,7 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
 #pragma unroll
                     for (int k = 0; k < W; ++k)
                         if ((u32)k < F.wpr) o[k] = rec[u].r[k];
+                    if (dig) dig[run[bk[u]] + rk[u]] = (uint16_t)dg[u];
                 }
             }
             __syncthreads();
