@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--exchange", choices=["abi", "torch"], default="abi",
                    help="N > 1, high cardinality: the library's RCCL exchange (dbg_agg_exchange / "
                         "dbg_agg_exchange_payload, what a Rust host drives) or torch.distributed all-to-all")
+    p.add_argument("--shuffle-chunks", type=int, default=4,
+                   help="before_partial at N > 1: add_groups in this many row chunks, each chunk's level-1 "
+                        "records shipped while the next chunk is scattered (dbg_agg_exchange_payload_chunk)")
     p.add_argument("--shuffle", choices=["auto", "before_partial", "before_merge"], default="auto",
                    help="N > 1, high cardinality: route level-1 records before any aggregation (group_by_shuffle_mode "
                         "= before_partial, partitioned payload) or partial states after it; auto = before_partial when "
@@ -296,6 +299,32 @@ def main():
             return pipe.drain()
         return 0
 
+    def dslice(c, lo, hi):  # rows [lo, hi) of a fixed-width non-null device column (a view)
+        from databend_amd.device import DeviceColumn
+        w = c.dtype.width
+        return DeviceColumn(c.dtype, c.data[lo * w:hi * w], None, None, hi - lo)
+
+    def chunked_shuffle(t, i):
+        """add_groups in row chunks, each chunk's level-1 records shipped while the next scatters."""
+        from databend_amd.exchange import PayloadShuffle
+        nchunk = args.shuffle_chunks
+        sh = None if comm is not None else PayloadShuffle(t, dev)
+        for c in range(nchunk):
+            lo, hi = (rows * c // nchunk) & ~7, (rows if c + 1 == nchunk else (rows * (c + 1) // nchunk) & ~7)
+            t.add_groups([dslice(x, lo, hi) for x in runner.key_abi[i]],
+                         [None if x is None else dslice(x, lo, hi) for x in runner.arg_cols[i]], rows=hi - lo, on_device=True)
+            if comm is not None:
+                comm.exchange_payload_chunk(t, last=c + 1 == nchunk)
+            else:
+                sh.ship()
+        if sh is not None:
+            sh.finish()
+
+    def chunkable(i):
+        cols = list(runner.key_abi[i]) + [x for x in runner.arg_cols[i] if x is not None]
+        return args.shuffle_chunks > 1 and runner.programs[i] is None and all(
+            x.dtype.width in (1, 2, 4, 8) and not x.dtype.nullable and x.offsets is None for x in cols)
+
     def step(k):
         if pipelined:
             return runner.pipe_step(k)
@@ -306,6 +335,10 @@ def main():
         i = k % len(runner.inputs)
         t = runner.table
         t.reset()
+        if before_partial and chunkable(i):  # the shuffle overlapped with level 1, chunk by chunk
+            chunked_shuffle(t, i)
+            n, sb = t.finalize()
+            return n
         t.add_groups(runner.key_abi[i], runner.arg_cols[i], rows=rows, filter_program=runner.programs[i], on_device=True)
         if before_partial:  # level-1 records to their partition's owner, aggregated once there
             if comm is not None:

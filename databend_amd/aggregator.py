@@ -430,6 +430,34 @@ class AggregateHashTable:
     def payload_export(self, n_ranks: int, dev_buf):
         check(lib().dbg_agg_payload_export(self.h, n_ranks, dev_buf.data_ptr()))
 
+    def payload_counts_from(self, first_seg):
+        """Counts of the level-1 segments from first_seg[kind] on: (counts [2][256], widths,
+        current segment counts) — one chunk of the chunked shuffle."""
+        import numpy as np
+        c = (C.c_uint64 * 512)()
+        w = (C.c_uint32 * 2)()
+        n = (C.c_uint32 * 2)()
+        f = (C.c_uint32 * 2)(*first_seg)
+        check(lib().dbg_agg_payload_counts_from(self.h, f, c, w, n))
+        return np.frombuffer(bytes(c), dtype=np.uint64).reshape(2, 256).copy(), (int(w[0]), int(w[1])), (int(n[0]), int(n[1]))
+
+    def payload_export_from(self, n_ranks: int, first_seg, dev_buf):
+        f = (C.c_uint32 * 2)(*first_seg)
+        check(lib().dbg_agg_payload_export_from(self.h, n_ranks, f, dev_buf.data_ptr()))
+
+    def payload_import_chunks(self, n_ranks: int, rank: int, chunk_counts, raws, states):
+        """chunk_counts: numpy u64 [n_chunks][n_ranks][2][256]; raws / states: per chunk the
+        received records (source-major), or None."""
+        import numpy as np
+        import torch
+        torch.cuda.current_stream().synchronize()
+        arr = np.ascontiguousarray(chunk_counts, dtype=np.uint64)
+        nc = arr.shape[0]
+        ptr = arr.ctypes.data_as(C.POINTER(C.c_uint64))
+        rp = (C.c_void_p * nc)(*[x.data_ptr() if x is not None else None for x in raws])
+        sp = (C.c_void_p * nc)(*[x.data_ptr() if x is not None else None for x in states])
+        check(lib().dbg_agg_payload_import_chunks(self.h, n_ranks, rank, nc, ptr, rp, sp))
+
     def payload_import(self, n_ranks: int, rank: int, all_counts, raw, state):
         """all_counts: numpy u64 [n_ranks][2][256]; raw / state: received records (source-major)."""
         import numpy as np

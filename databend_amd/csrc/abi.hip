@@ -194,6 +194,14 @@ struct dbg_agg_handle {
     // may reference them (merged since the last reset) — an exchange then allocates fresh ones
     DevBuf xrecv[2];
     bool xrecv_busy = false;
+    // chunked before-partial shuffle (dbg_agg_exchange_payload_chunk): level-1 segments from
+    // xfirst[k] on are not shipped yet; what arrived per call waits in xchunks until the last call
+    struct XChunk {
+        std::vector<u64> pc;  // [n][2][P] counts of the chunk, every source
+        DevBuf recv[2];
+    };
+    std::vector<XChunk> xchunks;
+    u32 xfirst[2] = {0, 0};
 
     // finalize state
     bool finalized = false;
@@ -901,6 +909,9 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto& b : h->owned) hipFree(b.p);
+    for (auto& x : h->xchunks)
+        for (auto& b : x.recv)
+            if (b.p) hipFree(b.p);
     for (auto& b : h->xrecv)
         if (b.p) hipFree(b.p);
     for (auto* p : h->pinned_chunks) hipHostFree(p);
@@ -962,6 +973,11 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     h->table_rows = 0;
     h->remerged = 0;
     h->xrecv_busy = false;  // no group references the exchange's receive buffers any more
+    for (auto& x : h->xchunks)  // an abandoned chunked shuffle (the last call never came)
+        for (auto& b : x.recv)
+            if (b.p) hipFree(b.p);
+    h->xchunks.clear();
+    h->xfirst[0] = h->xfirst[1] = 0;
     for (auto& K : h->ppk) {  // partitioned payload: records dropped, buffers kept (the mode too)
         K.l1_n = 0;
         K.dig_n = 0;
@@ -3110,6 +3126,15 @@ struct dbg_comm {
     u64 pay_send_cap = 0, pay_recv_cap[2] = {0, 0};
     u64* pay_dbuf = nullptr;  // counts all-gather: own row, then n rows
     u64 pay_dbuf_cap = 0;
+    // chunked payload shuffle: transfers on a stream of their own (overlapping the next chunk's
+    // level-1 work on the table's stream), two send buffers used in turn
+    hipStream_t xs = nullptr;
+    hipEvent_t xexp = nullptr;      // the table's stream after a chunk's export
+    hipEvent_t xsent[2] = {nullptr, nullptr};
+    bool xsent_valid[2] = {false, false};
+    u8* xsend[2] = {nullptr, nullptr};
+    u64 xsend_cap[2] = {0, 0};
+    int xi = 0;
 };
 
 extern "C" {
@@ -3144,7 +3169,11 @@ int dbg_comm_create(const uint8_t* id, int n_ranks, int rank, int device, dbg_co
     const u64 words = (2ull * n_ranks + 1) * (n_ranks + 1);  // own [2n + 1] sizes + ok word, then n rows
     if (dev_alloc((void**)&c->dsizes, words * 8) != DBG_OK || hipHostMalloc((void**)&c->hsizes, words * 8, hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->sent, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->merged, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->merged, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->xexp, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->xsent[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->xsent[1], hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking) != hipSuccess) {
         dbg_comm_destroy(c);
         return fail(DBG_ERR_OOM, "communicator scratch");
     }
@@ -3156,6 +3185,7 @@ void dbg_comm_destroy(dbg_comm* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->sent_valid) hipEventSynchronize(c->sent);
+    if (c->xs) hipStreamSynchronize(c->xs);
     RcclApi& R = rccl_api();
     if (c->comm && R.ok) R.CommDestroy(c->comm);
     if (c->dsizes) hipFree(c->dsizes);
@@ -3168,6 +3198,12 @@ void dbg_comm_destroy(dbg_comm* c) {
     if (c->hsizes) hipHostFree(c->hsizes);
     if (c->sent) hipEventDestroy(c->sent);
     if (c->merged) hipEventDestroy(c->merged);
+    for (int i = 0; i < 2; ++i) {
+        if (c->xsend[i]) hipFree(c->xsend[i]);
+        if (c->xsent[i]) hipEventDestroy(c->xsent[i]);
+    }
+    if (c->xexp) hipEventDestroy(c->xexp);
+    if (c->xs) hipStreamDestroy(c->xs);
     delete c;
 }
 
@@ -3186,39 +3222,56 @@ static int payload_check(dbg_agg_handle* h) {
     return DBG_OK;
 }
 
-int dbg_agg_payload_counts(dbg_agg_handle* h, uint64_t* part_counts, uint32_t* widths) {
-    if (!h || !part_counts) return fail(DBG_ERR_INVALID, "null argument");
-    HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_pending(h));
-    RETURN_IF(payload_check(h));
+// level-1 segments [first[k], end) of each record kind: per-partition counts
+static void payload_counts_range(const dbg_agg_handle* h, const u32 first[2], uint64_t* part_counts) {
     const u64 P = 1ull << PP_L1_BITS;
     for (int k = 0; k < 2; ++k) {
         for (u64 p = 0; p < P; ++p) part_counts[k * P + p] = 0;
-        for (const auto& sg : h->ppk[k].segs)
-            for (u64 p = 0; p < P; ++p) part_counts[k * P + p] += sg.off[p + 1] - sg.off[p];
+        const auto& segs = h->ppk[k].segs;
+        for (size_t i = first[k]; i < segs.size(); ++i)
+            for (u64 p = 0; p < P; ++p) part_counts[k * P + p] += segs[i].off[p + 1] - segs[i].off[p];
     }
+}
+
+int dbg_agg_payload_counts(dbg_agg_handle* h, uint64_t* part_counts, uint32_t* widths) {
+    const uint32_t first[2] = {0, 0};
+    return dbg_agg_payload_counts_from(h, first, part_counts, widths, nullptr);
+}
+
+int dbg_agg_payload_counts_from(dbg_agg_handle* h, const uint32_t first_seg[2], uint64_t* part_counts, uint32_t* widths,
+                                uint32_t* n_segs) {
+    if (!h || !part_counts || !first_seg) return fail(DBG_ERR_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    RETURN_IF(payload_check(h));
+    for (int k = 0; k < 2; ++k)
+        if (first_seg[k] > h->ppk[k].segs.size()) return fail(DBG_ERR_INVALID, "dbg_agg_payload_counts_from: first_seg past the payload");
+    payload_counts_range(h, first_seg, part_counts);
     if (widths) {
         widths[0] = h->spec.pp_rw_raw;
         widths[1] = h->spec.pp_rw_state;
     }
+    if (n_segs) {
+        n_segs[0] = (uint32_t)h->ppk[0].segs.size();
+        n_segs[1] = (uint32_t)h->ppk[1].segs.size();
+    }
     return DBG_OK;
 }
 
-int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf) {
-    if (!h || !dev_buf || n_ranks == 0 || n_ranks > (1u << PP_L1_BITS)) return fail(DBG_ERR_INVALID, "dbg_agg_payload_export: bad argument");
-    HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_pending(h));
-    RETURN_IF(payload_check(h));
+// segments [first[k], end) packed destination-major (partition-major within a destination, segment
+// order within a partition) into dev_buf, on the table's stream
+static int payload_export_range(dbg_agg_handle* h, u32 n_ranks, const u32 first[2], void* dev_buf) {
     u64 dst = 0;
     for (int k = 0; k < 2; ++k) {
         const auto& K = h->ppk[k];
         const u64 rw = k ? h->spec.pp_rw_state : h->spec.pp_rw_raw;
         std::vector<CopyRange> rs;
-        for (u32 d = 0; d < n_ranks; ++d) {  // destination-major, partition-major within a destination
+        for (u32 d = 0; d < n_ranks; ++d) {
             u32 lo, hi;
             payload_owned(d, n_ranks, lo, hi);
             for (u32 p = lo; p < hi; ++p)
-                for (const auto& sg : K.segs) {
+                for (size_t i = first[k]; i < K.segs.size(); ++i) {
+                    const auto& sg = K.segs[i];
                     const u64 n = sg.off[p + 1] - sg.off[p];
                     if (!n) continue;
                     if (!rs.empty() && rs.back().src + rs.back().n == (sg.base + sg.off[p]) * rw && rs.back().dst + rs.back().n == dst)
@@ -3236,40 +3289,58 @@ int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf) {
         launch_copy_ranges(h->stream, K.l1, (u8*)dev_buf, dr, (u32)rs.size());
         HIPCHECK(hipGetLastError());
     }
+    return DBG_OK;
+}
+
+int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf) {
+    const uint32_t first[2] = {0, 0};
+    return dbg_agg_payload_export_from(h, n_ranks, first, dev_buf);
+}
+
+int dbg_agg_payload_export_from(dbg_agg_handle* h, uint32_t n_ranks, const uint32_t first_seg[2], void* dev_buf) {
+    if (!h || !dev_buf || !first_seg || n_ranks == 0 || n_ranks > (1u << PP_L1_BITS))
+        return fail(DBG_ERR_INVALID, "dbg_agg_payload_export: bad argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    RETURN_IF(payload_check(h));
+    for (int k = 0; k < 2; ++k)
+        if (first_seg[k] > h->ppk[k].segs.size()) return fail(DBG_ERR_INVALID, "dbg_agg_payload_export_from: first_seg past the payload");
+    RETURN_IF(payload_export_range(h, n_ranks, first_seg, dev_buf));
     HIPCHECK(hipStreamSynchronize(h->stream));  // dev_buf is complete when the call returns
     return DBG_OK;
 }
 
-int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts, const void* raw_records,
-                           const void* state_records) {
-    if (!h || !part_counts || n_ranks == 0 || rank >= n_ranks || n_ranks > (1u << PP_L1_BITS))
-        return fail(DBG_ERR_INVALID, "dbg_agg_payload_import: bad argument");
-    HIPCHECK(hipSetDevice(h->device));
-    RETURN_IF(flush_pending(h));
-    RETURN_IF(payload_check(h));
+// The received records of n_chunks shipments become this rank's level-1 payload: per kind, chunk c's
+// buffer holds source-major (partition-major within a source) records of this rank's partitions;
+// part_counts[c][s][k][P]; one level-1 segment per (chunk, source).
+static int payload_import_chunks(dbg_agg_handle* h, u32 n_ranks, u32 rank, u32 n_chunks, const uint64_t* part_counts,
+                                 const void* const* raw, const void* const* state) {
     const u64 P = 1ull << PP_L1_BITS;
     u32 lo, hi;
     payload_owned(rank, n_ranks, lo, hi);
     for (int k = 0; k < 2; ++k) {
         auto& K = h->ppk[k];
         const u64 rw = k ? h->spec.pp_rw_state : h->spec.pp_rw_raw;
-        const void* src = k ? state_records : raw_records;
         std::vector<dbg_agg_handle::Seg> segs;
+        std::vector<u64> chunk_bytes(n_chunks, 0);
         u64 total = 0;
-        for (u32 s = 0; s < n_ranks; ++s) {  // one level-1 segment per source rank
-            const uint64_t* c = part_counts + ((u64)s * 2 + k) * P;
-            dbg_agg_handle::Seg sg{total, 0, std::vector<u64>(P + 1, 0)};
-            u64 run = 0;
-            for (u64 p = 0; p < P; ++p) {
-                sg.off[p] = run;
-                if (p >= lo && p < hi) run += c[p];
+        for (u32 c = 0; c < n_chunks; ++c)
+            for (u32 s = 0; s < n_ranks; ++s) {
+                const uint64_t* cnt = part_counts + (((u64)c * n_ranks + s) * 2 + k) * P;
+                dbg_agg_handle::Seg sg{total, 0, std::vector<u64>(P + 1, 0)};
+                u64 run = 0;
+                for (u64 p = 0; p < P; ++p) {
+                    sg.off[p] = run;
+                    if (p >= lo && p < hi) run += cnt[p];
+                }
+                sg.off[P] = run;
+                sg.n = run;
+                total += run;
+                chunk_bytes[c] += run * rw;
+                segs.push_back(std::move(sg));
             }
-            sg.off[P] = run;
-            sg.n = run;
-            total += run;
-            segs.push_back(std::move(sg));
-        }
-        if (total && !src) return fail(DBG_ERR_INVALID, "dbg_agg_payload_import: records missing");
+        for (u32 c = 0; c < n_chunks; ++c)
+            if (chunk_bytes[c] && !(k ? state[c] : raw[c])) return fail(DBG_ERR_INVALID, "dbg_agg_payload_import: records missing");
         HIPCHECK(hipStreamSynchronize(h->stream));  // the export has read the old payload
         if (total > K.l1_cap) {
             if (K.l1) HIPCHECK(hipFree(K.l1));
@@ -3278,7 +3349,11 @@ int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, c
             RETURN_IF(dev_alloc((void**)&K.l1, total * rw + 64));  // slack: the aggregation reads whole words
             K.l1_cap = total;
         }
-        if (total) HIPCHECK(hipMemcpyAsync(K.l1, src, total * rw, hipMemcpyDeviceToDevice, h->stream));
+        u64 at = 0;
+        for (u32 c = 0; c < n_chunks; ++c) {
+            if (chunk_bytes[c]) HIPCHECK(hipMemcpyAsync(K.l1 + at, k ? state[c] : raw[c], chunk_bytes[c], hipMemcpyDeviceToDevice, h->stream));
+            at += chunk_bytes[c];
+        }
         K.l1_n = total;
         K.dig_n = 0;  // imported records carry no digits
         K.segs = std::move(segs);
@@ -3286,7 +3361,24 @@ int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, c
     HIPCHECK(hipStreamSynchronize(h->stream));  // the caller may release the received buffers
     h->pp_grec_ready = false;
     h->finalized = false;
+    h->xfirst[0] = h->xfirst[1] = 0;
     return DBG_OK;
+}
+
+int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts, const void* raw_records,
+                           const void* state_records) {
+    return dbg_agg_payload_import_chunks(h, n_ranks, rank, 1, part_counts, &raw_records, &state_records);
+}
+
+int dbg_agg_payload_import_chunks(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, uint32_t n_chunks, const uint64_t* part_counts,
+                                  const void* const* raw_records, const void* const* state_records) {
+    if (!h || !part_counts || !raw_records || !state_records || n_chunks == 0 || n_ranks == 0 || rank >= n_ranks ||
+        n_ranks > (1u << PP_L1_BITS))
+        return fail(DBG_ERR_INVALID, "dbg_agg_payload_import: bad argument");
+    HIPCHECK(hipSetDevice(h->device));
+    RETURN_IF(flush_pending(h));
+    RETURN_IF(payload_check(h));
+    return payload_import_chunks(h, n_ranks, rank, n_chunks, part_counts, raw_records, state_records);
 }
 
 // Byte plan of the before-partial shuffle for one rank (host only): send_bytes[k * n + d] = this
@@ -3439,6 +3531,130 @@ int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats*
         stats->received_string_bytes = 0;
     }
     return DBG_OK;
+}
+
+// Chunked before-partial shuffle: ships the level-1 segments appended since the previous call
+// (one add_groups chunk, typically) while the caller goes on with the next chunk.  Per call: one
+// all-gather of the chunk's counts (and every rank's ok) on the communicator's stream — it needs
+// only the host-known segment counts, not the scatter's records; receive buffers for the chunk; a
+// collective ok; the export on the table's stream (behind the chunk's scatter) into one of two
+// send buffers; then the grouped send/recv on the communicator's stream behind that export — the
+// call returns without waiting for it, and the next add_groups' kernels on the table's stream
+// overlap the transfer.  The last call (last = 1) waits for every transfer and makes what arrived
+// the payload (one level-1 segment per chunk and source), like dbg_agg_exchange_payload.
+int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg_exchange_stats* stats) {
+    if (!c || !h) return fail(DBG_ERR_INVALID, "null argument");
+    if (h->device != c->device) return fail(DBG_ERR_INVALID, "communicator and table are on different devices");
+    RcclApi& R = rccl_api();
+    if (!R.ok) return fail(DBG_ERR_UNSUPPORTED, R.err);
+    HIPCHECK(hipSetDevice(c->device));
+    const u32 n = (u32)c->n, me = (u32)c->rank;
+    const u64 P = 1ull << PP_L1_BITS, W = 2 * P + 1;
+    hipStream_t s = h->stream, xs = c->xs;
+    std::vector<u64> mine(W, 0);
+    uint32_t widths[2] = {0, 0}, nseg[2] = {0, 0};
+    const int rc0 = dbg_agg_payload_counts_from(h, h->xfirst, mine.data(), widths, nseg);
+    mine[2 * P] = rc0 == DBG_OK ? 1 : 0;
+    // 1. the chunk's counts, every rank's, on the communicator's stream
+    if (c->pay_dbuf_cap < W * (n + 1)) {
+        HIPCHECK(hipStreamSynchronize(xs));
+        if (c->pay_dbuf) HIPCHECK(hipFree(c->pay_dbuf));
+        c->pay_dbuf = nullptr;
+        c->pay_dbuf_cap = 0;
+        RETURN_IF(dev_alloc((void**)&c->pay_dbuf, 8 * W * (n + 1)));
+        c->pay_dbuf_cap = W * (n + 1);
+    }
+    u64* dbuf = c->pay_dbuf;
+    std::vector<u64> all(W * n);
+    HIPCHECK(hipMemcpyAsync(dbuf, mine.data(), 8 * W, hipMemcpyHostToDevice, xs));
+    RCCLCHECK(R.AllGather(dbuf, dbuf + W, W, ncclUint64, c->comm, xs));
+    HIPCHECK(hipMemcpyAsync(all.data(), dbuf + W, 8 * W * n, hipMemcpyDeviceToHost, xs));
+    HIPCHECK(hipStreamSynchronize(xs));
+    for (u32 r = 0; r < n; ++r)
+        if (all[(u64)r * W + 2 * P] != 1)
+            return rc0 != DBG_OK ? rc0 : fail(DBG_ERR_UNSUPPORTED, "payload exchange: rank " + std::to_string(r) + " cannot take part");
+    // 2. plan, buffers (a collective ok before any transfer)
+    dbg_agg_handle::XChunk X;
+    X.pc.assign(2 * P * n, 0);
+    for (u32 r = 0; r < n; ++r)
+        for (u64 x = 0; x < 2 * P; ++x) X.pc[(u64)r * 2 * P + x] = all[(u64)r * W + x];
+    std::vector<u64> send_bytes(2 * n), recv_bytes(2 * n);
+    payload_plan(n, me, widths, X.pc.data(), send_bytes.data(), recv_bytes.data());
+    u64 kind_total[2] = {0, 0}, recv_total[2] = {0, 0};
+    for (int k = 0; k < 2; ++k)
+        for (u32 d = 0; d < n; ++d) {
+            kind_total[k] += send_bytes[(u64)k * n + d];
+            recv_total[k] += recv_bytes[(u64)k * n + d];
+        }
+    const int xi = c->xi;
+    int rc = DBG_OK;
+    if (c->xsent_valid[xi]) {  // this send buffer's previous transfer has left it
+        HIPCHECK(hipEventSynchronize(c->xsent[xi]));
+        c->xsent_valid[xi] = false;
+    }
+    if (kind_total[0] + kind_total[1] > c->xsend_cap[xi]) rc = grow_dev(&c->xsend[xi], &c->xsend_cap[xi], kind_total[0] + kind_total[1]);
+    for (int k = 0; k < 2 && rc == DBG_OK; ++k)
+        if (recv_total[k]) {
+            rc = dev_alloc(&X.recv[k].p, recv_total[k]);
+            if (rc == DBG_OK) X.recv[k].bytes = recv_total[k];
+        }
+    const std::string local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
+    int bad = -1;
+    RETURN_IF(all_ok(c, R, xs, rc == DBG_OK, &bad));
+    if (bad >= 0) {
+        for (auto& b : X.recv)
+            if (b.p) hipFree(b.p);
+        if (rc != DBG_OK) return fail(rc, local_err);
+        return fail(DBG_ERR_DEVICE, "payload exchange: rank " + std::to_string(bad) + " failed before the transfer");
+    }
+    // 3. export behind the chunk's scatter, transfer behind the export
+    const u32 first[2] = {h->xfirst[0], h->xfirst[1]};
+    RETURN_IF(payload_export_range(h, n, first, c->xsend[xi]));
+    HIPCHECK(hipEventRecord(c->xexp, s));
+    HIPCHECK(hipStreamWaitEvent(xs, c->xexp, 0));
+    RCCLCHECK(R.GroupStart());
+    for (int k = 0; k < 2; ++k) {
+        u64 so = k ? kind_total[0] : 0, ro = 0;
+        for (u32 p = 0; p < n; ++p) {
+            const u64 sb = send_bytes[(u64)k * n + p], rb = recv_bytes[(u64)k * n + p];
+            if (sb) RCCLCHECK(R.Send(c->xsend[xi] + so, sb, ncclUint8, (int)p, c->comm, xs));
+            if (rb) RCCLCHECK(R.Recv((u8*)X.recv[k].p + ro, rb, ncclUint8, (int)p, c->comm, xs));
+            so += sb;
+            ro += rb;
+        }
+    }
+    RCCLCHECK(R.GroupEnd());
+    HIPCHECK(hipEventRecord(c->xsent[xi], xs));
+    c->xsent_valid[xi] = true;
+    c->xi ^= 1;
+    h->xfirst[0] = nseg[0];
+    h->xfirst[1] = nseg[1];
+    h->xchunks.push_back(std::move(X));
+    if (stats) {
+        stats->sent_bytes = kind_total[0] + kind_total[1];
+        stats->remote_bytes = stats->sent_bytes - send_bytes[me] - send_bytes[(u64)n + me];
+        stats->received_records = 0;
+        for (int k = 0; k < 2; ++k) stats->received_records += recv_total[k] / std::max<u32>(widths[k], 1);
+        stats->received_string_bytes = 0;
+    }
+    if (!last) return DBG_OK;
+    // 4. the last chunk: every transfer done, the arrivals become the payload
+    HIPCHECK(hipStreamSynchronize(xs));
+    const u32 nc = (u32)h->xchunks.size();
+    std::vector<u64> pcs;
+    std::vector<const void*> raws(nc), states(nc);
+    for (u32 i = 0; i < nc; ++i) {
+        const auto& x = h->xchunks[i];
+        pcs.insert(pcs.end(), x.pc.begin(), x.pc.end());
+        raws[i] = x.recv[0].p;
+        states[i] = x.recv[1].p;
+    }
+    rc = payload_import_chunks(h, n, me, nc, pcs.data(), raws.data(), states.data());
+    for (auto& x : h->xchunks)
+        for (auto& b : x.recv)
+            if (b.p) hipFree(b.p);
+    h->xchunks.clear();
+    return rc;
 }
 
 // Byte plan of the before_merge exchange for one rank (host only; Payload::scatter's routing,

@@ -166,6 +166,62 @@ def exchange_payload(table, device) -> dict:
                 received_records=sum(recv[0]) // max(1, widths[0]) + sum(recv[1]) // max(1, widths[1]))
 
 
+class PayloadShuffle:
+    """The chunked before-partial shuffle over torch.distributed (the protocol
+    dbg_agg_exchange_payload_chunk runs over RCCL): after each add_groups chunk, `ship()` sends the
+    level-1 segments appended since the previous call — one all-gather of the chunk's counts, one
+    asynchronous all_to_all_single per record kind — and returns without waiting, so the next
+    chunk's level-1 work overlaps the transfer; `finish()` waits for every chunk and imports all of
+    them (one level-1 segment per chunk and source).  Every rank calls ship() the same number of
+    times."""
+
+    def __init__(self, table, device):
+        self.table, self.device = table, device
+        self.first = (0, 0)
+        self.chunks = []  # (all_counts [n][2][256], raw, state, works)
+
+    def ship(self) -> dict:
+        import numpy as np
+        import torch
+        dist = _dist()
+        world, rank = dist.get_world_size(), dist.get_rank()
+        counts, widths, nseg = self.table.payload_counts_from(self.first)
+        mine = torch.from_numpy(counts.astype(np.int64).reshape(-1)).to(self.device)
+        allc = torch.empty(world * mine.numel(), dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(allc, mine)
+        all_counts = allc.cpu().numpy().astype(np.uint64).reshape(world, 2, 256)
+        send, recv = payload_splits(counts, all_counts, widths, rank, world)
+        tot = [sum(send[0]), sum(send[1])]
+        buf = torch.empty(max(1, tot[0] + tot[1]), dtype=torch.uint8, device=self.device)
+        self.table.payload_export_from(world, self.first, buf)
+        got, works = [], []
+        for k in range(2):
+            inp = buf[(tot[0] if k else 0):(tot[0] if k else 0) + tot[k]]
+            out = torch.empty(max(1, sum(recv[k])), dtype=torch.uint8, device=self.device)
+            works.append(dist.all_to_all_single(out[:sum(recv[k])], inp, output_split_sizes=recv[k],
+                                                input_split_sizes=send[k], async_op=True))
+            got.append(out)
+        self.chunks.append((all_counts, got[0], got[1], works, buf))
+        self.first = nseg
+        sent = tot[0] + tot[1]
+        return dict(sent_bytes=sent, remote_bytes=sent - send[0][rank] - send[1][rank],
+                    received_records=sum(recv[0]) // max(1, widths[0]) + sum(recv[1]) // max(1, widths[1]))
+
+    def finish(self):
+        import numpy as np
+        dist = _dist()
+        for _, _, _, works, _ in self.chunks:
+            for w in works:
+                w.wait()
+        if not self.chunks:
+            return
+        cc = np.stack([c[0] for c in self.chunks])
+        self.table.payload_import_chunks(dist.get_world_size(), dist.get_rank(), cc, [c[1] for c in self.chunks],
+                                         [c[2] for c in self.chunks])
+        self.chunks = []
+        self.first = (0, 0)
+
+
 class AbiComm:
     """A communicator of the C ABI (dbg_comm_*): the exchange a Rust host drives without torch.
     `unique_id` is created by one rank and handed to every rank by the host's own channel (here
@@ -212,6 +268,16 @@ class AbiComm:
         from .ffi import check, lib
         st = abi.dbg_exchange_stats()
         check(lib().dbg_agg_exchange_payload(self.h, table.h, C.byref(st)))
+        return dict(sent_bytes=st.sent_bytes, remote_bytes=st.remote_bytes, received_records=st.received_records)
+
+    def exchange_payload_chunk(self, table, last: bool) -> dict:
+        """dbg_agg_exchange_payload_chunk: ship the segments since the previous call (asynchronous);
+        last=True also waits for every chunk and imports them."""
+        import ctypes as C
+        from . import abi
+        from .ffi import check, lib
+        st = abi.dbg_exchange_stats()
+        check(lib().dbg_agg_exchange_payload_chunk(self.h, table.h, 1 if last else 0, C.byref(st)))
         return dict(sent_bytes=st.sent_bytes, remote_bytes=st.remote_bytes, received_records=st.received_records)
 
     def close(self):

@@ -25,7 +25,8 @@ EXPORTED = [
     "dbg_agg_record_layout", "dbg_agg_set_host_staging",
     "dbg_take_string", "dbg_legacy_hash_method", "dbg_legacy_group_hash", "dbg_agg_serialized_stride", "dbg_agg_result_serialized", "dbg_agg_merge_serialized", "dbg_comm_get_unique_id", "dbg_comm_create", "dbg_comm_destroy", "dbg_agg_exchange",
     "dbg_agg_payload_counts", "dbg_agg_payload_export", "dbg_agg_payload_import", "dbg_agg_exchange_payload",
-    "dbg_payload_exchange_plan", "dbg_merge_exchange_plan",
+    "dbg_payload_exchange_plan", "dbg_merge_exchange_plan", "dbg_agg_payload_counts_from", "dbg_agg_payload_export_from",
+    "dbg_agg_payload_import_chunks", "dbg_agg_exchange_payload_chunk",
     "dbg_scan_create", "dbg_scan_destroy", "dbg_parquet_chunk_rows", "dbg_parquet_decode",
     "dbg_native_decode",
 ]
@@ -115,6 +116,10 @@ def lib():
         L.dbg_agg_payload_export.argtypes = [VP, C.c_uint32, VP]
         L.dbg_agg_payload_import.argtypes = [VP, C.c_uint32, C.c_uint32, P(U64), VP, VP]
         L.dbg_agg_exchange_payload.argtypes = [VP, VP, P(abi.dbg_exchange_stats)]
+        L.dbg_agg_payload_counts_from.argtypes = [VP, P(C.c_uint32), P(U64), P(C.c_uint32), P(C.c_uint32)]
+        L.dbg_agg_payload_export_from.argtypes = [VP, C.c_uint32, P(C.c_uint32), VP]
+        L.dbg_agg_payload_import_chunks.argtypes = [VP, C.c_uint32, C.c_uint32, C.c_uint32, P(U64), P(VP), P(VP)]
+        L.dbg_agg_exchange_payload_chunk.argtypes = [VP, VP, C.c_int, P(abi.dbg_exchange_stats)]
         L.dbg_payload_exchange_plan.argtypes = [P(abi.dbg_agg_params), C.c_uint32, C.c_uint32, P(C.c_uint64), P(C.c_uint32),
                                                 P(C.c_uint64), P(C.c_uint64)]
         L.dbg_merge_exchange_plan.argtypes = [P(abi.dbg_agg_params), C.c_uint32, C.c_uint32, P(C.c_uint64), P(C.c_uint32),

@@ -431,6 +431,26 @@ int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf);
 int dbg_agg_payload_import(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, const uint64_t* part_counts /* n x 2 x 256 */,
                            const void* raw_records, const void* state_records);
 int dbg_agg_exchange_payload(dbg_comm* c, dbg_agg_handle* h, dbg_exchange_stats* stats);
+/* Chunked form, overlapping the transfer with the next chunk's level-1 work.  The payload is a
+ * list of level-1 segments (one per add_groups batch); the _from variants count / export the
+ * segments from first_seg[kind] on (n_segs receives the current segment counts, may be NULL);
+ * import_chunks takes n_chunks shipments: raw_records[c] / state_records[c] laid out as for
+ * dbg_agg_payload_import, part_counts[c][source][kind][p].
+ * dbg_agg_exchange_payload_chunk ships the segments appended since its previous call on this
+ * handle: the chunk's counts all-gathered on the communicator's own stream (no wait for the
+ * chunk's scatter), receive buffers per chunk, a collective ok, the export on the table's stream
+ * into one of two send buffers, and the grouped send/recv on the communicator's stream behind
+ * it — it returns without waiting, so the caller's next add_groups overlaps the transfer.  With
+ * last = 1 it also waits for every transfer and imports all chunks (one level-1 segment per chunk
+ * and source); until then the handle's finalize must not run.  Every rank makes the same number
+ * of calls.  dbg_agg_reset drops an unfinished shuffle's arrivals. */
+int dbg_agg_payload_counts_from(dbg_agg_handle* h, const uint32_t first_seg[2], uint64_t* part_counts /* 2 x 256 */,
+                                uint32_t* widths, uint32_t* n_segs /* 2 */);
+int dbg_agg_payload_export_from(dbg_agg_handle* h, uint32_t n_ranks, const uint32_t first_seg[2], void* dev_buf);
+int dbg_agg_payload_import_chunks(dbg_agg_handle* h, uint32_t n_ranks, uint32_t rank, uint32_t n_chunks,
+                                  const uint64_t* part_counts /* n_chunks x n x 2 x 256 */, const void* const* raw_records,
+                                  const void* const* state_records);
+int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg_exchange_stats* stats);
 /* The byte plan dbg_agg_exchange_payload follows on rank `rank` (host only, no device work):
  * all_counts[source][kind][p] (n x 2 x 256) as gathered; widths[kind] receives the params' payload
  * record bytes (may be NULL); send_bytes[kind * n + d] = this rank's kind records of the partitions

@@ -134,3 +134,94 @@ def test_exchange_payload_rccl_world_1():
     comm.close()
     ok, oa = oracle_aggregate(keys, aggs)
     assert_results_equal(gk, ga, ok, oa)
+
+
+def test_payload_chunked_import_two_ranks_on_one_gpu():
+    """the chunked primitives (counts / export from a segment, import of several chunks): each
+    rank's batches shipped one at a time, routed like the all-to-all, imported as chunks."""
+    import torch
+    (k0, a0), (k1, a1) = _data(12, 240_000), _data(13, 180_000)
+    k1[0].data[:90_000] = k0[0].data[:90_000]
+    k1[1].data[:90_000] = k0[1].data[:90_000]
+    from tests.test_gpu_parity import slice_col
+    fns = [F.get(n, [], [c.dtype] if c is not None else []) for n, c in a0]
+    tabs = []
+    for keys in (k0, k1):
+        t = AggregateHashTable(AggregatorParams([k.dtype for k in keys], fns), HashTableConfig(True))
+        t.set_strategy(abi.STRATEGY_PARTITIONED)
+        tabs.append(t)
+    data = [(k0, a0), (k1, a1)]
+    first = [(0, 0), (0, 0)]
+    chunks = [[], []]  # per destination rank: (all_counts, raw, state) per chunk
+    for c in range(3):  # three add_groups chunks per rank, each shipped before the next is added
+        cws, bufs, splits = [], [], []
+        for r, t in enumerate(tabs):
+            keys, aggs = data[r]
+            n = len(keys[0])
+            lo, hi = n * c // 3, n * (c + 1) // 3
+            t.add_groups([DeviceColumn.from_host(slice_col(k, lo, hi)) for k in keys],
+                         [None if x is None else DeviceColumn.from_host(slice_col(x, lo, hi)) for _, x in aggs],
+                         rows=hi - lo, on_device=True)
+            cws.append(t.payload_counts_from(first[r]))
+        all_counts = np.stack([cw[0] for cw in cws])
+        widths = cws[0][1]
+        for r, t in enumerate(tabs):
+            send, recv = payload_splits(cws[r][0], all_counts, widths, r, 2)
+            b = torch.empty(max(1, sum(send[0]) + sum(send[1])), dtype=torch.uint8, device="cuda")
+            t.payload_export_from(2, first[r], b)
+            bufs.append(b)
+            splits.append(send)
+            first[r] = cws[r][2]
+        torch.cuda.synchronize()
+        for r in range(2):
+            got = []
+            for k in range(2):
+                parts = []
+                for s in range(2):
+                    base = 0 if k == 0 else sum(splits[s][0])
+                    off = base + sum(splits[s][k][:r])
+                    parts.append(bufs[s][off:off + splits[s][k][r]].clone())
+                got.append(torch.cat(parts) if sum(x.numel() for x in parts) else None)
+            chunks[r].append((all_counts, got[0], got[1]))
+    for r, t in enumerate(tabs):
+        cc = np.stack([x[0] for x in chunks[r]])
+        t.payload_import_chunks(2, r, cc, [x[1] for x in chunks[r]], [x[2] for x in chunks[r]])
+    res = [_result(t, len(a0)) for t in tabs]
+    for t in tabs:
+        t.close()
+    keys = [_cat(k0[i], k1[i]) for i in range(2)]
+    aggs = [(n, None if c is None else _cat(c, a1[j][1])) for j, (n, c) in enumerate(a0)]
+    ok, oa = oracle_aggregate(keys, aggs)
+    gk = [_cat(res[0][0][i], res[1][0][i]) for i in range(2)]
+    ga = [_cat(res[0][1][j], res[1][1][j]) for j in range(len(aggs))]
+    assert_results_equal(gk, ga, ok, oa)
+    s0 = set(zip(res[0][0][0].values(), res[0][0][1].values()))
+    s1 = set(zip(res[1][0][0].values(), res[1][0][1].values()))
+    assert not (s0 & s1) and s0 and s1
+
+
+def test_exchange_payload_chunk_rccl_world_1():
+    """dbg_agg_exchange_payload_chunk at world size 1: three add_groups chunks, each shipped (self
+    send / receive on the communicator's stream) before the next is added, the last call importing."""
+    from databend_amd.exchange import AbiComm
+    from tests.test_gpu_parity import slice_col
+    keys, aggs = _data(14, 300_000)
+    fns = [F.get(n, [], [c.dtype] if c is not None else []) for n, c in aggs]
+    t = AggregateHashTable(AggregatorParams([k.dtype for k in keys], fns), HashTableConfig(True))
+    t.set_strategy(abi.STRATEGY_PARTITIONED)
+    comm = AbiComm(AbiComm.unique_id(), 1, 0, 0)
+    received = 0
+    for c in range(3):
+        lo, hi = 100_000 * c, 100_000 * (c + 1)
+        t.add_groups([DeviceColumn.from_host(slice_col(k, lo, hi)) for k in keys],
+                     [None if x is None else DeviceColumn.from_host(slice_col(x, lo, hi)) for _, x in aggs],
+                     rows=hi - lo, on_device=True)
+        st = comm.exchange_payload_chunk(t, last=(c == 2))
+        assert st["remote_bytes"] == 0
+        received += st["received_records"]
+    assert received == 300_000
+    gk, ga = _result(t, len(aggs))
+    t.close()
+    comm.close()
+    ok, oa = oracle_aggregate(keys, aggs)
+    assert_results_equal(gk, ga, ok, oa)

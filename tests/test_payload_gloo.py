@@ -106,6 +106,101 @@ def test_payload_shuffle_protocol(world):
     assert all(v == "ok" for v in res.values()), res
 
 
+class FakeChunkedPayload:
+    """A payload of several level-1 segments (one per add_groups chunk): counts / export from a
+    segment on, and the chunked import.  Records: [src << 40 | seg << 32 | part << 16 | serial]."""
+
+    def __init__(self, rank, seed, n_segs):
+        rng = np.random.default_rng(seed)
+        self.rank = rank
+        self.segs = [rng.integers(0, 12, (2, 256)).astype(np.uint64) for _ in range(n_segs)]
+        for c in self.segs:
+            c[1, rng.random(256) < 0.7] = 0
+        self.widths = (8, 16)
+        self.n_visible = 0  # segments appended so far (the test appends them one ship at a time)
+        self.imported = None
+
+    def rec(self, k, g, p, i):
+        v = (self.rank << 40) | (g << 32) | (p << 16) | i
+        return [v] if k == 0 else [v, ~v & ((1 << 63) - 1)]
+
+    def payload_counts_from(self, first):
+        c = np.zeros((2, 256), np.uint64)
+        for k in range(2):
+            for g in range(first[k], self.n_visible):
+                c[k] += self.segs[g][k]
+        return c, self.widths, (self.n_visible, self.n_visible)
+
+    def payload_export_from(self, n, first, buf):
+        from databend_amd.exchange import payload_owned
+        words = []
+        for k in range(2):
+            for d in range(n):
+                lo, hi = payload_owned(d, n)
+                for p in range(lo, hi):
+                    for g in range(first[k], self.n_visible):
+                        for i in range(int(self.segs[g][k][p])):
+                            words += self.rec(k, g, p, i)
+        if words:
+            b = np.array(words, dtype=np.uint64).view(np.uint8)
+            buf[:len(b)] = __import__("torch").from_numpy(b.copy())
+
+    def payload_import_chunks(self, n, rank, cc, raws, states):
+        self.imported = (cc.copy(), [r.numpy().copy() for r in raws], [s.numpy().copy() for s in states])
+
+
+def _chunk_worker(rank, world, port, q, n_segs):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from databend_amd.exchange import PayloadShuffle, payload_owned
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = FakeChunkedPayload(rank, 200 + rank, n_segs)
+        sh = PayloadShuffle(t, "cpu")
+        for g in range(n_segs):  # one add_groups chunk, then its shipment
+            t.n_visible = g + 1
+            sh.ship()
+        sh.finish()
+        cc, raws, states = t.imported
+        assert cc.shape == (n_segs, world, 2, 256)
+        lo, hi = payload_owned(rank, world)
+        for g in range(n_segs):  # chunk g: source-major, partition-major within a source
+            for k, buf in ((0, raws[g]), (1, states[g])):
+                words = buf[:buf.size // 8 * 8].view(np.uint64)
+                exp = []
+                for s in range(world):
+                    src = FakeChunkedPayload(s, 200 + s, n_segs)
+                    assert (cc[g][s] == src.segs[g]).all()
+                    for p in range(lo, hi):
+                        for i in range(int(src.segs[g][k][p])):
+                            exp += src.rec(k, g, p, i)
+                assert list(words[:len(exp)]) == exp, (rank, g, k)
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_chunked_payload_shuffle_protocol(world):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_chunk_worker, args=(r, world, port, q, 3)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
+
+
 def test_payload_owned_covers_every_partition_once():
     from databend_amd.exchange import payload_owned
     for n in (1, 2, 3, 4, 5, 7, 8, 16, 256):
