@@ -27,6 +27,19 @@
 #define PP_AU 4                  // raw records per thread in flight (aggregation)
 #define PP_MAXK 1024
 #define PP_WINDOW 96
+// the literal pp_agg instances: PP_LIT_PER_CU workgroups of PP_LIT_NT lanes per CU, PP_LIT_RPT
+// records per lane.  C4 pp_agg: 512 x 16 (8 waves per CU) 36.4 ms, 1024 x 8 (16 waves: the inserts'
+// LDS round trips hidden by twice the waves) 32.1 ms; two 512 x 8 workgroups per CU cap a partition
+// at 4096 records, below what 18 partition bits leave C4 (3815 on average): the generic path, 58 ms
+#ifndef PP_LIT_NT
+#define PP_LIT_NT 1024
+#endif
+#ifndef PP_LIT_RPT
+#define PP_LIT_RPT 8
+#endif
+#ifndef PP_LIT_PER_CU
+#define PP_LIT_PER_CU 1  // workgroups per CU (each with 1 / PP_LIT_PER_CU of the LDS)
+#endif
 
 typedef __attribute__((address_space(3))) u8 l8;
 typedef __attribute__((address_space(3))) u16 l16;
@@ -2209,9 +2222,9 @@ static bool ps_desc(const Spec& S, PsDesc& D, u32& W) {
 }
 
 #define PS_LDS (152 * 1024)  // one workgroup per CU: the largest table, the fewest rounds
-static u32 ps_cap(u32 bw, u32 w) {
-    u32 cap = (u32)((PS_LDS - ps_lds_bytes(0, bw, w, PP_SPEC_NT) - 64) / (4 + 8 * bw + 2)) & ~3u;
-    while (cap > 64 && ps_lds_bytes(cap, bw, w, PP_SPEC_NT) + 64 > PS_LDS) cap -= 4;
+static u32 ps_cap(u32 bw, u32 w, u32 nt = PP_SPEC_NT, size_t budget = PS_LDS) {
+    u32 cap = (u32)((budget - ps_lds_bytes(0, bw, w, nt) - 64) / (4 + 8 * bw + 2)) & ~3u;
+    while (cap > 64 && ps_lds_bytes(cap, bw, w, nt) + 64 > budget) cap -= 4;
     return std::min<u32>(cap, 65532);
 }
 
@@ -2313,7 +2326,7 @@ struct PsShape {
 };
 
 template <int MODE, int W, int RPT, int SNT, int K0, int K1, int A0, int A1, int A2>
-__global__ void __launch_bounds__(SNT, 1) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
+__global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
                                                                u32 sub_bits, u32 cap, PPAggOut out, u32* __restrict__ spill, u32 spill_cap) {
     typedef PsShape<K0, K1, A0, A1, A2> SH;
     constexpr u32 KW = SH::KW, BW = SH::BW;
@@ -2650,8 +2663,8 @@ static int ps_literal_shape(const Spec& S, u32* cap, u32* max_records) {
     PS_SHAPES(PS_TRY)
 #undef PS_TRY
     if (found >= 0) {
-        *cap = ps_cap(bw, w);
-        *max_records = PP_SPEC_NT * PP_SPEC_RPT;
+        *cap = ps_cap(bw, w, PP_LIT_NT, PS_LDS / PP_LIT_PER_CU);
+        *max_records = PP_LIT_NT * PP_LIT_RPT;
     }
     return found;
 }
@@ -2659,21 +2672,21 @@ static int ps_literal_shape(const Spec& S, u32* cap, u32* max_records) {
 static void launch_ps_literal(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
                               const PPAggOut& out, u32* spill, u32 spill_cap) {
     if (!n_parts) return;
-    const u32 grid = n_parts < 256 ? n_parts : 256;  // one persistent workgroup per CU
+    const u32 grid = n_parts < 256u * PP_LIT_PER_CU ? n_parts : 256u * PP_LIT_PER_CU;  // persistent workgroups
     // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
     const char* cx = getenv("DBG_X_PPSPEC_CAP");
     const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
     int id = 0;
 #define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
     if (shape == id) {                                                                                                  \
-        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW), cap_x);                          \
-        const size_t lds = ps_lds_bytes(cap, bw, WW, PP_SPEC_NT) + 16;                                                  \
+        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW, PP_LIT_NT, PS_LDS / PP_LIT_PER_CU), cap_x); \
+        const size_t lds = ps_lds_bytes(cap, bw, WW, PP_LIT_NT) + 16;                                                   \
         if (mode == 0)                                                                                                  \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
-                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_LIT_RPT, PP_LIT_NT, K0, K1, A0, A1, A2>), dim3(grid),         \
+                               dim3(PP_LIT_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);      \
         else                                                                                                            \
-            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_SPEC_RPT, PP_SPEC_NT, K0, K1, A0, A1, A2>), dim3(grid),       \
-                               dim3(PP_SPEC_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);     \
+            hipLaunchKernelGGL((pp_agg_spec_kernel<1, WW, PP_LIT_RPT, PP_LIT_NT, K0, K1, A0, A1, A2>), dim3(grid),         \
+                               dim3(PP_LIT_NT), lds, s, n_parts, raw_off, raw, sub_bits, cap, out, spill, spill_cap);      \
     }                                                                                                                   \
     ++id;
     PS_SHAPES(PS_LAUNCH)
