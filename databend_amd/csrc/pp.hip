@@ -605,8 +605,11 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* wtot, u32& total) {
 // per-thread LDS scratch slot where a raw row's record is built (W == 0).  Three barriers per tile;
 // the records of one bucket land contiguously within the tile, so the XCD's L2 merges them into
 // whole lines.  LDS: hist u32 [K] | run u64 [K] | scratch [T * U * rw] (W == 0).
+#ifndef PP_DIRECT_U2
+#define PP_DIRECT_U2 4  // records per thread per tile at W <= 2 (8: longer runs, half the occupancy — C4 level 2 14.8 -> 17.2 ms)
+#endif
 __host__ __device__ __forceinline__ u32 pp_direct_u(int W, u32 rw) {  // rows per thread per step
-    if (W > 0) return W <= 2 ? 4 : (W <= 4 ? 2 : 1);
+    if (W > 0) return W <= 2 ? PP_DIRECT_U2 : (W <= 4 ? 2 : 1);
     const u32 u = PP_SCRATCH_BYTES / (PP_NT * rw);
     return u >= 4 ? 4 : (u >= 1 ? u : 1);
 }
@@ -650,7 +653,7 @@ __global__ void __launch_bounds__(PP_NT) pp_scatter_direct_kernel(const Spec* __
     l32* hist = (l32*)lds_raw;
     l64* run = (l64*)(hist + K + (K & 1));
     l8* scratch = (l8*)(run + K);
-    constexpr u32 UMAX = 4;
+    constexpr u32 UMAX = (W > 0 && W <= 2) ? PP_DIRECT_U2 : 4;
     const u32 U = pp_direct_u(W, rw);
     const u32 T = W > 0 ? PP_NT : pp_direct_t(rw);
     const PPChunk ch = chunks[blockIdx.x];
