@@ -1824,7 +1824,7 @@ __device__ __forceinline__ u64 ps_arg(const PsDesc& D, const RegRec<W>& r, u32 a
 }
 
 template <int MODE, int W, int RPT, int SNT>
-__global__ void __launch_bounds__(SNT, 1) pp_agg_desc_kernel(const PsDesc D, u32 n_parts, const u64* __restrict__ raw_off,
+__global__ void __launch_bounds__(SNT, SNT / 256) pp_agg_desc_kernel(const PsDesc D, u32 n_parts, const u64* __restrict__ raw_off,
                                                                const u8* __restrict__ raw, u32 sub_bits, u32 cap, PPAggOut out,
                                                                u32* __restrict__ spill, u32 spill_cap) {
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
@@ -2130,14 +2130,15 @@ __global__ void __launch_bounds__(SNT, 1) pp_agg_desc_kernel(const PsDesc D, u32
     }
 }
 
-#define PP_SPEC_NT 512
+#define PP_SPEC_NT 1024  // 16 waves per CU (C4 shape: 512 lanes x 16 records 36 ms, 1024 x 8 32 ms)
 #define PS_MAXW 6  // raw record words: 16 key bytes + 4 x 8 argument bytes
 // records per lane: the two register sets (the partition and the next one's prefetch) stay at
 // <= 128 VGPRs
 #ifndef PS_RPT2
-#define PS_RPT2 16
+#define PS_RPT2 8
 #endif
-__host__ __device__ constexpr int ps_rpt(int w) { return w <= 1 ? 16 : (w <= 2 ? PS_RPT2 : (w <= 4 ? 8 : 4)); }
+// records per lane (x PP_SPEC_NT lanes: 8192 records at W <= 2, 4096 at W <= 4, 2048 beyond)
+__host__ __device__ constexpr int ps_rpt(int w) { return w <= 1 ? 8 : (w <= 2 ? PS_RPT2 : (w <= 4 ? 4 : 2)); }
 
 static bool ps_int_type(int t) {
     return t == DBG_INT8 || t == DBG_INT16 || t == DBG_INT32 || t == DBG_INT64 || t == DBG_UINT8 || t == DBG_UINT16 ||
