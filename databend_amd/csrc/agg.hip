@@ -3005,21 +3005,38 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
 
 // Fused finalize tail: bit-pack every nullable output's validity and close the string offsets,
 // with the group count read from device memory (totals[0]; totals[1 + c] string bytes).
+// 8 flag bytes (any nonzero = set) -> 8 bits, LSB first
+__device__ __forceinline__ u32 pack8(u64 x) {
+    const u64 hi = 0x8080808080808080ULL, lo7 = 0x7F7F7F7F7F7F7F7FULL;
+    const u64 nz = (((x & lo7) + lo7) | x) & hi;  // bit 7 of every nonzero byte
+    return (u32)(((nz >> 7) * 0x0102040810204080ULL) >> 56);
+}
+
+// bytes [8k, 8k + 8) -> bits byte k: one 8-byte load per lane (consecutive lanes, consecutive
+// words) where whole and aligned
+__device__ __forceinline__ void pack_bits_at(const u8* __restrict__ bytes, u64 n, u8* __restrict__ bits, u64 k) {
+    const u64 i0 = k * 8;
+    if (i0 >= n) return;
+    u32 b = 0;
+    if (i0 + 8 <= n && !((uintptr_t)(bytes + i0) & 7)) {
+        b = pack8(*(const u64*)(bytes + i0));
+    } else {
+        for (u64 i = i0; i < n && i < i0 + 8; ++i)
+            if (bytes[i]) b |= 1u << (i - i0);
+    }
+    bits[k] = (u8)b;
+}
+
 __global__ void finish_outputs_kernel(OutDesc out, const u64* totals, int n_keys, int n_aggs) {
     u64 n = totals[0];
     if (n > out.cap_groups) n = out.cap_groups;
-    u64 nb = (n + 7) / 8;
+    const u64 nb = (n + 7) / 8;
     for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) {
         for (int c = 0; c < n_keys + n_aggs; ++c) {
             const u8* bytes = c < n_keys ? out.key_valid[c] : out.agg_valid[c - n_keys];
             u8* bits = c < n_keys ? out.key_bits[c] : out.agg_bits[c - n_keys];
             if (!bytes || !bits) continue;
-            u8 b = 0;
-            for (int j = 0; j < 8; ++j) {
-                u64 i = k * 8 + j;
-                if (i < n && bytes[i]) b |= (u8)(1u << j);
-            }
-            bits[k] = b;
+            pack_bits_at(bytes, n, bits, k);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -3042,15 +3059,8 @@ void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& S, const
 }
 
 __global__ void pack_bits_kernel(const u8* bytes, u64 n, u8* bits) {
-    u64 nb = (n + 7) / 8;
-    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) {
-        u8 b = 0;
-        for (int j = 0; j < 8; ++j) {
-            u64 i = k * 8 + j;
-            if (i < n && bytes[i]) b |= (u8)(1u << j);
-        }
-        bits[k] = b;
-    }
+    const u64 nb = (n + 7) / 8;
+    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) pack_bits_at(bytes, n, bits, k);
 }
 
 void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits) {
