@@ -1212,6 +1212,12 @@ static PPFast pp_fast_desc(const Spec& S, const BatchDesc& B, u32 bid, int kind)
     return F;
 }
 
+// a result that is never NULL for a group: the aggregate's argument is never NULL (COUNT(*) or a
+// non-nullable column), and SUM / AVG / MIN / MAX of one or more values is a value
+static bool agg_always_valid(const DAgg& A) {
+    return A.arg_type < 0 || !A.arg_nullable;
+}
+
 static int pp_count_scan(dbg_agg_handle* h, int level, int src, int kind, const u8* recs, const std::vector<PPChunk>& ch,
                          const std::vector<u32>& c0, u32 shift, u32 kbits, u64* part_out, const PPFast* F = nullptr,
                          bool counted = false, const u16* dig = nullptr) {
@@ -1910,7 +1916,10 @@ static int result_impl(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_colu
         }
         if (on_device) od.agg_data[a] = out_aggs[a].data;
         else rc = tmp(n * type_width(t.type), &od.agg_data[a]);
-        if (rc == DBG_OK && t.nullable) rc = tmp(n, (void**)&od.agg_valid[a]);
+        if (rc == DBG_OK && t.nullable) {
+            if (agg_always_valid(S.aggs[a])) od.all_valid |= 1u << a;
+            else rc = tmp(n, (void**)&od.agg_valid[a]);
+        }
     }
     if (rc != DBG_OK) {
         free_temps();
@@ -1984,7 +1993,8 @@ static int result_impl(dbg_agg_handle* h, dbg_out_column* out_aggs, dbg_out_colu
                 free_temps();
                 return DBG_ERR_OOM;
             }
-            if (bits) launch_pack_bits(h->stream, od.agg_valid[a], n, bits);
+            if (bits && od.agg_valid[a]) launch_pack_bits(h->stream, od.agg_valid[a], n, bits);
+            else if (bits) launch_fill_valid(h->stream, n, bits);
             if (!on_device && out_aggs[a].validity)
                 hipMemcpyAsync(out_aggs[a].validity, bits, (n + 7) / 8, hipMemcpyDeviceToHost, h->stream);
         }
@@ -2139,9 +2149,13 @@ static int fin_launch(dbg_agg_handle* h) {
     for (int a = 0; a < S.n_aggs; ++a) {
         od.agg_data[a] = F.aggs[a].data;
         if (h->result_types[a].nullable) {
-            od.agg_valid[a] = vb;
             od.agg_bits[a] = F.aggs[a].validity;
-            vb += F.max_groups + 1;
+            if (agg_always_valid(S.aggs[a])) {
+                od.all_valid |= 1u << a;
+            } else {
+                od.agg_valid[a] = vb;
+                vb += F.max_groups + 1;
+            }
         }
     }
     if (h->pp) {

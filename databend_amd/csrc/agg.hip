@@ -1814,7 +1814,7 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
     bool has_bits = false, dec_err = false;  // uniform
     for (int c = 0; c < S.n_keys; ++c) has_bits |= out.key_valid[c] && out.key_bits[c];
     for (int a = 0; a < S.n_aggs; ++a) {
-        has_bits |= out.agg_valid[a] && out.agg_bits[a];
+        has_bits |= (out.agg_valid[a] || ((out.all_valid >> a) & 1)) && out.agg_bits[a];
         dec_err |= S.aggs[a].dec_check || (S.aggs[a].kind == DBG_AGG_AVG && S.aggs[a].sumk == SUMK_I128);
     }
     // the table counters, in flight while the table is scanned (final: every inserting workgroup
@@ -1895,6 +1895,10 @@ __device__ __forceinline__ bool finalize_small_body(const Spec& S, const BatchDe
             {
                 const u8* bytes = c < S.n_keys ? out.key_valid[c] : out.agg_valid[c - S.n_keys];
                 u8* bits = c < S.n_keys ? out.key_bits[c] : out.agg_bits[c - S.n_keys];
+                if (!bytes && bits && c >= S.n_keys && ((out.all_valid >> (c - S.n_keys)) & 1)) {
+                    bits[k] = all_valid_byte(n, k);
+                    continue;
+                }
                 if (!bytes || !bits) continue;
                 u8 b = 0;
                 for (int j = 0; j < 8; ++j) {
@@ -3035,6 +3039,10 @@ __global__ void finish_outputs_kernel(OutDesc out, const u64* totals, int n_keys
         for (int c = 0; c < n_keys + n_aggs; ++c) {
             const u8* bytes = c < n_keys ? out.key_valid[c] : out.agg_valid[c - n_keys];
             u8* bits = c < n_keys ? out.key_bits[c] : out.agg_bits[c - n_keys];
+            if (!bytes && bits && c >= n_keys && ((out.all_valid >> (c - n_keys)) & 1)) {
+                bits[k] = all_valid_byte(n, k);
+                continue;
+            }
             if (!bytes || !bits) continue;
             pack_bits_at(bytes, n, bits, k);
         }
@@ -3061,6 +3069,19 @@ void launch_write_results(hipStream_t s, const Spec* dspec, const Spec& S, const
 __global__ void pack_bits_kernel(const u8* bytes, u64 n, u8* bits) {
     const u64 nb = (n + 7) / 8;
     for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) pack_bits_at(bytes, n, bits, k);
+}
+
+__global__ void fill_valid_kernel(u64 n, u8* bits) {
+    const u64 nb = (n + 7) / 8;
+    for (u64 k = blockIdx.x * (u64)blockDim.x + threadIdx.x; k < nb; k += (u64)gridDim.x * blockDim.x) bits[k] = all_valid_byte(n, k);
+}
+
+void launch_fill_valid(hipStream_t s, u64 n, u8* bits) {
+    const u64 nb = (n + 7) / 8;
+    u64 blocks = (nb + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (!blocks) return;
+    hipLaunchKernelGGL(fill_valid_kernel, dim3((u32)blocks), dim3(256), 0, s, n, bits);
 }
 
 void launch_pack_bits(hipStream_t s, const u8* bytes, u64 n, u8* bits) {

@@ -271,7 +271,16 @@ struct OutDesc {
     // at row * ser_stride[a], agg_valid[a] its length in bytes
     int32_t ser;
     u32 ser_stride[DBG_MAX_AGGS];
+    // aggregates whose every group is valid (non-nullable argument): no validity bytes are
+    // written (agg_valid[a] null) and the packers set agg_bits[a] to all ones
+    u32 all_valid;
 };
+// validity bits byte k of an all-valid column of n rows
+__host__ __device__ __forceinline__ u8 all_valid_byte(u64 n, u64 k) {
+    const u64 i0 = k * 8;
+    return i0 + 8 <= n ? (u8)0xFF : (i0 < n ? (u8)((1u << (n - i0)) - 1) : (u8)0);
+}
+void launch_fill_valid(hipStream_t s, u64 n, u8* bits);
 #define FIN_SMALL_SLOTS 16384  // tables up to this many slots finalize in one workgroup
 void launch_finalize_small(hipStream_t s, const Spec* dspec, const BatchDesc* batches, const TableDesc& t, const OutDesc& out,
                            u64* totals, u64* host_mirror /* mapped pinned: counters, totals, recycled, seq */,
