@@ -1159,6 +1159,7 @@ namespace {
 enum { NC_NONE = 0, NC_LZ4 = 1, NC_ZSTD = 2, NC_SNAPPY = 3, NC_RLE = 10, NC_DICT = 11, NC_ONE = 12, NC_FREQ = 13, NC_BP = 14,
        NC_DBP = 15, NC_PATAS = 16 };
 constexpr u64 NT_CHUNK = 0, NT_STAGE = 1ULL << 62, NT_TAB = 2ULL << 62, NT_MASK = (1ULL << 62) - 1;
+enum { NC_BITMAP = 100 };  // a Boolean page's basic-codec payload: the values as an LSB-first bitmap
 
 struct NatBlock {  // one integer block: the values, or a Dict's u32 indices
     u64 src;       // tagged: raw little-endian values (None, or inflated), OneValue's value, Rle runs, Bitpacking data
@@ -1169,7 +1170,7 @@ struct NatBlock {  // one integer block: the values, or a Dict's u32 indices
 struct NatPage {
     u64 row0;
     u32 n;
-    u32 kind;      // 0 integer, 1 String
+    u32 kind;      // 0 integer (Float32 / Float64: their bits), 1 String, 2 Boolean (one byte per row)
     u32 tw;        // integer width (Dict indices: 4)
     u32 dict;      // values through a dictionary: `blk` holds the indices
     NatBlock blk;
@@ -1281,6 +1282,14 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = x;
         for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) put8(i0, min(8u, hi - i0), v);
+    } else if (b.codec == NC_BITMAP) {  // 8 rows per lane from one bitmap byte (lo is a multiple of 8)
+        for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) {
+            const u32 byte = src[i0 >> 3];
+            u64 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = (byte >> k) & 1;
+            put8(i0, min(8u, hi - i0), v);
+        }
     } else if (b.codec == NC_RLE) {  // runs [u32 count][value]: fixed-size records, NAT_NT runs per round
         const u32 rs = 4 + tw;
         u64 row = 0;
@@ -1463,6 +1472,16 @@ __global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __res
         nat_block(pg.blk, pg.n, lo, hi, tw, B, err, [&](u32 i0, u32 cnt, const u64 (&v)[8]) { nat_store8(o, i0, cnt, v, tw); });
         return;
     }
+    if (pg.kind == 2) {  // Boolean: a byte per row (nonzero = true), bit-packed afterwards
+        u8* o = out + pg.row0;
+        nat_block(pg.blk, pg.n, lo, hi, 1, B, err, [&](u32 i0, u32 cnt, const u64 (&v)[8]) {
+            u64 t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = v[k] != 0;
+            nat_store8(o, i0, cnt, t, 1);
+        });
+        return;
+    }
     if (pg.smode == 1) {
         const u64 a = (u64)B.at(pg.sdata);
         for (u32 i = lo + threadIdx.x; i < hi; i += NAT_NT) {
@@ -1499,6 +1518,7 @@ struct NatParse {
     u64 stage = 0;                  // staging bytes
     std::vector<u64> tab;           // host-built table (u64 words)
     std::string err;
+    int vkind = 0;                  // the column's values: 0 integer, 1 Float32 / Float64, 2 Boolean
     u32 rd32(u64 p) const { u32 v; memcpy(&v, h + p, 4); return v; }
     u64 rd64(u64 p) const { u64 v; memcpy(&v, h + p, 8); return v; }
     bool fail(const std::string& m) {
@@ -1532,6 +1552,17 @@ struct NatParse {
         if (pl + comp > end) return fail("integer block past the page");
         q = pl + comp;
         memset(&b, 0, sizeof(b));
+        const int vk = allow_dict ? vkind : 0;  // a Dict's nested index block holds integers
+        // Float32 / Float64 (DoubleCompressor, compression/double/mod.rs): the integer layouts minus
+        // the bit-packings; Boolean (compression/boolean/mod.rs): basic codecs hold the bitmap, its
+        // uncompressed field the row count, plus Rle and OneValue of one byte
+        if (vk == 1 && (codec == NC_BP || codec == NC_DBP)) return fail("Bitpacking in a Float column");
+        if (vk == 2 && (codec == NC_BP || codec == NC_DBP || codec == NC_DICT)) return fail("codec " + std::to_string(codec) + " in a Boolean column");
+        if (vk == 2 && codec <= NC_SNAPPY) {
+            if (uncomp != n) return fail("Boolean block: uncompressed field != rows");
+            b.codec = NC_BITMAP;
+            return basic(codec, pl, comp, (u32)(((u64)n + 7) / 8), b.src);
+        }
         switch (codec) {
             case NC_NONE: case NC_LZ4: case NC_ZSTD: case NC_SNAPPY:
                 if ((u64)uncomp != (u64)n * tw) return fail("integer block: uncompressed size != rows x width");
@@ -1646,6 +1677,9 @@ struct NatParse {
 
 bool nat_int_target(int t, u32& w) {
     switch (t) {
+        case DBG_BOOLEAN: w = 1; return true;
+        case DBG_FLOAT32: w = 4; return true;
+        case DBG_FLOAT64: w = 8; return true;
         case DBG_INT8: case DBG_UINT8: w = 1; return true;
         case DBG_INT16: case DBG_UINT16: w = 2; return true;
         case DBG_INT32: case DBG_UINT32: case DBG_DATE: w = 4; return true;
@@ -1668,8 +1702,10 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
     u32 tw = 0;
     if (!is_str && !nat_int_target(target.type, tw))
         return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_native: target type " + std::to_string(target.type) + " is decoded on the CPU");
+    const bool is_bool = target.type == DBG_BOOLEAN;
     NatParse P;
     P.h = col->host;
+    P.vkind = is_bool ? 2 : ((target.type == DBG_FLOAT32 || target.type == DBG_FLOAT64) ? 1 : 0);
     std::vector<NatPage> pages(col->n_pages);
     u64 pos = 0, row = 0;
     for (u32 k = 0; k < col->n_pages; ++k) {
@@ -1680,7 +1716,7 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
         const u64 end = pos + len;
         pg.row0 = row;
         pg.n = (u32)n;
-        pg.kind = is_str ? 1 : 0;
+        pg.kind = is_str ? 1 : (is_bool ? 2 : 0);
         pg.tw = tw;
         pg.valid = ~0ULL;
         u64 p = pos;
@@ -1731,6 +1767,7 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
     for (int c = 1; c <= 3; ++c) njobs += P.jobs[c].size();
     SCAN_RET(ensure(&ctx->pages, &ctx->pages_cap, njobs + 1));
     if (is_str) SCAN_RET(ensure(&ctx->sptr, &ctx->sptr_cap, row + 1));
+    if (is_bool) SCAN_RET(ensure(&ctx->bools, &ctx->bools_cap, row + 8));
     if (!P.jobs[NC_ZSTD].empty()) SCAN_RET(ensure(&ctx->zlit, &ctx->zlit_cap, (u64)P.jobs[NC_ZSTD].size() * ZS_MAX_BLOCK + 16));
     // the small tables are copied synchronously from pageable memory (staged by the runtime)
     if (!pages.empty()) SCAN_HIP(hipMemcpyAsync(ctx->npg, pages.data(), pages.size() * sizeof(NatPage), hipMemcpyHostToDevice, s));
@@ -1774,7 +1811,7 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
         u32 split = (u32)std::max<u64>(1, std::min<u64>({16, (4096 + pages.size() - 1) / pages.size(), (maxn + 1023) / 1024}));
         void* ps = prof_scope_begin("nat_decode", s);
         hipLaunchKernelGGL(nat_decode_kernel, dim3((u32)pages.size(), split), dim3(NAT_NT), 0, s, (const NatPage*)ctx->npg, B,
-                           (u8*)out->data, want_vb ? ctx->vbytes : nullptr, ctx->sptr, out->offsets, ctx->err);
+                           is_bool ? ctx->bools : (u8*)out->data, want_vb ? ctx->vbytes : nullptr, ctx->sptr, out->offsets, ctx->err);
         prof_scope_end(ps);
         SCAN_HIP(hipGetLastError());
     }
@@ -1787,6 +1824,7 @@ int dbg_native_decode(dbg_scan_ctx* ctx, const dbg_native_column* col, dbg_datat
                                (u8*)out->data, max_string_bytes);
         SCAN_HIP(hipGetLastError());
     }
+    if (is_bool && row) launch_pack_bits(s, ctx->bools, row, (u8*)out->data);
     if (target.nullable && row && out->validity) {
         if (want_vb) launch_pack_bits(s, ctx->vbytes, row, out->validity);
         else SCAN_HIP(hipMemsetAsync(out->validity, 0xFF, (row + 7) / 8, s));

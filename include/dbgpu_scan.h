@@ -76,10 +76,11 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
  * [ColumnMeta::offset, + total_len) with PageMeta {length, num_values} per page (mod.rs:27-72).
  * Page structure (validity, codec headers, Dict / Bitpacking tables) is parsed on the host from
  * `host`; values are decoded on the device.  Codecs: None / Lz4 / Zstd / Snappy, Rle, Dict,
- * OneValue, Bitpacking, DeltaBitpacking for integers (Int8..UInt64, Date, Timestamp); None / Lz4 /
- * Zstd / Snappy, OneValue, Dict for String.  Freq (roaring exceptions), Patas, floats, Booleans,
- * Decimals and nested columns return DBG_ERR_UNSUPPORTED (the CPU reader).  Outputs as
- * dbg_parquet_decode. */
+ * OneValue, Bitpacking, DeltaBitpacking for integers (Int8..UInt64, Date, Timestamp); the same
+ * minus the bit-packings for Float32 / Float64; None / Lz4 / Zstd / Snappy (the bitmap), Rle,
+ * OneValue for Boolean; None / Lz4 / Zstd / Snappy, OneValue, Dict for String.  Freq (roaring
+ * exceptions), Patas, Decimals and nested columns return DBG_ERR_UNSUPPORTED (the CPU reader).
+ * Outputs as dbg_parquet_decode. */
 typedef struct dbg_native_column {
     const uint8_t* host;          /* the column's pages in host memory */
     const uint8_t* device;        /* the same bytes resident in HBM, or NULL: the call uploads them */

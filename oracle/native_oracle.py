@@ -29,6 +29,10 @@ values of a String (LargeUtf8) column (compression/binary/mod.rs:37-104): Basic 
 blocks — the (n + 1) zero-based i64 offsets, then the bytes — each [codec][comp][uncomp][payload];
 OneValue (binary/one_value.rs:48-58) [u32 len][bytes]; Dict (binary/dict.rs:54-85) the nested u32
 index block, [u32 count], per entry [u64 len][bytes]; Freq (binary/freq.rs).
+Float32 / Float64 columns (compression/double/mod.rs:45-120) use the integer layouts of their bits
+(basic, Rle, Dict, OneValue; no bit-packing) plus Freq / Patas; Boolean columns
+(compression/boolean/mod.rs:35-103) the basic codecs over the LSB-first bitmap — the uncompressed
+field then holds the row count — plus Rle ([u32 count][u8 value]) and OneValue (one byte).
 
 BitPacker4x is the `bitpacking` crate (0.8.x, src/common/arrow/Cargo.toml:95; absent from
 /root/reference): the simdcomp 4-lane layout — value i of a 128-value block is lane i % 4, slot
@@ -282,6 +286,45 @@ def decode_binary_block(buf: bytes, p: int, n: int) -> Tuple[List[bytes], int]:
     raise NotImplementedError(f"native codec {codec} (Freq) is not restated")
 
 
+# ---- Boolean blocks (compression/boolean/mod.rs:35-103, rle.rs, one_value.rs) ----
+def encode_bool_block(vals, codec: int, valid: Optional[np.ndarray] = None) -> bytes:
+    """[codec][compressed u32][uncompressed u32 = rows][payload]: basic codecs hold the values as an
+    LSB-first bitmap; Rle runs of [u32 count][u8 value] (nulls extend the current run); OneValue
+    one byte (the first valid value)."""
+    v = np.asarray(vals, bool)
+    n = len(v)
+    if codec in BASIC:
+        bm = np.packbits(v, bitorder="little").tobytes()
+        return _block(codec, basic_compress(codec, bm), n)
+    if codec == RLE:
+        body = encode_int_block(v.astype(np.uint8), 1, RLE, valid)[9:]
+        return _block(RLE, body, n)
+    if codec == ONE_VALUE:
+        first = next((bool(v[i]) for i in range(n) if valid is None or valid[i]), False)
+        return _block(ONE_VALUE, bytes([1 if first else 0]), n)
+    raise ValueError(f"codec {codec} is not a Boolean codec")
+
+
+def decode_bool_block(buf: bytes, p: int, n: int) -> Tuple[np.ndarray, int]:
+    codec, comp, uncomp = struct.unpack_from("<BII", buf, p)
+    q = p + 9
+    end = q + comp
+    if codec in BASIC:
+        bm = basic_decompress(codec, buf[q:end], (n + 7) // 8)
+        return np.unpackbits(np.frombuffer(bm, np.uint8), bitorder="little")[:n].astype(bool), end
+    if codec == RLE:
+        out, k = [], 0
+        while k < n:
+            cnt = struct.unpack_from("<I", buf, q)[0]
+            out.append(np.full(cnt, buf[q + 4] != 0, bool))
+            k += cnt
+            q += 5
+        return (np.concatenate(out)[:n] if out else np.zeros(0, bool)), end
+    if codec == ONE_VALUE:
+        return np.full(n, buf[q] > 0, bool), end
+    raise ValueError(f"codec {codec} is not a Boolean codec")
+
+
 # ---- validity ----
 def encode_validity(valid: Optional[np.ndarray], n: int) -> bytes:
     """write_validity (serialize.rs:202-217): u32 length + encode_bool of the definition levels
@@ -375,6 +418,8 @@ def encode_page(vals, kind: str, width: int = 0, valid: Optional[np.ndarray] = N
         if c == FREQ:
             c = basic  # Freq (roaring exceptions) is not restated: the plain codec instead
         return head + encode_int_block(v, width, c, valid, basic, nested)
+    if kind == "bool":
+        return head + encode_bool_block(vals, codec if codec is not None else basic, valid)
     c = codec if codec is not None else basic
     return head + encode_binary_block(list(vals), c, valid, nested)
 
@@ -385,6 +430,8 @@ def decode_page(buf: bytes, p: int, n: int, kind: str, width: int = 0, signed: b
         valid, p = decode_validity(buf, p, n)
     if kind == "int":
         v, p = decode_int_block(buf, p, n, width, signed)
+    elif kind == "bool":
+        v, p = decode_bool_block(buf, p, n)
     else:
         v, p = decode_binary_block(buf, p, n)
     return v, valid, p
@@ -417,10 +464,12 @@ def read_column(buf: bytes, lens: Sequence[int], rows: Sequence[int], kind: str,
     p, vals, valid = 0, [], []
     for ln, n in zip(lens, rows):
         v, va, q = decode_page(buf, p, n, kind, width, signed, nullable)
-        vals.append(v if kind == "int" else list(v))
+        vals.append(v if kind in ("int", "bool") else list(v))
         valid.append(np.ones(n, bool) if va is None else va)
         p += ln
-    if kind == "int":
+    if kind == "bool":
+        values = np.concatenate(vals) if vals else np.zeros(0, bool)
+    elif kind == "int":
         values = np.concatenate(vals) if vals else np.zeros(0, _dtype(width, signed))
     else:
         values = [x for v in vals for x in v]

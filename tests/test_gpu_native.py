@@ -301,7 +301,11 @@ def test_errors_not_faults(dec):
     with pytest.raises(Unsupported):
         dec.decode_native(NativeColumnChunk(bytes(fb), good[1], good[2]), T)
     with pytest.raises(Unsupported):
-        dec.decode_native(NativeColumnChunk(*good), col.DataType(abi.FLOAT64))
+        dec.decode_native(NativeColumnChunk(*good), col.DataType(abi.DECIMAL128, 20, 2))
+    # Bitpacking is not a Float codec
+    bp = nat.write_column(np.arange(256, dtype=np.int32), "int", 4, codecs=[nat.BITPACK])
+    with pytest.raises(DbgError):
+        dec.decode_native(NativeColumnChunk(*bp), col.DataType(abi.FLOAT32))
     # a NULL in a non-nullable target
     valid = np.ones(2000, bool)
     valid[1234] = False
@@ -312,3 +316,49 @@ def test_errors_not_faults(dec):
     assert (gvalid == valid).all()
     # the context still decodes after every error
     check_int(dec, v, 4, True, abi.INT32, codecs=[nat.LZ4], page_rows=1000)
+
+
+@pytest.mark.parametrize("codec", [nat.NONE, nat.LZ4, nat.ZSTD, nat.SNAPPY, nat.RLE, nat.DICT, nat.ONE_VALUE])
+def test_float_columns(dec, codec):
+    """Float32 / Float64 pages: their bits in the integer layouts (compression/double/mod.rs)."""
+    rng = np.random.default_rng(60 + codec)
+    for ttype, width, fdt, idt in [(abi.FLOAT64, 8, np.float64, np.int64), (abi.FLOAT32, 4, np.float32, np.int32)]:
+        n = 1500
+        base = rng.standard_normal(n).astype(fdt)
+        base[::97] = np.nan
+        if codec in (nat.RLE, nat.DICT):
+            base = np.repeat(base[:40], n // 40 + 1)[:n]
+        if codec == nat.ONE_VALUE:
+            base = np.full(n, -0.0, fdt)
+        for nullable in (False, True):
+            valid = rng.random(n) > 0.2 if nullable else None
+            if valid is not None:
+                valid[0] = True
+            buf, lens, rows = nat.write_column(base.view(idt), "int", width, valid, nullable, page_rows=512, codecs=[codec])
+            ev, evalid = nat.read_column(buf, lens, rows, "int", width, True, nullable)
+            c = dec.decode_native(NativeColumnChunk(buf, lens, rows, nullable), col.DataType(ttype, nullable=True)).to_host()
+            got = np.asarray(c.data).view(idt)
+            assert (got == ev).all(), (ttype, codec, nullable)
+            gvalid = c.validity if c.validity is not None else np.ones(n, bool)
+            assert (gvalid == evalid).all()
+
+
+@pytest.mark.parametrize("codec", [nat.NONE, nat.LZ4, nat.ZSTD, nat.SNAPPY, nat.RLE, nat.ONE_VALUE])
+def test_bool_columns(dec, codec):
+    """Boolean pages (compression/boolean/mod.rs): the bitmap under the basic codecs, Rle of
+    [u32 count][u8 value], OneValue; ragged pages so page bitmaps start mid-byte in the output."""
+    rng = np.random.default_rng(70 + codec)
+    n = 3001
+    v = np.repeat(rng.random(n // 11 + 1) < 0.5, 11)[:n] if codec == nat.RLE else (
+        np.zeros(n, bool) if codec == nat.ONE_VALUE else rng.random(n) < 0.4)
+    for nullable in (False, True):
+        valid = rng.random(n) > 0.25 if nullable else None
+        if valid is not None:
+            valid[0] = True
+        buf, lens, rows = nat.write_column(v, "bool", 0, valid, nullable, page_rows=1000, codecs=[codec])
+        ev, evalid = nat.read_column(buf, lens, rows, "bool", 0, True, nullable)
+        c = dec.decode_native(NativeColumnChunk(buf, lens, rows, nullable), col.DataType(abi.BOOLEAN, nullable=True)).to_host()
+        got = np.asarray(c.data).astype(bool)
+        assert (got == ev).all(), (codec, nullable, np.nonzero(got != ev)[0][:5])
+        gvalid = c.validity if c.validity is not None else np.ones(n, bool)
+        assert (gvalid == evalid).all()

@@ -99,3 +99,31 @@ def test_codec_choice():
     assert nat.choose_int_codec(np.repeat(rng.integers(0, 1 << 40, n // 256), 256).astype(np.int64), 8, None) in (nat.RLE, nat.DICT)
     assert nat.choose_int_codec(rng.integers(0, 1 << 62, n).astype(np.int64), 8, None) == nat.LZ4
     assert nat.choose_int_codec(np.sort(rng.integers(0, 1 << 20, n)).astype(np.int32), 4, None) == nat.DELTA_BITPACK
+
+
+@pytest.mark.parametrize("codec", [nat.NONE, nat.LZ4, nat.ZSTD, nat.SNAPPY, nat.RLE, nat.ONE_VALUE])
+@pytest.mark.parametrize("nullable", [False, True])
+def test_bool_codecs_round_trip(codec, nullable):
+    rng = np.random.default_rng(codec + 5 * nullable)
+    n = 1000
+    v = np.repeat(rng.random(n // 9 + 1) < 0.5, 9)[:n] if codec == nat.RLE else (
+        np.ones(n, bool) if codec == nat.ONE_VALUE else rng.random(n) < 0.3)
+    valid = rng.random(n) > 0.2 if nullable else None
+    if valid is not None:
+        valid[0] = True
+    buf, lens, rows = nat.write_column(v, "bool", 0, valid, nullable, page_rows=333, codecs=[codec])
+    got, gv = nat.read_column(buf, lens, rows, "bool", 0, True, nullable)
+    ok = np.ones(n, bool) if valid is None else valid
+    assert (gv == ok).all()
+    assert (got[ok] == v[ok]).all()
+
+
+def test_float_bits_round_trip():
+    """Float columns store their bits in the integer layouts: every codec but the bit-packings."""
+    rng = np.random.default_rng(3)
+    v = rng.standard_normal(700)
+    for codec in (nat.NONE, nat.LZ4, nat.RLE, nat.DICT, nat.ONE_VALUE):
+        x = np.repeat(v[:100], 7) if codec in (nat.RLE, nat.DICT) else (np.full(700, 2.5) if codec == nat.ONE_VALUE else v)
+        buf, lens, rows = nat.write_column(x.view(np.int64), "int", 8, page_rows=256, codecs=[codec])
+        got, _ = nat.read_column(buf, lens, rows, "int", 8, True)
+        assert (got.view(np.float64) == x).all()
