@@ -3273,8 +3273,13 @@ int dbg_agg_payload_counts_from(dbg_agg_handle* h, const uint32_t first_seg[2], 
 }
 
 // segments [first[k], end) packed destination-major (partition-major within a destination, segment
-// order within a partition) into dev_buf, on the table's stream
-static int payload_export_range(dbg_agg_handle* h, u32 n_ranks, const u32 first[2], void* dev_buf) {
+// order within a partition) into dev_buf, on the table's stream.  prepare: the copy ranges built
+// and uploaded (the steps that can fail); launch: the copies
+struct ExportPlan {
+    const CopyRange* dr[2] = {nullptr, nullptr};
+    u32 n[2] = {0, 0};
+};
+static int payload_export_prepare(dbg_agg_handle* h, u32 n_ranks, const u32 first[2], ExportPlan& X) {
     u64 dst = 0;
     for (int k = 0; k < 2; ++k) {
         const auto& K = h->ppk[k];
@@ -3300,10 +3305,25 @@ static int payload_export_range(dbg_agg_handle* h, u32 n_ranks, const u32 first[
         RETURN_IF(dev_alloc((void**)&dr, rs.size() * sizeof(CopyRange)));
         h->owned.push_back({dr, rs.size() * sizeof(CopyRange)});  // freed at the next reset
         HIPCHECK(hipMemcpy(dr, rs.data(), rs.size() * sizeof(CopyRange), hipMemcpyHostToDevice));
-        launch_copy_ranges(h->stream, K.l1, (u8*)dev_buf, dr, (u32)rs.size());
+        X.dr[k] = dr;
+        X.n[k] = (u32)rs.size();
+    }
+    return DBG_OK;
+}
+
+static int payload_export_launch(dbg_agg_handle* h, const ExportPlan& X, void* dev_buf) {
+    for (int k = 0; k < 2; ++k) {
+        if (!X.n[k]) continue;
+        launch_copy_ranges(h->stream, h->ppk[k].l1, (u8*)dev_buf, X.dr[k], X.n[k]);
         HIPCHECK(hipGetLastError());
     }
     return DBG_OK;
+}
+
+static int payload_export_range(dbg_agg_handle* h, u32 n_ranks, const u32 first[2], void* dev_buf) {
+    ExportPlan X;
+    RETURN_IF(payload_export_prepare(h, n_ranks, first, X));
+    return payload_export_launch(h, X, dev_buf);
 }
 
 int dbg_agg_payload_export(dbg_agg_handle* h, uint32_t n_ranks, void* dev_buf) {
@@ -3612,6 +3632,10 @@ int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg
             rc = dev_alloc(&X.recv[k].p, recv_total[k]);
             if (rc == DBG_OK) X.recv[k].bytes = recv_total[k];
         }
+    // the export's ranges (what can still fail) before the collective ok
+    const u32 first[2] = {h->xfirst[0], h->xfirst[1]};
+    ExportPlan EP;
+    if (rc == DBG_OK) rc = payload_export_prepare(h, n, first, EP);
     const std::string local_err = rc == DBG_OK ? std::string() : std::string(dbg_last_error());
     int bad = -1;
     RETURN_IF(all_ok(c, R, xs, rc == DBG_OK, &bad));
@@ -3622,8 +3646,7 @@ int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg
         return fail(DBG_ERR_DEVICE, "payload exchange: rank " + std::to_string(bad) + " failed before the transfer");
     }
     // 3. export behind the chunk's scatter, transfer behind the export
-    const u32 first[2] = {h->xfirst[0], h->xfirst[1]};
-    RETURN_IF(payload_export_range(h, n, first, c->xsend[xi]));
+    RETURN_IF(payload_export_launch(h, EP, c->xsend[xi]));
     HIPCHECK(hipEventRecord(c->xexp, s));
     HIPCHECK(hipStreamWaitEvent(xs, c->xexp, 0));
     RCCLCHECK(R.GroupStart());
