@@ -98,27 +98,46 @@ static void resolve_locked() {
     pending.clear();
 }
 
+struct Scope;
+static thread_local Scope* cur = nullptr;  // the innermost open scope of this thread
 struct Scope {
     bool on;
+    bool ext = false;  // a kernel launch stamped a / b itself (prof_ext_events)
     hipStream_t s;
     hipEvent_t a, b;
     const char* name;
-    Scope(const char* n, hipStream_t st) : on(enabled), s(st), name(n) {
+    Scope* outer;
+    Scope(const char* n, hipStream_t st) : on(enabled), s(st), name(n), outer(cur) {
         if (on) {
             a = get_event();
             b = get_event();
             (void)hipEventRecord(a, s);
+            cur = this;
         }
     }
     ~Scope() {
         if (on) {
-            (void)hipEventRecord(b, s);
+            cur = outer;
+            if (!ext) (void)hipEventRecord(b, s);
             std::lock_guard<std::mutex> g(mu);
             pending.push_back({name, a, b});
         }
     }
 };
 }  // namespace prof
+
+// A kernel that is the timed work of the innermost open scope: launched with
+// hipExtLaunchKernelGGL and these two events, they are stamped at the kernel's own start and end
+// (what rocprofv3 reports), not at the stream's event packets around it.  The scope then measures
+// that kernel alone.
+bool prof_ext_events(hipEvent_t* a, hipEvent_t* b) {
+    prof::Scope* c = prof::cur;
+    if (!c || !c->on || c->ext) return false;
+    c->ext = true;
+    *a = c->a;
+    *b = c->b;
+    return true;
+}
 
 // the same HIP-event scopes for the other translation units (scan.hip)
 void* prof_scope_begin(const char* name, hipStream_t s) { return prof::enabled ? new prof::Scope(name, s) : nullptr; }

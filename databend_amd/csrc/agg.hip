@@ -19,6 +19,7 @@
 
 #include "legacy.hpp"
 #include "agg.hpp"
+#include <hip/hip_ext.h>
 #include "agg_dev.hpp"
 
 #define BLOCK 256
@@ -2844,6 +2845,8 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
 }
 
 
+bool prof_ext_events(hipEvent_t* a, hipEvent_t* b);  // abi.hip
+
 static size_t fast_shmem(size_t table_bytes) { return table_bytes + (size_t)(1024 / 64) * WQW * 8; }
 static size_t fast_table_bytes(const Spec& S) { return (size_t)lds_slots_for(S, 16 * 1024) * S.stride_words * 8 + 16; }
 
@@ -2883,9 +2886,18 @@ static void launch_fast_t(hipStream_t s, const Spec* dspec, const BatchDesc* bat
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
     if (blocks < 1) blocks = 1;
-#define FAST_LAUNCH(P, N, F)                                                                                                  \
-    hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, rows, t, \
-                       lslots, (T)lo, (T)hi, neg, ff)
+    // profiling on: the kernel stamps the enclosing scope's events itself (abi.hip, prof_ext_events)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    const bool ext = prof_ext_events(&ev0, &ev1);
+#define FAST_LAUNCH(P, N, F)                                                                                                     \
+    do {                                                                                                                         \
+        if (ext)                                                                                                                 \
+            hipExtLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, ev0, ev1, 0, dspec, \
+                                  batches, bid, rows, t, lslots, (T)lo, (T)hi, neg, ff);                                        \
+        else                                                                                                                     \
+            hipLaunchKernelGGL((agg_insert_fast_kernel<T, P, N, F>), dim3((u32)blocks), dim3(N), shmem, s, dspec, batches, bid, \
+                               rows, t, lslots, (T)lo, (T)hi, neg, ff);                                                          \
+    } while (0)
     // CO: COUNT(*) is the only aggregate (ClickBench Q8/Q16 shape) — the kernel then carries no
     // apply_row code at all (smaller hot loop, fewer registers)
     if (count_only) {
