@@ -867,7 +867,7 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
                                                            u32* __restrict__ cnt, const u64* __restrict__ off,
                                                            const u64* __restrict__ part_off, u8* __restrict__ dst, int sorted) {
     constexpr u32 K = 1u << PP_L1_BITS;
-    constexpr int U = pp_l1_u(W);
+    constexpr int U = pp_l1_u(W);  // (the count at twice this: 3.6 -> 4.8 ms on C4)
     __shared__ u32 hist[K];
     __shared__ u64 run[K];
     __shared__ u32 hist_total_;
