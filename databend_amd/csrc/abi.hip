@@ -1334,6 +1334,13 @@ static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 row
     return DBG_OK;
 }
 
+// the specialised aggregation's table load per LDS round (linear probing in a 96-slot window;
+// records whose window is full wait for a further mini-round).  0.7 halves C4's rounds (4 -> 2)
+// but the longer probes cost more: pp_agg 32 -> 45 ms
+#ifndef PS_LOAD
+#define PS_LOAD 0.45
+#endif
+
 // EXPERIMENT (DBG_X_PPDIG=0): level 2 counts from the records instead of the digit array
 static bool kX_no_dig() {
     static const bool off = X_ENV("DBG_X_PPDIG") && X_ENV("DBG_X_PPDIG")[0] == '0';
@@ -1396,8 +1403,8 @@ static int pp_prepare(dbg_agg_handle* h, bool spec_ok) {
         while ((double)nr / (double)(1ULL << b2) > fill && b2 < PP_L1_BITS + 10) ++b2;
         const double gp = g / (double)(1ULL << b2);
         u32 sub = 0;
-        while (gp / (double)(1u << sub) > 0.45 * (double)scap && sub < 5) ++sub;
-        if ((double)nr / (double)(1ULL << b2) <= fill && gp / (double)(1u << sub) <= 0.45 * (double)scap && B >= b2) {
+        while (gp / (double)(1u << sub) > PS_LOAD * (double)scap && sub < 5) ++sub;
+        if ((double)nr / (double)(1ULL << b2) <= fill && gp / (double)(1u << sub) <= PS_LOAD * (double)scap && B >= b2) {
             B = b2;
             k2 = B - PP_L1_BITS;
             k3 = 0;
