@@ -1242,18 +1242,25 @@ __device__ __forceinline__ u64 nat_scan(u64 v, u64* wsum, u64& tot) {
 // (cnt = 8 and i0 a multiple of 8 except at a slice's or an Rle round's edges).  lo is a multiple
 // of 8.  Rle walks all runs (few) and expands only the slice; DeltaBitpacking needs the page's
 // prefix sum, so its page is one slice (lo = 0, hi = n) and puts one row at a time.
+// Decimal128 (16-byte values) runs twice, once per 8-byte half: vs = 16 (the value stride), vo =
+// 0 / 8 (the half), tw = 8.
 template <typename PUT8>
-__device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 hi, u32 tw, const NatBases& B, u64* err, PUT8 put8) {
+__device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 hi, u32 tw, const NatBases& B, u64* err, PUT8 put8,
+                                          u32 vs = 0, u32 vo = 0) {
     __shared__ u64 wsum[NAT_NT / 64];
     __shared__ u64 rstart[NAT_NT];
     __shared__ u64 rval[NAT_NT];
+    if (!vs) vs = tw;
     const u8* src = B.at(b.src);
     if (b.codec == NC_NONE) {
         for (u32 i0 = lo + 8 * threadIdx.x; i0 < hi; i0 += 8 * NAT_NT) {
             const u32 cnt = min(8u, hi - i0);
-            const u8* p = src + (u64)i0 * tw;
+            const u8* p = src + (u64)i0 * vs + vo;
             u64 v[8];
-            if (cnt == 8 && tw == 1) {
+            if (vs != tw) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = (u32)k < cnt ? nat_ld(p + (u64)k * vs, tw) : 0;
+            } else if (cnt == 8 && tw == 1) {
                 u64 x;
                 __builtin_memcpy(&x, p, 8);
 #pragma unroll
@@ -1277,7 +1284,7 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 
             put8(i0, cnt, v);
         }
     } else if (b.codec == NC_ONE) {
-        const u64 x = nat_ld(src, tw);
+        const u64 x = nat_ld(src + vo, tw);
         u64 v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = x;
@@ -1291,7 +1298,7 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 
             put8(i0, min(8u, hi - i0), v);
         }
     } else if (b.codec == NC_RLE) {  // runs [u32 count][value]: fixed-size records, NAT_NT runs per round
-        const u32 rs = 4 + tw;
+        const u32 rs = 4 + vs;
         u64 row = 0;
         for (u32 r0 = 0; r0 < b.nrec && row < hi; r0 += NAT_NT) {
             const u32 r = r0 + threadIdx.x;
@@ -1299,7 +1306,7 @@ __device__ __forceinline__ void nat_block(const NatBlock& b, u32 n, u32 lo, u32 
             u64 tot;
             const u64 incl = nat_scan(cnt, wsum, tot);
             rstart[threadIdx.x] = row + incl - cnt;
-            rval[threadIdx.x] = r < b.nrec ? nat_ld(src + (u64)r * rs + 4, tw) : 0;
+            rval[threadIdx.x] = r < b.nrec ? nat_ld(src + (u64)r * rs + 4 + vo, tw) : 0;
             __syncthreads();
             const u64 a = row > lo ? row : lo, e = row + tot < hi ? row + tot : hi;
             for (u64 g = (a & ~7ULL) + 8 * threadIdx.x; g < e; g += 8 * NAT_NT) {
@@ -1428,23 +1435,34 @@ __global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __res
         const u32 dn = pg.dn;
         u32 bad = 0;
         if (pg.kind == 0) {
-            const bool lds = dn <= NAT_LDS_DICT;
-            if (lds) {
-                for (u32 k = threadIdx.x; k < dn; k += NAT_NT) sdict[k] = nat_ld(d + (u64)k * tw, tw);
-                __syncthreads();
-            }
-            u8* o = out + pg.row0 * tw;
-            nat_block(pg.blk, pg.n, lo, hi, 4, B, err, [&](u32 i0, u32 cnt, const u64 (&ix)[8]) {
-                u64 v[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const u64 x = ix[k];
-                    const bool in = x < dn;
-                    bad |= (u32)k < cnt && !in;
-                    v[k] = !in ? 0 : (lds ? sdict[x] : nat_ld(d + x * tw, tw));
+            // Decimal128: the dictionary and the output in two 8-byte halves
+            const u32 halves = tw == 16 ? 2 : 1, hw = tw == 16 ? 8 : tw;
+            for (u32 hv = 0; hv < halves; ++hv) {
+                const bool lds = dn <= NAT_LDS_DICT;
+                if (lds) {
+                    if (hv) __syncthreads();  // every lane is done with the previous half's entries
+                    for (u32 k = threadIdx.x; k < dn; k += NAT_NT) sdict[k] = nat_ld(d + (u64)k * tw + 8 * hv, hw);
+                    __syncthreads();
                 }
-                nat_store8(o, i0, cnt, v, tw);
-            });
+                u8* o = out + pg.row0 * tw + 8 * hv;
+                nat_block(pg.blk, pg.n, lo, hi, 4, B, err, [&](u32 i0, u32 cnt, const u64 (&ix)[8]) {
+                    u64 v[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const u64 x = ix[k];
+                        const bool in = x < dn;
+                        bad |= (u32)k < cnt && !in;
+                        v[k] = !in ? 0 : (lds ? sdict[x] : nat_ld(d + x * tw + 8 * hv, hw));
+                    }
+                    if (halves == 1) {
+                        nat_store8(o, i0, cnt, v, tw);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if ((u32)k < cnt) *(u64*)(o + (u64)(i0 + k) * 16) = v[k];
+                    }
+                });
+            }
         } else {
             const u64* e = (const u64*)d;
             nat_block(pg.blk, pg.n, lo, hi, 4, B, err, [&](u32 i0, u32 cnt, const u64 (&ix)[8]) {
@@ -1465,6 +1483,18 @@ __global__ void __launch_bounds__(NAT_NT) nat_decode_kernel(const NatPage* __res
             });
         }
         if (bad) atomicOr((unsigned long long*)err, (unsigned long long)NERR_RANGE);
+        return;
+    }
+    if (pg.kind == 0 && tw == 16) {  // Decimal128: each 8-byte half in turn, at a 16-byte stride
+        for (u32 hv = 0; hv < 2; ++hv) {
+            u8* o = out + pg.row0 * 16 + 8 * hv;
+            nat_block(pg.blk, pg.n, lo, hi, 8, B, err, [&](u32 i0, u32 cnt, const u64 (&v)[8]) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if ((u32)k < cnt) *(u64*)(o + (u64)(i0 + k) * 16) = v[k];
+            }, 16, 8 * hv);
+            __syncthreads();  // the Rle run tables in LDS are reused by the second half
+        }
         return;
     }
     if (pg.kind == 0) {
@@ -1585,7 +1615,7 @@ struct NatParse {
                 return true;
             }
             case NC_BP: case NC_DBP: {
-                if (tw != 4) return fail("Bitpacking of a non-4-byte type");
+                if (tw != 4) return fail("Bitpacking of a non-4-byte type");  // (Decimal128 included)
                 b.codec = codec;
                 b.src = NT_CHUNK | pl;
                 b.nrec = (n + 127) / 128;
@@ -1680,6 +1710,7 @@ bool nat_int_target(int t, u32& w) {
         case DBG_BOOLEAN: w = 1; return true;
         case DBG_FLOAT32: w = 4; return true;
         case DBG_FLOAT64: w = 8; return true;
+        case DBG_DECIMAL128: w = 16; return true;  // i128 pages (write/primitive.rs: compress_integer)
         case DBG_INT8: case DBG_UINT8: w = 1; return true;
         case DBG_INT16: case DBG_UINT16: w = 2; return true;
         case DBG_INT32: case DBG_UINT32: case DBG_DATE: w = 4; return true;

@@ -77,9 +77,9 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
  * Page structure (validity, codec headers, Dict / Bitpacking tables) is parsed on the host from
  * `host`; values are decoded on the device.  Codecs: None / Lz4 / Zstd / Snappy, Rle, Dict,
  * OneValue, Bitpacking, DeltaBitpacking for integers (Int8..UInt64, Date, Timestamp); the same
- * minus the bit-packings for Float32 / Float64; None / Lz4 / Zstd / Snappy (the bitmap), Rle,
+ * minus the bit-packings for Decimal128 (i128 pages) and Float32 / Float64; None / Lz4 / Zstd / Snappy (the bitmap), Rle,
  * OneValue for Boolean; None / Lz4 / Zstd / Snappy, OneValue, Dict for String.  Freq (roaring
- * exceptions), Patas, Decimals and nested columns return DBG_ERR_UNSUPPORTED (the CPU reader).
+ * exceptions), Patas, Decimal256 and nested columns return DBG_ERR_UNSUPPORTED (the CPU reader).
  * Outputs as dbg_parquet_decode. */
 typedef struct dbg_native_column {
     const uint8_t* host;          /* the column's pages in host memory */

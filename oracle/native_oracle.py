@@ -58,10 +58,16 @@ BASIC = (NONE, LZ4, ZSTD, SNAPPY)
 PAGE_ROWS = 131072  # DEFAULT_ROW_PER_PAGE (fuse/src/constants.rs:35)
 DEFAULT_RATIO = 2.10  # block_writer.rs:83-86 (3.72 under TableCompression::Zstd)
 
-_NP = {1: (np.int8, np.uint8), 2: (np.int16, np.uint16), 4: (np.int32, np.uint32), 8: (np.int64, np.uint64)}
+# 16: Decimal128's i128 pages (write/primitive.rs:67-70, compress_integer over i128) as opaque
+# little-endian 16-byte values
+_I128 = np.dtype([("lo", "<u8"), ("hi", "<u8")])
+_NP = {1: (np.int8, np.uint8), 2: (np.int16, np.uint16), 4: (np.int32, np.uint32), 8: (np.int64, np.uint64),
+       16: (_I128, _I128)}
 
 
 def _dtype(width: int, signed: bool):
+    if width == 16:
+        return _I128
     return np.dtype(_NP[width][0 if signed else 1]).newbyteorder("<")
 
 

@@ -127,3 +127,19 @@ def test_float_bits_round_trip():
         buf, lens, rows = nat.write_column(x.view(np.int64), "int", 8, page_rows=256, codecs=[codec])
         got, _ = nat.read_column(buf, lens, rows, "int", 8, True)
         assert (got.view(np.float64) == x).all()
+
+
+@pytest.mark.parametrize("codec", [nat.NONE, nat.LZ4, nat.RLE, nat.DICT, nat.ONE_VALUE])
+def test_decimal128_round_trip(codec):
+    rng = np.random.default_rng(codec)
+    n = 600
+    v = np.zeros(n, nat._I128)
+    v["lo"] = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    v["hi"] = rng.integers(0, 3, n, dtype=np.uint64)
+    if codec in (nat.RLE, nat.DICT):
+        v = np.repeat(v[:20], 30)
+    if codec == nat.ONE_VALUE:
+        v = np.repeat(v[:1], n)
+    buf, lens, rows = nat.write_column(v, "int", 16, page_rows=250, codecs=[codec])
+    got, _ = nat.read_column(buf, lens, rows, "int", 16, True)
+    assert (got == v).all()
