@@ -728,6 +728,16 @@ struct Compact {
         return b[p++];
     }
     u64 varint() {
+        if (p + 10 <= n) {  // fast path: no per-byte bound checks
+            u64 v = 0;
+            for (int sh = 0; sh < 64; sh += 7) {
+                const u32 c = b[p++];
+                v |= (u64)(c & 0x7F) << sh;
+                if (!(c & 0x80)) return v;
+            }
+            ok = false;
+            return 0;
+        }
         u64 v = 0;
         for (int sh = 0; sh < 64 && ok; sh += 7) {
             const u32 c = byte();
@@ -794,6 +804,7 @@ struct HostPage {
 // page type 0 DATA_PAGE, 1 INDEX_PAGE, 2 DICTIONARY_PAGE, 3 DATA_PAGE_V2
 int parse_pages(const dbg_parquet_chunk& c, std::vector<HostPage>& out) {
     out.clear();
+    out.reserve(std::min<u64>(c.len / 4096 + 16, 1u << 20));
     u64 pos = 0;
     while (pos < c.len) {
         Compact r{c.host, c.len, pos};
