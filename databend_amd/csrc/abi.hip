@@ -160,6 +160,7 @@ struct FinState {
     u64 cap_str[DBG_MAX_KEYS] = {};
     bool zero_copy = false;
     u64 seq = 0;
+    bool direct = false;  // the held-back partitioned insert's direct stage wrote the results (part_slice_direct)
 };
 
 struct dbg_agg_handle {
@@ -214,10 +215,13 @@ struct dbg_agg_handle {
     DevBuf xrecv[2];
     bool xrecv_busy = false;
     // chunked before-partial shuffle (dbg_agg_exchange_payload_chunk): level-1 segments from
-    // xfirst[k] on are not shipped yet; what arrived per call waits in xchunks until the last call
+    // xfirst[k] on are not shipped yet; what arrived per call waits in xchunks until the last call.
+    // The receive buffers belong to the communicator (one grow-only pair per chunk slot, received
+    // into on its stream), so no step allocates or frees them and the handle never frees memory a
+    // transfer may still be writing.
     struct XChunk {
         std::vector<u64> pc;  // [n][2][P] counts of the chunk, every source
-        DevBuf recv[2];
+        const void* recv[2] = {nullptr, nullptr};
     };
     std::vector<XChunk> xchunks;
     u32 xfirst[2] = {0, 0};
@@ -263,6 +267,15 @@ struct dbg_agg_handle {
     u64 part_bounds_cap = 0;
     void* part_temp = nullptr;
     size_t part_temp_cap = 0;
+    // A partitioned insert into an empty table in recycle mode holds back its table stage (the
+    // keys are sorted already): a finalize_into that comes next runs the direct stage instead —
+    // groups straight into the result columns, the table never written (launch_part_direct);
+    // anything else that touches the table launches the regular slice stage first (part_flush).
+    bool def_part = false;
+    u32 def_part_sb = 0;
+    int def_part_kw = 0;
+    u64* part_status = nullptr;  // the direct stage's look-back words
+    u64 part_status_cap = 0;
     u64 table_rows = 0;  // rows / records inserted into the HBM table since the last reset
     u64 remerged = 0;    // of which records dbg_agg_compact merged back (groups, not input rows)
     int strategy = DBG_STRATEGY_AUTO;
@@ -546,8 +559,12 @@ static void table_init_now(dbg_agg_handle* h) {
     launch_table_init(h->stream, h->dspec, h->spec, h->slots, h->cap, nullptr);
 }
 
-// The table as the kernels see it; a deferred initialisation is launched first (stream order).
+static int part_flush(dbg_agg_handle* h);
+
+// The table as the kernels see it; a deferred initialisation, or a held-back partitioned table
+// stage, is launched first (stream order).
 static TableDesc table_desc(dbg_agg_handle* h) {
+    if (h->def_part) (void)part_flush(h);  // launch errors surface from the stream's next check
     table_init_now(h);
     TableDesc t;
     t.slots = h->slots;
@@ -566,6 +583,7 @@ static TableDesc table_desc(dbg_agg_handle* h) {
 }
 
 static int flush_deferred(dbg_agg_handle* h) {
+    if (h->def_part) RETURN_IF(part_flush(h));
     if (!h->def_on) return DBG_OK;
     h->def_on = false;
     {
@@ -928,15 +946,12 @@ void dbg_agg_destroy(dbg_agg_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto& b : h->owned) hipFree(b.p);
-    for (auto& x : h->xchunks)
-        for (auto& b : x.recv)
-            if (b.p) hipFree(b.p);
     for (auto& b : h->xrecv)
         if (b.p) hipFree(b.p);
     for (auto* p : h->pinned_chunks) hipHostFree(p);
     void* bufs[] = {h->scratch, h->slots, h->counters, h->ovf_rows, h->ovf_recs, h->dbatches, h->dspec, h->d_pos, h->d_str_pos,
                     h->d_part_pos, h->d_part_str_pos, h->d_part_str_base, h->d_lpart, h->vbytes, h->part_sorted, h->part_bounds,
-                    h->part_temp, h->ser_err, h->dense};
+                    h->part_temp, h->ser_err, h->dense, h->part_status};
     for (void* p : bufs)
         if (p) hipFree(p);
     for (auto& K : h->ppk) {
@@ -977,6 +992,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     if (!h) return fail(DBG_ERR_INVALID, "null handle");
     HIPCHECK(hipSetDevice(h->device));
     h->def_on = false;  // the held-back insert is discarded with the groups
+    h->def_part = false;
     h->stage.clear();   // and so are staged host rows
     // inputs copied by earlier batches, and the pinned batch descriptors reused below, may still
     // be read by queued work: wait if any were queued since the last synchronisation
@@ -992,10 +1008,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
     h->table_rows = 0;
     h->remerged = 0;
     h->xrecv_busy = false;  // no group references the exchange's receive buffers any more
-    for (auto& x : h->xchunks)  // an abandoned chunked shuffle (the last call never came)
-        for (auto& b : x.recv)
-            if (b.p) hipFree(b.p);
-    h->xchunks.clear();
+    h->xchunks.clear();  // an abandoned chunked shuffle (the last call never came): its buffers are the communicator's
     h->xfirst[0] = h->xfirst[1] = 0;
     for (auto& K : h->ppk) {  // partitioned payload: records dropped, buffers kept (the mode too)
         K.l1_n = 0;
@@ -1016,7 +1029,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
 static int ensure_buf(u64** p, u64* cap, u64 n);
 
 // Radix-partitioned COUNT(*) insert of a high-cardinality batch (part.hip); buffers grow only.
-static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, u32 sb) {
+static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, u32 sb, bool on_device_insert) {
     (void)bid;
     const int width = (int)st->keys[0].width;
     size_t tb = part_temp_bytes(width, rows, sb, h->cap);
@@ -1035,8 +1048,29 @@ static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows
     // an empty table whose initialisation is still deferred: the slice kernel writes every slot
     const bool empty = h->init_pending;
     h->init_pending = false;
-    hipError_t e = launch_part_insert(h->stream, *st, rows, table_desc(h), sb, h->part_temp, h->part_temp_cap, h->part_sorted,
-                                      h->part_bounds, empty, &step);
+    hipError_t e = launch_part_sort(h->stream, *st, rows, h->cap, sb, h->part_temp, h->part_temp_cap, h->part_sorted, h->part_bounds,
+                                    &step);
+    // EXPERIMENT (EXP=1 build): DBG_X_PART_DIRECT=0 keeps the table stage in the insert
+    static const bool direct_on = !(X_ENV("DBG_X_PART_DIRECT") && X_ENV("DBG_X_PART_DIRECT")[0] == '0');
+    if (e == hipSuccess && empty && h->recycle && on_device_insert && direct_on) {  // the table stage waits for the next call
+        h->def_part = true;
+        h->def_part_sb = sb;
+        h->def_part_kw = width;
+        return DBG_OK;
+    }
+    if (e == hipSuccess) e = launch_part_slices(h->stream, table_desc(h), sb, h->part_sorted, h->part_bounds, empty, &step);
+    if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("partitioned insert (") + step + "): " + hipGetErrorString(e));
+    return DBG_OK;
+}
+
+// The held-back table stage of a partitioned insert into an empty table: the regular slices.
+static int part_flush(dbg_agg_handle* h) {
+    if (!h->def_part) return DBG_OK;
+    h->def_part = false;
+    h->init_pending = false;  // part_slice<EMPTY> writes every slot
+    prof::Scope ps("part_slice", h->stream);
+    const char* step = "";
+    hipError_t e = launch_part_slices(h->stream, table_desc(h), h->def_part_sb, h->part_sorted, h->part_bounds, true, &step);
     if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("partitioned insert (") + step + "): " + hipGetErrorString(e));
     return DBG_OK;
 }
@@ -1691,7 +1725,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
         RETURN_IF(ensure_ovf(h, 0, rows));
     }
     if (u32 sb = part_slice_bits(S, *st, rows, h->cap)) {
-        RETURN_IF(part_insert(h, st, bid, rows, sb));
+        RETURN_IF(part_insert(h, st, bid, rows, sb, on_device != 0));
         if (!on_device) RETURN_IF(resolve_overflow(h));
         return DBG_OK;
     }
@@ -2144,12 +2178,22 @@ static int fin_launch(dbg_agg_handle* h) {
     u64 nb = finalize_blocks(h->cap);
     RETURN_IF(ensure_buf(&h->d_pos, &h->pos_cap, nb + 16));
     RETURN_IF(ensure_buf(&h->d_str_pos, &h->str_pos_cap, (u64)S.n_keys * nb + 8));
-    TableDesc t = table_desc(h);
+    // the held-back partitioned insert's table stage writes the result columns directly (one
+    // non-nullable integer key, COUNT(*): what part_slice_bits admits; the table stays empty)
+    const bool direct = h->def_part && !h->pp && S.n_keys == 1 && S.n_aggs == 1 && !S.key_types[0].nullable &&
+                        !h->result_types[0].nullable && type_width(h->result_types[0].type) == 8 && F.keys[0].data && F.aggs[0].data &&
+                        type_width(S.key_types[0].type) == (u32)h->def_part_kw;
+    if (direct) {
+        h->def_part = false;
+        RETURN_IF(ensure_buf(&h->part_status, &h->part_status_cap, part_direct_status_words(h->cap, h->def_part_sb)));
+    }
+    TableDesc t = direct ? TableDesc{} : table_desc(h);
     const bool small = h->cap + 1 <= FIN_SMALL_SLOTS;
     const bool fuse = h->def_on && !h->pp && small && h->hcounters_dev && insert_can_fuse(S, h->def_hb, h->cap);
     if (!fuse) RETURN_IF(flush_deferred(h));
     u64* totals = h->d_pos + nb;
-    if (!small && !h->pp) {
+    F.direct = direct;
+    if (!small && !h->pp && !direct) {
         prof::Scope ps("count_groups", h->stream);
         launch_count_groups(h->stream, h->dspec, S, h->dbatches, t, 1, 0, nullptr, h->d_pos, h->d_str_pos);
         launch_exclusive_scan(h->stream, h->d_pos, nb, totals);
@@ -2191,9 +2235,15 @@ static int fin_launch(dbg_agg_handle* h) {
         F.active = true;
         return DBG_OK;
     }
-    F.zero_copy = small && h->hcounters_dev != nullptr;
+    F.zero_copy = small && !direct && h->hcounters_dev != nullptr;
     F.seq = ++h->fin_seq;
-    if (fuse) {  // the held-back insert and this finalize in one launch
+    if (direct) {
+        prof::Scope ps("part_direct", h->stream);
+        hipError_t e = launch_part_direct(h->stream, h->cap, h->def_part_sb, h->part_sorted, h->part_bounds, h->part_status,
+                                          h->def_part_kw, od.key_data[0], (u64*)od.agg_data[0], od.cap_groups, totals);
+        if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("partitioned insert (direct stage): ") + hipGetErrorString(e));
+        launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);
+    } else if (fuse) {  // the held-back insert and this finalize in one launch
         FusedFin ff;
         ff.out = od;
         ff.totals = totals;
@@ -2281,6 +2331,7 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
     F.active = false;
     if (h->pp) return pp_fin_complete(h, n_groups, string_bytes);
     bool recycled = false;
+    const bool direct_done = F.direct;
     if (!F.zero_copy) {
         HIPCHECK(hipStreamSynchronize(h->stream));
     } else {
@@ -2316,6 +2367,20 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
         recycled = h->hcounters[CNT_WORDS + 1 + DBG_MAX_KEYS] != 0;
     }
     h->uploads_pending = false;
+    if (F.direct) {
+        F.direct = false;
+        if (h->hcounters[CNT_WORDS] == ~0ULL) {
+            // a slice held more keys than its slots, or the result columns are too short: the
+            // regular table stage from the same sorted keys (the table was never written), then
+            // the table finalize (which reports short buffers with the table intact)
+            h->def_part = true;
+            RETURN_IF(part_flush(h));
+            *retry = true;
+            return DBG_OK;
+        }
+        h->hcounters[CNT_CLAIMS] = h->hcounters[CNT_WORDS];  // the table's own counters were never touched
+        recycled = true;
+    }
     if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
     if (h->hcounters[CNT_ERR] & ERR_MINMAX_SPIN) return fail(DBG_ERR_INTERNAL, MINMAX_SPIN_MSG);
     if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
@@ -2343,8 +2408,9 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
         return fail(DBG_ERR_INTERNAL, "group count mismatch: " + std::to_string(h->n_groups) + " vs claims " +
                                           std::to_string(h->hcounters[CNT_CLAIMS]));
     h->finalized = true;
-    if (recycled) {  // the table was re-initialised by the kernel: dbg_agg_reset state
+    if (recycled) {  // the table was re-initialised by the kernel (or never written): dbg_agg_reset state
         h->clean = true;
+        h->init_pending = h->init_pending || direct_done;
         h->finalized = false;
         h->n_batches = h->n_cached;
         h->pending_rows = h->pending_recs = 0;
@@ -3175,6 +3241,13 @@ struct dbg_comm {
     u8* xsend[2] = {nullptr, nullptr};
     u64 xsend_cap[2] = {0, 0};
     int xi = 0;
+    // receive buffers per chunk slot (records, states), grown only; chunk i of every shuffle lands
+    // in slot i.  Receives run on xs, so a slot's next use is stream-ordered behind its last one.
+    struct XRecv {
+        u8* p[2] = {nullptr, nullptr};
+        u64 cap[2] = {0, 0};
+    };
+    std::vector<XRecv> xrecv;
 };
 
 extern "C" {
@@ -3242,6 +3315,9 @@ void dbg_comm_destroy(dbg_comm* c) {
         if (c->xsend[i]) hipFree(c->xsend[i]);
         if (c->xsent[i]) hipEventDestroy(c->xsent[i]);
     }
+    for (auto& x : c->xrecv)
+        for (int k = 0; k < 2; ++k)
+            if (x.p[k]) hipFree(x.p[k]);
     if (c->xexp) hipEventDestroy(c->xexp);
     if (c->xs) hipStreamDestroy(c->xs);
     delete c;
@@ -3653,10 +3729,18 @@ int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg
         c->xsent_valid[xi] = false;
     }
     if (kind_total[0] + kind_total[1] > c->xsend_cap[xi]) rc = grow_dev(&c->xsend[xi], &c->xsend_cap[xi], kind_total[0] + kind_total[1]);
+    // this chunk's receive slot: reused as is when large enough (the steady state); a slot that
+    // must grow waits for the transfers still queued on xs (an abandoned shuffle's receives)
+    const size_t slot = h->xchunks.size();
+    if (c->xrecv.size() <= slot) c->xrecv.resize(slot + 1);
+    auto& XR = c->xrecv[slot];
     for (int k = 0; k < 2 && rc == DBG_OK; ++k)
         if (recv_total[k]) {
-            rc = dev_alloc(&X.recv[k].p, recv_total[k]);
-            if (rc == DBG_OK) X.recv[k].bytes = recv_total[k];
+            if (recv_total[k] > XR.cap[k]) {
+                if (hipStreamSynchronize(xs) != hipSuccess) rc = fail(DBG_ERR_DEVICE, "hipStreamSynchronize");
+                else rc = grow_dev(&XR.p[k], &XR.cap[k], recv_total[k]);
+            }
+            if (rc == DBG_OK) X.recv[k] = XR.p[k];
         }
     // the export's ranges (what can still fail) before the collective ok
     const u32 first[2] = {h->xfirst[0], h->xfirst[1]};
@@ -3666,8 +3750,6 @@ int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg
     int bad = -1;
     RETURN_IF(all_ok(c, R, xs, rc == DBG_OK, &bad));
     if (bad >= 0) {
-        for (auto& b : X.recv)
-            if (b.p) hipFree(b.p);
         if (rc != DBG_OK) return fail(rc, local_err);
         return fail(DBG_ERR_DEVICE, "payload exchange: rank " + std::to_string(bad) + " failed before the transfer");
     }
@@ -3681,7 +3763,7 @@ int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg
         for (u32 p = 0; p < n; ++p) {
             const u64 sb = send_bytes[(u64)k * n + p], rb = recv_bytes[(u64)k * n + p];
             if (sb) RCCLCHECK(R.Send(c->xsend[xi] + so, sb, ncclUint8, (int)p, c->comm, xs));
-            if (rb) RCCLCHECK(R.Recv((u8*)X.recv[k].p + ro, rb, ncclUint8, (int)p, c->comm, xs));
+            if (rb) RCCLCHECK(R.Recv((u8*)X.recv[k] + ro, rb, ncclUint8, (int)p, c->comm, xs));
             so += sb;
             ro += rb;
         }
@@ -3709,13 +3791,10 @@ int dbg_agg_exchange_payload_chunk(dbg_comm* c, dbg_agg_handle* h, int last, dbg
     for (u32 i = 0; i < nc; ++i) {
         const auto& x = h->xchunks[i];
         pcs.insert(pcs.end(), x.pc.begin(), x.pc.end());
-        raws[i] = x.recv[0].p;
-        states[i] = x.recv[1].p;
+        raws[i] = x.recv[0];
+        states[i] = x.recv[1];
     }
-    rc = payload_import_chunks(h, n, me, nc, pcs.data(), raws.data(), states.data());
-    for (auto& x : h->xchunks)
-        for (auto& b : x.recv)
-            if (b.p) hipFree(b.p);
+    rc = payload_import_chunks(h, n, me, nc, pcs.data(), raws.data(), states.data());  // copies, then synchronises
     h->xchunks.clear();
     return rc;
 }

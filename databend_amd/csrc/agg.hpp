@@ -236,6 +236,13 @@ u32 part_slice_bits(const Spec& S, const BatchDesc& hb, u64 rows, u64 cap);  // 
 size_t part_temp_bytes(int width, u64 rows, u32 sb, u64 cap);
 hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, const TableDesc& t, u32 sb, void* temp,
                               size_t temp_bytes, u64* sorted, u64* bounds, bool table_empty, const char** step);
+hipError_t launch_part_sort(hipStream_t s, const BatchDesc& hb, u64 rows, u64 cap, u32 sb, void* temp, size_t temp_bytes,
+                            u64* sorted, u64* bounds, const char** step);
+hipError_t launch_part_slices(hipStream_t s, const TableDesc& t, u32 sb, const u64* sorted, const u64* bounds, bool table_empty,
+                              const char** step);
+u64 part_direct_status_words(u64 cap, u32 sb);
+hipError_t launch_part_direct(hipStream_t s, u64 cap, u32 sb, const u64* sorted, const u64* bounds, u64* status, int key_width,
+                              void* out_key, u64* out_cnt, u64 cap_groups, u64* totals);
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,
                    bool records, const TableDesc& t, bool use_lds, const BatchDesc* host_batch = nullptr,

@@ -397,6 +397,179 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
     if (threadIdx.x == 0 && lclaims) atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lclaims);
 }
 
+// Direct variant for a recycled one-shot step (reset -> add_groups -> finalize_into with
+// dbg_agg_set_recycle, the table empty when the batch arrived): the slice's groups go straight to
+// the result columns and the HBM table is never written.  The slice's LDS table is self-contained
+// (a probe wraps around inside the slice instead of continuing into the next one), so no overflow
+// record is needed; the result rows of a slice start at the group count of all earlier slices,
+// found by a decoupled look-back over per-slice status words.  Slices are taken in order from a
+// ticket (status[n_slices]), so a workgroup only ever waits for slices whose workgroups are
+// already running.  The last workgroup to finish appends the all-ones key (the table's sentinel
+// slot; only an 8-byte key can take it) and writes the group total.  A slice with more distinct
+// keys than its S slots, or more groups than the result columns hold, sets status[n + 2]: the
+// host then replays the regular slice kernel from the same sorted keys (the table path), which
+// reports short buffers with the table intact.
+//   status: [n_slices] look-back words, [n] ticket, [n + 1] sentinel rows, [n + 2] fail, [n + 3] done
+template <int SB, int PART_NT, int KW>
+__global__ void __launch_bounds__(PART_NT) part_slice_direct_kernel(const u64* __restrict__ sorted, const u64* __restrict__ bounds,
+                                                                    u64 n_slices, u64 cap, u64* __restrict__ status, u8* __restrict__ out_key,
+                                                                    u64* __restrict__ out_cnt, u64 cap_groups, u64* __restrict__ totals) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    __shared__ u32 s_slice, s_fail, s_last;
+    __shared__ u32 wtot[PART_NT / 64];
+    __shared__ u64 s_base;
+    constexpr u32 S = 1u << SB;
+    constexpr int PER = (int)(S / PART_NT);
+    static_assert(PER >= 1 && S % PART_NT == 0, "slice size");
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    u64* lkey = lds;
+    u32* lcnt = (u32*)(lds + S);
+    if (tid == 0) {
+        s_slice = atomicAdd((unsigned*)(status + n_slices), 1u);
+        s_fail = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        lkey[tid + k * PART_NT] = SLOT_EMPTY;
+        lcnt[tid + k * PART_NT] = 0;
+    }
+    __syncthreads();
+    const u64 b = s_slice;
+    const u64 s0 = b * S, mask = cap - 1;
+    const u64 lo = bounds[b], hi = bounds[b + 1];
+    const u64 __attribute__((address_space(1)))* src = (const u64 __attribute__((address_space(1)))*)sorted;
+    const u64 last = hi > lo ? hi - 1 : 0;
+    u64 r = lo + tid;
+    u64 cur[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) cur[k] = src[min<u64>(r + (u64)k * PART_NT, last)];
+    u32 sent = 0;  // rows of the all-ones key seen by this thread
+    bool fail = false;
+    auto one = [&](u64 m) {
+        const u64 key = slot_unmix(m);
+        if (key == SLOT_EMPTY) {
+            ++sent;
+            return;
+        }
+        u32 ls = (u32)((m & mask) - s0);
+        u32 q = 0;
+        int st = 0;  // 0 probing, 1 found, 3 slice full
+        while (st == 0) {
+            wptr<AS_LDS> e = asp<AS_LDS>(lkey + ls);
+            u64 ev = *e;
+            if (ev == SLOT_EMPTY) {
+                const u64 old = at_cas<AS_LDS>(e, SLOT_EMPTY, key);
+                ev = old == SLOT_EMPTY ? key : old;
+            }
+            if (ev == key) st = 1;
+            else if (++q >= S) st = 3;
+            else ls = (ls + 1) & (S - 1);
+        }
+        if (st == 1) __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)(lcnt + ls), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else fail = true;
+    };
+    while (r < hi) {
+        const u64 rn = r + (u64)RB * PART_NT;
+        u64 nxt[RB];
+        if (rn < hi) {
+#pragma unroll
+            for (int k = 0; k < RB; ++k) nxt[k] = src[min<u64>(rn + (u64)k * PART_NT, last)];
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k)
+            if (r + (u64)k * PART_NT < hi) one(cur[k]);
+        if (rn >= hi) break;
+#pragma unroll
+        for (int k = 0; k < RB; ++k) cur[k] = nxt[k];
+        r = rn;
+    }
+    if (sent) atomicAdd((unsigned long long*)(status + n_slices + 1), (unsigned long long)sent);
+    if (fail) s_fail = 1;
+    __syncthreads();
+    // this thread's PER consecutive slots: occupied count, block exclusive scan
+    u32 occ = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) occ += lkey[tid * PER + k] != SLOT_EMPTY ? 1u : 0u;
+    u32 x = occ;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    u32 off = x - occ, total = 0;
+#pragma unroll
+    for (u32 w = 0; w < PART_NT / 64; ++w) {
+        off += w < wave ? wtot[w] : 0u;
+        total += wtot[w];
+    }
+    // publish the slice's count, then look back over the earlier slices
+    if (tid == 0) {
+        u64 acc = 0;
+        if (b == 0) {
+            __hip_atomic_store(status + b, RP_INC | (u64)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(status + b, RP_AGG | (u64)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u64* sp = status + b - 1;
+            for (;;) {
+                const u64 v = __hip_atomic_load((u64*)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                acc += v & RP_VAL;
+                if (v & RP_INC) break;
+                --sp;
+            }
+            __hip_atomic_store(status + b, RP_INC | (acc + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_base = acc;
+        if (acc + total > cap_groups) s_fail = 1;
+    }
+    __syncthreads();
+    const u64 base = s_base + off;
+    if (!s_fail) {
+        u32 j = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const u64 key = lkey[tid * PER + k];
+            if (key == SLOT_EMPTY) continue;
+            const u64 row = base + j++;
+            if (KW == 8) ((u64*)out_key)[row] = key;
+            else if (KW == 4) ((u32*)out_key)[row] = (u32)key;
+            else if (KW == 2) ((uint16_t*)out_key)[row] = (uint16_t)key;
+            else out_key[row] = (u8)key;
+            out_cnt[row] = lcnt[tid * PER + k];
+        }
+    } else if (tid == 0) {
+        atomicOr((unsigned long long*)(status + n_slices + 2), 1ULL);
+    }
+    // the last workgroup to finish: sentinel group, total (or the failure mark ~0)
+    if (tid == 0) {
+        __threadfence();
+        s_last = atomicAdd((unsigned long long*)(status + n_slices + 3), 1ULL) == n_slices - 1;
+    }
+    __syncthreads();
+    if (s_last && tid == 0) {
+        __threadfence();
+        const u64 grand = __hip_atomic_load(status + n_slices - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & RP_VAL;
+        const u64 ns = __hip_atomic_load(status + n_slices + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool bad = __hip_atomic_load(status + n_slices + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        u64 n = grand;
+        if (ns && !bad) {
+            if (KW == 8 && grand < cap_groups) {  // only an 8-byte key can be all ones
+                ((u64*)out_key)[grand] = SLOT_EMPTY;
+                out_cnt[grand] = ns;
+                n = grand + 1;
+            } else {
+                bad = true;
+            }
+        }
+        totals[0] = bad ? ~0ULL : n;
+    }
+}
+
 // Merge the overflow records of this launch (and any still pending) into the HBM table right
 // away, so finalize sees no pending overflow and needs no second round.  Merged records are
 // tombstoned (entry = EMPTY, never a record key in inline mode: the all-ones key lives in the
@@ -574,22 +747,32 @@ size_t part_temp_bytes(int width, u64 rows, u32 sb, u64 cap) {
     return rp_temp_bytes(rows);
 }
 
-// sorted: rows u64; bounds: (cap >> sb) + 1 u64; temp: part_temp_bytes.  table_empty: the table
-// holds no group and its initialisation was deferred (part_slice writes every slot).  *step
-// names the failing step on error.
-hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, const TableDesc& t, u32 sb, void* temp,
-                              size_t temp_bytes, u64* sorted, u64* bounds, bool table_empty, const char** step) {
+// sorted: rows u64; bounds: (cap >> sb) + 1 u64; temp: part_temp_bytes.  The keys of the batch
+// sorted by their slot's slice, and every slice's first sorted position.  *step names the failing
+// step on error.
+hipError_t launch_part_sort(hipStream_t s, const BatchDesc& hb, u64 rows, u64 cap, u32 sb, void* temp, size_t temp_bytes,
+                            u64* sorted, u64* bounds, const char** step) {
     const int width = (int)hb.keys[0].width;
     if (sb != PART_SB || temp_bytes < rp_temp_bytes(rows) || rows >= (1ULL << 32)) return hipErrorInvalidValue;
-    const RadixPlan P = rp_plan(sb, t.cap);
+    const RadixPlan P = rp_plan(sb, cap);
     if (P.npass < 1 || P.npass > RP_MAXP) return hipErrorInvalidValue;
     hipError_t e = rp_sort(s, width, hb.keys[0].data, rows, P, (u8*)temp, sorted, step);
     if (e != hipSuccess) return e;
-    const u64 n_slices = t.cap >> sb;
+    const u64 n_slices = cap >> sb;
     *step = "part_bounds";
-    hipLaunchKernelGGL(part_bounds_kernel, dim3((u32)((n_slices + 1 + 255) / 256)), dim3(256), 0, s, sorted, rows, t.cap - 1, sb,
+    hipLaunchKernelGGL(part_bounds_kernel, dim3((u32)((n_slices + 1 + 255) / 256)), dim3(256), 0, s, sorted, rows, cap - 1, sb,
                        n_slices, bounds);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+// The table stage of a sorted batch: one workgroup per slice, then the overflow merge.
+// table_empty: the table holds no group and its initialisation was deferred (part_slice writes
+// every slot).
+hipError_t launch_part_slices(hipStream_t s, const TableDesc& t, u32 sb, const u64* sorted, const u64* bounds, bool table_empty,
+                              const char** step) {
+    if (sb != PART_SB) return hipErrorInvalidValue;
+    const u64 n_slices = t.cap >> sb;
+    hipError_t e;
     *step = "part_slice";
     static const int slice_nt = X_ENV("DBG_X_SLICE_NT") ? atoi(X_ENV("DBG_X_SLICE_NT")) : PART_NT_DEFAULT;
     const size_t sh = (size_t)(12ULL << PART_SB);
@@ -604,5 +787,38 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *step = "part_fixup";
     hipLaunchKernelGGL(part_fixup_kernel, dim3(512), dim3(256), 0, s, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, const TableDesc& t, u32 sb, void* temp,
+                              size_t temp_bytes, u64* sorted, u64* bounds, bool table_empty, const char** step) {
+    hipError_t e = launch_part_sort(s, hb, rows, t.cap, sb, temp, temp_bytes, sorted, bounds, step);
+    if (e != hipSuccess) return e;
+    return launch_part_slices(s, t, sb, sorted, bounds, table_empty, step);
+}
+
+u64 part_direct_status_words(u64 cap, u32 sb) { return (cap >> sb) + 4; }
+
+// The direct stage (part_slice_direct_kernel) of a sorted batch into result columns: keys of
+// key_width bytes, u64 counts; totals[0] = groups, or ~0 when the host must replay the table path.
+// status: part_direct_status_words() words.
+hipError_t launch_part_direct(hipStream_t s, u64 cap, u32 sb, const u64* sorted, const u64* bounds, u64* status, int key_width,
+                              void* out_key, u64* out_cnt, u64 cap_groups, u64* totals) {
+    if (sb != PART_SB) return hipErrorInvalidValue;
+    const u64 n_slices = cap >> sb;
+    hipError_t e = hipMemsetAsync(status, 0, part_direct_status_words(cap, sb) * 8, s);
+    if (e != hipSuccess) return e;
+    const size_t sh = (size_t)(12ULL << PART_SB);
+#define DIRECT_GO(KW)                                                                                                       \
+    hipLaunchKernelGGL((part_slice_direct_kernel<PART_SB, PART_NT_DEFAULT, KW>), dim3((u32)n_slices), dim3(PART_NT_DEFAULT), sh, s, \
+                       sorted, bounds, n_slices, cap, status, (u8*)out_key, out_cnt, cap_groups, totals)
+    switch (key_width) {
+        case 1: DIRECT_GO(1); break;
+        case 2: DIRECT_GO(2); break;
+        case 4: DIRECT_GO(4); break;
+        case 8: DIRECT_GO(8); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef DIRECT_GO
     return hipGetLastError();
 }

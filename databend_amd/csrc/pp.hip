@@ -1827,6 +1827,7 @@ template <int MODE, int W, int RPT, int SNT>
 __global__ void __launch_bounds__(SNT, SNT / 256) pp_agg_desc_kernel(const PsDesc D, u32 n_parts, const u64* __restrict__ raw_off,
                                                                const u8* __restrict__ raw, u32 sub_bits, u32 cap, PPAggOut out,
                                                                u32* __restrict__ spill, u32 spill_cap) {
+    static_assert(RPT < 32, "per-lane record mask");
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     const u32 KW = D.kw, BW = D.bw;
     l32* tags = (l32*)lds_raw;                                     // [cap] 0 empty, 1 being claimed, else tag
@@ -1984,9 +1985,9 @@ __global__ void __launch_bounds__(SNT, SNT / 256) pp_agg_desc_kernel(const PsDes
         // top bits, the slot position the top bits of the low word)
         u32 lo[RPT];  // slot hash bits; the round is the low sub_bits
         ps_hash<W, RPT>(D, rr, lo);
-        u32 valid = 0;
-#pragma unroll
-        for (int u = 0; u < RPT; ++u) valid |= ((u64)u * SNT + tid < n) ? (1u << u) : 0u;
+        // records this lane holds: register u is row u * SNT + tid (32-bit: n <= SNT * RPT; a 64-bit
+        // row test per register had the compiler keep RPT 64-bit row constants live, and spill them)
+        const u32 valid = (1u << ((u32)n > tid ? ((u32)n - 1 - tid) / SNT + 1 : 0u)) - 1;
         tick(0);  // the partition's loads landed, hashed
         for (u32 round = 0; round <= smask; ++round) {
             u32 act = 0;
@@ -2335,6 +2336,7 @@ __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_
     typedef PsShape<K0, K1, A0, A1, A2> SH;
     constexpr u32 KW = SH::KW, BW = SH::BW;
     static_assert(KW <= (u32)W && SH::END <= 8u * W, "record words");
+    static_assert(RPT < 32, "per-lane record mask");
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     l32* tags = (l32*)lds_raw;                                     // [cap] 0 empty, 1 being claimed, else tag
     l64* body = (l64*)lds_raw + (cap + 1) / 2;                     // [cap][BW]
@@ -2488,12 +2490,11 @@ __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_
             return (u32)pp_mix(h);
         };
         u32 lo[RPT];  // slot hash bits; the round is the low sub_bits
-        u32 valid = 0;
 #pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            lo[u] = slot_hash(rr[u]);
-            valid |= ((u64)u * SNT + tid < n) ? (1u << u) : 0u;
-        }
+        for (int u = 0; u < RPT; ++u) lo[u] = slot_hash(rr[u]);
+        // records this lane holds: register u is row u * SNT + tid (32-bit: n <= SNT * RPT; a 64-bit
+        // row test per register had the compiler keep RPT 64-bit row constants live, and spill them)
+        const u32 valid = (1u << ((u32)n > tid ? ((u32)n - 1 - tid) / SNT + 1 : 0u)) - 1;
         tick(0);  // the partition's loads landed, hashed
         for (u32 round = 0; round <= smask; ++round) {
             u32 act = 0;

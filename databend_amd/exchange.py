@@ -208,8 +208,18 @@ class PayloadShuffle:
                     received_records=sum(recv[0]) // max(1, widths[0]) + sum(recv[1]) // max(1, widths[1]))
 
     def finish(self):
+        """Ship what add_groups appended after the last ship() (dbg_agg_exchange_payload_chunk with
+        last = 1 does the same), wait for every chunk and import them all.  The decision to ship a
+        last chunk is collective (one all-reduce of "segments pending"), so ranks that have nothing
+        left still take part in the shipment of the ranks that have."""
         import numpy as np
+        import torch
         dist = _dist()
+        _, _, nseg = self.table.payload_counts_from(self.first)
+        pending = torch.tensor([1 if tuple(nseg) != tuple(self.first) else 0], dtype=torch.int64, device=self.device)
+        dist.all_reduce(pending, op=dist.ReduceOp.MAX)
+        if int(pending.item()):
+            self.ship()
         for _, _, _, works, _ in self.chunks:
             for w in works:
                 w.wait()

@@ -149,7 +149,9 @@ class FakeChunkedPayload:
         self.imported = (cc.copy(), [r.numpy().copy() for r in raws], [s.numpy().copy() for s in states])
 
 
-def _chunk_worker(rank, world, port, q, n_segs):
+def _chunk_worker(rank, world, port, q, n_segs, shipped=None):
+    """`shipped`: how many segments are shipped one by one before finish() (None = all of them);
+    finish() must ship the rest as one last chunk."""
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -160,24 +162,29 @@ def _chunk_worker(rank, world, port, q, n_segs):
     try:
         t = FakeChunkedPayload(rank, 200 + rank, n_segs)
         sh = PayloadShuffle(t, "cpu")
-        for g in range(n_segs):  # one add_groups chunk, then its shipment
+        k_ship = n_segs if shipped is None else shipped
+        for g in range(n_segs):  # one add_groups chunk, then (for the first k_ship) its shipment
             t.n_visible = g + 1
-            sh.ship()
+            if g < k_ship:
+                sh.ship()
         sh.finish()
         cc, raws, states = t.imported
-        assert cc.shape == (n_segs, world, 2, 256)
+        # chunk j holds segment j for j < k_ship; the last chunk holds every segment after that
+        groups = [[g] for g in range(k_ship)] + ([list(range(k_ship, n_segs))] if k_ship < n_segs else [])
+        assert cc.shape == (len(groups), world, 2, 256)
         lo, hi = payload_owned(rank, world)
-        for g in range(n_segs):  # chunk g: source-major, partition-major within a source
-            for k, buf in ((0, raws[g]), (1, states[g])):
+        for j, segs in enumerate(groups):  # source-major, partition-major within a source, segments in order
+            for k, buf in ((0, raws[j]), (1, states[j])):
                 words = buf[:buf.size // 8 * 8].view(np.uint64)
                 exp = []
                 for s in range(world):
                     src = FakeChunkedPayload(s, 200 + s, n_segs)
-                    assert (cc[g][s] == src.segs[g]).all()
+                    assert (cc[j][s] == sum(src.segs[g] for g in segs)).all()
                     for p in range(lo, hi):
-                        for i in range(int(src.segs[g][k][p])):
-                            exp += src.rec(k, g, p, i)
-                assert list(words[:len(exp)]) == exp, (rank, g, k)
+                        for g in segs:
+                            for i in range(int(src.segs[g][k][p])):
+                                exp += src.rec(k, g, p, i)
+                assert list(words[:len(exp)]) == exp, (rank, j, k)
         q.put((rank, "ok"))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -186,13 +193,15 @@ def _chunk_worker(rank, world, port, q, n_segs):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_chunked_payload_shuffle_protocol(world):
+@pytest.mark.parametrize("world,shipped", [(2, None), (3, None), (4, None), (2, 1), (3, 0)])
+def test_chunked_payload_shuffle_protocol(world, shipped):
+    """shipped = 1: records added after the last ship() reach their owners through finish();
+    shipped = 0: finish() alone shuffles (no rank keeps an unshuffled payload)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_chunk_worker, args=(r, world, port, q, 3)) for r in range(world)]
+    ps = [ctx.Process(target=_chunk_worker, args=(r, world, port, q, 3, shipped)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in ps)
