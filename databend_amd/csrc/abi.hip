@@ -269,7 +269,8 @@ struct dbg_agg_handle {
     size_t part_temp_cap = 0;
     // A partitioned insert into an empty table in recycle mode holds back its table stage (the
     // keys are sorted already): a finalize_into that comes next runs the direct stage instead —
-    // groups straight into the result columns, the table never written (launch_part_direct);
+    // groups into the result columns without the table-wide count and write passes, the slots used
+    // as scratch and left to be initialised like a reset table (launch_part_direct);
     // anything else that touches the table launches the regular slice stage first (part_flush).
     bool def_part = false;
     u32 def_part_sb = 0;
@@ -1029,7 +1030,7 @@ int dbg_agg_reset(dbg_agg_handle* h) {
 static int ensure_buf(u64** p, u64* cap, u64 n);
 
 // Radix-partitioned COUNT(*) insert of a high-cardinality batch (part.hip); buffers grow only.
-static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, u32 sb, bool on_device_insert) {
+static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, u32 sb, bool on_device_insert, bool was_clean) {
     (void)bid;
     const int width = (int)st->keys[0].width;
     size_t tb = part_temp_bytes(width, rows, sb, h->cap);
@@ -1052,7 +1053,9 @@ static int part_insert(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows
                                     &step);
     // EXPERIMENT (EXP=1 build): DBG_X_PART_DIRECT=0 keeps the table stage in the insert
     static const bool direct_on = !(X_ENV("DBG_X_PART_DIRECT") && X_ENV("DBG_X_PART_DIRECT")[0] == '0');
-    if (e == hipSuccess && empty && h->recycle && on_device_insert && direct_on) {  // the table stage waits for the next call
+    // (was_clean: no group since the last reset or recycling finalize, the slots EMPTY or their
+    // initialisation pending — the slices may start from EMPTY either way)
+    if (e == hipSuccess && (empty || was_clean) && h->recycle && on_device_insert && direct_on) {  // the table stage waits for the next call
         h->def_part = true;
         h->def_part_sb = sb;
         h->def_part_kw = width;
@@ -1725,7 +1728,7 @@ static int add_groups_now(dbg_agg_handle* h, const dbg_column* group_cols, const
         RETURN_IF(ensure_ovf(h, 0, rows));
     }
     if (u32 sb = part_slice_bits(S, *st, rows, h->cap)) {
-        RETURN_IF(part_insert(h, st, bid, rows, sb, on_device != 0));
+        RETURN_IF(part_insert(h, st, bid, rows, sb, on_device != 0, was_clean));
         if (!on_device) RETURN_IF(resolve_overflow(h));
         return DBG_OK;
     }
@@ -2239,7 +2242,10 @@ static int fin_launch(dbg_agg_handle* h) {
     F.seq = ++h->fin_seq;
     if (direct) {
         prof::Scope ps("part_direct", h->stream);
-        hipError_t e = launch_part_direct(h->stream, h->cap, h->def_part_sb, h->part_sorted, h->part_bounds, h->part_status,
+        TableDesc td{};
+        td.slots = h->slots;
+        td.cap = h->cap;
+        hipError_t e = launch_part_direct(h->stream, td, h->def_part_sb, h->part_sorted, h->part_bounds, h->part_status,
                                           h->def_part_kw, od.key_data[0], (u64*)od.agg_data[0], od.cap_groups, totals);
         if (e != hipSuccess) return fail(DBG_ERR_DEVICE, std::string("partitioned insert (direct stage): ") + hipGetErrorString(e));
         launch_finish_outputs(h->stream, od, totals, S.n_keys, S.n_aggs);

@@ -241,7 +241,7 @@ hipError_t launch_part_sort(hipStream_t s, const BatchDesc& hb, u64 rows, u64 ca
 hipError_t launch_part_slices(hipStream_t s, const TableDesc& t, u32 sb, const u64* sorted, const u64* bounds, bool table_empty,
                               const char** step);
 u64 part_direct_status_words(u64 cap, u32 sb);
-hipError_t launch_part_direct(hipStream_t s, u64 cap, u32 sb, const u64* sorted, const u64* bounds, u64* status, int key_width,
+hipError_t launch_part_direct(hipStream_t s, const TableDesc& t, u32 sb, const u64* sorted, const u64* bounds, u64* status, int key_width,
                               void* out_key, u64* out_cnt, u64 cap_groups, u64* totals);
 void launch_table_init(hipStream_t s, const Spec* dspec, const Spec& hspec, u64* slots, u64 cap, u64* zero_counters = nullptr);
 void launch_insert(hipStream_t s, const Spec* dspec, const Spec& hspec, const BatchDesc* batches, u32 bid, u64 rows,

@@ -398,43 +398,46 @@ __global__ void __launch_bounds__(PART_NT) part_slice_kernel(const u64* __restri
 }
 
 // Direct variant for a recycled one-shot step (reset -> add_groups -> finalize_into with
-// dbg_agg_set_recycle, the table empty when the batch arrived): the slice's groups go straight to
-// the result columns and the HBM table is never written.  The slice's LDS table is self-contained
-// (a probe wraps around inside the slice instead of continuing into the next one), so no overflow
-// record is needed; the result rows of a slice start at the group count of all earlier slices,
-// found by a decoupled look-back over per-slice status words.  Slices are taken in order from a
-// ticket (status[n_slices]), so a workgroup only ever waits for slices whose workgroups are
-// already running.  The last workgroup to finish appends the all-ones key (the table's sentinel
-// slot; only an 8-byte key can take it) and writes the group total.  A slice with more distinct
-// keys than its S slots, or more groups than the result columns hold, sets status[n + 2]: the
-// host then replays the regular slice kernel from the same sorted keys (the table path), which
-// reports short buffers with the table intact.
-//   status: [n_slices] look-back words, [n] ticket, [n + 1] sentinel rows, [n + 2] fail, [n + 3] done
-template <int SB, int PART_NT, int KW>
+// dbg_agg_set_recycle, the table empty when the batch arrived): the groups reach the result
+// columns without a table-wide count and write pass.  Two kernels:
+//   part_slice_direct_kernel (one workgroup per slice): the slice's LDS table is self-contained
+//     (a probe wraps around inside the slice instead of continuing into the next one, so no
+//     overflow record is needed); its groups are written compacted, as (key, count) pairs, to the
+//     start of the slice's own 64 KB of the table (which the step does not keep: it is left
+//     uninitialised, like a reset table), and its group count to counts[b];
+//   part_direct_emit_kernel (one workgroup per 64 slices, chunk ids from a ticket): the chunk's
+//     group offset by a decoupled look-back over chunk totals (every count is known, so no chunk
+//     waits on work), then the pairs copied to the result columns; the last workgroup appends the
+//     all-ones key (the table's sentinel slot: only an 8-byte key can take it) and writes the total.
+// (One kernel with a look-back per slice measured slower, 8.9 vs 7.6 ms for C3's table stage and
+// finalize: a slice's results wait for every earlier slice's rows, so the slowest slice of the
+// resident window held up all the others.)
+// A slice with more distinct keys than its 4096 slots, or more groups than the result columns
+// hold, makes totals[0] = ~0: the host then replays the regular slice kernel from the same sorted
+// keys (the table path), which reports short buffers with the table intact.
+//   status: [n_slices] counts, [n_chunks] look-back words, then ticket, sentinel rows, fail, done
+#define PD_CHUNK 64
+template <int SB, int PART_NT>
 __global__ void __launch_bounds__(PART_NT) part_slice_direct_kernel(const u64* __restrict__ sorted, const u64* __restrict__ bounds,
-                                                                    u64 n_slices, u64 cap, u64* __restrict__ status, u8* __restrict__ out_key,
-                                                                    u64* __restrict__ out_cnt, u64 cap_groups, u64* __restrict__ totals) {
+                                                                    u64 n_slices, u64 cap, u64* __restrict__ slots, u64* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
-    __shared__ u32 s_slice, s_fail, s_last;
     __shared__ u32 wtot[PART_NT / 64];
-    __shared__ u64 s_base;
+    __shared__ u32 s_fail;
     constexpr u32 S = 1u << SB;
     constexpr int PER = (int)(S / PART_NT);
     static_assert(PER >= 1 && S % PART_NT == 0, "slice size");
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u64 n_chunks = (n_slices + PD_CHUNK - 1) / PD_CHUNK;
+    u64* tail = status + n_slices + n_chunks;  // ticket, sentinel rows, fail, done
     u64* lkey = lds;
     u32* lcnt = (u32*)(lds + S);
-    if (tid == 0) {
-        s_slice = atomicAdd((unsigned*)(status + n_slices), 1u);
-        s_fail = 0;
-    }
+    if (tid == 0) s_fail = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         lkey[tid + k * PART_NT] = SLOT_EMPTY;
         lcnt[tid + k * PART_NT] = 0;
     }
-    __syncthreads();
-    const u64 b = s_slice;
+    const u64 b = blockIdx.x;
     const u64 s0 = b * S, mask = cap - 1;
     const u64 lo = bounds[b], hi = bounds[b + 1];
     const u64 __attribute__((address_space(1)))* src = (const u64 __attribute__((address_space(1)))*)sorted;
@@ -443,6 +446,7 @@ __global__ void __launch_bounds__(PART_NT) part_slice_direct_kernel(const u64* _
     u64 cur[RB];
 #pragma unroll
     for (int k = 0; k < RB; ++k) cur[k] = src[min<u64>(r + (u64)k * PART_NT, last)];
+    __syncthreads();
     u32 sent = 0;  // rows of the all-ones key seen by this thread
     bool fail = false;
     auto one = [&](u64 m) {
@@ -483,7 +487,7 @@ __global__ void __launch_bounds__(PART_NT) part_slice_direct_kernel(const u64* _
         for (int k = 0; k < RB; ++k) cur[k] = nxt[k];
         r = rn;
     }
-    if (sent) atomicAdd((unsigned long long*)(status + n_slices + 1), (unsigned long long)sent);
+    if (sent) atomicAdd((unsigned long long*)(tail + 1), (unsigned long long)sent);
     if (fail) s_fail = 1;
     __syncthreads();
     // this thread's PER consecutive slots: occupied count, block exclusive scan
@@ -504,58 +508,97 @@ __global__ void __launch_bounds__(PART_NT) part_slice_direct_kernel(const u64* _
         off += w < wave ? wtot[w] : 0u;
         total += wtot[w];
     }
-    // publish the slice's count, then look back over the earlier slices
+    // the slice's pairs, compacted at the start of its own table region
+    v2u64 __attribute__((address_space(1)))* osl = (v2u64 __attribute__((address_space(1)))*)(slots + s0 * 2);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const u64 key = lkey[tid * PER + k];
+        if (key == SLOT_EMPTY) continue;
+        osl[off++] = v2u64{key, (u64)lcnt[tid * PER + k]};
+    }
     if (tid == 0) {
-        u64 acc = 0;
-        if (b == 0) {
-            __hip_atomic_store(status + b, RP_INC | (u64)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(status + b, RP_AGG | (u64)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u64* sp = status + b - 1;
-            for (;;) {
-                const u64 v = __hip_atomic_load((u64*)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                acc += v & RP_VAL;
-                if (v & RP_INC) break;
-                --sp;
-            }
-            __hip_atomic_store(status + b, RP_INC | (acc + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        status[b] = total;
+        if (s_fail) atomicOr((unsigned long long*)(tail + 2), 1ULL);
+    }
+}
+
+template <int KW>
+__global__ void __launch_bounds__(1024) part_direct_emit_kernel(const u64* __restrict__ slots, u64 n_slices, u64* __restrict__ status,
+                                                                u8* __restrict__ out_key, u64* __restrict__ out_cnt, u64 cap_groups,
+                                                                u64* __restrict__ totals) {
+    constexpr u32 S = 1u << PART_SB;
+    __shared__ u64 pre[PD_CHUNK + 1];
+    __shared__ u32 s_chunk, s_last;
+    __shared__ u64 s_base;
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u64 n_chunks = (n_slices + PD_CHUNK - 1) / PD_CHUNK;
+    u64* look = status + n_slices;
+    u64* tail = look + n_chunks;
+    if (tid == 0) s_chunk = (u32)atomicAdd((unsigned long long*)tail, 1ULL);
+    __syncthreads();
+    const u64 q = s_chunk;
+    const u64 b0 = q * PD_CHUNK, nb = min<u64>(PD_CHUNK, n_slices - b0);
+    if (wave == 0) {  // the chunk's counts, their inclusive scan, the chunk's offset
+        u64 c = lane < nb ? status[b0 + lane] : 0, x = c;
+#pragma unroll
+        for (u32 o = 1; o < 64; o <<= 1) {
+            const u64 y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
-        s_base = acc;
-        if (acc + total > cap_groups) s_fail = 1;
+        pre[lane] = x - c;
+        const u64 tot = __shfl(x, 63, 64);
+        if (lane == 0) {
+            u64 acc = 0;
+            if (q == 0) {
+                __hip_atomic_store(look, RP_INC | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(look + q, RP_AGG | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u64* sp = look + q - 1;
+                for (;;) {
+                    const u64 v = __hip_atomic_load((u64*)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v == 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    acc += v & RP_VAL;
+                    if (v & RP_INC) break;
+                    --sp;
+                }
+                __hip_atomic_store(look + q, RP_INC | (acc + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_base = acc;
+            pre[PD_CHUNK] = tot;
+        }
     }
     __syncthreads();
-    const u64 base = s_base + off;
-    if (!s_fail) {
-        u32 j = 0;
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const u64 key = lkey[tid * PER + k];
-            if (key == SLOT_EMPTY) continue;
-            const u64 row = base + j++;
-            if (KW == 8) ((u64*)out_key)[row] = key;
-            else if (KW == 4) ((u32*)out_key)[row] = (u32)key;
-            else if (KW == 2) ((uint16_t*)out_key)[row] = (uint16_t)key;
-            else out_key[row] = (u8)key;
-            out_cnt[row] = lcnt[tid * PER + k];
+    // each wave copies whole slices: lanes stride over the slice's pairs
+    for (u32 j = wave; j < nb; j += 1024 / 64) {
+        const u64 b = b0 + j;
+        const u64 n = (j + 1 < nb ? pre[j + 1] : pre[PD_CHUNK]) - pre[j];
+        const u64 row0 = s_base + pre[j];
+        const v2u64 __attribute__((address_space(1)))* isl = (const v2u64 __attribute__((address_space(1)))*)(slots + b * S * 2);
+        for (u64 i = lane; i < n; i += 64) {
+            const v2u64 pr = isl[i];
+            const u64 row = row0 + i;
+            if (row >= cap_groups) break;
+            if (KW == 8) ((u64*)out_key)[row] = pr.x;
+            else if (KW == 4) ((u32*)out_key)[row] = (u32)pr.x;
+            else if (KW == 2) ((uint16_t*)out_key)[row] = (uint16_t)pr.x;
+            else out_key[row] = (u8)pr.x;
+            out_cnt[row] = pr.y;
         }
-    } else if (tid == 0) {
-        atomicOr((unsigned long long*)(status + n_slices + 2), 1ULL);
     }
-    // the last workgroup to finish: sentinel group, total (or the failure mark ~0)
+    // the last workgroup: sentinel group, total (or the failure mark ~0)
     if (tid == 0) {
         __threadfence();
-        s_last = atomicAdd((unsigned long long*)(status + n_slices + 3), 1ULL) == n_slices - 1;
+        s_last = atomicAdd((unsigned long long*)(tail + 3), 1ULL) == n_chunks - 1;
     }
     __syncthreads();
     if (s_last && tid == 0) {
         __threadfence();
-        const u64 grand = __hip_atomic_load(status + n_slices - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & RP_VAL;
-        const u64 ns = __hip_atomic_load(status + n_slices + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool bad = __hip_atomic_load(status + n_slices + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        const u64 grand = __hip_atomic_load(look + n_chunks - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & RP_VAL;
+        const u64 ns = __hip_atomic_load(tail + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool bad = __hip_atomic_load(tail + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || grand > cap_groups;
         u64 n = grand;
         if (ns && !bad) {
             if (KW == 8 && grand < cap_groups) {  // only an 8-byte key can be all ones
@@ -797,28 +840,35 @@ hipError_t launch_part_insert(hipStream_t s, const BatchDesc& hb, u64 rows, cons
     return launch_part_slices(s, t, sb, sorted, bounds, table_empty, step);
 }
 
-u64 part_direct_status_words(u64 cap, u32 sb) { return (cap >> sb) + 4; }
+u64 part_direct_status_words(u64 cap, u32 sb) {
+    const u64 n = cap >> sb;
+    return n + (n + PD_CHUNK - 1) / PD_CHUNK + 4;
+}
 
-// The direct stage (part_slice_direct_kernel) of a sorted batch into result columns: keys of
-// key_width bytes, u64 counts; totals[0] = groups, or ~0 when the host must replay the table path.
-// status: part_direct_status_words() words.
-hipError_t launch_part_direct(hipStream_t s, u64 cap, u32 sb, const u64* sorted, const u64* bounds, u64* status, int key_width,
+// The direct stage (part_slice_direct_kernel + part_direct_emit_kernel) of a sorted batch into
+// result columns: keys of key_width bytes, u64 counts; totals[0] = groups, or ~0 when the host must
+// replay the table path.  status: part_direct_status_words() words.  The table's slots are
+// scratch here (left to be initialised, like a reset table).
+hipError_t launch_part_direct(hipStream_t s, const TableDesc& t, u32 sb, const u64* sorted, const u64* bounds, u64* status, int key_width,
                               void* out_key, u64* out_cnt, u64 cap_groups, u64* totals) {
     if (sb != PART_SB) return hipErrorInvalidValue;
-    const u64 n_slices = cap >> sb;
-    hipError_t e = hipMemsetAsync(status, 0, part_direct_status_words(cap, sb) * 8, s);
+    const u64 n_slices = t.cap >> sb, n_chunks = (n_slices + PD_CHUNK - 1) / PD_CHUNK;
+    hipError_t e = hipMemsetAsync(status + n_slices, 0, (n_chunks + 4) * 8, s);
     if (e != hipSuccess) return e;
     const size_t sh = (size_t)(12ULL << PART_SB);
-#define DIRECT_GO(KW)                                                                                                       \
-    hipLaunchKernelGGL((part_slice_direct_kernel<PART_SB, PART_NT_DEFAULT, KW>), dim3((u32)n_slices), dim3(PART_NT_DEFAULT), sh, s, \
-                       sorted, bounds, n_slices, cap, status, (u8*)out_key, out_cnt, cap_groups, totals)
+    hipLaunchKernelGGL((part_slice_direct_kernel<PART_SB, PART_NT_DEFAULT>), dim3((u32)n_slices), dim3(PART_NT_DEFAULT), sh, s, sorted,
+                       bounds, n_slices, t.cap, t.slots, status);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+#define EMIT_GO(KW)                                                                                                                \
+    hipLaunchKernelGGL((part_direct_emit_kernel<KW>), dim3((u32)n_chunks), dim3(1024), 0, s, t.slots, n_slices, status, (u8*)out_key, \
+                       out_cnt, cap_groups, totals)
     switch (key_width) {
-        case 1: DIRECT_GO(1); break;
-        case 2: DIRECT_GO(2); break;
-        case 4: DIRECT_GO(4); break;
-        case 8: DIRECT_GO(8); break;
+        case 1: EMIT_GO(1); break;
+        case 2: EMIT_GO(2); break;
+        case 4: EMIT_GO(4); break;
+        case 8: EMIT_GO(8); break;
         default: return hipErrorInvalidValue;
     }
-#undef DIRECT_GO
+#undef EMIT_GO
     return hipGetLastError();
 }

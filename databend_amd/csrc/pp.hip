@@ -2319,6 +2319,19 @@ struct PsShape {
     static constexpr u32 END = ps_next(ps_next(ps_next(KB, A0), A1), A2);
     static constexpr int NSUM = (ps_has_arg(A0) ? 1 : 0) + (ps_has_arg(A1) ? 1 : 0) + (ps_has_arg(A2) ? 1 : 0);
     static constexpr u32 BW = KW + 1 + NSUM;  // slot body words: key, row count, sums
+    // Narrow slots: a partition holds at most PP_LIT_NT x PP_LIT_RPT (8192) records, so the row
+    // count fits 32 bits, and so does a sum of arguments of at most 2 bytes (|sum| < 8192 x 2^16):
+    // [key as u32 words][count u32][one i32 sum per SUM / AVG] — C4's slot 40 -> 24 bytes, so the
+    // LDS table holds 1.7x the groups and a partition needs half the rounds.  Keys must fill
+    // whole u32 words (their bytes are compared word by word).
+    static constexpr bool small_arg(int a) { return !ps_has_arg(a) || ps_tw(ps_type(a)) <= 2; }
+    static constexpr bool NARROW = (KB % 4 == 0) && small_arg(A0) && small_arg(A1) && small_arg(A2);
+    static constexpr u32 KW32 = KB / 4;
+    static constexpr u32 BW32 = KW32 + 1 + NSUM;
+    static constexpr u32 BWL = NARROW ? (BW32 + 1) / 2 : BW;  // the slot's LDS size in u64 words
+    static constexpr u32 sum32(int a) {
+        return KW32 + 1 + (a > 0 && ps_has_arg(A0) ? 1 : 0) + (a > 1 && ps_has_arg(A1) ? 1 : 0);
+    }
     // Spec state words (build_spec: COUNT 1, SUM 1, AVG 2 — sum, count) and the state record bytes
     static constexpr u32 swords(int a) { return a == 0 ? 0u : (ps_kind(a) == PS_AVG ? 2u : 1u); }
     static constexpr u32 REC_BYTES = 8 * (KW + swords(A0) + swords(A1) + swords(A2));
@@ -2334,8 +2347,10 @@ template <int MODE, int W, int RPT, int SNT, int K0, int K1, int A0, int A1, int
 __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_kernel(u32 n_parts, const u64* __restrict__ raw_off, const u8* __restrict__ raw,
                                                                u32 sub_bits, u32 cap, PPAggOut out, u32* __restrict__ spill, u32 spill_cap) {
     typedef PsShape<K0, K1, A0, A1, A2> SH;
-    constexpr u32 KW = SH::KW, BW = SH::BW;
+    constexpr u32 KW = SH::KW, BW = SH::BWL;
+    constexpr bool NW = SH::NARROW;
     static_assert(KW <= (u32)W && SH::END <= 8u * W, "record words");
+    static_assert(!NW || SNT * RPT <= 8192, "narrow slots: counts and 2-byte sums of <= 8192 records fit 32 bits");
     static_assert(RPT < 32, "per-lane record mask");
     extern __shared__ __attribute__((aligned(16))) u64 lds_raw[];
     l32* tags = (l32*)lds_raw;                                     // [cap] 0 empty, 1 being claimed, else tag
@@ -2400,12 +2415,23 @@ __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_
                 __hip_atomic_compare_exchange_strong(tp, &old, 1u, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (old == 0) {  // claimed: key words, the record's own contribution, then the tag
                     l64* e = body + (size_t)pos * BW;
+                    if constexpr (NW) {
+                        l32* e32 = (l32*)e;
 #pragma unroll
-                    for (u32 w = 0; w < KW; ++w) e[w] = w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w];
-                    e[KW] = 1;
+                        for (u32 w = 0; w < SH::KW32; ++w) e32[w] = (u32)(rk.r[w / 2] >> (32 * (w & 1)));
+                        e32[SH::KW32] = 1;
 #pragma unroll
-                    for (int a = 0; a < 3; ++a)
-                        if (ps_has_arg(SH::agg(a))) e[SH::sumw(a)] = ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a)));
+                        for (int a = 0; a < 3; ++a)
+                            if (ps_has_arg(SH::agg(a)))
+                                e32[SH::sum32(a)] = (u32)ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a)));
+                    } else {
+#pragma unroll
+                        for (u32 w = 0; w < KW; ++w) e[w] = w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w];
+                        e[KW] = 1;
+#pragma unroll
+                        for (int a = 0; a < 3; ++a)
+                            if (ps_has_arg(SH::agg(a))) e[SH::sumw(a)] = ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a)));
+                    }
                     __hip_atomic_store(tp, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     claimed = true;
                     at = (int)pos;
@@ -2417,15 +2443,33 @@ __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_
             if (t == tag) {
                 l64* e = body + (size_t)pos * BW;
                 bool eq = true;
+                if constexpr (NW) {
+                    l32* e32 = (l32*)e;
 #pragma unroll
-                for (u32 w = 0; w < KW; ++w) eq &= e[w] == (w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w]);
+                    for (u32 w = 0; w < SH::KW32; ++w) eq &= e32[w] == (u32)(rk.r[w / 2] >> (32 * (w & 1)));
+                    if (eq) {
+                        auto add32 = [](l32* p, u32 v) {
+                            __hip_atomic_fetch_add((__attribute__((address_space(3))) u32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        };
+                        add32(e32 + SH::KW32, 1u);
+#pragma unroll
+                        for (int a = 0; a < 3; ++a)
+                            if (ps_has_arg(SH::agg(a)))
+                                add32(e32 + SH::sum32(a), (u32)ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a))));
+                    }
+                } else {
+#pragma unroll
+                    for (u32 w = 0; w < KW; ++w) eq &= e[w] == (w + 1 == KW ? (rk.r[w] & SH::KLAST) : rk.r[w]);
+                    if (eq) {
+                        at_add<AS_LDS>((wptr<AS_LDS>)(e + KW), 1ULL);
+#pragma unroll
+                        for (int a = 0; a < 3; ++a)
+                            if (ps_has_arg(SH::agg(a)))
+                                at_add<AS_LDS>((wptr<AS_LDS>)(e + SH::sumw(a)),
+                                               ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a))));
+                    }
+                }
                 if (eq) {
-                    at_add<AS_LDS>((wptr<AS_LDS>)(e + KW), 1ULL);
-#pragma unroll
-                    for (int a = 0; a < 3; ++a)
-                        if (ps_has_arg(SH::agg(a)))
-                            at_add<AS_LDS>((wptr<AS_LDS>)(e + SH::sumw(a)),
-                                           ps_ext(rk.le(SH::off(a), ps_tw(ps_type(SH::agg(a)))), ps_type(SH::agg(a))));
                     at = (int)pos;
                     break;
                 }
@@ -2556,36 +2600,58 @@ __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_
                     const u32 pos = list[k];
                     const l64* e = body + (size_t)pos * BW;
                     const u64 row = gbase + k;
+                    // the slot's key words, row count and sums, read where they are stored (narrow slots
+                    // widened: a sum of signed arguments sign-extended)
+                    auto key_word = [&](u32 w) -> u64 {
+                        if constexpr (NW) {
+                            const l32* e32 = (const l32*)e;
+                            const u64 lo = e32[2 * w], hi = 2 * w + 1 < SH::KW32 ? (u64)e32[2 * w + 1] : 0;
+                            return lo | (hi << 32);
+                        } else {
+                            return e[w];
+                        }
+                    };
+                    auto count_of = [&]() -> u64 {
+                        if constexpr (NW) return ((const l32*)e)[SH::KW32];
+                        else return e[KW];
+                    };
+                    auto sum_of = [&](int a) -> u64 {
+                        if constexpr (NW) {
+                            const u32 v = ((const l32*)e)[SH::sum32(a)];
+                            return ps_signed(ps_type(SH::agg(a))) ? (u64)(i64)(int32_t)v : (u64)v;
+                        } else {
+                            return e[SH::sumw(a)];
+                        }
+                    };
                     if (MODE == 1) {  // group records in the state-record format: [key words][Spec state words]
                         if (row < out.grec_cap) {
                             u64* d = (u64*)(out.grec + row * SH::REC_BYTES);
 #pragma unroll
-                            for (u32 w = 0; w < KW; ++w) d[w] = e[w];
+                            for (u32 w = 0; w < KW; ++w) d[w] = key_word(w);
                             u32 q = KW;
-                            const u64 cnt = e[KW];
 #pragma unroll
                             for (int a = 0; a < 3; ++a) {
                                 const int A = SH::agg(a);
                                 if (A == 0) continue;
-                                if (ps_kind(A) == PS_COUNT) d[q++] = cnt;
-                                else if (ps_kind(A) == PS_SUM) d[q++] = e[SH::sumw(a)];
+                                if (ps_kind(A) == PS_COUNT) d[q++] = count_of();
+                                else if (ps_kind(A) == PS_SUM) d[q++] = sum_of(a);
                                 else {
-                                    d[q++] = e[SH::sumw(a)];
-                                    d[q++] = cnt;
+                                    d[q++] = sum_of(a);
+                                    d[q++] = count_of();
                                 }
                             }
                         }
                     } else if (row < out.cols.cap_groups) {
                         RegRec<KW> kr;
 #pragma unroll
-                        for (u32 w = 0; w < KW; ++w) kr.r[w] = e[w];
+                        for (u32 w = 0; w < KW; ++w) kr.r[w] = key_word(w);
+                        const u64 cnt = count_of();
                         write_bytes(out.cols.key_data[0], row, ps_tw(K0), kr.le(0, ps_tw(K0)), 0);
                         if (out.cols.key_valid[0]) out.cols.key_valid[0][row] = 1;
                         if (K1 >= 0) {
                             write_bytes(out.cols.key_data[1], row, ps_tw(K1), kr.le(ps_tw(K0), ps_tw(K1)), 0);
                             if (out.cols.key_valid[1]) out.cols.key_valid[1][row] = 1;
                         }
-                        const u64 cnt = e[KW];
 #pragma unroll
                         for (int a = 0; a < 3; ++a) {
                             const int A = SH::agg(a);
@@ -2594,9 +2660,9 @@ __global__ void __launch_bounds__(SNT, (SNT / 256) * PP_LIT_PER_CU) pp_agg_spec_
                             if (ps_kind(A) == PS_COUNT) {
                                 v = cnt;
                             } else if (ps_kind(A) == PS_SUM) {
-                                v = e[SH::sumw(a)];
+                                v = sum_of(a);
                             } else {  // AVG: the sum as i64 (u64 for unsigned arguments) / count, as f64
-                                const u64 sv = e[SH::sumw(a)];
+                                const u64 sv = sum_of(a);
                                 const double sum = ps_signed(ps_type(A)) ? (double)(i64)sv : (double)sv;
                                 v = (u64)__double_as_longlong(sum / (double)cnt);
                             }
@@ -2661,7 +2727,7 @@ static int ps_literal_shape(const Spec& S, u32* cap, u32* max_records) {
 #define PS_TRY(WW, K0, K1, A0, A1, A2)                        \
     if (found < 0 && ps_match<K0, K1, A0, A1, A2>(S)) {     \
         found = id;                                         \
-        bw = PsShape<K0, K1, A0, A1, A2>::BW;               \
+        bw = PsShape<K0, K1, A0, A1, A2>::BWL;              \
         w = WW;                                             \
     }                                                       \
     ++id;
@@ -2684,7 +2750,7 @@ static void launch_ps_literal(hipStream_t s, int shape, int mode, u32 n_parts, c
     int id = 0;
 #define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
     if (shape == id) {                                                                                                  \
-        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BW, cap = std::min(ps_cap(bw, WW, PP_LIT_NT, PS_LDS / PP_LIT_PER_CU), cap_x); \
+        const u32 bw = PsShape<K0, K1, A0, A1, A2>::BWL, cap = std::min(ps_cap(bw, WW, PP_LIT_NT, PS_LDS / PP_LIT_PER_CU), cap_x); \
         const size_t lds = ps_lds_bytes(cap, bw, WW, PP_LIT_NT) + 16;                                                   \
         if (mode == 0)                                                                                                  \
             hipLaunchKernelGGL((pp_agg_spec_kernel<0, WW, PP_LIT_RPT, PP_LIT_NT, K0, K1, A0, A1, A2>), dim3(grid),         \

@@ -10,7 +10,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from databend_amd import abi
+from databend_amd import abi, ffi
 from databend_amd import column as col
 from databend_amd.aggregates import AggregateFunctionFactory
 from databend_amd.aggregator import AggregateHashTable, AggregatorParams, HashTableConfig
@@ -102,7 +102,7 @@ def test_direct_stage_steps(kind, distinct, n, hint):
         exp_groups = len(np.unique(vals))
         check(lib().dbg_agg_reset(tab.ht.h))
         tab.add(dev)
-        rc, g = tab.finalize(1024)
+        rc, g = tab.finalize(exp_groups // 2)
         assert rc == abi.DBG_ERR_INVALID and g == exp_groups
         rc, g = tab.finalize(exp_groups + 10)  # the table was kept: finalize again
         check(rc)
@@ -110,7 +110,11 @@ def test_direct_stage_steps(kind, distinct, n, hint):
         for step in range(2):
             check(lib().dbg_agg_reset(tab.ht.h))
             tab.add(dev)
+            ffi.prof_reset()
+            ffi.prof_enable(True)
             rc, g = tab.finalize(exp_groups + 10)
+            ffi.prof_enable(False)
+            assert "part_direct" in ffi.prof_read(), "the direct stage did not run"
             check(rc)
             _check(tab, g, vals)
             # recycled: the handle is empty again
@@ -125,20 +129,25 @@ def test_direct_stage_full_slice_replays():
     """More distinct keys in one 4096-slot slice than it has slots: the direct stage gives up, the
     regular slices (overflow records + fixup) from the same sorted keys produce the result."""
     rng = np.random.default_rng(7)
-    hi = rng.integers(1, 1 << 43, 5000, dtype=np.int64)
-    crowd = np.array([slot_unmix((int(h) << 20) | int(i % 4096)) for i, h in enumerate(hi)], dtype=np.uint64).view(np.int64)
-    other = rng.integers(-2**63, 2**63 - 1, 200_000, dtype=np.int64)
-    pool = np.concatenate([crowd, other])
-    vals = pool[rng.integers(0, len(pool), 1 << 21)]
-    vals[: len(crowd)] = crowd  # every crowded key present
-    tab = _Table(col.Int64, 1 << 20)
+    tab = _Table(col.Int64, 1 << 19)
     try:
+        cap = C.c_uint64()
+        check(lib().dbg_agg_capacity(tab.ht.h, C.byref(cap)))
+        lg = cap.value.bit_length() - 1
+        assert cap.value == 1 << lg and lg >= 20
+        hi = rng.integers(1, 1 << (63 - lg), 5000, dtype=np.int64)
+        # slot_mix(key) & (cap - 1) = i % 4096: every crowded key in slice 0
+        crowd = np.array([slot_unmix((int(h) << lg) | int(i % 4096)) for i, h in enumerate(hi)], dtype=np.uint64).view(np.int64)
+        other = rng.integers(-2**63, 2**63 - 1, 200_000, dtype=np.int64)
+        pool = np.concatenate([crowd, other])
+        vals = pool[rng.integers(0, len(pool), 1 << 21)]
+        vals[: len(crowd)] = crowd  # every crowded key present
         dev = DeviceColumn.from_host(Column.from_numbers(col.Int64, vals))
         check(lib().dbg_agg_reset(tab.ht.h))
         tab.add(dev)
-        cap = C.c_uint64()
-        check(lib().dbg_agg_capacity(tab.ht.h, C.byref(cap)))
-        assert cap.value == 1 << 20  # the crowd lands in slice 0 only at this capacity
+        cap2 = C.c_uint64()
+        check(lib().dbg_agg_capacity(tab.ht.h, C.byref(cap2)))
+        assert cap2.value == cap.value
         rc, g = tab.finalize(len(np.unique(vals)) + 10)
         check(rc)
         _check(tab, g, vals)
