@@ -121,6 +121,9 @@ __device__ __forceinline__ u64 scan256(u64 v, u64* tmp) {
 // predecessors are running or done when it looks back (no circular wait).  Rows keep their
 // relative order within a digit (LSD needs a stable pass): a wave ranks its 16 rounds of 64
 // rows in order, lanes ranked among equal digits by ballot, wave counts prefixed in wave order.
+// Measured and not kept (round 6): the next tile's rows loaded into registers while the current
+// tile is ranked (a second register set: 168 VGPRs, C3 insert 16.7 -> 19.1 ms) or while it is
+// written out (the same registers, but the loads in flight still held them: 138 VGPRs, 19.2 ms).
 template <int W, bool RAW, int RP_NT, int RP_IPT>
 __global__ void __launch_bounds__(RP_NT) rp_scatter_kernel(const u8* __restrict__ src, u64 rows, u32 shift, u32 bits,
                                                            const u32* __restrict__ hist, u64* __restrict__ status,

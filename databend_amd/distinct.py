@@ -276,11 +276,14 @@ class DistinctPartial:
         batch of its own groups (or pairs), so the copies of earlier host blocks are released and
         the partial's memory follows its groups and value sets, not the rows it saw.  Compaction
         synchronises the table's stream, so the device columns kept for staged launches are free
-        to go too."""
-        self.table.compact()
+        to go too — but only when every table compacted: dbg_agg_compact returns early (no
+        synchronisation) for inline-key or partitioned handles, whose staged launches may still
+        read the kept columns."""
+        done = self.table.compact()
         for t in self.pairs.values():
-            t.compact()
-        self._keep.clear()
+            done = t.compact() and done
+        if done:
+            self._keep.clear()
 
     def on_finish(self, n_parts: int) -> List[AggregateMeta]:
         t_b = export_buckets(self.table, n_parts)
