@@ -57,8 +57,9 @@ def parse():
                         "records shipped while the next chunk is scattered (dbg_agg_exchange_payload_chunk)")
     p.add_argument("--shuffle", choices=["auto", "before_partial", "before_merge"], default="auto",
                    help="N > 1, high cardinality: route level-1 records before any aggregation (group_by_shuffle_mode "
-                        "= before_partial, partitioned payload) or partial states after it; auto = before_partial when "
-                        "every rank's cardinality probe chose the partitioned payload")
+                        "= before_partial, partitioned payload) or partial states after it; auto = before_partial when, "
+                        "on every rank, the probe chose the partitioned payload or the rows' raw records are fewer "
+                        "bytes than the rank's group records (exchange.prefer_before_partial)")
     p.add_argument("--scaling", choices=["weak", "strong"], default=None,
                    help="weak: every GPU aggregates the config's rows; strong: the config's rows are split over "
                         "the GPUs (default: strong for the 1B-row configs 3-5, weak for 1-2)")
@@ -285,7 +286,15 @@ def main():
         t.reset()
         t.add_groups(runner.key_abi[0], runner.arg_cols[0], rows=rows, filter_program=runner.programs[0], on_device=True)
         fixed = all(runner.inputs[0][k].dtype.type_id != abi.STRING for k in shape.keys)
-        vote = torch.tensor([1 if (t.strategy()[0] and fixed) else 0], dtype=torch.int32, device=dev)
+        # before_partial when shipping the rows is fewer bytes than shipping this rank's groups
+        # (exchange.prefer_before_partial), or when the probe already chose the partitioned payload;
+        # the same choice on every rank (one all-reduce, untimed).  String keys stay before_merge
+        # (a payload record references a local row).
+        from databend_amd.exchange import payload_widths, prefer_before_partial
+        want = bool(t.strategy()[0])
+        if fixed and not want:
+            want = prefer_before_partial(rows, t.finalize()[0], payload_widths(runner.params))
+        vote = torch.tensor([1 if (want and fixed) else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(vote, op=dist.ReduceOp.MIN)
         before_partial = args.shuffle == "before_partial" or (args.shuffle == "auto" and int(vote.item()) == 1)
         t.reset()

@@ -2389,6 +2389,8 @@ static int fin_complete(dbg_agg_handle* h, bool* retry, uint64_t* n_groups, uint
     }
     if (h->hcounters[CNT_ERR] & ERR_OVF_LOST) return fail(DBG_ERR_INTERNAL, "overflow list exhausted");
     if (h->hcounters[CNT_ERR] & ERR_MINMAX_SPIN) return fail(DBG_ERR_INTERNAL, MINMAX_SPIN_MSG);
+    if (h->hcounters[CNT_ERR] & ERR_CHAIN_SPIN)
+        return fail(DBG_ERR_INTERNAL, "fused finalize: a parked row was not posted in time (GPU hand-off stalled)");
     if (h->hcounters[CNT_ERR] & ERR_FIXED_INCOMPLETE)
         return fail(DBG_ERR_INVALID, "fixed-capacity exchange incomplete (a partial held more groups than the "
                                      "buffer, or unresolved overflow): use dbg_agg_partition + export_records");

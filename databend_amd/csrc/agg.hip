@@ -2434,6 +2434,243 @@ __device__ __forceinline__ void fused_chain(const Spec& S, const BatchDesc* batc
     if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
 }
 
+// The fused chain for COUNT(*) over a key of <= 16 bits (ClickBench Q8's Int16 AdvEngineID), with
+// self-validating parked rows so that every hand-off costs one round trip instead of three.  The
+// chain above parks a table, drains the stores, takes a ticket, and the last arrival then loads
+// the rows: store drain + ticket + loads on the critical path at both levels.  Here a workgroup
+// takes its ticket FIRST and parks only if it is not the last: the last arrival merges its own
+// table in place (no park, no reload) and loads the others' rows while they may still be landing.
+// A parked entry is one word, [key 16 b | count 24 b (level 2: 28 b) | tag 24 b (level 2: 20 b)],
+// the tag the launch's sequence number, so an entry is accepted only once this launch's word is
+// visible; the row's entry count is posted as [seq 44 b | entries 20 b] after the entries.  A
+// reader spins (bounded) on an item until both are current — no acquire / release pair, no
+// second round trip.  (A workgroup covers < 2^24 rows, a group of 16 < 2^28: the host launches
+// at most 256 workgroups over < 2^32 rows, and a grid below 256 covers <= 32768 rows each.)
+#ifndef CHAIN_TAGGED
+#define CHAIN_TAGGED 1  // 0: the generic chain for these launches too (A/B builds: make EXP=1 EXTRA=-DCHAIN_TAGGED=0)
+#endif
+constexpr bool kChainTagged = CHAIN_TAGGED != 0;
+#define TAG1_BITS 24
+#define TAG2_BITS 20
+__device__ __forceinline__ u64 chain_pack(u64 key, u64 cnt, u64 seq, int level) {
+    const int tb = level == 1 ? TAG1_BITS : TAG2_BITS;
+    return key | (cnt << 16) | ((seq & ((1ULL << tb) - 1)) << (64 - tb));
+}
+
+template <typename T>
+__device__ __forceinline__ void fused_chain_tagged(const Spec& S, const BatchDesc* batches, const BatchDesc& B, u64* lds, u32 lds_slots,
+                                                   u32 sw, u32* lcount, u32 nt, const TableDesc& t, u32 my_claims, u32 my_ovf,
+                                                   const FusedFin& ff) {
+    constexpr int OWN = 4;  // own slots per thread the last leader holds in registers (lds_slots <= 4 x nt, host-checked)
+    __shared__ u32 role, bad, vcl, wg_ovf;
+    __shared__ u64 hbm_claims, ovf_seen;
+    const u32 lmask = lds_slots - 1;
+    const u32 llimit = lds_slots - lds_slots / 4;
+    u64* counts = t.scratch;
+    u64* tickets = t.scratch + t.scr_blocks;
+    u64* gmeta = tickets + t.scr_blocks / 2;
+    u64* rows = t.scratch + 2 * (u64)t.scr_blocks;  // SCR_ENTRIES words per workgroup (one word per entry)
+    u64* grows = rows + (u64)t.scr_blocks * SCR_ENTRIES * sw;
+    const u32 n_groups = (gridDim.x + SCR_GROUP - 1) / SCR_GROUP;
+    const u32 g = blockIdx.x / SCR_GROUP;
+    const u32 gsize = min((u32)SCR_GROUP, gridDim.x - g * SCR_GROUP);
+    const u64 seq = ff.seq & ((1ULL << 44) - 1);
+    if (threadIdx.x == 0) wg_ovf = 0;
+    __syncthreads();
+    // A table too large for a row goes to the HBM table before the ticket, so its claims and
+    // possible overflow pushes ride on the ticket (uniform: lcount[0] is final).
+    auto flush_if_large = [&]() -> bool {
+        if (lcount[0] <= SCR_ENTRIES) return false;
+        flush_lds_direct<true, false>(S, batches, B, lds, lds_slots, sw, nt, t, my_claims);
+        my_ovf += threadIdx.x == 0 ? 1u : 0u;
+        return true;
+    };
+    auto claims_and_ticket = [&](u64* ticket, u64 carried_claims, u64 carried_ovf) -> u64 {
+        if (my_claims) atomicAdd(&lcount[1], my_claims);
+        if (my_ovf) atomicAdd(&wg_ovf, my_ovf);
+        my_claims = my_ovf = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        u64 tk = 0;
+        if (threadIdx.x == 0) {
+            if (lcount[1]) {
+                atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)lcount[1]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const u64 add = 1 + ((carried_claims + lcount[1]) << 16) + ((carried_ovf + wg_ovf) << 40);
+            tk = atomicAdd((unsigned long long*)ticket, (unsigned long long)add) + add;
+        }
+        return tk;
+    };
+    // park the LDS table as packed words (sc1), then post the entry count (sc1, after the drain)
+    auto park_tagged = [&](u64* dst, u64* meta, int level) {
+        if (threadIdx.x == 0) lcount[2] = 0;
+        __syncthreads();
+        for (u32 s = threadIdx.x; s < lds_slots; s += nt) {
+            const u64* p = lds + (u64)s * sw;
+            if (p[0] == SLOT_EMPTY) continue;
+            const u32 k = atomicAdd(&lcount[2], 1u);
+            st_sc1(dst + k, chain_pack(p[0], p[1], seq, level));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) st_sc1(meta, (seq << 20) | lcount[2]);
+    };
+    // an overflow record [key][count] (the host grows the table and finalizes again)
+    auto push_kc = [&](u64 key, u64 c) {
+        const u64 k = atomicAdd((unsigned long long*)(t.counters + CNT_OVF_RECS), 1ULL);
+        if (k >= t.ovf_recs_cap) {
+            atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_OVF_LOST);
+            return;
+        }
+        u64* r = t.ovf_recs + k * t.stride_words;
+        r[0] = key;
+        r[1] = c;
+    };
+    // item k of a parked row: spins until the row's count and (k < count) the entry are this
+    // launch's; false = no entry k.  A spin that does not settle raises ERR_CHAIN_SPIN.
+    auto read_item = [&](const u64* meta, const u64* row, u32 k, int level, u64& key, u64& cnt) -> bool {
+        const int tb = level == 1 ? TAG1_BITS : TAG2_BITS;
+        const u64 tag = seq & ((1ULL << tb) - 1);
+        for (u32 it = 0; it < (1u << 22); ++it) {
+            const u64 m = ld_sc1(meta);
+            const u64 w = ld_sc1(row + k);
+            if ((m >> 20) == seq) {
+                if (k >= (m & 0xFFFFF)) return false;
+                if ((w >> (64 - tb)) == tag) {
+                    key = w & 0xFFFF;
+                    cnt = (w << tb) >> (tb + 16);
+                    return true;
+                }
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        atomicOr((unsigned long long*)(t.counters + CNT_ERR), (unsigned long long)ERR_CHAIN_SPIN);
+        bad = 1;
+        return false;
+    };
+    // 1. ticket first; a workgroup that is not its group's last parks
+    bool flushed = flush_if_large();
+    {
+        const u64 tk = claims_and_ticket(tickets + g, 0, 0);
+        if (threadIdx.x == 0) {
+            role = (tk & 0xFFFF) == gsize ? 1u : 0u;
+            hbm_claims = (tk >> 16) & 0xFFFFFF;
+            ovf_seen = tk >> 40;
+            wg_ovf = 0;
+            bad = 0;
+        }
+    }
+    __syncthreads();
+    if (!role) {
+        if (flushed) {
+            if (threadIdx.x == 0) st_sc1(counts + blockIdx.x, seq << 20);
+        } else {
+            park_tagged(rows + (u64)blockIdx.x * SCR_ENTRIES * sw, counts + blockIdx.x, 1);
+        }
+        return;
+    }
+    // 2. group leader: the members' rows merged into its own LDS table
+    if (threadIdx.x == 0) tickets[g] = 0;  // all members have added
+    for (u32 f = threadIdx.x; f < gsize * SCR_ENTRIES; f += nt) {
+        const u64 b = (u64)g * SCR_GROUP + f / SCR_ENTRIES;
+        if (b == blockIdx.x) continue;
+        u64 key, c;
+        if (!read_item(counts + b, rows + b * SCR_ENTRIES * sw, f % SCR_ENTRIES, 1, key, c)) continue;
+        const int ls = lds_find<true>(S, batches, B.keys, 0, key, 0, lds, lmask, sw, lcount, llimit);
+        if (ls >= 0) {
+            at_add<AS_LDS>(asp<AS_LDS>(lds + (u64)ls * sw + 1), c);
+            continue;
+        }
+        bool claimed;
+        const u64 gs = g_find<true>(S, batches, B.keys, 0, key, 0, t, t.probe_limit, claimed);
+        if (gs == ~0ULL) {
+            push_kc(key, c);
+            my_ovf++;
+            continue;
+        }
+        my_claims += claimed ? 1 : 0;
+        at_add<AS_GLB>(asp<AS_GLB>(t.slots + gs * t.stride_words + 1), c);
+    }
+    __syncthreads();
+    // 3. level 2: ticket first again; a leader that is not the last parks its group's table
+    flushed = flush_if_large();
+    {
+        const u64 tk = claims_and_ticket(t.counters + CNT_FIN_TICKET, hbm_claims, ovf_seen);
+        if (threadIdx.x == 0) {
+            role = (tk & 0xFFFF) == n_groups ? 2u : 0u;
+            hbm_claims = (tk >> 16) & 0xFFFFFF;
+            ovf_seen = tk >> 40;
+        }
+    }
+    __syncthreads();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) atomicMax((unsigned long long*)ff.trace + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (role != 2) {
+        if (flushed) {
+            if (threadIdx.x == 0) st_sc1(gmeta + g, seq << 20);
+        } else {
+            park_tagged(grows + (u64)g * SCR_ENTRIES * sw, gmeta + g, 2);
+        }
+        return;
+    }
+    // 4. the last leader: its own table into registers, the view of the HBM table, own entries
+    //    and the other group rows merged into the view, finalize
+    if (threadIdx.x == 0) {
+        atomicExch((unsigned long long*)(t.counters + CNT_FIN_TICKET), 0ULL);
+        atomicExch((unsigned long long*)(t.counters + CNT_TAIL), 0ULL);
+        vcl = 0;
+        if (kPhaseTrace && ff.trace) ff.trace[4] = __builtin_amdgcn_s_memrealtime();
+    }
+    u64 okey[OWN], ocnt[OWN];
+#pragma unroll
+    for (int j = 0; j < OWN; ++j) {
+        const u32 s = threadIdx.x + (u32)j * nt;
+        okey[j] = SLOT_EMPTY;
+        ocnt[j] = 0;
+        if (!flushed && s < lds_slots) {
+            okey[j] = lds[(u64)s * sw];
+            ocnt[j] = lds[(u64)s * sw + 1];
+        }
+    }
+    __syncthreads();  // the view overwrites the table
+    const u64 n = (t.cap + 1) * sw;  // host: <= the launch's dynamic LDS
+    if (ff.table_empty && hbm_claims == 0)
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = S.slot_init[i % sw];
+    else
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = ld_sc1(t.slots + i);
+    __syncthreads();
+    u32 vclaims = 0;
+    auto to_view = [&](u64 key, u64 c) {
+        u64 slot;
+        if (view_find(lds, t, key, vclaims, slot)) {
+            at_add<AS_LDS>(asp<AS_LDS>(lds + slot * sw + 1), c);
+        } else {
+            push_kc(key, c);
+            bad = 1;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < OWN; ++j)
+        if (okey[j] != SLOT_EMPTY) to_view(okey[j], ocnt[j]);
+    for (u32 f = threadIdx.x; f < n_groups * SCR_ENTRIES; f += nt) {
+        const u64 gg = f / SCR_ENTRIES;
+        if (gg == g) continue;
+        u64 key, c;
+        if (read_item(gmeta + gg, grows + gg * SCR_ENTRIES * sw, f % SCR_ENTRIES, 2, key, c)) to_view(key, c);
+    }
+    if (vclaims) atomicAdd(&vcl, vclaims);
+    __syncthreads();
+    const bool known = ff.table_empty && ovf_seen == 0 && !bad;
+    if (threadIdx.x == 0 && vcl && !known) {
+        atomicAdd((unsigned long long*)(t.counters + CNT_CLAIMS), (unsigned long long)vcl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
+    finalize_count_only<T>(t, lds, ff, known, vcl);
+    if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
+}
+
 // ------------------------------------------------------------------------------------------
 // agg_insert_fast: one non-null integer key column, optional `key <cmp> constant` predicate on
 // that same column (GROUP BY x WHERE x <> c: ClickBench Q8; or no predicate: Q16).  Streams the
@@ -2836,6 +3073,12 @@ __global__ void __launch_bounds__(NT) agg_insert_fast_kernel(const Spec* __restr
         }
     }
     if (ff.on && t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks) {
+        if constexpr (CO && sizeof(T) <= 2) {
+            if (kChainTagged && lds_slots <= 4 * NT) {
+                fused_chain_tagged<T>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims, my_ovf, ff);
+                return;
+            }
+        }
         fused_chain<T, CO>(S, batches, B, lds, lds_slots, sw, lcount, NT, t, my_claims, my_ovf, ff);
         return;
     }

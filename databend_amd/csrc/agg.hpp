@@ -102,7 +102,7 @@ inline size_t scr_words(u32 blocks, u32 stride_words) {
 
 enum { CNT_CLAIMS = 0, CNT_OVF_ROWS = 1, CNT_OVF_RECS = 2, CNT_ERR = 3, CNT_FIX_FAIL = 4, CNT_FIX_TICKET = 5, CNT_FIN_TICKET = 6,
        CNT_TAIL = 7, CNT_WORDS = 8 };
-enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4, ERR_MINMAX_SPIN = 8 };
+enum { ERR_DEC_OVERFLOW = 1, ERR_OVF_LOST = 2, ERR_FIXED_INCOMPLETE = 4, ERR_MINMAX_SPIN = 8, ERR_CHAIN_SPIN = 16 };
 
 // ---- device helpers shared by agg.hip and part.hip ----
 // Slot placement for inline keys: any good mixer works (placement is not observable); the

@@ -225,3 +225,42 @@ def test_exchange_payload_chunk_rccl_world_1():
     comm.close()
     ok, oa = oracle_aggregate(keys, aggs)
     assert_results_equal(gk, ga, ok, oa)
+
+
+def test_payload_shuffle_finish_ships_late_chunks_world_1():
+    """exchange.PayloadShuffle over torch.distributed (RCCL, world 1) on a real partitioned table:
+    chunk 0 shipped, chunks 1 and 2 added after the last ship() — finish() must ship them (the
+    library's last=1 does the same), so the result is every row's aggregation."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    from databend_amd.exchange import PayloadShuffle
+    from tests.test_gpu_parity import slice_col
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    keys, aggs = _data(15, 300_000)
+    fns = [F.get(n, [], [c.dtype] if c is not None else []) for n, c in aggs]
+    t = AggregateHashTable(AggregatorParams([k.dtype for k in keys], fns), HashTableConfig(True))
+    t.set_strategy(abi.STRATEGY_PARTITIONED)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        sh = PayloadShuffle(t, torch.device("cuda", torch.cuda.current_device()))
+        for c in range(3):
+            lo, hi = 100_000 * c, 100_000 * (c + 1)
+            t.add_groups([DeviceColumn.from_host(slice_col(k, lo, hi)) for k in keys],
+                         [None if x is None else DeviceColumn.from_host(slice_col(x, lo, hi)) for _, x in aggs],
+                         rows=hi - lo, on_device=True)
+            if c == 0:
+                sh.ship()
+        sh.finish()
+        torch.cuda.synchronize()
+        gk, ga = _result(t, len(aggs))
+    finally:
+        t.close()
+        dist.destroy_process_group()
+    ok, oa = oracle_aggregate(keys, aggs)
+    assert_results_equal(gk, ga, ok, oa)

@@ -221,3 +221,105 @@ def test_payload_owned_covers_every_partition_once():
                 owner[p] = d
                 assert p * n // 256 == d
         assert sorted(owner) == list(range(256))
+
+
+class KeyPayload:
+    """ClickBench Q17's shape (one Int64 UserID key, COUNT(*)) as the level-1 payload a
+    partitioned-mode table holds: one raw record per row — the key's 8 bytes (the library's raw
+    width for this shape, exchange.payload_widths: (8, 16)) — in the level-1 partition given by the
+    top 8 bits of the group hash (oracle.group_hash, the restated group_hash_columns), and no state
+    records.  Export: destination-major, partition-major within a destination."""
+
+    def __init__(self, rank, seed, pool, n):
+        from oracle import oracle
+        from databend_amd import column as col
+        from databend_amd.column import Column
+        rng = np.random.default_rng(seed)
+        self.keys = pool[rng.zipf(1.3, n) % len(pool)]
+        h = oracle.group_hash([Column.from_numbers(col.Int64, self.keys)])
+        self.part = (h >> np.uint64(56)).astype(np.int64)
+        self.counts = np.zeros((2, 256), np.uint64)
+        np.add.at(self.counts[0], self.part, 1)
+        self.widths = (8, 16)
+        self.imported = None
+
+    def payload_counts(self):
+        return self.counts.copy(), self.widths
+
+    def payload_export(self, n, buf):
+        import torch
+        order = np.argsort(self.part, kind="stable")  # partition-major = destination-major
+        b = self.keys[order].astype(np.int64).view(np.uint8)
+        buf[:len(b)] = torch.from_numpy(b.copy())
+
+    def payload_import(self, n, rank, all_counts, raw, state):
+        self.imported = (all_counts.copy(), raw.numpy().copy())
+
+
+def _q17_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from databend_amd.exchange import exchange_payload, payload_owned
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pool = np.random.default_rng(5).integers(-2**63, 2**63 - 1, 20_000, dtype=np.int64)
+        t = KeyPayload(rank, 300 + rank, pool, 30_000)
+        exchange_payload(t, "cpu")
+        all_counts, raw = t.imported
+        lo, hi = payload_owned(rank, world)
+        n_in = int(all_counts[:, 0, lo:hi].sum())
+        got = raw[:8 * n_in].view(np.int64)
+        mine = {}
+        for s in range(world):  # what every source holds of this rank's partitions
+            src = KeyPayload(s, 300 + s, pool, 30_000)
+            sel = (src.part >= lo) & (src.part < hi)
+            for k in src.keys[sel]:
+                mine[int(k)] = mine.get(int(k), 0) + 1
+        u, c = np.unique(got, return_counts=True)
+        assert dict(zip(u.tolist(), c.tolist())) == mine, rank  # the owner's GROUP BY key, COUNT(*)
+        groups = [None] * world
+        dist.all_gather_object(groups, sorted(mine))
+        seen = set()
+        for gset in groups:  # disjoint group sets, together every key of every rank
+            assert not (seen & set(gset))
+            seen |= set(gset)
+        every = set()
+        for s in range(world):
+            every |= set(KeyPayload(s, 300 + s, pool, 30_000).keys.tolist())
+        assert seen == every
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_q17_shape_before_partial_shuffle(world):
+    """C3's shape through the before-partial shuffle: every key's rows meet on the rank that owns
+    its level-1 partition, so one aggregation there gives its full COUNT(*), and the ranks' group
+    sets are disjoint and cover every key."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_q17_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
+
+
+def test_prefer_before_partial_rule():
+    """group_by_shuffle_mode chosen by bytes: Q17 at 8 GPUs (1.25e8 rows, ~8e7 groups per GPU)
+    ships rows; Q8-like low cardinality ships groups."""
+    from databend_amd.exchange import prefer_before_partial
+    assert prefer_before_partial(125_000_000, 80_000_000, (8, 16))
+    assert not prefer_before_partial(125_000_000, 32, (8, 16))
+    assert not prefer_before_partial(1_000, 499, (8, 16)) and prefer_before_partial(1_000, 500, (8, 16))
