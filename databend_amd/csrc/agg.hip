@@ -2028,7 +2028,7 @@ __device__ __forceinline__ void merge_parked(const Spec& S, u64* st, const u64* 
 // cache, so its length is latency.
 template <typename T>
 __device__ __forceinline__ void finalize_count_only(const TableDesc& t, const u64* view, const FusedFin& ff, bool known,
-                                                    u32 view_claims) {
+                                                    u32 view_claims, bool hbm_clean = false) {
     __shared__ u64 wsum[FIN_NT / 64];
     __shared__ u64 cnts[CNT_WORDS];
     auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
@@ -2095,7 +2095,8 @@ __device__ __forceinline__ void finalize_count_only(const TableDesc& t, const u6
     }
     if (!rc)  // the table outlives this finalize: the view holds groups the HBM table does not
         for (u64 i = threadIdx.x; i < n_slots * 2; i += FIN_NT) t.slots[i] = view[i];
-    if (rc)  // table_init of the claimed slots of the view (the HBM copy may hold fewer: same values)
+    if (rc && !hbm_clean)  // table_init of the claimed slots of the view (the HBM copy may hold fewer: same
+                           // values); hbm_clean: empty at launch and never written since — nothing to undo
 #pragma unroll
         for (u32 k = 0; k < PER; ++k)
             if ((occ >> k) & 1) {
@@ -2641,8 +2642,9 @@ __device__ __forceinline__ void fused_chain_tagged(const Spec& S, const BatchDes
     }
     __syncthreads();  // the view overwrites the table
     const u64 n = (t.cap + 1) * sw;  // host: <= the launch's dynamic LDS
-    if (ff.table_empty && hbm_claims == 0)
-        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = S.slot_init[i % sw];
+    const bool hbm_clean = ff.table_empty && hbm_claims == 0;
+    if (hbm_clean)  // COUNT(*) slots start [EMPTY][0]: no load of the Spec's initial slot
+        for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = (i % sw) == 0 ? SLOT_EMPTY : 0ULL;
     else
         for (u64 i = threadIdx.x; i < n; i += nt) lds[i] = ld_sc1(t.slots + i);
     __syncthreads();
@@ -2674,7 +2676,7 @@ __device__ __forceinline__ void fused_chain_tagged(const Spec& S, const BatchDes
     }
     __syncthreads();
     if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[5] = __builtin_amdgcn_s_memrealtime();
-    finalize_count_only<T>(t, lds, ff, known, vcl);
+    finalize_count_only<T>(t, lds, ff, known, vcl, hbm_clean && !bad);
     if (kPhaseTrace && ff.trace && threadIdx.x == 0) ff.trace[6] = __builtin_amdgcn_s_memrealtime();
 }
 
