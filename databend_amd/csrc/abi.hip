@@ -1083,6 +1083,12 @@ static int pp_scatter(dbg_agg_handle* h, int level, int src, int kind, const u8*
 // Level 1 (TransformPartialAggregate::transform in partitioned mode): the batch's selected rows
 // become records appended to the payload, grouped into 256 partitions (PartitionedPayload::
 // append_rows, EAGG/partitioned_payload.rs:100-143).
+// EXPERIMENT (DBG_X_PPDIG=0): level 2 counts from the records instead of the digit array
+static bool kX_no_dig() {
+    static const bool off = X_ENV("DBG_X_PPDIG") && X_ENV("DBG_X_PPDIG")[0] == '0';
+    return off;
+}
+
 static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 rows, int kind) {
     const Spec& S = h->spec;
     auto& K = h->ppk[kind];
@@ -1112,7 +1118,8 @@ static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 row
         K.l1_cap = ncap;
     }
     // the level-2 digits ride along while every record so far has them (fixed-shape raw batches)
-    const bool with_dig = F.kind == 1 && kind == 0 && K.dig_n == K.l1_n;
+    // (EXPERIMENT, DBG_X_PPDIG=0: no digits at all)
+    const bool with_dig = F.kind == 1 && kind == 0 && K.dig_n == K.l1_n && !kX_no_dig();
     if (with_dig && K.l1_n + total > K.dig_cap) {
         const u64 ncap = std::max<u64>(K.l1_n + total, K.dig_n ? 2 * K.dig_cap : 0);
         u16* nd = nullptr;
@@ -1141,11 +1148,6 @@ static int pp_add_batch(dbg_agg_handle* h, const BatchDesc* st, u32 bid, u64 row
 #define PS_LOAD 0.45
 #endif
 
-// EXPERIMENT (DBG_X_PPDIG=0): level 2 counts from the records instead of the digit array
-static bool kX_no_dig() {
-    static const bool off = X_ENV("DBG_X_PPDIG") && X_ENV("DBG_X_PPDIG")[0] == '0';
-    return off;
-}
 
 // Levels 2 and 3 (NewTransformPartitionBucket + the final bucket split): every level-1 partition
 // of both record kinds is re-scattered by the next hash bits until the estimated groups of a
