@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
     __shared__ RunTable rt;
     __shared__ u32 wtot[DEC_NT / 64];
     __shared__ u32 s_bad;
-    const ScanPage pg = a.pages[blockIdx.x];
+    const ScanPage& pg = a.pages[blockIdx.x];  // read in place (uniform: scalar loads); a private copy would go to scratch
     if (pg.kind == PG_DICT) return;
     if (threadIdx.x == 0) s_bad = 0;
     __syncthreads();
@@ -612,20 +612,24 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
     };
     if (split && (pw == 4 || pw == 8) && a.ptype != DBG_PQ_FIXED_LEN_BYTE_ARRAY && a.ttype != DBG_DECIMAL128 && a.twidth <= pw &&
         (u64)vp + (u64)n * pw <= pg.uncomp) {
-        // required PLAIN 4- / 8-byte values into an integer / float target: 4 values per lane from
-        // aligned dword loads (the page's values start at any byte: funnel shifts), narrowed to the
-        // target width and stored as one 4 x width word when the row is aligned
+        // required PLAIN 4- / 8-byte values into an integer / float target: 8 values per lane from
+        // unaligned 16 B loads (the page's values start at any byte), narrowed to the target width
+        // and stored as whole words when the row is aligned
         const u32 per = (n + gridDim.y - 1) / gridDim.y;
-        const u32 lo = min(n, ((blockIdx.y * per) + 3) & ~3u), hi = min(n, (((blockIdx.y + 1) * per) + 3) & ~3u);
+        const u32 lo = min(n, ((blockIdx.y * per) + 7) & ~7u), hi = min(n, (((blockIdx.y + 1) * per) + 7) & ~7u);
         const u8* vbase = base + vp;
         const u32 tw = a.twidth;
-        for (u32 k0 = lo + 4 * threadIdx.x; k0 < hi; k0 += 4 * DEC_NT) {
-            const u32 cnt = min(4u, hi - k0);
+        const u64 row0 = pg.row0;  // a register copy: the lambdas below capture `pg` by reference (scratch)
+        u8* const out = a.out_data;
+        // load 4 values of a lane (all loads of an unrolled round are issued before its stores:
+        // the output may alias the chunk as far as the compiler knows)
+        auto load4 = [&](u32 k0, u64 (&v)[4]) {
+            const u32 cnt = k0 < hi ? min(4u, hi - k0) : 0u;
             const u8* p = vbase + (u64)k0 * pw;
             // byte-aligned values: gfx950 global loads take unaligned addresses (the compiler emits
             // whole-dword loads for these memcpys), consecutive lanes read consecutive 16 B
             // (every index below is a constant: the arrays stay in registers, no scratch)
-            u64 v[4] = {0, 0, 0, 0};
+            v[0] = v[1] = v[2] = v[3] = 0;
             if (cnt == 4 && pw == 4) {
                 u32 w[4];
                 __builtin_memcpy(w, p, 16);
@@ -648,7 +652,11 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
                     }
                 }
             }
-            u8* dst = a.out_data + (pg.row0 + k0) * (u64)tw;
+        };
+        auto store4 = [&](u32 k0, const u64 (&v)[4]) {
+            if (k0 >= hi) return;
+            const u32 cnt = min(4u, hi - k0);
+            u8* dst = out + (row0 + k0) * (u64)tw;
             if (tw == 2 && cnt == 4 && !((uintptr_t)dst & 7)) {
                 *(u64*)dst = (v[0] & 0xFFFF) | ((v[1] & 0xFFFF) << 16) | ((v[2] & 0xFFFF) << 32) | ((v[3] & 0xFFFF) << 48);
             } else if (tw == 4 && cnt == 4 && !((uintptr_t)dst & 15)) {
@@ -665,6 +673,32 @@ __global__ void __launch_bounds__(DEC_NT) pq_decode_kernel(ScanArgs a) {
                         case 4: *(u32*)dj = (u32)v[j]; break;
                         default: *(u64*)dj = v[j]; break;
                     }
+                }
+            }
+        };
+        // 8 consecutive values per lane and round (32 B read, 16 B written for Int16), two rounds'
+        // loads issued before their stores
+        constexpr u32 U = 2;
+        for (u32 k0 = lo + 8 * threadIdx.x; k0 < hi; k0 += U * 8 * DEC_NT) {
+            u64 v[U][2][4];
+#pragma unroll
+            for (u32 u = 0; u < U; ++u) {
+                load4(k0 + u * 8 * DEC_NT, v[u][0]);
+                load4(k0 + u * 8 * DEC_NT + 4, v[u][1]);
+            }
+#pragma unroll
+            for (u32 u = 0; u < U; ++u) {
+                const u32 k = k0 + u * 8 * DEC_NT;
+                u8* dst = out + (row0 + k) * (u64)tw;
+                if (tw == 2 && k + 8 <= hi && !((uintptr_t)dst & 15)) {
+                    typedef u32 v4u32 __attribute__((ext_vector_type(4)));
+                    const u64 (&x)[4] = v[u][0];
+                    const u64 (&y)[4] = v[u][1];
+                    *(v4u32*)dst = v4u32{(u32)((x[0] & 0xFFFF) | (x[1] << 16)), (u32)((x[2] & 0xFFFF) | (x[3] << 16)),
+                                         (u32)((y[0] & 0xFFFF) | (y[1] << 16)), (u32)((y[2] & 0xFFFF) | (y[3] << 16))};
+                } else {
+                    store4(k, v[u][0]);
+                    store4(k + 4, v[u][1]);
                 }
             }
         }
@@ -1006,10 +1040,24 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
                                                  std::to_string(target.type));
     std::vector<HostPage> hp;
     SCAN_RET(parse_pages(c, hp));
-    // page table
-    std::vector<ScanPage> pages;
+    // page table, built straight into the pinned staging buffer (every call that uploads from it
+    // ends synchronised, so the previous upload has finished reading it)
+    if (ctx->hpages_cap < hp.size() + 2) {
+        SCAN_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->hpages) SCAN_HIP(hipHostFree(ctx->hpages));
+        ctx->hpages = nullptr;
+        ctx->hpages_cap = 0;
+        const u64 cap = hp.size() + hp.size() / 2 + 17;
+        SCAN_HIP(hipHostMalloc((void**)&ctx->hpages, cap * sizeof(ScanPage), hipHostMallocDefault));
+        ctx->hpages_cap = cap;
+    }
+    // slot 0 stages the zeroed error words (one upload resets them and ships the table)
+    memset(ctx->hpages, 0, sizeof(ScanPage));
+    ScanPage* const pages = ctx->hpages + 1;
+    u64 n_pages = 0, maxn = 0;
     u64 dst = 0, row = 0, vk = 0;
     int dict = -1;
+    bool mismatch = false;
     for (auto& p : hp) {
         if (p.type == 1) continue;  // INDEX_PAGE
         if (p.type != 0 && p.type != 2 && p.type != 3) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: page type " + std::to_string(p.type));
@@ -1026,7 +1074,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
             if (dict >= 0) return abi_fail(DBG_ERR_INVALID, "dbg_parquet: two dictionary pages");
             if (p.encoding != ENC_PLAIN && p.encoding != ENC_PLAIN_DICT) return abi_fail(DBG_ERR_UNSUPPORTED, "dbg_parquet: dictionary encoding");
             s.kind = PG_DICT;
-            dict = (int)pages.size();
+            dict = (int)n_pages;
         } else {
             const bool dict_enc = p.encoding == ENC_PLAIN_DICT || p.encoding == ENC_RLE_DICT;
             if (!(p.encoding == ENC_PLAIN || dict_enc || (p.encoding == ENC_RLE && c.physical_type == DBG_PQ_BOOLEAN)))
@@ -1046,8 +1094,12 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         s.vk0 = vk;
         vk += (u64)p.num_values;
         dst += ((u64)p.uncomp + 15) & ~15ULL;
-        pages.push_back(s);
+        mismatch |= s.comp != s.uncomp;
+        maxn = std::max<u64>(maxn, s.num_values);
+        pages[n_pages++] = s;
     }
+    // uncompressed pages are decoded where they lie; only a size mismatch is checked
+    if (c.codec == DBG_PQ_UNCOMPRESSED && mismatch) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: uncompressed page sizes differ");
     *rows_out = row;
     if (row > max_rows) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: " + std::to_string(row) + " rows exceed max_rows");
     if (target.type != DBG_STRING && target.type != DBG_BOOLEAN && !out->data && row) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null data buffer");
@@ -1058,10 +1110,10 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         SCAN_HIP(hipMemcpyAsync(ctx->chunk, c.host, c.len, hipMemcpyHostToDevice, s));
     }
     SCAN_RET(ensure(&ctx->buf, &ctx->buf_cap, dst + 16));
-    SCAN_RET(ensure(&ctx->pages, &ctx->pages_cap, pages.size() + 1));
+    SCAN_RET(ensure(&ctx->pages, &ctx->pages_cap, n_pages + 2));
     SCAN_RET(ensure(&ctx->vbytes, &ctx->vbytes_cap, row + 1));
     SCAN_RET(ensure(&ctx->idx, &ctx->idx_cap, vk + 1));
-    SCAN_RET(ensure(&ctx->nwalk, &ctx->nwalk_cap, pages.size() + 1));
+    SCAN_RET(ensure(&ctx->nwalk, &ctx->nwalk_cap, n_pages + 1));
     const bool is_str = target.type == DBG_STRING, is_bool = target.type == DBG_BOOLEAN;
     if (is_str) {
         SCAN_RET(ensure(&ctx->vstart, &ctx->vstart_cap, vk + 1));
@@ -1069,28 +1121,17 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         if (!out->offsets) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: String output needs offsets");
     }
     if (is_bool) SCAN_RET(ensure(&ctx->bools, &ctx->bools_cap, row + 1));
-    if (c.codec == DBG_PQ_ZSTD) SCAN_RET(ensure(&ctx->zlit, &ctx->zlit_cap, (u64)pages.size() * ZS_MAX_BLOCK + 16));
+    if (c.codec == DBG_PQ_ZSTD) SCAN_RET(ensure(&ctx->zlit, &ctx->zlit_cap, n_pages * ZS_MAX_BLOCK + 16));
     if (target.nullable && c.max_def_level && !out->validity && row) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: null validity buffer");
-    if (ctx->hpages_cap < pages.size() + 1) {
-        // the previous call's upload may still read the old staging buffer
-        SCAN_HIP(hipStreamSynchronize(s));
-        if (ctx->hpages) SCAN_HIP(hipHostFree(ctx->hpages));
-        ctx->hpages = nullptr;
-        ctx->hpages_cap = 0;
-        const u64 cap = pages.size() + pages.size() / 2 + 16;
-        SCAN_HIP(hipHostMalloc((void**)&ctx->hpages, cap * sizeof(ScanPage), hipHostMallocDefault));
-        ctx->hpages_cap = cap;
-    }
-    memcpy(ctx->hpages, pages.data(), pages.size() * sizeof(ScanPage));
-    SCAN_HIP(hipMemcpyAsync(ctx->pages, ctx->hpages, pages.size() * sizeof(ScanPage), hipMemcpyHostToDevice, s));
-    SCAN_HIP(hipMemsetAsync(ctx->err, 0, 16, s));
-    if (c.physical_type == DBG_PQ_BYTE_ARRAY) SCAN_HIP(hipMemsetAsync(ctx->nwalk, 0, pages.size() * 4, s));
+    SCAN_HIP(hipMemcpyAsync(ctx->pages, ctx->hpages, (n_pages + 1) * sizeof(ScanPage), hipMemcpyHostToDevice, s));
+    u64* const perr = (u64*)ctx->pages;
+    if (c.physical_type == DBG_PQ_BYTE_ARRAY) SCAN_HIP(hipMemsetAsync(ctx->nwalk, 0, n_pages * 4, s));
     ScanArgs a;
     memset(&a, 0, sizeof(a));
     a.chunk = upload ? ctx->chunk : c.device;
     a.buf = ctx->buf;
-    a.pages = ctx->pages;
-    a.n_pages = (u32)pages.size();
+    a.pages = ctx->pages + 1;
+    a.n_pages = (u32)n_pages;
     a.ptype = c.physical_type;
     a.tlen = c.type_length;
     a.max_def = c.max_def_level;
@@ -1107,34 +1148,27 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     a.out_data = is_bool ? ctx->bools : (u8*)out->data;
     a.need_vb = (target.nullable || c.max_def_level) ? 1 : 0;
     a.out_offs = out->offsets;
-    a.err = ctx->err;
-    if (!pages.empty()) {
-        const dim3 g((u32)pages.size());
+    a.err = perr;
+    if (n_pages) {
+        const dim3 g((u32)n_pages);
         void* ps = c.codec != DBG_PQ_UNCOMPRESSED ? prof_scope_begin("pq_inflate", s) : nullptr;
         switch (c.codec) {
             case DBG_PQ_SNAPPY: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_SNAPPY>, g, dim3(64), 0, s, a); break;
             case DBG_PQ_LZ4_RAW: hipLaunchKernelGGL(pq_inflate_kernel<DBG_PQ_LZ4_RAW>, g, dim3(64), 0, s, a); break;
             case DBG_PQ_ZSTD: hipLaunchKernelGGL(pq_zstd_kernel, g, dim3(64), 0, s, a, ctx->zlit); break;
-            default: {  // uncompressed pages are decoded where they lie; only a size mismatch is checked
-                bool mismatch = false;
-                for (const auto& pg : pages) mismatch |= pg.comp != pg.uncomp;
-                if (mismatch) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: uncompressed page sizes differ");
-                break;
-            }
+            default: break;
         }
         prof_scope_end(ps);
         SCAN_HIP(hipGetLastError());
         if (c.physical_type == DBG_PQ_BYTE_ARRAY) {
-            hipLaunchKernelGGL(pq_walk_kernel, dim3((u32)((pages.size() + 63) / 64)), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(pq_walk_kernel, dim3((u32)((n_pages + 63) / 64)), dim3(64), 0, s, a);
             SCAN_HIP(hipGetLastError());
         }
         // required PLAIN pages are split over the grid's y dimension into pieces of >= 8192 values
         // (writers cap pages at 20 000 rows — pyarrow, parquet-rs — or at 1 MiB: up to 16 pieces)
-        u64 maxn = 0;
-        for (const auto& pg : pages) maxn = std::max<u64>(maxn, pg.num_values);
         const u32 ysplit = c.max_def_level ? 1u : (u32)std::min<u64>(16, std::max<u64>(1, (maxn + 8191) / 8192));
         ps = prof_scope_begin("pq_decode", s);
-        hipLaunchKernelGGL(pq_decode_kernel, dim3((u32)pages.size(), ysplit), dim3(DEC_NT), 0, s, a);
+        hipLaunchKernelGGL(pq_decode_kernel, dim3((u32)n_pages, ysplit), dim3(DEC_NT), 0, s, a);
         prof_scope_end(ps);
         SCAN_HIP(hipGetLastError());
     }
@@ -1142,7 +1176,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         // lengths -> offsets (exclusive scan, total into offsets[rows]), then the payload
         if (row) launch_exclusive_scan(s, out->offsets, row, out->offsets + row);
         else SCAN_HIP(hipMemsetAsync(out->offsets, 0, 8, s));
-        SCAN_HIP(hipMemcpyAsync(ctx->err + 1, out->offsets + row, 8, hipMemcpyDeviceToDevice, s));
+        SCAN_HIP(hipMemcpyAsync(perr + 1, out->offsets + row, 8, hipMemcpyDeviceToDevice, s));
         if (row && out->data)
             hipLaunchKernelGGL(pq_strings_kernel, dim3((u32)((row + 255) / 256)), dim3(256), 0, s, ctx->sptr, out->offsets, row,
                                (u8*)out->data, max_string_bytes);
@@ -1152,10 +1186,10 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     if (target.nullable && row && out->validity) launch_pack_bits(s, ctx->vbytes, row, out->validity);
     if (!target.nullable && c.max_def_level && row) {
         hipLaunchKernelGGL(pq_null_check_kernel, dim3((u32)std::min<u64>(1024, (row + 255) / 256)), dim3(256), 0, s, ctx->vbytes, row,
-                           ctx->err);
+                           perr);
         SCAN_HIP(hipGetLastError());
     }
-    SCAN_HIP(hipMemcpyAsync(ctx->herr, ctx->err, 16, hipMemcpyDeviceToHost, s));
+    SCAN_HIP(hipMemcpyAsync(ctx->herr, perr, 16, hipMemcpyDeviceToHost, s));
     SCAN_HIP(hipStreamSynchronize(s));
     const u64 e = ctx->herr[0];
     if (e & SERR_MALFORMED) return abi_fail(DBG_ERR_INVALID, "dbg_parquet_decode: malformed page data");
