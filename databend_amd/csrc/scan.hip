@@ -79,20 +79,24 @@ struct ScanArgs {
     int32_t need_vb;   // the definition bytes are read afterwards (nullable target / NULL check)
     u64* out_offs;     // String: lengths, then the scan
     u64* err;
+    u32 xflags;        // experiment builds only (DBG_X_INFLATE): 1 = no output stores, 2 = no ring reads
 };
 
 // ---------------------------------------------------------------------------------------------
 // Decompression (one wave per page): the compressed stream is staged into an LDS window with
 // coalesced loads and its tags parsed from there (wave-uniform); literal and match bytes are
-// copied by all 64 lanes.
+// copied by all 64 lanes.  The last RING output bytes stay in an LDS ring for back-references;
+// a farther one (Snappy / LZ4 offsets reach 64 KiB - 1) reads the page's own output in HBM.
+// 32 KiB + 8 KiB of LDS per wave: four pages in flight per CU (a serial tag parse is latency-
+// bound, so pages in flight is the throughput).
 // ---------------------------------------------------------------------------------------------
-#define RING 65536
+#define RING 32768
 
-#define IWIN 16384  // the compressed stream's window in LDS: tags are parsed from LDS, not HBM
+#define IWIN (8192 - 16)  // the compressed stream's window in LDS (+ 16 bytes of over-read pad: 40 KiB per wave)
 template <int CODEC>
 __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     __shared__ u8 ring[RING];
-    __shared__ u8 inw[IWIN];
+    __shared__ __attribute__((aligned(16))) u8 inw[IWIN + 16];  // + 16: peek's over-read
     const ScanPage pg = a.pages[blockIdx.x];
     const u32 lane = threadIdx.x;
     // an uncompressed page is decoded where it lies in the chunk (page_base): nothing to copy
@@ -109,34 +113,76 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     const u32 sn = pg.comp - pg.lv, on = pg.uncomp - pg.lv;
     bool bad = false;
     u32 p = 0, w = 0;  // input / output cursors (uniform)
-    // bytes [wb, we) of the stream are staged in inw; rd(q) reads stream byte q (wb <= q < we),
-    // need(k) restages from p when fewer than k bytes (or the end of the stream) remain staged
-    u32 wb = 0, we = 0;
+    // stream bytes [wl, wh) (offsets from s) are staged in inw; s + wl is 16-byte aligned (whole-
+    // granule loads: wl may be up to 15 bytes before the payload, the chunk's own bytes); need(k)
+    // restages from p when fewer than k bytes (or the end of the stream) remain staged.  32-bit
+    // offsets keep the checks on the scalar unit.
+    const int sa = (int)((uintptr_t)s & 15);
+    int wl = 0, wh = 0;
     auto need = [&](u32 k) {
-        if (p >= wb && (p + k <= we || we == sn)) return;
-        wb = p;
-        we = sn - p < IWIN ? sn : p + IWIN;
+        if ((int)p >= wl && ((int)(p + k) <= wh || wh == (int)sn)) return;
+        wl = (int)(((u32)p + (u32)sa) & ~15u) - sa;
+        wh = (int)sn - wl <= IWIN ? (int)sn : wl + IWIN;
+        const u8* g0 = s + wl;
+        const u32 nb = (u32)(wh - wl), ng = nb >> 4;
         __builtin_amdgcn_wave_barrier();  // every lane is done reading the old window
-        for (u32 j = lane; j < we - wb; j += 64) inw[j] = s[wb + j];
+        for (u32 g = lane; g < ng; g += 64) ((uint4*)inw)[g] = ((const uint4*)g0)[g];
+        for (u32 j = 16 * ng + lane; j < nb; j += 64) inw[j] = g0[j];
         __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
-    auto rd = [&](u32 q) -> u32 { return inw[q - wb]; };
+    auto rd = [&](u32 q) -> u32 { return inw[(int)q - wl]; };
+    // 8 stream bytes from q (staged) in one LDS round trip: three aligned dwords, funnel-shifted;
+    // bytes past wh are garbage, every use is bounded by sn first
+    auto peek = [&](u32 q) -> u64 {
+        const u32 i = (u32)((int)q - wl), b = i & ~3u, sh = 8 * (i & 3);
+        const u32 d0 = *(const u32*)(inw + b), d1 = *(const u32*)(inw + b + 4), d2 = *(const u32*)(inw + b + 8);
+        const u64 lo = (u64)d0 | ((u64)d1 << 32);
+        return sh ? (lo >> sh) | ((u64)d2 << (64 - sh)) : lo;
+    };
     // bounds are compared without wrapping (p <= sn and w <= on hold throughout): a 4-byte
     // Snappy literal length near 2^32 must fail here, not wrap past the check
     auto copy_lit = [&](u64 len) {
         if (len > (u64)(sn - p) || len > (u64)(on - w)) { bad = true; return; }
-        for (u32 j = lane; j < (u32)len; j += 64) {
-            const u8 b = s[p + j];
-            o[w + j] = b;
-            ring[(w + j) & (RING - 1)] = b;
+        const u8* q = s + p;
+        if ((int)p >= wl && (int)(p + (u32)len) <= wh) {  // staged: from LDS, no HBM round trip
+            const u32 i = (u32)((int)p - wl);
+            for (u32 j = lane; j < (u32)len; j += 64) {
+                const u8 b = inw[i + j];
+                if (!(a.xflags & 1)) o[w + j] = b;
+                ring[(w + j) & (RING - 1)] = b;
+            }
+        } else {
+            for (u32 j = lane; j < (u32)len; j += 64) {
+                const u8 b = q[j];
+                o[w + j] = b;
+                ring[(w + j) & (RING - 1)] = b;
+            }
         }
         __builtin_amdgcn_wave_barrier();
         p += (u32)len;
         w += (u32)len;
     };
     auto copy_back = [&](u32 off, u64 len) {
-        if (off == 0 || off > w || off >= RING || len > (u64)(on - w)) { bad = true; return; }
+        if (off == 0 || off > w || len > (u64)(on - w)) { bad = true; return; }
+        if (off >= RING) {
+            // beyond the ring: read this wave's own output back from HBM, in segments of at most
+            // `off` bytes (every source byte was written before its segment starts); the fence
+            // makes the wave's earlier stores visible to its loads (L1 invalidated)
+            while (len) {
+                const u32 seg = (u32)(len < (u64)off ? len : (u64)off);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+                for (u32 j = lane; j < seg; j += 64) {
+                    const u8 b = o[w - off + j];
+                    o[w + j] = b;
+                    ring[(w + j) & (RING - 1)] = b;
+                }
+                __builtin_amdgcn_wave_barrier();
+                w += seg;
+                len -= seg;
+            }
+            return;
+        }
         // byte j repeats the last `off` bytes: out[w + j] = out[w - off + j % off], read from the
         // ring in segments of at most RING - off bytes (a longer one would overwrite ring slots it
         // still reads when off > RING / 2), 64 bytes per step, each step's reads before its writes
@@ -144,10 +190,10 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
             for (u32 c0 = 0; c0 < seg; c0 += 64) {
                 const u32 j = c0 + lane;
                 u8 b = 0;
-                if (j < seg) b = ring[(w - off + (j % off)) & (RING - 1)];
+                if (j < seg && !(a.xflags & 2)) b = ring[(w - off + (j < off ? j : j % off)) & (RING - 1)];
                 __builtin_amdgcn_wave_barrier();
                 if (j < seg) {
-                    o[w + j] = b;
+                    if (!(a.xflags & 1)) o[w + j] = b;
                     ring[(w + j) & (RING - 1)] = b;
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -176,36 +222,38 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
         }
         if (n != on) bad = true;
         while (!bad && p < sn) {
-            need(5);  // a tag and its length / offset bytes
-            const u32 tag = rd(p++);
+            need(5);  // a tag and its length / offset bytes, read together
+            const u64 x = peek(p);
+            const u32 tag = (u32)x & 0xFF;
             const u32 kind = tag & 3;
             if (kind == 0) {
                 u32 len = tag >> 2;
                 if (len >= 60) {
                     const u32 nb = len - 59;
-                    if (p + nb > sn) { bad = true; break; }
-                    len = 0;
-                    for (u32 k = 0; k < nb; ++k) len |= rd(p + k) << (8 * k);
-                    p += nb;
+                    if (p + 1 + nb > sn) { bad = true; break; }
+                    len = (u32)((x >> 8) & (nb == 4 ? 0xFFFFFFFFull : ((1ull << (8 * nb)) - 1)));
+                    p += 1 + nb;
+                } else {
+                    p += 1;
                 }
                 copy_lit((u64)len + 1);
             } else {
                 u32 len, off;
                 if (kind == 1) {
-                    if (p + 1 > sn) { bad = true; break; }
-                    len = ((tag >> 2) & 7) + 4;
-                    off = ((tag >> 5) << 8) | rd(p);
-                    p += 1;
-                } else if (kind == 2) {
                     if (p + 2 > sn) { bad = true; break; }
-                    len = (tag >> 2) + 1;
-                    off = rd(p) | (rd(p + 1) << 8);
+                    len = ((tag >> 2) & 7) + 4;
+                    off = ((tag >> 5) << 8) | ((u32)(x >> 8) & 0xFF);
                     p += 2;
-                } else {
-                    if (p + 4 > sn) { bad = true; break; }
+                } else if (kind == 2) {
+                    if (p + 3 > sn) { bad = true; break; }
                     len = (tag >> 2) + 1;
-                    off = rd(p) | (rd(p + 1) << 8) | (rd(p + 2) << 16) | (rd(p + 3) << 24);
-                    p += 4;
+                    off = (u32)(x >> 8) & 0xFFFF;
+                    p += 3;
+                } else {
+                    if (p + 5 > sn) { bad = true; break; }
+                    len = (tag >> 2) + 1;
+                    off = (u32)(x >> 8);
+                    p += 5;
                 }
                 copy_back(off, len);
             }
@@ -213,7 +261,9 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
     } else {  // LZ4 block: [token][literal length+][literals][offset u16][match length+]
         while (!bad && p < sn) {
             need(16);
-            const u32 tok = rd(p++);
+            const u64 x = peek(p);
+            const u32 tok = (u32)x & 0xFF;
+            p += 1;
             u64 lit = tok >> 4;
             if (lit == 15)
                 for (;;) {
@@ -224,11 +274,16 @@ __global__ void __launch_bounds__(64) pq_inflate_kernel(ScanArgs a) {
                     if (c != 255) break;
                 }
             if (bad) break;
-            copy_lit(lit);
+            if (lit) copy_lit(lit);
             if (bad || p >= sn) break;  // the last sequence has literals only
             if (p + 2 > sn) { bad = true; break; }
-            need(2);
-            const u32 off = rd(p) | (rd(p + 1) << 8);
+            u32 off;
+            if (lit) {
+                need(2);
+                off = (u32)peek(p) & 0xFFFF;
+            } else {  // no literals: the offset follows the token (peeked with it)
+                off = (u32)(x >> 8) & 0xFFFF;
+            }
             p += 2;
             u64 ml = tok & 15;
             if (ml == 15)
@@ -1149,6 +1204,7 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
     a.need_vb = (target.nullable || c.max_def_level) ? 1 : 0;
     a.out_offs = out->offsets;
     a.err = perr;
+    if (const char* x = X_ENV("DBG_X_INFLATE")) a.xflags = (u32)atoi(x);  // experiment builds only
     if (n_pages) {
         const dim3 g((u32)n_pages);
         void* ps = c.codec != DBG_PQ_UNCOMPRESSED ? prof_scope_begin("pq_inflate", s) : nullptr;

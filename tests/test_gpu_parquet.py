@@ -70,6 +70,26 @@ def test_fuse_writer_shape_large(dec):
         assert n == 5
 
 
+@pytest.mark.parametrize("comp", ["SNAPPY", "LZ4"])
+def test_far_back_references(dec, comp):
+    """Matches farther back than the inflate kernel's 32 KiB LDS ring (read back from the page's
+    own output in HBM), including an LZ4 match longer than its offset: a random 40 000-byte block
+    repeated, then a 60 000-byte one with a few values changed.  pyarrow's LZ4 writes the first
+    page as one literal and one 119 995-byte match at offset 40 000; its Snappy skips ahead in
+    random bytes and finds none (that leg checks the literal path on the same data)."""
+    import pyarrow as pa
+    rng = np.random.default_rng(11)
+    a = rng.integers(-2**62, 2**62, 5_000)
+    b = rng.integers(-2**62, 2**62, 7_500)
+    b2 = b.copy()
+    b2[::997] += 1
+    v = np.concatenate([a, a, a, a, b, rng.integers(0, 7, 3_000), b2, a])
+    t = pa.table({"x": pa.array(v, pa.int64())}, schema=pa.schema([pa.field("x", pa.int64(), nullable=False)]))
+    buf = write(t, compression=comp, use_dictionary=False, data_page_size=1 << 20, row_group_size=1 << 30)
+    (name, _, ch, at), = file_chunks(buf)
+    assert gpu_values(dec, ch, at, nullable=False) == v.tolist()
+
+
 def test_integer_decimals(dec):
     t = sample_table(5000).select(["d9", "d20"])
     buf = write(t, store_decimal_as_integer=True, compression="SNAPPY")
