@@ -181,6 +181,7 @@ static int result_type_of(const dbg_agg_spec& s, dbg_datatype* out) {
 
 int build_spec(const dbg_agg_params* p, Spec& S, std::vector<dbg_datatype>& rtypes) {
     memset(&S, 0, sizeof(S));
+    S.x_pp_cap = ~0u;  // no test hook (dbg_agg_create reads them)
     if (p->n_group_cols < 1 || p->n_group_cols > DBG_MAX_KEYS) return fail(DBG_ERR_UNSUPPORTED, "1..8 group columns supported");
     if (p->n_aggs < 0 || p->n_aggs > DBG_MAX_AGGS) return fail(DBG_ERR_UNSUPPORTED, "at most 32 aggregates");
     S.n_keys = p->n_group_cols;
@@ -677,6 +678,12 @@ int dbg_agg_create(const dbg_agg_params* params, dbg_agg_handle** out) {
     if ((rc = dev_alloc((void**)&h->counters, CNT_WORDS * 8)) != DBG_OK) return cleanup(rc);
     if (hipMemset(h->counters, 0, CNT_WORDS * 8) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "memset"));
     h->spec.err = h->counters + CNT_ERR;  // error bits raised from inside state updates
+    {
+        const char* cx = getenv("DBG_X_PPSPEC_CAP");
+        const char* fd = getenv("DBG_X_PPSPEC_DESC");
+        h->spec.x_pp_cap = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
+        h->spec.x_pp_desc = (fd && fd[0] == '1') ? 1 : 0;
+    }
     if ((rc = dev_alloc((void**)&h->dspec, sizeof(Spec))) != DBG_OK) return cleanup(rc);
     if (hipMemcpy(h->dspec, &h->spec, sizeof(Spec), hipMemcpyHostToDevice) != hipSuccess) return cleanup(fail(DBG_ERR_DEVICE, "spec upload"));
     if (hipHostMalloc((void**)&h->hcounters, (CNT_WORDS + DBG_MAX_KEYS + 8) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return cleanup(fail(DBG_ERR_OOM, "pinned"));

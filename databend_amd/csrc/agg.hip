@@ -1208,6 +1208,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
         if (shortk && l1) b1 = load_partial(B.keys[1].data + r.o[2], l1);
         const bool pass = B.n_nodes == 0 || eval_pred(B.nodes, B.n_nodes, B.fcols, i);
         if (!pass) return;
+        // timing ablation (EXP=1 builds only): the loads and the predicate alone (no probe, adds
+        // or flush); the key bytes stay live through an improbable compare
+        if (kExperiments && xmode == 5 && (b0 ^ b1) != 0x5A5A5A5A5A5A5A5AULL) return;
         if (!shortk) {
             generic_row(i);
             return;

@@ -52,6 +52,11 @@ struct Spec {
     uint16_t pp_aoff[DBG_MAX_AGGS];  // raw arg value offset (0: the aggregate takes no argument)
     int16_t pp_avbit[DBG_MAX_AGGS];  // raw arg validity bit (-1: always valid)
     u64* err;               // the handle's CNT_ERR word (device): errors raised inside state updates
+    // result-neutral test hooks, read once when the handle is created (host side only):
+    // DBG_X_PPSPEC_CAP (a smaller specialised-aggregation LDS table), DBG_X_PPSPEC_DESC=1 (the
+    // descriptor kernel for a shape that also has a compile-time instance)
+    uint32_t x_pp_cap;      // ~0: none
+    int32_t x_pp_desc;
 };
 #define PP_BLOB 39        // inline blob bytes of a string key part
 #define PP_KLEN_LONG 0xFF  // key too long for the blob: reference into the retained input

@@ -2250,9 +2250,7 @@ static void launch_ps_desc(hipStream_t s, const Spec& S, int shape, int mode, u3
     if (!ps_desc(S, D, W) || (int)W != shape) return;  // the host planned with pp_spec_shape: never taken
     const u32 grid = n_parts < 256 ? n_parts : 256;  // one persistent workgroup per CU
     // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
-    const char* cx = getenv("DBG_X_PPSPEC_CAP");
-    const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
-    const u32 cap = std::min(ps_cap(D.bw, W), cap_x);
+    const u32 cap = std::min(ps_cap(D.bw, W), S.x_pp_cap);
     const size_t lds = ps_lds_bytes(cap, D.bw, W, PP_SPEC_NT) + 16;
 #define PS_LAUNCH(WW)                                                                                                            \
     case WW:                                                                                                                     \
@@ -2740,13 +2738,12 @@ static int ps_literal_shape(const Spec& S, u32* cap, u32* max_records) {
     return found;
 }
 
-static void launch_ps_literal(hipStream_t s, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
+static void launch_ps_literal(hipStream_t s, const Spec& S, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw, u32 sub_bits,
                               const PPAggOut& out, u32* spill, u32 spill_cap) {
     if (!n_parts) return;
     const u32 grid = n_parts < 256u * PP_LIT_PER_CU ? n_parts : 256u * PP_LIT_PER_CU;  // persistent workgroups
     // test hook: a smaller LDS table than the plan assumed (probe-window misses, pending rounds)
-    const char* cx = getenv("DBG_X_PPSPEC_CAP");
-    const u32 cap_x = cx ? std::max<u32>(64, (u32)atoi(cx) & ~3u) : ~0u;
+    const u32 cap_x = S.x_pp_cap;
     int id = 0;
 #define PS_LAUNCH(WW, K0, K1, A0, A1, A2)                                                                               \
     if (shape == id) {                                                                                                  \
@@ -2773,8 +2770,7 @@ static void launch_ps_literal(hipStream_t s, int shape, int mode, u32 n_parts, c
 #define PS_DESC_ID 64
 int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
     // test hook: the descriptor kernel for a literal shape too (same results)
-    const char* fd = getenv("DBG_X_PPSPEC_DESC");
-    const int lit = (fd && fd[0] == '1') ? -1 : ps_literal_shape(S, cap, max_records);
+    const int lit = S.x_pp_desc ? -1 : ps_literal_shape(S, cap, max_records);
     if (lit >= 0) return lit;
     const int w = ps_desc_shape(S, cap, max_records);
     return w >= 0 ? PS_DESC_ID + w : -1;
@@ -2783,7 +2779,7 @@ int pp_spec_shape(const Spec& S, u32* cap, u32* max_records) {
 void launch_pp_agg_spec(hipStream_t s, const Spec& S, int shape, int mode, u32 n_parts, const u64* raw_off, const u8* raw,
                         u32 sub_bits, const PPAggOut& out, u32* spill, u32 spill_cap) {
     if (shape >= PS_DESC_ID) launch_ps_desc(s, S, shape - PS_DESC_ID, mode, n_parts, raw_off, raw, sub_bits, out, spill, spill_cap);
-    else launch_ps_literal(s, shape, mode, n_parts, raw_off, raw, sub_bits, out, spill, spill_cap);
+    else launch_ps_literal(s, S, shape, mode, n_parts, raw_off, raw, sub_bits, out, spill, spill_cap);
 }
 
 // ------------------------------------------------------------------------------------------
