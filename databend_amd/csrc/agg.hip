@@ -1120,8 +1120,18 @@ __device__ __forceinline__ void short_tree_flush(const Spec& S, const BatchDesc*
 
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6))) agg_insert_short_kernel(const Spec* __restrict__ spec, const BatchDesc* __restrict__ batches,
                                                                 u32 bid, u64 rows, u64 rows_per_block, TableDesc t, u32 lds_slots,
-                                                                u32 rep_mask, int xmode, u32 narrow, int tree_ok) {
+                                                                u32 rep_mask, int xmode, u32 narrow, int tree_ok, u64* trace) {
     extern __shared__ __attribute__((aligned(16))) u64 lds[];
+    // EXPERIMENT (TRACE=1 builds, DBG_X_TRACE_SHORT): [0] first workgroup start, [1] / [2] first /
+    // last row loop end, [3] last flush start, [4] last workgroup end (s_memrealtime, 100 MHz)
+    auto tmark = [&](int k, bool mx) {
+        if (kPhaseTrace && trace && threadIdx.x == 0) {
+            const unsigned long long v = __builtin_amdgcn_s_memrealtime();
+            if (mx) atomicMax((unsigned long long*)trace + k, v);
+            else atomicMin((unsigned long long*)trace + k, v);
+        }
+    };
+    tmark(0, false);
     const Spec& S = *spec;
     const BatchDesc& B = batches[bid];
     const u32 sw = S.stride_words;
@@ -1300,6 +1310,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
         }
     }
     __syncthreads();
+    tmark(1, false);
+    tmark(2, true);
     if (kExperiments && xmode >= 3) return;  // timing ablation (EXP=1 builds only: no flush)
     if (narrow) {  // short slots: narrow partials -> Decimal128 state (high word = sign)
         for (u32 s = threadIdx.x; s < lds_slots; s += BLOCK) {
@@ -1312,8 +1324,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(6)))
         __syncthreads();
     }
     const bool tree = tree_ok && t.scratch != nullptr && gridDim.x > 1 && gridDim.x <= t.scr_blocks;  // uniform
+    tmark(3, true);
     if (tree) short_tree_flush(S, batches, B, lds, lds_slots, sw, lcount, pk0, pk1, t, my_claims);
     else block_flush<false, false>(S, batches, B, lds, lds_slots, sw, lcount, BLOCK, t, my_claims);
+    tmark(4, true);
 }
 
 // host: the short-key specialisation applies (hb = host copy of the batch descriptor)
@@ -3230,6 +3244,8 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
     // HBM path serves those far better than this kernel's per-row fallback (C5: 31 vs 95 ms)
     if (!records && use_lds && hb && !x_noshort && t.cap + 1 <= SHORT_MAX_SLOTS && short_eligible(S, *hb)) {
         u64 blocks = (rows + (u64)BLOCK * 16 - 1) / ((u64)BLOCK * 16);
+        static const u64 x_blocks = X_ENV("DBG_X_SHORT_BLOCKS") ? (u64)atoll(X_ENV("DBG_X_SHORT_BLOCKS")) : 0;
+        if (x_blocks) blocks = x_blocks;  // EXPERIMENT: grid size
         if (blocks > DBG_INSERT_MAX_BLOCKS) blocks = DBG_INSERT_MAX_BLOCKS;
         if (blocks < 1) blocks = 1;
         u64 rpb = (rows + blocks - 1) / blocks;
@@ -3248,8 +3264,39 @@ void launch_insert(hipStream_t s, const Spec* dspec, const Spec& S, const BatchD
         static const bool x_wide = X_ENV("DBG_X_NARROW") && X_ENV("DBG_X_NARROW")[0] == '0';
         if (x_wide) narrow = 0;
         static const bool x_tree = X_ENV("DBG_X_TREE") && X_ENV("DBG_X_TREE")[0] == '1';
+        u64* x_tr = nullptr;
+        if (kPhaseTrace && X_ENV("DBG_X_TRACE_SHORT")) {  // EXPERIMENT: 8 words per launch, 4096 launches
+            static u64* buf = nullptr;
+            static u32 launch = 0;
+            static const u64 init[8] = {~0ULL, ~0ULL, 0, 0, 0, 0, 0, 0};
+            if (!buf) {
+                if (hipMalloc((void**)&buf, 4096 * 64) != hipSuccess) buf = nullptr;
+                if (buf) hipMemset(buf, 0, 4096 * 64);
+                atexit([] {
+                    std::vector<u64> hb(4096 * 8);
+                    (void)hipDeviceSynchronize();
+                    (void)hipMemcpy(hb.data(), buf, hb.size() * 8, hipMemcpyDeviceToHost);
+                    std::vector<std::vector<double>> d(4);
+                    for (int k = 0; k < 4096; ++k) {
+                        const u64* r = &hb[k * 8];
+                        if (r[0] == 0 || r[0] == ~0ULL || r[4] == 0) continue;
+                        for (int p = 1; p <= 4; ++p) d[p - 1].push_back((double)(r[p] - r[0]) * 0.01);
+                    }
+                    const char* nm[] = {"first row loop end", "last row loop end", "last flush start", "last workgroup end"};
+                    for (int p = 0; p < 4; ++p) {
+                        if (d[p].empty()) continue;
+                        std::sort(d[p].begin(), d[p].end());
+                        fprintf(stderr, "short trace %-20s median %7.2f us  (n=%zu)\n", nm[p], d[p][d[p].size() / 2], d[p].size());
+                    }
+                });
+            }
+            if (buf) {
+                x_tr = buf + (u64)(launch++ & 4095) * 8;
+                (void)hipMemcpyAsync(x_tr, init, sizeof(init), hipMemcpyHostToDevice, s);
+            }
+        }
         hipLaunchKernelGGL(agg_insert_short_kernel, dim3((u32)blocks), dim3(BLOCK), shmem, s, dspec, batches, bid, rows, rpb, t, lslots,
-                           x_rep ? x_rep - 1 : 0u, x_short, narrow, x_tree && S.stride_words >= S.n_words + 3 ? 1 : 0);
+                           x_rep ? x_rep - 1 : 0u, x_short, narrow, x_tree && S.stride_words >= S.n_words + 3 ? 1 : 0, x_tr);
         return;
     }
     // enough workgroups to fill 256 CUs several times over, each a contiguous row range
