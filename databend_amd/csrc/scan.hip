@@ -390,6 +390,9 @@ __global__ void __launch_bounds__(64) pq_walk_kernel(ScanArgs a) {
 // RLE / bit-packed hybrid, expanded by a whole workgroup
 // ---------------------------------------------------------------------------------------------
 #define DEC_NT 256
+#ifndef PQ_PIECE
+#define PQ_PIECE 8192  // values per y-piece of a required PLAIN page
+#endif
 #define RMAX 512
 struct RunTable {
     u32 start[RMAX + 1];  // first value index of each run (start[nr] = end of the last one)
@@ -1222,7 +1225,9 @@ int dbg_parquet_decode(dbg_scan_ctx* ctx, const dbg_parquet_chunk* chunk, dbg_da
         }
         // required PLAIN pages are split over the grid's y dimension into pieces of >= 8192 values
         // (writers cap pages at 20 000 rows — pyarrow, parquet-rs — or at 1 MiB: up to 16 pieces)
-        const u32 ysplit = c.max_def_level ? 1u : (u32)std::min<u64>(16, std::max<u64>(1, (maxn + 8191) / 8192));
+        static const u64 x_piece = X_ENV("DBG_X_PQ_PIECE") ? (u64)atoll(X_ENV("DBG_X_PQ_PIECE")) : 0;  // EXPERIMENT
+        const u64 piece = x_piece ? x_piece : PQ_PIECE;
+        const u32 ysplit = c.max_def_level ? 1u : (u32)std::min<u64>(16, std::max<u64>(1, (maxn + piece - 1) / piece));
         ps = prof_scope_begin("pq_decode", s);
         hipLaunchKernelGGL(pq_decode_kernel, dim3((u32)n_pages, ysplit), dim3(DEC_NT), 0, s, a);
         prof_scope_end(ps);
