@@ -2700,10 +2700,16 @@ __device__ __forceinline__ void fused_chain_tagged(const Spec& S, const BatchDes
 // ------------------------------------------------------------------------------------------
 // agg_insert_fast: one non-null integer key column, optional `key <cmp> constant` predicate on
 // that same column (GROUP BY x WHERE x <> c: ClickBench Q8; or no predicate: Q16).  Streams the
-// key column with 16-byte loads (4 in flight per lane), evaluates the predicate on every value,
-// and stages the selected rows in the LDS table exactly like agg_insert.
+// key column with 16-byte loads (FAST_UNROLL per lane per grid round, the next round's issued
+// before this one is filtered), evaluates the predicate on every value, and stages the selected
+// rows in the LDS table exactly like agg_insert.
 // ------------------------------------------------------------------------------------------
-#define FAST_UNROLL 4
+#ifndef FAST_UNROLL
+// 16-byte loads per lane and round: C2 kernel (200 steps, three alternating rounds,
+// scripts/gpu_c2_variants.sh) 1 / 2 / 3 / 4 / 8 -> 45.5 / 40.6 / 41.9 / 43.4 / 55 us: two rounds
+// of two in flight keep each wave's window of the column to 2 x 2 grid strides
+#define FAST_UNROLL 2
+#endif
 #ifndef TAIL_ON
 // dynamic stream tail of fused-chain launches: measured and not kept (C2 step 45.7 -> 51.3 us,
 // profiles/r04/c2_tail_ab.json); make TAIL=1 builds it for A/B runs
