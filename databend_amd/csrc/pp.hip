@@ -856,7 +856,10 @@ __device__ __forceinline__ bool pp_fast_pred(const PPFast& F, u64 v) {
 // threads, so consecutive lanes store consecutive 8-byte words of one bucket's run — whole lines
 // per wave instead of 64 scattered records per store instruction.  LDS (dynamic): staged words
 // [NT * U * W] u64 | bucket of each staged record [NT * U] u16 | tile offsets [K] u32.
-__host__ __device__ constexpr int pp_l1_u(int W) { return W <= 2 ? 4 : (W <= 4 ? 2 : 1); }
+// rows per thread of a level-1 tile: C4 (W = 2) scatter at 1 / 2 / 4 -> 19.7-20.2 / 17.2-18.3 /
+// 18.6-19.9 ms, step 64.0-65.2 at 2 against 65.0-66.6 at 4 (alternating runs on one box,
+// scripts/gpu_cfg_variants.sh); the count 4.4 / 3.6 / 3.6 ms
+__host__ __device__ constexpr int pp_l1_u(int W) { return W <= 4 ? 2 : 1; }
 __host__ __device__ constexpr size_t pp_l1_sorted_lds(int W) {  // + the staged level-2 digits (u16 each)
     return (size_t)PP_NT * pp_l1_u(W) * W * 8 + (size_t)PP_NT * pp_l1_u(W) * 2 + 4 * (1u << PP_L1_BITS) +
            (size_t)PP_NT * pp_l1_u(W) * 2;
@@ -867,7 +870,7 @@ __global__ void __launch_bounds__(PP_NT) pp_l1_fixed_kernel(const PPFast F, cons
                                                            u32* __restrict__ cnt, const u64* __restrict__ off,
                                                            const u64* __restrict__ part_off, u8* __restrict__ dst, int sorted) {
     constexpr u32 K = 1u << PP_L1_BITS;
-    constexpr int U = pp_l1_u(W);  // (the count at twice this: 3.6 -> 4.8 ms on C4)
+    constexpr int U = pp_l1_u(W);  // rows per thread and tile
     __shared__ u32 hist[K];
     __shared__ u64 run[K];
     __shared__ u32 hist_total_;
